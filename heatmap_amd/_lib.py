@@ -1,0 +1,102 @@
+"""ctypes binding of the C-ABI in include/heatmap_amd.h.
+
+This module is the reference-side binding INTEGRATION.md describes: it is
+exactly what a maintainer of timfpark/heatmap would add to call the library.
+There is no CPU fallback: without the built library or a GPU every entry
+point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+from . import build as _build
+
+HM_OK = 0
+HM_E_NAN = 1
+HM_E_DOMAIN = 2
+HM_E_INF = 3
+HM_E_RANGE = 8
+HM_E_EXOTIC = 9
+HM_E_ARG = 16
+HM_E_CAPACITY = 17
+HM_E_HIP = 18
+HM_E_NOMEM = 19
+HM_COUNT_MAX_ZOOM = 22
+
+EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
+           "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats"]
+
+_LIB = None
+_LOCK = threading.Lock()
+
+
+class DeviceUnavailable(RuntimeError):
+    pass
+
+
+class DevicePathUnsupported(NotImplementedError):
+    """Input the reference accepts but this device path does not bin yet."""
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load() -> ctypes.CDLL:
+    """Load the native library (building it first if sources are newer)."""
+    global _LIB
+    with _LOCK:
+        if _LIB is not None:
+            return _LIB
+        path = _build.LIB
+        if not os.path.exists(path) or _build._stale():
+            try:
+                _build.build(verbose=False)
+            except Exception as e:  # pragma: no cover - surfaced to the caller
+                raise DeviceUnavailable("heatmap_amd: cannot build %s: %s" % (path, e)) from e
+        L = ctypes.CDLL(path)
+        c = ctypes
+        P = c.POINTER
+        vp = c.c_void_p
+        L.hm_abi_version.restype = c.c_int
+        L.hm_status_string.argtypes = [c.c_int]
+        L.hm_status_string.restype = c.c_char_p
+        L.hm_ctx_create.argtypes = [P(vp), c.c_int, vp]
+        L.hm_ctx_set_stream.argtypes = [vp, vp]
+        L.hm_ctx_destroy.argtypes = [vp]
+        L.hm_project.argtypes = [vp, vp, vp, c.c_int64, c.c_int, vp, vp, vp]
+        L.hm_count.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_count_tiles.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
+        L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
+        for name in EXPORTS:
+            getattr(L, name).restype = getattr(L, name).restype or c.c_int
+        L.hm_status_string.restype = c.c_char_p
+        _LIB = L
+        return L
+
+
+def status_string(st: int) -> str:
+    return load().hm_status_string(int(st)).decode()
+
+
+def raise_for(st: int, index: int = -1):
+    """Raise the reference's exception for a per-point error kind."""
+    if st == HM_OK:
+        return
+    where = "" if index < 0 else " (point %d)" % index
+    if st == HM_E_NAN:
+        raise ValueError("cannot convert float NaN to integer")
+    if st == HM_E_DOMAIN:
+        raise ValueError("math domain error")
+    if st == HM_E_INF:
+        raise OverflowError("cannot convert float infinity to integer")
+    if st in (HM_E_RANGE, HM_E_EXOTIC):
+        raise DevicePathUnsupported(status_string(st) + where)
+    if st == HM_E_HIP:
+        raise DeviceUnavailable(status_string(st))
+    if st == HM_E_NOMEM:
+        raise MemoryError(status_string(st))
+    raise RuntimeError("heatmap_amd: %s%s" % (status_string(st), where))

@@ -1,0 +1,532 @@
+/* C-ABI of heatmap_amd (include/heatmap_amd.h): context, device memory arena
+ * and the host-side orchestration of the count pipeline.
+ *
+ * Per hm_count call (Z = zmax, zb = max(0, Z-7)):
+ *   levels z_1 = min(6, zb), z_{l+1} = min(z_l + 5, zb) ... z_L = zb
+ *   k_project_partition (level 1) -> [k_runscan, scan, k_compact, k_partition]*
+ *   -> k_aggregate (zooms Z..zb+1) -> k_pool for l = L..1 (zooms zb..0).
+ * The host reads back two or three scalars per level (bucket and work-item
+ * counts) to size the next grid; everything else stays on the device.
+ */
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+#include "../../include/heatmap_amd.h"
+#include "hm_pipeline.h"
+
+namespace {
+
+struct Buf {
+    void* p = nullptr;
+    size_t cap = 0;
+};
+
+struct Level {
+    int zc;              /* child zoom z_l */
+    int dbits;           /* 2*(z_l - z_{l-1}) */
+    uint32_t nparents;   /* |B_{l-1}| */
+    uint64_t nchildren;  /* nparents << dbits */
+    uint32_t count = 0;  /* |B_l| */
+    uint32_t items = 0;  /* work items of the next stage */
+    bool out16 = false;
+};
+
+}  // namespace
+
+struct hm_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::vector<Buf> bufs;
+    unsigned long long* state = nullptr;      /* device: err, exotic, slow, cursor, nslots */
+    unsigned long long* host_state = nullptr; /* pinned mirror */
+    int64_t last_err_index = -1;
+    int last_err_kind = 0;
+    int64_t last_slow = 0;
+    double stage_us[8] = {0};
+    hipEvent_t ev[10];
+};
+
+enum {
+    ST_ERR = 0,
+    ST_EXOTIC = 1,
+    ST_SLOW = 2,
+    ST_CURSOR = 3,
+    ST_NSLOTS = 4,
+    ST_COUNT = 8
+};
+
+static int hip_fail(hipError_t e, const char* what)
+{
+    if (e == hipSuccess) return HM_OK;
+    fprintf(stderr, "heatmap_amd: HIP error in %s: %s\n", what, hipGetErrorString(e));
+    return HM_E_HIP;
+}
+
+#define HIPCHK(x)                                  \
+    do {                                           \
+        int _st = hip_fail((x), #x);               \
+        if (_st != HM_OK) return _st;              \
+    } while (0)
+
+/* named arena slots */
+enum {
+    B_KEYS_A, B_KEYS_B, B_RUNS_A, B_RUNS_B, B_RUNPRE_A, B_RUNPRE_B, B_NRUNS, B_NKEYS, B_VALS, B_PREFIX,
+    B_PARTIAL, B_TOTAL, B_ROOT,
+    B_BK0, /* 4 levels x 8 arrays */
+    B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
+    B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
+    B_SLOTS = B_TOT0 + HM_MAX_LEVELS + 1,
+    B_SLOTBKT, B_GSLOTS, B_COUNT
+};
+
+static int ensure(hm_ctx* c, int slot, size_t bytes, void** out)
+{
+    if (bytes == 0) bytes = 16;
+    Buf& b = c->bufs[slot];
+    if (b.cap < bytes) {
+        if (b.p) HIPCHK(hipFree(b.p));
+        b.p = nullptr;
+        b.cap = 0;
+        size_t want = bytes + bytes / 8;
+        if (hipMalloc(&b.p, want) != hipSuccess) {
+            (void)hipGetLastError();
+            b.p = nullptr;
+            return HM_E_NOMEM;
+        }
+        b.cap = want;
+    }
+    *out = b.p;
+    return HM_OK;
+}
+
+#define ENSURE(slot, bytes, ptr)                                         \
+    do {                                                                 \
+        void* _p = nullptr;                                              \
+        int _st = ensure(ctx, (slot), (size_t)(bytes), &_p);             \
+        if (_st != HM_OK) return _st;                                    \
+        ptr = (decltype(ptr))_p;                                         \
+    } while (0)
+
+extern "C" {
+
+int hm_abi_version(void) { return HM_ABI_VERSION; }
+
+const char* hm_status_string(int s)
+{
+    switch (s) {
+    case HM_OK: return "ok";
+    case HM_E_NAN: return "cannot convert float NaN to integer";
+    case HM_E_DOMAIN: return "math domain error";
+    case HM_E_INF: return "cannot convert float infinity to integer";
+    case HM_E_RANGE: return "value outside the range supported by the device path";
+    case HM_E_EXOTIC: return "tile outside [0, 2^zmax)^2 is not binned by the device path";
+    case HM_E_ARG: return "invalid argument";
+    case HM_E_CAPACITY: return "output capacity too small";
+    case HM_E_HIP: return "HIP runtime error";
+    case HM_E_NOMEM: return "device allocation failed";
+    default: return "unknown status";
+    }
+}
+
+int hm_ctx_create(hm_ctx** out, int device, void* stream)
+{
+    if (!out) return HM_E_ARG;
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= device || device < 0) {
+        (void)hipGetLastError();
+        fprintf(stderr, "heatmap_amd: no HIP device %d (found %d); there is no CPU fallback\n", device, n);
+        return HM_E_HIP;
+    }
+    HIPCHK(hipSetDevice(device));
+    hm_ctx* c = new hm_ctx();
+    c->device = device;
+    c->stream = (hipStream_t)stream;
+    c->bufs.resize(B_COUNT);
+    if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc(&c->host_state, 4 * ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
+        delete c;
+        return HM_E_NOMEM;
+    }
+    for (int i = 0; i < 10; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    *out = c;
+    return HM_OK;
+}
+
+int hm_ctx_set_stream(hm_ctx* c, void* stream)
+{
+    if (!c) return HM_E_ARG;
+    c->stream = (hipStream_t)stream;
+    return HM_OK;
+}
+
+int hm_ctx_destroy(hm_ctx* c)
+{
+    if (!c) return HM_OK;
+    hipSetDevice(c->device);
+    for (auto& b : c->bufs)
+        if (b.p) hipFree(b.p);
+    if (c->state) hipFree(c->state);
+    if (c->host_state) hipHostFree(c->host_state);
+    for (int i = 0; i < 10; i++) hipEventDestroy(c->ev[i]);
+    delete c;
+    return HM_OK;
+}
+
+int hm_last_error(hm_ctx* c, int64_t* index, int* kind)
+{
+    if (!c) return HM_E_ARG;
+    if (index) *index = c->last_err_index;
+    if (kind) *kind = c->last_err_kind;
+    return HM_OK;
+}
+
+int hm_last_stats(hm_ctx* c, int64_t* slow_points, double* stage_us, int n_stages)
+{
+    if (!c) return HM_E_ARG;
+    if (slow_points) *slow_points = c->last_slow;
+    for (int i = 0; i < n_stages && i < 8; i++) stage_us[i] = c->stage_us[i];
+    return HM_OK;
+}
+
+}  // extern "C"
+
+static int reset_state(hm_ctx* ctx)
+{
+    HIPCHK(hipMemsetAsync(ctx->state, 0, ST_COUNT * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->state + ST_ERR, 0xFF, 2 * sizeof(unsigned long long), ctx->stream));
+    return HM_OK;
+}
+
+static int read_state(hm_ctx* ctx)
+{
+    HIPCHK(hipMemcpyAsync(ctx->host_state, ctx->state, ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          ctx->stream));
+    HIPCHK(hipStreamSynchronize(ctx->stream));
+    return HM_OK;
+}
+
+static int take_error(hm_ctx* ctx)
+{
+    const unsigned long long e = ctx->host_state[ST_ERR];
+    const unsigned long long x = ctx->host_state[ST_EXOTIC];
+    ctx->last_slow = (int64_t)ctx->host_state[ST_SLOW];
+    /* the first failing point in input order wins; a projection error at a
+     * smaller index than an exotic point is reported first */
+    const unsigned long long w = e < x ? e : x;
+    if (w == ~0ull) {
+        ctx->last_err_index = -1;
+        ctx->last_err_kind = HM_OK;
+        return HM_OK;
+    }
+    ctx->last_err_index = (int64_t)(w >> 8);
+    ctx->last_err_kind = (int)(w & 0xFF);
+    return ctx->last_err_kind;
+}
+
+extern "C" int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
+                          int64_t* col, uint8_t* status)
+{
+    if (!ctx || n < 0 || zoom < 0 || zoom > 30 || (n > 0 && (!lat || !lon || !row || !col || !status)))
+        return HM_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    int st = reset_state(ctx);
+    if (st) return st;
+    if (n > 0)
+        hm_launch_project(ctx->stream, lat, lon, n, zoom, row, col, status, ctx->state + ST_ERR, ctx->state + ST_SLOW);
+    HIPCHK(hipGetLastError());
+    if ((st = read_state(ctx))) return st;
+    return take_error(ctx);
+}
+
+/* ------------------------------------------------------------------------ */
+
+static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows, const int64_t* cols,
+                      const uint8_t* keep, int64_t n, int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out,
+                      int64_t capacity, int64_t* n_out)
+{
+    if (!ctx || !n_out || n < 0 || n >= (int64_t)0xFFFFFFF0ll || zmin < 0 || zmax < zmin ||
+        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && (!keys_out || !counts_out)))
+        return HM_E_ARG;
+    *n_out = 0;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int Z = zmax;
+    const int zb = Z > HM_AG_LG ? Z - HM_AG_LG : 0;
+    int zs[HM_MAX_LEVELS];
+    int L = 0;
+    {
+        int z = zb < 6 ? zb : 6;
+        zs[L++] = z;
+        while (z < zb) {
+            z = std::min(z + 5, zb);
+            if (L >= HM_MAX_LEVELS) return HM_E_ARG;
+            zs[L++] = z;
+        }
+    }
+    /* key bits after level l: 2*(Z - zs[l]); must fit u32 (level 1 output) */
+    if (2 * (Z - zs[0]) > 32) return HM_E_ARG;
+    int st = reset_state(ctx);
+    if (st) return st;
+
+    hipEvent_t* ev = ctx->ev;
+    int nev = 0;
+    for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
+    HIPCHK(hipEventRecord(ev[nev++], s));
+
+    /* root bucket list B_0: one bucket (the zoom-0 tile) */
+    const uint32_t tiles1 = (uint32_t)((n + HM_T1 - 1) / HM_T1);
+    uint32_t* root = nullptr;
+    ENSURE(B_ROOT, 4 * sizeof(uint32_t) + 2 * sizeof(uint64_t), root);
+    {
+        /* staged through the pinned scratch: [0, tiles1, 0, 0 | morton 0, 0] */
+        unsigned long long* up = ctx->host_state + ST_COUNT;
+        HIPCHK(hipStreamSynchronize(s));
+        up[0] = (unsigned long long)tiles1 << 32;
+        up[1] = 0;
+        up[2] = 0;
+        up[3] = 0;
+        HIPCHK(hipMemcpyAsync(root, up, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+    }
+    const uint32_t* parent_item_begin = root;
+    const uint64_t* parent_morton = (const uint64_t*)(root + 4);
+    uint32_t nparents = 1;
+
+    Level lv[HM_MAX_LEVELS];
+    HmBuckets B[HM_MAX_LEVELS];
+    memset(B, 0, sizeof(B));
+    void* keys_cur = nullptr;
+    uint2* runs_cur = nullptr;
+    uint32_t* runpre_cur = nullptr;
+    int slot_k = 0; /* ping-pong A/B */
+    uint32_t nslots = 0;
+    int32_t* slots = nullptr;
+    uint32_t* slot_bucket = nullptr;
+
+    for (int l = 0; l < L; l++) {
+        Level& V = lv[l];
+        V.zc = zs[l];
+        V.dbits = 2 * (zs[l] - (l ? zs[l - 1] : 0));
+        V.nparents = nparents;
+        V.nchildren = (uint64_t)nparents << V.dbits;
+        V.out16 = (l == L - 1);
+        const int restbits = 2 * (Z - zs[l]);
+        const uint64_t ntiles = (l == 0) ? tiles1 : lv[l - 1].items;
+        const uint64_t tile_keys = (l == 0) ? HM_T1 : HM_TN;
+        if (V.nchildren > (uint64_t)HM_SCAN_LIMIT) return HM_E_NOMEM;
+
+        /* outputs of the level's partition kernel */
+        void* keys_out;
+        uint2* runs_out;
+        uint32_t* runpre_out;
+        uint32_t* nruns;
+        ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, ntiles * tile_keys * (V.out16 ? 2 : 4), keys_out);
+        ENSURE(slot_k ? B_RUNS_B : B_RUNS_A, (ntiles << V.dbits) * sizeof(uint2), runs_out);
+        ENSURE(slot_k ? B_RUNPRE_B : B_RUNPRE_A, (ntiles << V.dbits) * sizeof(uint32_t), runpre_out);
+        ENSURE(B_NRUNS, V.nchildren * sizeof(uint32_t), nruns);
+        HIPCHK(hipMemsetAsync(nruns, 0, V.nchildren * sizeof(uint32_t), s));
+
+        if (l == 0) {
+            HmPart1Args a;
+            memset(&a, 0, sizeof(a));
+            a.lat = lat;
+            a.lon = lon;
+            a.rows_in = rows;
+            a.cols_in = cols;
+            a.keep = keep;
+            a.n = n;
+            a.Z = Z;
+            a.dbits = V.dbits;
+            a.restbits = restbits;
+            a.tiles = tiles1;
+            a.keys_out = keys_out;
+            a.nruns = nruns;
+            a.runs = runs_out;
+            a.err_word = ctx->state + ST_ERR;
+            a.exotic_word = ctx->state + ST_EXOTIC;
+            a.slow_count = ctx->state + ST_SLOW;
+            hm_launch_part1(s, a, V.out16, rows != nullptr);
+            HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(ev[nev++], s));
+            if ((st = read_state(ctx))) return st;
+            if ((st = take_error(ctx))) return st;
+        } else {
+            HmPartNArgs a;
+            memset(&a, 0, sizeof(a));
+            a.parent = B[l - 1];
+            a.keys_in = (const uint32_t*)keys_cur;
+            a.runs_in = runs_cur;
+            a.runpre_in = runpre_cur;
+            a.dbits = V.dbits;
+            a.restbits = restbits;
+            a.keys_out = keys_out;
+            a.nruns_out = nruns;
+            a.runs_out = runs_out;
+            hm_launch_partN(s, a, lv[l - 1].items, V.out16);
+            HIPCHK(hipGetLastError());
+        }
+
+        /* run scan + compaction into B_l */
+        uint32_t* nkeys;
+        uint64_t *vals, *prefix, *partial, *total;
+        ENSURE(B_NKEYS, V.nchildren * sizeof(uint32_t), nkeys);
+        ENSURE(B_VALS, V.nchildren * sizeof(uint64_t), vals);
+        ENSURE(B_PREFIX, V.nchildren * sizeof(uint64_t), prefix);
+        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+        ENSURE(B_TOTAL, sizeof(uint64_t), total);
+        HmScanArgs sa;
+        sa.nchildren = V.nchildren;
+        sa.dbits = V.dbits;
+        sa.nruns = nruns;
+        sa.runs = runs_out;
+        sa.runpre = runpre_out;
+        sa.parent_item_begin = parent_item_begin;
+        sa.item_keys = (l == L - 1) ? HM_TA : HM_TN;
+        sa.nkeys = nkeys;
+        sa.vals = vals;
+        hm_launch_runscan(s, sa);
+        hm_launch_scan(s, vals, V.nchildren, partial, prefix, total);
+        HIPCHK(hipGetLastError());
+
+        /* B_l arrays: sized by nchildren (upper bound of |B_l|) */
+        const uint64_t cap = V.nchildren + 1;
+        HmCompactArgs ca;
+        memset(&ca, 0, sizeof(ca));
+        ENSURE(B_BK0 + l * 8 + 0, cap * 4, ca.out.nkeys);
+        ENSURE(B_BK0 + l * 8 + 1, cap * 4, ca.out.nruns);
+        ENSURE(B_BK0 + l * 8 + 2, cap * 4, ca.out.rbase);
+        ENSURE(B_BK0 + l * 8 + 3, cap * 4, ca.out.item_begin);
+        ENSURE(B_BK0 + l * 8 + 4, cap * 4, ca.out.digit);
+        ENSURE(B_BK0 + l * 8 + 5, cap * 8, ca.out.morton);
+        uint32_t* child_begin;
+        ENSURE(B_CHILD0 + l, ((uint64_t)nparents + 1) * 4, child_begin);
+        ca.nchildren = V.nchildren;
+        ca.nparents = nparents;
+        ca.dbits = V.dbits;
+        ca.vals = vals;
+        ca.prefix = prefix;
+        ca.total = total;
+        ca.nkeys = nkeys;
+        ca.nruns = nruns;
+        ca.parent_item_begin = parent_item_begin;
+        ca.parent_morton = parent_morton;
+        ca.child_begin = child_begin;
+        if (l == L - 1) {
+            ENSURE(B_SLOTS, cap * 4, slots);
+            ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
+            ca.slots = slots;
+            ca.nslots = (uint32_t*)(ctx->state + ST_NSLOTS);
+            ca.slot_bucket = slot_bucket;
+        }
+        hm_launch_compact(s, ca);
+        HIPCHK(hipGetLastError());
+        unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+        HIPCHK(hipMemcpyAsync(down, total, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        if ((st = read_state(ctx))) return st;
+        const uint64_t tot_h = down[0];
+        V.count = (uint32_t)(tot_h >> 32);
+        V.items = (uint32_t)(tot_h & 0xFFFFFFFFull);
+        if (l == L - 1) nslots = (uint32_t)(ctx->host_state[ST_NSLOTS] & 0xFFFFFFFFull);
+
+        HmBuckets& b = B[l];
+        b.count = V.count;
+        b.nkeys = ca.out.nkeys;
+        b.nruns = ca.out.nruns;
+        b.rbase = ca.out.rbase;
+        b.item_begin = ca.out.item_begin;
+        b.digit = ca.out.digit;
+        b.morton = ca.out.morton;
+        b.slots = (l == L - 1) ? slots : nullptr;
+
+        keys_cur = keys_out;
+        runs_cur = runs_out;
+        runpre_cur = runpre_out;
+        parent_item_begin = ca.out.item_begin;
+        parent_morton = ca.out.morton;
+        nparents = V.count;
+        slot_k ^= 1;
+    }
+    HIPCHK(hipEventRecord(ev[nev++], s));
+
+    /* final aggregation over B_L */
+    HmOut o;
+    o.keys = keys_out;
+    o.counts = counts_out;
+    o.capacity = (uint64_t)capacity;
+    o.cursor = ctx->state + ST_CURSOR;
+    o.zmin = zmin;
+    o.zmax = zmax;
+    unsigned long long* totals[HM_MAX_LEVELS + 1];
+    for (int l = 0; l < L; l++) ENSURE(B_TOT0 + l, ((uint64_t)lv[l].count + 1) * 8, totals[l]);
+    {
+        const int l = L - 1;
+        uint32_t* gslots = nullptr;
+        ENSURE(B_GSLOTS, (uint64_t)(nslots ? nslots : 1) * HM_AG_CELLS * 4, gslots);
+        if (nslots) HIPCHK(hipMemsetAsync(gslots, 0, (size_t)nslots * HM_AG_CELLS * 4, s));
+        HIPCHK(hipMemsetAsync(totals[l], 0, ((size_t)lv[l].count + 1) * 8, s));
+        HmAggArgs a;
+        memset(&a, 0, sizeof(a));
+        a.B = B[l];
+        a.keys = (const uint16_t*)keys_cur;
+        a.runs = runs_cur;
+        a.runpre = runpre_cur;
+        a.Z = Z;
+        a.lg = Z - zb;
+        a.totals = totals[l];
+        a.gslots = gslots;
+        a.slot_bucket = slot_bucket;
+        a.out = o;
+        hm_launch_aggregate(s, a, lv[l].items, nslots);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[nev++], s));
+    /* pooling: level l children -> parents in B_{l-1} (root for l = 0) */
+    for (int l = L - 1; l >= 0; l--) {
+        HmPoolArgs pa;
+        memset(&pa, 0, sizeof(pa));
+        pa.dbits = lv[l].dbits;
+        pa.z_child = lv[l].zc;
+        pa.emit_root = (l == 0);
+        void* cb = ctx->bufs[B_CHILD0 + l].p;
+        pa.child_begin = (const uint32_t*)cb;
+        pa.child_digit = B[l].digit;
+        pa.child_totals = totals[l];
+        pa.parent_morton = l ? B[l - 1].morton : nullptr;
+        pa.parent_totals = l ? totals[l - 1] : nullptr;
+        pa.out = o;
+        hm_launch_pool(s, pa, lv[l].nparents);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(ev[nev++], s));
+    if ((st = read_state(ctx))) return st;
+    for (int i = 0; i + 1 < nev; i++) {
+        float ms = 0;
+        hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+        ctx->stage_us[i] = ms * 1000.0;
+    }
+    const unsigned long long nc = ctx->host_state[ST_CURSOR];
+    *n_out = (int64_t)nc;
+    if (nc > (unsigned long long)capacity) return HM_E_CAPACITY;
+    return HM_OK;
+}
+
+extern "C" int hm_count(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep, int64_t n, int zmin,
+                        int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+{
+    if (n > 0 && (!lat || !lon)) return HM_E_ARG;
+    return count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out);
+}
+
+extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep, int64_t n,
+                              int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
+                              int64_t* n_out)
+{
+    if (n > 0 && (!row || !col)) return HM_E_ARG;
+    return count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out);
+}

@@ -1,0 +1,682 @@
+/* gfx950 kernels of the heatmap hot path.
+ *
+ * Path (SURVEY.md section 8a, a-1 .. a-11), one hm_count() call:
+ *
+ *   k_project_partition   fp64 lat/lon SoA -> tile row/col at zoom Z (exact,
+ *                         hm_project.h) -> Morton key -> LDS counting sort of an
+ *                         8192-point tile by the key's top digit (zoom z1
+ *                         tile); writes the tile's keys (u32/u16, top digit
+ *                         dropped) contiguously and one run record per
+ *                         non-empty digit.  Reads 16 B/point, writes 4 B/point.
+ *   k_partition           the same counting sort one level down, gathering a
+ *                         parent bucket's runs (wave per run).  Levels stop at
+ *                         zoom zb = Z - 7, whose buckets hold 128x128 zoom-Z
+ *                         bins.
+ *   k_aggregate           per zoom-zb bucket: LDS-privatised dense 128x128 u32
+ *                         histogram of the u16 in-bucket keys (wave-aggregated
+ *                         atomics), then an in-LDS 4:1 pyramid emitting every
+ *                         non-empty cell of zooms Z .. zb+1.  Buckets larger
+ *                         than one work item merge through global atomics and
+ *                         k_aggregate_merged emits them.
+ *   k_pool                per parent bucket: dense LDS array of its children's
+ *                         totals -> 4:1 pyramid -> zooms z_l .. z_{l-1}+1; the
+ *                         root emits zooms z1 .. 0.
+ *   k_runscan / scans / k_compact: turn per-digit run counters into compact,
+ *                         Morton-ordered bucket lists and work-item prefixes.
+ *
+ * The Morton key makes every parent a right shift (key >> 2), which is the
+ * reference's tile-centre re-projection on the shift window
+ * and the direct projection at every zoom (a-1).  Counts are integers (u32
+ * per call, u64 out): the reference's float sums of 1.0 are exact below 2^53.
+ */
+#include <hip/hip_runtime.h>
+#include "hm_device.h"
+#include "hm_project.h"
+#include "hm_pipeline.h"
+
+/* ------------------------------------------------------------------------ */
+/* projection API kernel (hm_project)                                        */
+/* ------------------------------------------------------------------------ */
+
+__global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat, const double* __restrict__ lon,
+                                                 int64_t n, int zoom, int64_t* __restrict__ row,
+                                                 int64_t* __restrict__ col, uint8_t* __restrict__ status,
+                                                 unsigned long long* err_word, unsigned long long* slow_count)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        int64_t r = 0, c = 0;
+        int slow = 0;
+        const int st = hm_project_point(lat[i], lon[i], zoom, &r, &c, &slow);
+        row[i] = st == HM_OK ? r : 0;
+        col[i] = st == HM_OK ? c : 0;
+        status[i] = (uint8_t)st;
+        if (HM_UNLIKELY(st != HM_OK)) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+        const uint64_t sm = __ballot(slow);
+        if (sm && hm_lane() == __ffsll((unsigned long long)sm) - 1) atomicAdd(slow_count, (unsigned long long)__popcll(sm));
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* level 1: projection fused with the first partition                        */
+/* ------------------------------------------------------------------------ */
+
+template <typename OutT, bool FROM_TILES>
+__global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args a)
+{
+    __shared__ uint32_t cur[HM_MAX_F1];
+    __shared__ OutT stage[HM_T1];
+    __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
+    const int tid = threadIdx.x;
+    const int F = 1 << a.dbits;
+    for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
+    __syncthreads();
+
+    const int64_t base = (int64_t)blockIdx.x * HM_T1;
+    const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
+    const uint32_t lim = 1u << a.Z;
+    uint32_t dig[HM_P1_PPT];
+    uint32_t rest[HM_P1_PPT];
+    int nslow = 0;
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT / 2; k++) {
+        const int64_t i0 = base + 2 * ((int64_t)k * HM_P1_THREADS + tid);
+#pragma unroll
+        for (int h = 0; h < 2; h++) {
+            const int64_t i = i0 + h;
+            dig[2 * k + h] = 0xFFFFFFFFu;
+            rest[2 * k + h] = 0;
+            if (i >= a.n) continue;
+            int64_t r = 0, c = 0;
+            int st, slow = 0;
+            if (FROM_TILES) {
+                r = a.rows_in[i];
+                c = a.cols_in[i];
+                st = HM_OK;
+            } else {
+                st = hm_project_point(a.lat[i], a.lon[i], a.Z, &r, &c, &slow);
+            }
+            nslow += slow;
+            if (HM_UNLIKELY(st != HM_OK)) {
+                atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+                continue;
+            }
+            if (a.keep && !a.keep[i]) continue;
+            if (HM_UNLIKELY((uint64_t)r >= lim || (uint64_t)c >= lim)) {
+                atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
+                continue;
+            }
+            const uint64_t m = hm_morton((uint32_t)r, (uint32_t)c);
+            dig[2 * k + h] = (uint32_t)(m >> a.restbits);
+            rest[2 * k + h] = (uint32_t)m & restmask;
+        }
+    }
+    if (!FROM_TILES) {
+        const uint32_t ws = hm_wave_sum((uint32_t)nslow);
+        if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
+    }
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, dig[k], dig[k] != 0xFFFFFFFFu);
+    __syncthreads();
+
+    /* exclusive scan of the digit histogram; one run record per digit */
+    constexpr int PER = HM_MAX_F1 / HM_P1_THREADS;
+    uint32_t cnt[PER];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        cnt[q] = d < F ? cur[d] : 0u;
+        s += cnt[q];
+    }
+    uint32_t total;
+    uint32_t off = hm_block_excl_scan<HM_P1_THREADS>(s, scr, &total);
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F) {
+            cur[d] = off;
+            if (cnt[q]) {
+                const uint32_t idx = atomicAdd(&a.nruns[d], 1u);
+                a.runs[(uint64_t)d * a.tiles + idx] = make_uint2((uint32_t)base + off, cnt[q]);
+            }
+        }
+        off += cnt[q];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT; k++) {
+        const bool v = dig[k] != 0xFFFFFFFFu;
+        const uint32_t pos = hm_lds_claim(cur, dig[k], v);
+        if (v) stage[pos] = (OutT)rest[k];
+    }
+    __syncthreads();
+    OutT* out = (OutT*)a.keys_out + base;
+    for (uint32_t i = tid; i < total; i += HM_P1_THREADS) out[i] = stage[i];
+}
+
+/* ------------------------------------------------------------------------ */
+/* shared: locate a work item and stream its keys                            */
+/* ------------------------------------------------------------------------ */
+
+__device__ __forceinline__ uint32_t hm_upper_bound(const uint32_t* a, uint32_t n, uint32_t v)
+{
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] <= v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+struct HmItem {
+    uint32_t bucket;   /* compact parent bucket */
+    uint32_t j;        /* work item within the bucket */
+    uint32_t nitems;   /* work items of the bucket */
+    uint32_t a, b;     /* logical key range */
+    uint32_t rb, nr;   /* run list */
+    uint32_t r0;       /* first run overlapping [a, b) */
+};
+
+__device__ __forceinline__ HmItem hm_locate(const HmBuckets& B, uint32_t g, uint32_t T, const uint32_t* runpre)
+{
+    HmItem it;
+    it.bucket = hm_upper_bound(B.item_begin, B.count + 1, g) - 1;
+    it.j = g - B.item_begin[it.bucket];
+    it.nitems = B.item_begin[it.bucket + 1] - B.item_begin[it.bucket];
+    const uint32_t nk = B.nkeys[it.bucket];
+    it.a = it.j * T;
+    it.b = min(it.a + T, nk);
+    it.rb = B.rbase[it.bucket];
+    it.nr = B.nruns[it.bucket];
+    it.r0 = hm_upper_bound(runpre + it.rb, it.nr, it.a);
+    return it;
+}
+
+/* Calls f(key, valid) for every key of [a, b); one wave per run. Wave-uniform. */
+template <typename InT, int THREADS, typename F>
+__device__ __forceinline__ void hm_stream_item(const HmItem& it, const InT* keys, const uint2* runs,
+                                               const uint32_t* runpre, F f)
+{
+    const int w = threadIdx.x >> 6;
+    const int lane = hm_lane();
+    for (uint32_t r = it.r0 + w; r < it.nr; r += THREADS / 64) {
+        const uint2 run = runs[it.rb + r];
+        const uint32_t re = runpre[it.rb + r];
+        const uint32_t rs = re - run.y;
+        if (rs >= it.b) break;
+        const uint32_t s = max(rs, it.a);
+        const uint32_t e = min(re, it.b);
+        const InT* src = keys + run.x + (s - rs);
+        for (uint32_t i0 = 0; i0 < e - s; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const bool v = i < e - s;
+            const uint32_t key = v ? (uint32_t)src[i] : 0u;
+            f(key, v);
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* levels >= 2: gather a parent's runs, counting sort by the next digit      */
+/* ------------------------------------------------------------------------ */
+
+template <typename OutT>
+__global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
+{
+    __shared__ uint32_t stage_in[HM_TN];
+    __shared__ OutT stage_out[HM_TN];
+    __shared__ uint32_t cur[HM_MAX_FN];
+    __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
+    __shared__ uint32_t scnt;
+    const int tid = threadIdx.x;
+    const int F = 1 << a.dbits;
+    for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
+    if (tid == 0) scnt = 0;
+    __syncthreads();
+    const HmItem it = hm_locate(a.parent, blockIdx.x, HM_TN, a.runpre_in);
+    const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
+    hm_stream_item<uint32_t, HM_PN_THREADS>(it, a.keys_in, a.runs_in, a.runpre_in, [&](uint32_t key, bool v) {
+        const uint32_t d = key >> a.restbits;
+        hm_lds_count(cur, d, v);
+        const uint64_t vm = __ballot(v);
+        uint32_t wp = 0;
+        if (hm_lane() == 0) wp = atomicAdd(&scnt, (uint32_t)__popcll(vm));
+        wp = __shfl(wp, 0, 64);
+        if (v) stage_in[wp + hm_mbcnt(vm)] = key;
+    });
+    __syncthreads();
+    const uint32_t total = scnt;
+    constexpr int PER = HM_MAX_FN / HM_PN_THREADS;
+    uint32_t cnt[PER];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        cnt[q] = d < F ? cur[d] : 0u;
+        s += cnt[q];
+    }
+    uint32_t tot2;
+    uint32_t off = hm_block_excl_scan<HM_PN_THREADS>(s, scr, &tot2);
+    const uint32_t tile0 = a.parent.item_begin[it.bucket];
+    const uint64_t gtile = blockIdx.x;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F) {
+            cur[d] = off;
+            if (cnt[q]) {
+                const uint64_t child = (uint64_t)it.bucket * F + d;
+                const uint32_t idx = atomicAdd(&a.nruns_out[child], 1u);
+                const uint64_t rb = (uint64_t)tile0 * F + (uint64_t)d * it.nitems;
+                a.runs_out[rb + idx] = make_uint2((uint32_t)(gtile * HM_TN) + off, cnt[q]);
+            }
+        }
+        off += cnt[q];
+    }
+    __syncthreads();
+    for (uint32_t i0 = 0; i0 < total; i0 += HM_PN_THREADS) {
+        const uint32_t i = i0 + tid;
+        const bool v = i < total;
+        const uint32_t key = v ? stage_in[i] : 0u;
+        const uint32_t d = key >> a.restbits;
+        const uint32_t pos = hm_lds_claim(cur, d, v);
+        if (v) stage_out[pos] = (OutT)(key & restmask);
+    }
+    __syncthreads();
+    OutT* out = (OutT*)a.keys_out + gtile * HM_TN;
+    for (uint32_t i = tid; i < total; i += HM_PN_THREADS) out[i] = stage_out[i];
+}
+
+/* ------------------------------------------------------------------------ */
+/* run scan + compaction of dense children into a Morton-ordered bucket list */
+/* ------------------------------------------------------------------------ */
+
+/* one wave per dense child c = p*F + d: inclusive prefix of its run counts,
+ * key total, and the packed scan value (1 << 32 | work items) */
+__global__ __launch_bounds__(256) void k_runscan(HmScanArgs a)
+{
+    const int lane = hm_lane();
+    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
+    for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < a.nchildren; c += nwaves) {
+        const uint32_t nr = a.nruns[c];
+        if (nr == 0) {
+            if (lane == 0) {
+                a.nkeys[c] = 0;
+                a.vals[c] = 0;
+            }
+            continue;
+        }
+        const uint64_t p = c >> a.dbits;
+        const uint64_t d = c & ((1ull << a.dbits) - 1);
+        const uint32_t t0 = a.parent_item_begin[p];
+        const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+        const uint64_t rb = (uint64_t)t0 * (1ull << a.dbits) + d * tp;
+        uint32_t carry = 0;
+        for (uint32_t i0 = 0; i0 < nr; i0 += 64) {
+            const uint32_t i = i0 + lane;
+            const uint32_t v = i < nr ? a.runs[rb + i].y : 0u;
+            const uint32_t inc = hm_wave_incl_scan(v) + carry;
+            if (i < nr) a.runpre[rb + i] = inc;
+            carry = __shfl(inc, 63, 64);
+        }
+        if (lane == 0) {
+            a.nkeys[c] = carry;
+            const uint64_t items = (carry + a.item_keys - 1) / a.item_keys;
+            a.vals[c] = (1ull << 32) | items;
+        }
+    }
+}
+
+#define HM_SCAN_ITEMS 4096
+#define HM_SCAN_THREADS 256
+
+__global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_reduce(const uint64_t* v, uint64_t n, uint64_t* partial)
+{
+    __shared__ uint64_t red[HM_SCAN_THREADS / 64];
+    const uint64_t b0 = (uint64_t)blockIdx.x * HM_SCAN_ITEMS;
+    uint64_t s = 0;
+    for (int k = threadIdx.x; k < HM_SCAN_ITEMS; k += HM_SCAN_THREADS) {
+        const uint64_t i = b0 + k;
+        if (i < n) s += v[i];
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (hm_lane() == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t t = 0;
+        for (int w = 0; w < HM_SCAN_THREADS / 64; w++) t += red[w];
+        partial[blockIdx.x] = t;
+    }
+}
+
+/* single block: exclusive scan of up to 4096 partials; total -> *total */
+__global__ __launch_bounds__(1024) void k_scan_partials(uint64_t* partial, uint32_t nb, uint64_t* total)
+{
+    __shared__ uint64_t ws[17];
+    const int tid = threadIdx.x;
+    uint64_t v[4];
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t i = tid * 4 + q;
+        v[q] = i < nb ? partial[i] : 0;
+        s += v[q];
+    }
+    const uint64_t inc = hm_wave_incl_scan64(s);
+    const int w = tid >> 6;
+    if (hm_lane() == 63) ws[w] = inc;
+    __syncthreads();
+    if (tid == 0) {
+        uint64_t acc = 0;
+        for (int k = 0; k < 16; k++) {
+            const uint64_t t = ws[k];
+            ws[k] = acc;
+            acc += t;
+        }
+        ws[16] = acc;
+    }
+    __syncthreads();
+    uint64_t off = ws[w] + inc - s;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        const uint32_t i = tid * 4 + q;
+        if (i < nb) partial[i] = off;
+        off += v[q];
+    }
+    if (tid == 0) *total = ws[16];
+}
+
+__global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v, uint64_t n, const uint64_t* partial,
+                                                               uint64_t* out)
+{
+    __shared__ uint64_t ws[HM_SCAN_THREADS / 64 + 1];
+    constexpr int PER = HM_SCAN_ITEMS / HM_SCAN_THREADS;
+    const uint64_t b0 = (uint64_t)blockIdx.x * HM_SCAN_ITEMS + (uint64_t)threadIdx.x * PER;
+    uint64_t x[PER];
+    uint64_t s = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        x[q] = (b0 + q < n) ? v[b0 + q] : 0;
+        s += x[q];
+    }
+    const uint64_t inc = hm_wave_incl_scan64(s);
+    const int w = threadIdx.x >> 6;
+    if (hm_lane() == 63) ws[w] = inc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint64_t acc = 0;
+        for (int k = 0; k < HM_SCAN_THREADS / 64; k++) {
+            const uint64_t t = ws[k];
+            ws[k] = acc;
+            acc += t;
+        }
+    }
+    __syncthreads();
+    uint64_t off = partial[blockIdx.x] + ws[w] + inc - s;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        if (b0 + q < n) out[b0 + q] = off;
+        off += x[q];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t F = 1ull << a.dbits;
+    const uint32_t count = (uint32_t)(*a.total >> 32);
+    const uint32_t items = (uint32_t)(*a.total & 0xFFFFFFFFull);
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < a.nchildren; c += stride) {
+        const uint64_t pre = a.prefix[c];
+        const uint32_t idx = (uint32_t)(pre >> 32);
+        const uint32_t ib = (uint32_t)(pre & 0xFFFFFFFFull);
+        const uint64_t p = c >> a.dbits;
+        const uint64_t d = c & (F - 1);
+        if (d == 0) a.child_begin[p] = idx;
+        if (a.vals[c] >> 32) {
+            const uint32_t t0 = a.parent_item_begin[p];
+            const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+            a.out.nkeys[idx] = a.nkeys[c];
+            a.out.nruns[idx] = a.nruns[c];
+            a.out.rbase[idx] = (uint32_t)((uint64_t)t0 * F + d * tp);
+            a.out.item_begin[idx] = ib;
+            a.out.digit[idx] = (uint32_t)d;
+            a.out.morton[idx] = (a.parent_morton[p] << a.dbits) | d;
+            if (a.slots) {
+                const uint32_t nit = (uint32_t)(a.vals[c] & 0xFFFFFFFFull);
+                int32_t sl = -1;
+                if (nit > 1) {
+                    sl = (int32_t)atomicAdd(a.nslots, 1u);
+                    a.slot_bucket[sl] = idx;
+                }
+                a.slots[idx] = sl;
+            }
+        }
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        a.out.item_begin[count] = items;
+        a.child_begin[a.nparents] = count;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* emission helpers                                                          */
+/* ------------------------------------------------------------------------ */
+
+/* Emit the non-zero cells v[0..n) of zoom z whose Morton index is
+ * (prefix << (2*lg)) | i.  All threads of the block must call. */
+template <typename T, int THREADS>
+__device__ void hm_emit_level(const T* v, uint32_t n, int z, uint64_t prefix, int lg, const HmOut& o,
+                              uint32_t* scr, unsigned long long* sbase)
+{
+    const uint32_t per = (n + THREADS - 1) / THREADS;
+    const uint32_t i0 = threadIdx.x * per;
+    const uint32_t i1 = min(i0 + per, n);
+    uint32_t c = 0;
+    for (uint32_t i = i0; i < i1; i++) c += v[i] != 0;
+    uint32_t tot;
+    uint32_t off = hm_block_excl_scan<THREADS>(c, scr, &tot);
+    if (tot == 0) return;
+    if (threadIdx.x == 0) *sbase = atomicAdd(o.cursor, (unsigned long long)tot);
+    __syncthreads();
+    const uint64_t base = *sbase;
+    __syncthreads();
+    for (uint32_t i = i0; i < i1; i++) {
+        const T x = v[i];
+        if (x != 0) {
+            const uint64_t pos = base + off;
+            if (pos < o.capacity) {
+                o.keys[pos] = hm_out_key(z, (prefix << (2 * lg)) | i);
+                o.counts[pos] = (uint64_t)x;
+            }
+            off++;
+        }
+    }
+}
+
+/* In-LDS 4:1 pyramid over v[0..4^lg): emits zooms z_top .. z_top-lg+1 (those in
+ * [zmin, zmax]) and leaves the total in v[0]. */
+template <typename T, int THREADS>
+__device__ void hm_pyramid(T* v, int lg, int z_top, uint64_t prefix, const HmOut& o, uint32_t* scr,
+                           unsigned long long* sbase)
+{
+    uint32_t n = 1u << (2 * lg);
+    for (int k = 0; k < lg; k++) {
+        const int z = z_top - k;
+        if (z >= o.zmin && z <= o.zmax) hm_emit_level<T, THREADS>(v, n, z, prefix, lg - k, o, scr, sbase);
+        __syncthreads();
+        n >>= 2;
+        constexpr int MAXPER = (HM_AG_CELLS / 4 + THREADS - 1) / THREADS;
+        T acc[MAXPER];
+#pragma unroll
+        for (int m = 0; m < MAXPER; m++) {
+            const uint32_t i = threadIdx.x + m * THREADS;
+            acc[m] = i < n ? (T)(v[4 * i] + v[4 * i + 1] + v[4 * i + 2] + v[4 * i + 3]) : (T)0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MAXPER; m++) {
+            const uint32_t i = threadIdx.x + m * THREADS;
+            if (i < n) v[i] = acc[m];
+        }
+        __syncthreads();
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* final level: dense 128x128 LDS histogram per zoom-zb bucket               */
+/* ------------------------------------------------------------------------ */
+
+__global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate(HmAggArgs a)
+{
+    __shared__ uint32_t grid[HM_AG_CELLS];
+    __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
+    __shared__ unsigned long long sbase;
+    const int tid = threadIdx.x;
+    const uint32_t ncell = 1u << (2 * a.lg);
+    for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
+    __syncthreads();
+    const HmItem it = hm_locate(a.B, blockIdx.x, HM_TA, a.runpre);
+    hm_stream_item<uint16_t, HM_AG_THREADS>(it, a.keys, a.runs, a.runpre,
+                                            [&](uint32_t key, bool v) { hm_lds_count(grid, key, v); });
+    __syncthreads();
+    if (it.nitems == 1) {
+        hm_pyramid<uint32_t, HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[it.bucket], a.out, scr, &sbase);
+        if (tid == 0) a.totals[it.bucket] = grid[0];
+    } else {
+        uint32_t* g = a.gslots + (uint64_t)a.B.slots[it.bucket] * HM_AG_CELLS;
+        uint32_t s = 0;
+        for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) {
+            const uint32_t x = grid[i];
+            if (x) atomicAdd(&g[i], x);
+            s += x;
+        }
+        s = hm_wave_sum(s);
+        if (hm_lane() == 0 && s) atomicAdd(&a.totals[it.bucket], (unsigned long long)s);
+    }
+}
+
+__global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
+{
+    __shared__ uint32_t grid[HM_AG_CELLS];
+    __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
+    __shared__ unsigned long long sbase;
+    const uint32_t ncell = 1u << (2 * a.lg);
+    const uint32_t b = a.slot_bucket[blockIdx.x];
+    const uint32_t* g = a.gslots + (uint64_t)blockIdx.x * HM_AG_CELLS;
+    for (uint32_t i = threadIdx.x; i < ncell; i += HM_AG_THREADS) grid[i] = g[i];
+    __syncthreads();
+    hm_pyramid<uint32_t, HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[b], a.out, scr, &sbase);
+}
+
+/* ------------------------------------------------------------------------ */
+/* pooling of bucket totals: zooms z_l .. z_{l-1}+1 (root: down to 0)        */
+/* ------------------------------------------------------------------------ */
+
+__global__ __launch_bounds__(HM_POOL_THREADS) void k_pool(HmPoolArgs a)
+{
+    __shared__ unsigned long long v[HM_MAX_F1];
+    __shared__ uint32_t scr[HM_POOL_THREADS / 64 + 1];
+    __shared__ unsigned long long sbase;
+    const uint32_t p = blockIdx.x;
+    const uint32_t F = 1u << a.dbits;
+    for (uint32_t i = threadIdx.x; i < F; i += HM_POOL_THREADS) v[i] = 0;
+    __syncthreads();
+    const uint32_t c0 = a.child_begin[p], c1 = a.child_begin[p + 1];
+    for (uint32_t c = c0 + threadIdx.x; c < c1; c += HM_POOL_THREADS) v[a.child_digit[c]] = a.child_totals[c];
+    __syncthreads();
+    const uint64_t pm = a.parent_morton ? a.parent_morton[p] : 0ull;
+    hm_pyramid<unsigned long long, HM_POOL_THREADS>(v, a.dbits / 2, a.z_child, pm, a.out, scr, &sbase);
+    if (threadIdx.x == 0) {
+        if (a.parent_totals) a.parent_totals[p] = v[0];
+        if (a.emit_root && v[0] && a.out.zmin == 0) {
+            const uint64_t pos = atomicAdd(a.out.cursor, 1ull);
+            if (pos < a.out.capacity) {
+                a.out.keys[pos] = hm_out_key(0, 0);
+                a.out.counts[pos] = v[0];
+            }
+        }
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* host launchers                                                            */
+/* ------------------------------------------------------------------------ */
+
+void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
+                       int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow)
+{
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 256 * 16) blocks = 256 * 16;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_project, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, n, zoom, row, col, status,
+                       err_word, slow);
+}
+
+void hm_launch_part1(hipStream_t s, const HmPart1Args& a, bool out16, bool from_tiles)
+{
+    if (a.tiles == 0) return;
+    dim3 g(a.tiles), b(HM_P1_THREADS);
+    if (from_tiles) {
+        if (out16)
+            hipLaunchKernelGGL((k_project_partition<uint16_t, true>), g, b, 0, s, a);
+        else
+            hipLaunchKernelGGL((k_project_partition<uint32_t, true>), g, b, 0, s, a);
+    } else {
+        if (out16)
+            hipLaunchKernelGGL((k_project_partition<uint16_t, false>), g, b, 0, s, a);
+        else
+            hipLaunchKernelGGL((k_project_partition<uint32_t, false>), g, b, 0, s, a);
+    }
+}
+
+void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool out16)
+{
+    if (tiles == 0) return;
+    if (out16)
+        hipLaunchKernelGGL(k_partition<uint16_t>, dim3(tiles), dim3(HM_PN_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_partition<uint32_t>, dim3(tiles), dim3(HM_PN_THREADS), 0, s, a);
+}
+
+void hm_launch_runscan(hipStream_t s, const HmScanArgs& a)
+{
+    uint64_t waves = a.nchildren;
+    uint64_t blocks = (waves + 3) / 4;
+    if (blocks > 16384) blocks = 16384;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_runscan, dim3((unsigned)blocks), dim3(256), 0, s, a);
+}
+
+void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total)
+{
+    const uint32_t nb = (uint32_t)((n + HM_SCAN_ITEMS - 1) / HM_SCAN_ITEMS);
+    const uint32_t g = nb ? nb : 1;
+    hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, partial);
+    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, partial, g, total);
+    hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, partial, out);
+}
+
+void hm_launch_compact(hipStream_t s, const HmCompactArgs& a)
+{
+    uint64_t blocks = (a.nchildren + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_compact, dim3((unsigned)blocks), dim3(256), 0, s, a);
+}
+
+void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots)
+{
+    if (items) hipLaunchKernelGGL(k_aggregate, dim3(items), dim3(HM_AG_THREADS), 0, s, a);
+    if (nslots) hipLaunchKernelGGL(k_aggregate_merged, dim3(nslots), dim3(HM_AG_THREADS), 0, s, a);
+}
+
+void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
+{
+    if (nparents) hipLaunchKernelGGL(k_pool, dim3(nparents), dim3(HM_POOL_THREADS), 0, s, a);
+}

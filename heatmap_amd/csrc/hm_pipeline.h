@@ -1,0 +1,141 @@
+/* Shared host/device declarations of the count pipeline (see hm_kernels.hip). */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+/* level 1: projection + partition by the zoom-z1 digit */
+#define HM_P1_THREADS 512
+#define HM_P1_PPT 16
+#define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 8192 points per tile */
+#define HM_MAX_F1 4096                      /* z1 <= 6 */
+/* levels >= 2 */
+#define HM_PN_THREADS 512
+#define HM_TN 8192
+#define HM_MAX_FN 1024                      /* <= 5 zooms per level */
+/* final aggregation: zoom-zb bucket = 128 x 128 zoom-Z bins */
+#define HM_AG_THREADS 512
+#define HM_AG_CELLS 16384
+#define HM_AG_LG 7
+#define HM_TA (1u << 20)                    /* keys per aggregation work item */
+#define HM_POOL_THREADS 256
+#define HM_MAX_LEVELS 4
+#define HM_COUNT_MAX_ZOOM 22
+#define HM_SCAN_LIMIT (4096ull * 4096ull)   /* dense children per level */
+
+struct HmBuckets {
+    uint32_t count;        /* compact buckets */
+    const uint32_t* nkeys;
+    const uint32_t* nruns;
+    const uint32_t* rbase;      /* first run record */
+    const uint32_t* item_begin; /* [count+1] work-item prefix for the next stage */
+    const uint32_t* digit;
+    const uint64_t* morton;     /* Morton index of the bucket at its zoom */
+    const int32_t* slots;       /* last level: merge slot or -1 */
+};
+
+struct HmOut {
+    uint64_t* keys;
+    uint64_t* counts;
+    uint64_t capacity;
+    unsigned long long* cursor;
+    int zmin, zmax;
+};
+
+struct HmPart1Args {
+    const double* lat;
+    const double* lon;
+    const int64_t* rows_in;   /* hm_count_tiles */
+    const int64_t* cols_in;
+    const uint8_t* keep;
+    int64_t n;
+    int Z, dbits, restbits;
+    uint32_t tiles;
+    void* keys_out;
+    uint32_t* nruns;
+    uint2* runs;
+    unsigned long long* err_word;
+    unsigned long long* exotic_word;
+    unsigned long long* slow_count;
+};
+
+struct HmPartNArgs {
+    HmBuckets parent;
+    const uint32_t* keys_in;
+    const uint2* runs_in;
+    const uint32_t* runpre_in;
+    int dbits, restbits;
+    void* keys_out;
+    uint32_t* nruns_out;
+    uint2* runs_out;
+};
+
+struct HmScanArgs {
+    uint64_t nchildren;
+    int dbits;
+    const uint32_t* nruns;
+    const uint2* runs;
+    uint32_t* runpre;
+    const uint32_t* parent_item_begin;
+    uint32_t item_keys;
+    uint32_t* nkeys;
+    uint64_t* vals;
+};
+
+struct HmCompactOut {
+    uint32_t* nkeys;
+    uint32_t* nruns;
+    uint32_t* rbase;
+    uint32_t* item_begin;
+    uint32_t* digit;
+    uint64_t* morton;
+};
+
+struct HmCompactArgs {
+    uint64_t nchildren;
+    uint32_t nparents;
+    int dbits;
+    const uint64_t* vals;
+    const uint64_t* prefix;
+    const uint64_t* total;
+    const uint32_t* nkeys;
+    const uint32_t* nruns;
+    const uint32_t* parent_item_begin;
+    const uint64_t* parent_morton;
+    HmCompactOut out;
+    uint32_t* child_begin;
+    int32_t* slots;         /* last level only */
+    uint32_t* nslots;
+    uint32_t* slot_bucket;
+};
+
+struct HmAggArgs {
+    HmBuckets B;
+    const uint16_t* keys;
+    const uint2* runs;
+    const uint32_t* runpre;
+    int Z, lg;
+    unsigned long long* totals;
+    uint32_t* gslots;
+    const uint32_t* slot_bucket;
+    HmOut out;
+};
+
+struct HmPoolArgs {
+    int dbits, z_child, emit_root;
+    const uint32_t* child_begin;
+    const uint32_t* child_digit;
+    const unsigned long long* child_totals;
+    const uint64_t* parent_morton;
+    unsigned long long* parent_totals;
+    HmOut out;
+};
+
+void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
+                       int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow);
+void hm_launch_part1(hipStream_t s, const HmPart1Args& a, bool out16, bool from_tiles);
+void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool out16);
+void hm_launch_runscan(hipStream_t s, const HmScanArgs& a);
+void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total);
+void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
+void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots);
+void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);

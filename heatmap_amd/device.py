@@ -1,0 +1,209 @@
+"""Device-side entry points (columnar): projection and the count pyramid.
+
+Inputs may be numpy arrays (copied to HBM first) or torch CUDA tensors
+(used in place, zero copy).  PyTorch is only the memory/stream plumbing; all
+arithmetic runs in the gfx950 kernels behind include/heatmap_amd.h.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+
+_CTX = {}
+_CTX_LOCK = threading.Lock()
+
+
+def _torch():
+    import torch
+
+    if not torch.cuda.is_available():
+        raise _lib.DeviceUnavailable("heatmap_amd needs a gfx950 GPU (torch.cuda.is_available() is False); "
+                                     "there is no CPU fallback")
+    return torch
+
+
+class Context:
+    """One hm_ctx per (device, host thread)."""
+
+    def __init__(self, device: int = 0):
+        torch = _torch()
+        self.L = _lib.load()
+        self.device = device
+        p = ctypes.c_void_p()
+        with torch.cuda.device(device):
+            st = self.L.hm_ctx_create(ctypes.byref(p), device, ctypes.c_void_p(torch.cuda.current_stream().cuda_stream))
+        if st != _lib.HM_OK:
+            _lib.raise_for(st)
+        self.ptr = p
+
+    def bind_stream(self):
+        torch = _torch()
+        self.L.hm_ctx_set_stream(self.ptr, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+
+    def last_error(self):
+        idx = ctypes.c_int64(-1)
+        kind = ctypes.c_int(0)
+        self.L.hm_last_error(self.ptr, ctypes.byref(idx), ctypes.byref(kind))
+        return idx.value, kind.value
+
+    def last_stats(self):
+        slow = ctypes.c_int64(0)
+        us = (ctypes.c_double * 8)()
+        self.L.hm_last_stats(self.ptr, ctypes.byref(slow), us, 8)
+        return slow.value, list(us)
+
+    def __del__(self):  # pragma: no cover
+        try:
+            if getattr(self, "ptr", None):
+                self.L.hm_ctx_destroy(self.ptr)
+        except Exception:
+            pass
+
+
+def context(device: int = 0) -> Context:
+    key = (device, threading.get_ident())
+    with _CTX_LOCK:
+        c = _CTX.get(key)
+        if c is None:
+            c = _CTX[key] = Context(device)
+    c.bind_stream()
+    return c
+
+
+def _dev(x, dtype, device):
+    torch = _torch()
+    if isinstance(x, torch.Tensor):
+        t = x
+        if t.dtype != dtype:
+            t = t.to(dtype)
+        if t.device.type != "cuda":
+            t = t.to("cuda:%d" % device)
+        return t.contiguous()
+    a = np.ascontiguousarray(x)
+    return torch.from_numpy(a).to(device="cuda:%d" % device, dtype=dtype)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else ctypes.c_void_p(0)
+
+
+@dataclass
+class Projection:
+    row: np.ndarray
+    col: np.ndarray
+    status: np.ndarray
+    first_error_index: int
+    first_error_kind: int
+    slow_points: int
+
+
+def project(lat, lon, zoom: int, device: int = 0, raise_errors: bool = False) -> Projection:
+    """Tile rows/cols of every point at `zoom` (reference tile.py:15-21)."""
+    torch = _torch()
+    ctx = context(device)
+    la = _dev(lat, torch.float64, device)
+    lo = _dev(lon, torch.float64, device)
+    n = la.numel()
+    if lo.numel() != n:
+        raise ValueError("lat and lon must have the same length")
+    row = torch.empty(n, dtype=torch.int64, device=la.device)
+    col = torch.empty(n, dtype=torch.int64, device=la.device)
+    st = torch.empty(n, dtype=torch.uint8, device=la.device)
+    rc = ctx.L.hm_project(ctx.ptr, _ptr(la), _ptr(lo), n, int(zoom), _ptr(row), _ptr(col), _ptr(st))
+    idx, kind = ctx.last_error()
+    slow, _ = ctx.last_stats()
+    if rc not in (_lib.HM_OK, _lib.HM_E_NAN, _lib.HM_E_DOMAIN, _lib.HM_E_INF, _lib.HM_E_RANGE):
+        _lib.raise_for(rc)
+    if raise_errors and rc != _lib.HM_OK:
+        _lib.raise_for(kind, idx)
+    return Projection(row.cpu().numpy(), col.cpu().numpy(), st.cpu().numpy(), idx, kind, slow)
+
+
+@dataclass
+class Counts:
+    zoom: np.ndarray
+    row: np.ndarray
+    col: np.ndarray
+    count: np.ndarray
+    slow_points: int
+    stage_us: list
+
+    def sorted(self) -> "Counts":
+        o = np.lexsort((self.col, self.row, self.zoom))
+        return Counts(self.zoom[o], self.row[o], self.col[o], self.count[o], self.slow_points, self.stage_us)
+
+    def as_dict(self):
+        """{zoom: {(row, col): count}}"""
+        out = {}
+        for z, r, c, n in zip(self.zoom.tolist(), self.row.tolist(), self.col.tolist(), self.count.tolist()):
+            out.setdefault(z, {})[(r, c)] = n
+        return out
+
+
+def decode_keys(keys: np.ndarray):
+    keys = keys.astype(np.uint64)
+    z = (keys >> np.uint64(58)).astype(np.int32)
+    r = ((keys >> np.uint64(29)) & np.uint64(0x1FFFFFFF)).astype(np.int64)
+    c = (keys & np.uint64(0x1FFFFFFF)).astype(np.int64)
+    return z, r, c
+
+
+class CountBuffers:
+    """Reusable device output buffers for count() (bench / streaming)."""
+
+    def __init__(self, capacity: int, device: int = 0):
+        torch = _torch()
+        self.capacity = int(capacity)
+        self.keys = torch.empty(max(self.capacity, 1), dtype=torch.int64, device="cuda:%d" % device)
+        self.counts = torch.empty(max(self.capacity, 1), dtype=torch.int64, device="cuda:%d" % device)
+
+
+def count_device(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, buffers=None,
+                 tiles: bool = False):
+    """Run the count pyramid; returns (n_cells, buffers) with results left in HBM."""
+    torch = _torch()
+    ctx = context(device)
+    if tiles:
+        a = _dev(lat, torch.int64, device)
+        b = _dev(lon, torch.int64, device)
+    else:
+        a = _dev(lat, torch.float64, device)
+        b = _dev(lon, torch.float64, device)
+    n = a.numel()
+    if b.numel() != n:
+        raise ValueError("coordinate arrays must have the same length")
+    kp = None
+    if keep is not None:
+        kp = _dev(keep, torch.uint8, device)
+        if kp.numel() != n:
+            raise ValueError("keep must have one entry per point")
+    if buffers is None:
+        buffers = CountBuffers(max(1024, 4 * n + 64), device)
+    fn = ctx.L.hm_count_tiles if tiles else ctx.L.hm_count
+    while True:
+        nout = ctypes.c_int64(0)
+        rc = fn(ctx.ptr, _ptr(a), _ptr(b), _ptr(kp), n, int(zmin), int(zmax), _ptr(buffers.keys),
+                _ptr(buffers.counts), buffers.capacity, ctypes.byref(nout))
+        if rc == _lib.HM_E_CAPACITY:
+            buffers = CountBuffers(int(nout.value * 1.25) + 64, device)
+            continue
+        if rc != _lib.HM_OK:
+            idx, kind = ctx.last_error()
+            _lib.raise_for(rc, idx)
+        return nout.value, buffers
+
+
+def count(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, tiles: bool = False) -> Counts:
+    """Per-(zoom, row, col) counts for zooms zmin..zmax (host arrays)."""
+    m, buf = count_device(lat, lon, keep, zmin, zmax, device, tiles=tiles)
+    ctx = context(device)
+    slow, us = ctx.last_stats()
+    keys = buf.keys[:m].cpu().numpy().view(np.uint64)
+    cnt = buf.counts[:m].cpu().numpy()
+    z, r, c = decode_keys(keys)
+    return Counts(z, r, c, cnt, slow, us)

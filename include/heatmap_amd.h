@@ -1,0 +1,120 @@
+/* heatmap_amd — C-ABI of the MI355X heatmap aggregation hot path.
+ *
+ * Drop-in boundary for timfpark/heatmap's hot path.
+ * The reference has no FFI: its boundary is the set of Python callables Spark
+ * invokes per record.  Each entry point below replaces one of them; the
+ * ctypes binding a maintainer would add on the reference side is shown in
+ * INTEGRATION.md, and heatmap_amd/tile.py + heatmap_amd/heatmap.py are that
+ * binding, re-exposing the reference's own names.
+ *
+ *   hm_project      <- Tile.row_from_latitude + Tile.column_from_longitude
+ *                      (reference tile.py:15-21), vectorised; the per-point
+ *                      status reproduces tile_id_from_lat_long's exceptions
+ *                      (tile.py:9-13: row is evaluated before column).
+ *   hm_count        <- dataframe_loader projection at zoom MAX_ZOOM_LEVEL +
+ *                      DETAIL_ZOOM_DELTA (heatmap.py:25-29) fused with the
+ *                      per-zoom reduceByKey count pyramid of build_heatmaps
+ *                      (heatmap.py:107-118, shuffle 1 at :111) for one user
+ *                      group; the row layout (heatmap.py:79-90,120-129) is
+ *                      assembled from these counts by heatmap_amd/heatmap.py.
+ *   hm_count_tiles  <- the same pyramid starting from already projected tile
+ *                      ids (build_heatmaps on locations whose "tileId" is a
+ *                      zoom-zmax id, heatmap.py:60-61).
+ *   hm_last_error   <- the exception a Spark task would raise: first failing
+ *                      point in input order and its kind.
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (hipMalloc'd or torch CUDA
+ *     tensors) owned by the caller; nothing is allocated across the boundary
+ *     except the opaque context.
+ *   - Work is enqueued on the context's HIP stream (hm_ctx_set_stream).  Calls
+ *     that return results through host scalars (n_out, status) synchronise
+ *     that stream before returning.
+ *   - Return value: HM_OK or an HM_E_* status.  Per-point errors set the
+ *     status of the first failing point (input order) and hm_last_error()
+ *     reports its index.
+ *   - Thread-compatible: one context per host thread / stream.
+ *   - Every call fails loudly (HM_E_HIP) when no gfx950 device is present;
+ *     there is no CPU fallback in this library.
+ */
+#ifndef HEATMAP_AMD_H
+#define HEATMAP_AMD_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HM_ABI_VERSION 1
+
+/* status / per-point error kinds */
+#define HM_OK 0
+#define HM_E_NAN 1       /* ValueError("cannot convert float NaN to integer")   tile.py:17,21 */
+#define HM_E_DOMAIN 2    /* ValueError("math domain error")  tan(+-inf) / log(<=0), tile.py:17 */
+#define HM_E_INF 3       /* OverflowError("cannot convert float infinity to integer") tile.py:21 */
+#define HM_E_RANGE 8     /* representable by the reference but not by this path:
+                            |col| >= 2^63, or |lat*pi/180| beyond glibc's
+                            non-Payne-Hanek range (|lat| >~ 6.0e9 degrees) */
+#define HM_E_EXOTIC 9    /* hm_count*: a valid point whose zoom-zmax tile lies
+                            outside [0, 2^zmax)^2 (|lat| > 85.0511..., or
+                            lon outside [-180, 180)); not binned on device yet */
+#define HM_E_ARG 16      /* bad argument (zoom range, null pointer, n < 0) */
+#define HM_E_CAPACITY 17 /* output arrays too small; *n_out holds the size needed */
+#define HM_E_HIP 18      /* HIP runtime error (no device, launch failure) */
+#define HM_E_NOMEM 19    /* device allocation failed */
+
+/* Output cell key of hm_count: zoom in bits 58..63, row in 29..57, col in 0..28.
+ * Sorting keys sorts by (zoom, row, col). */
+#define HM_KEY(z, r, c) (((uint64_t)(z) << 58) | ((uint64_t)(r) << 29) | (uint64_t)(c))
+#define HM_KEY_ZOOM(k) ((int)((k) >> 58))
+#define HM_KEY_ROW(k) ((int64_t)(((k) >> 29) & 0x1FFFFFFFull))
+#define HM_KEY_COL(k) ((int64_t)((k) & 0x1FFFFFFFull))
+#define HM_MAX_ZOOM 28   /* largest zmax accepted by hm_count* */
+
+typedef struct hm_ctx hm_ctx;
+
+int hm_abi_version(void);
+const char* hm_status_string(int status);
+
+/* device: HIP device ordinal; stream: hipStream_t (NULL = default stream). */
+int hm_ctx_create(hm_ctx** out, int device, void* stream);
+int hm_ctx_set_stream(hm_ctx* ctx, void* stream);
+int hm_ctx_destroy(hm_ctx* ctx);
+
+/* Project n points at one zoom (0..30).  row/col: int64[n]; status: uint8[n]
+ * (HM_OK or the point's error kind; row/col are 0 for failed points).
+ * Returns HM_OK if every point projected, else the first failing point's kind.
+ * Replaces Tile.row_from_latitude / column_from_longitude (tile.py:15-21). */
+int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int64_t n, int zoom,
+               int64_t* row, int64_t* col, uint8_t* status);
+
+/* Count points per (zoom, row, col) for every zoom in [zmin, zmax].
+ * keep: uint8[n] or NULL (NULL = keep all); every point is projected (and
+ * can fail) whether kept or not, as dataframe_loader does (heatmap.py:27-29).
+ * keys_out/counts_out: capacity entries each (device); *n_out (host) receives
+ * the number of non-empty cells written.  Cell order is unspecified.
+ * Replaces dataframe_loader + build_heatmaps' reduceByKey (heatmap.py:25-111). */
+int hm_count(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
+             int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
+             int64_t* n_out);
+
+/* Same pyramid from zoom-zmax tile coordinates (int64 row/col). */
+int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep,
+                   int64_t n, int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out,
+                   int64_t capacity, int64_t* n_out);
+
+/* First failing point of the last call: index in input order (-1 if none)
+ * and its HM_E_* kind. */
+int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
+
+/* Diagnostics of the last hm_project/hm_count call: points resolved by the
+ * bit-exact glibc-restating slow path (guard band / out-of-window), and the
+ * per-stage device time in microseconds of the last hm_count (0 if unmeasured). */
+int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_stages);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif
