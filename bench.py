@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: points binned/s over zooms 0-18 on Gaussian-hotspot point clouds.
+
+BASELINE.json metric: "points binned/sec (whole node, zooms 0-18) + % HBM
+roofline".  One step = one hm_count() over the resident cloud: projection of
+every point at zoom 18 (bit-exact with reference tile.py:15-21), the count
+pyramid for zooms 0..18 (heatmap.py:107-111 semantics), every non-empty cell
+written to HBM as (key, count).
+
+    python bench.py                                   # 1 GPU, 1e9 points (config 2)
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+        # N GPUs, 1.25e9 points per GPU (config 3 at N=8: 1e10), weak scaling:
+        # each rank bins its shard, then the sparse cells are hash-partitioned
+        # by heatmap row over RCCL all-to-all and merged
+
+Rank 0 prints one JSON line.  `roofline` is for the dominant kernel
+(k_project_partition), timed with HIP events on the library's stream inside
+the timed region; `traffic` is the per-launch HBM byte count from the
+committed rocprofv3 PMC summary for the same workload (profiles/), or null.
+`cpu_baseline` times the C oracle (oracle/hm_oracle.c, OpenMP) on a bounded
+sample of the same generator on this host's cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ALG_BYTES_PER_POINT = 16   # lat + lon fp64 read once
+ALG_BYTES_PER_CELL = 16    # u64 key + u64 count per non-empty output cell
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--points", type=float, default=0, help="points per GPU (default 1e9, or 1.25e9 when N>1)")
+    ap.add_argument("--kind", default="hotspots", choices=["hotspots", "uniform", "skew"])
+    ap.add_argument("--zmin", type=int, default=0)
+    ap.add_argument("--zmax", type=int, default=18)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cpu-sample", type=float, default=3e7, help="points timed on the CPU oracle (0 = skip)")
+    ap.add_argument("--no-check", action="store_true")
+    return ap.parse_args()
+
+
+def dist_init(args):
+    ws = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws > 1:
+        import torch.distributed as dist
+
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl")
+    return ws, rank, local
+
+
+def barrier(ws):
+    if ws > 1:
+        import torch.distributed as dist
+
+        dist.barrier()
+
+
+def profile_traffic(workload_tag):
+    """Per-launch HBM bytes of k_project_partition from the committed PMC summary."""
+    path = os.path.join(REPO, "profiles", "pmc_summary.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        e = d.get(workload_tag)
+        if not e:
+            return None, None
+        return e.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+    except Exception:
+        return None, None
+
+
+def cpu_baseline(args):
+    if args.cpu_sample <= 0:
+        return None
+    from heatmap_amd import synth
+    from oracle import oracle
+
+    n = int(args.cpu_sample)
+    lat, lon = synth.generate(args.kind, n, seed=args.seed)
+    t0 = time.perf_counter()
+    r = oracle.count(lat, lon, None, args.zmin, args.zmax)
+    dt = time.perf_counter() - t0
+    assert r["status"] == 0
+    return {"value": n / dt, "unit": "points/s", "cores": int(r["threads"]), "kind": "port",
+            "sample": "%d %s points (seed %d, first points of the same stream), zooms %d-%d; C oracle "
+                      "(glibc projection OpenMP x%d, serial radix sort + RLE cascade), %.1f s"
+                      % (n, args.kind, args.seed, args.zmin, args.zmax, int(r["threads"]), dt)}
+
+
+def main():
+    args = parse()
+    ws, rank, local = dist_init(args)
+    import torch
+
+    from heatmap_amd import device, synth
+    from heatmap_amd import multigpu
+
+    torch.cuda.set_device(local)
+    per = int(args.points) if args.points else (1_000_000_000 if ws == 1 else 1_250_000_000)
+    lat = torch.empty(per, dtype=torch.float64, device="cuda")
+    lon = torch.empty(per, dtype=torch.float64, device="cuda")
+    device.synth(args.kind, lat, lon, seed=args.seed, start=rank * per)
+    torch.cuda.synchronize()
+    bufs = device.CountBuffers(64 << 20)
+    ctx = device.context(local)
+
+    def step():
+        m, b = device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=bufs)
+        if ws > 1:
+            m = multigpu.merge_cells(b, m, ws, rank)
+        return m, b
+
+    for _ in range(args.warmup):
+        m, bufs = step()
+    torch.cuda.synchronize()
+    barrier(ws)
+    k1, stages = [], []
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        m, bufs = step()
+        _, us = ctx.last_stats()
+        k1.append(us[0])
+        stages.append(us[:4])
+    torch.cuda.synchronize()
+    barrier(ws)
+    dt = time.perf_counter() - t0
+    if ws > 1:
+        import torch.distributed as dist
+
+        t = torch.tensor([dt, float(m)], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
+        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
+        dt, cells = float(t[0]), int(t[1])
+    else:
+        cells = int(m)
+    check = None
+    if not args.no_check and ws == 1:
+        # every zoom's counts sum to the number of points
+        tot = int(bufs.counts[:m].sum().item())
+        check = "ok" if tot == per * (args.zmax - args.zmin + 1) else "FAIL sum %d" % tot
+    ms = dt / args.steps * 1e3
+    total_points = per * ws
+    k1_us = float(np.mean(k1))
+    achieved = ALG_BYTES_PER_POINT * per / (k1_us * 1e-6) / 1e9
+    tag = "%s_%d_z%d-%d" % (args.kind, per, args.zmin, args.zmax)
+    traffic, traffic_src = profile_traffic(tag)
+    out = {
+        "metric": "points binned/sec (whole node, zooms 0-18) + % HBM roofline at 1/2/4/8 GPU",
+        "value": total_points / (dt / args.steps),
+        "unit": "points/s",
+        "n_gpus": ws,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (heatmap_amd.synth %s, generated on device, resident in HBM)" % args.kind,
+        "config": {"workload": "%.3g %s points per GPU, zooms %d-%d, %d x MI355X" % (per, args.kind, args.zmin,
+                                                                                    args.zmax, ws),
+                   "points_per_gpu": per, "zmin": args.zmin, "zmax": args.zmax,
+                   "parallelism": "points sharded, dp%d" % ws},
+        "roofline": {"bound": "hbm", "kernel": "k_project_partition", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "traffic_source": traffic_src, "avg_launch_us": k1_us,
+                     "alg_bytes_per_launch": ALG_BYTES_PER_POINT * per},
+        "pipeline": {"cells": cells, "alg_bytes": ALG_BYTES_PER_POINT * total_points + ALG_BYTES_PER_CELL * cells,
+                     "alg_GBps": (ALG_BYTES_PER_POINT * total_points + ALG_BYTES_PER_CELL * cells) / (dt / args.steps) / 1e9,
+                     "frac_of_8TBps": (ALG_BYTES_PER_POINT * total_points + ALG_BYTES_PER_CELL * cells)
+                     / (dt / args.steps) / 1e9 / HBM_PEAK_GBS,
+                     "stage_us_mean": [float(x) for x in np.mean(np.array(stages), axis=0)],
+                     "stages": ["project+partition", "partition levels+scans", "aggregate", "pool"],
+                     "slow_path_points": ctx.last_stats()[0], "check": check},
+    }
+    if rank == 0:
+        out["cpu_baseline"] = cpu_baseline(args)
+        print(json.dumps(out), flush=True)
+    barrier(ws)
+
+
+if __name__ == "__main__":
+    main()

@@ -26,7 +26,7 @@ HM_E_NOMEM = 19
 HM_COUNT_MAX_ZOOM = 22
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
-           "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats"]
+           "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats", "hm_synth"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -71,6 +71,7 @@ def load() -> ctypes.CDLL:
         L.hm_count_tiles.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
+        L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]
         for name in EXPORTS:
             getattr(L, name).restype = getattr(L, name).restype or c.c_int
         L.hm_status_string.restype = c.c_char_p

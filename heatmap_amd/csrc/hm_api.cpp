@@ -278,7 +278,6 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     hipEvent_t* ev = ctx->ev;
     int nev = 0;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
-    HIPCHK(hipEventRecord(ev[nev++], s));
 
     /* root bucket list B_0: one bucket (the zoom-0 tile) */
     const uint32_t tiles1 = (uint32_t)((n + HM_T1 - 1) / HM_T1);
@@ -351,6 +350,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.err_word = ctx->state + ST_ERR;
             a.exotic_word = ctx->state + ST_EXOTIC;
             a.slow_count = ctx->state + ST_SLOW;
+            HIPCHK(hipEventRecord(ev[nev++], s));
             hm_launch_part1(s, a, V.out16, rows != nullptr);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[nev++], s));
@@ -529,4 +529,15 @@ extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* co
 {
     if (n > 0 && (!row || !col)) return HM_E_ARG;
     return count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out);
+}
+
+extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
+                        const double* table, int k)
+{
+    if (!ctx || n < 0 || kind < 0 || kind > 2 || (n > 0 && (!lat || !lon)) || (kind == 1 && (!table || k <= 0)))
+        return HM_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (n > 0) hm_launch_synth(ctx->stream, kind, seed, start, n, lat, lon, table, k);
+    HIPCHK(hipGetLastError());
+    return HM_OK;
 }

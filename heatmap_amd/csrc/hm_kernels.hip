@@ -680,3 +680,71 @@ void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {
     if (nparents) hipLaunchKernelGGL(k_pool, dim3(nparents), dim3(HM_POOL_THREADS), 0, s, a);
 }
+
+/* ------------------------------------------------------------------------ */
+/* synthetic point clouds (bit-identical to heatmap_amd/synth.py)            */
+/* ------------------------------------------------------------------------ */
+
+__device__ __forceinline__ uint64_t hm_splitmix(uint64_t x)
+{
+    uint64_t z = x + 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__device__ __forceinline__ double hm_u01(uint64_t seed, uint64_t idx, uint32_t lane, uint32_t lanes)
+{
+    const uint64_t ctr = seed * 0x100000001B3ull + idx * lanes + lane;
+    return (double)(hm_splitmix(ctr) >> 11) * 0x1p-53;
+}
+
+__global__ __launch_bounds__(256) void k_synth(int kind, uint64_t seed, int64_t start, int64_t n, double* lat,
+                                               double* lon, const double* tab, int k)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t idx = (uint64_t)(start + i);
+        double la, lo;
+        if (kind == 0) {
+            const double u1 = hm_u01(seed, idx, 0, 2), u2 = hm_u01(seed, idx, 1, 2);
+            la = (u1 * 2.0 - 1.0) * 85.0511287798066;
+            lo = u2 * 360.0 - 180.0;
+        } else if (kind == 1) {
+            const double u0 = hm_u01(seed, idx, 0, 9);
+            int c = 0;
+            while (c < k - 1 && !(tab[3 * k + c] > u0)) c++;
+            double sy = hm_u01(seed, idx, 1, 9) + hm_u01(seed, idx, 2, 9);
+            sy = sy + hm_u01(seed, idx, 3, 9);
+            sy = sy + hm_u01(seed, idx, 4, 9);
+            double sx = hm_u01(seed, idx, 5, 9) + hm_u01(seed, idx, 6, 9);
+            sx = sx + hm_u01(seed, idx, 7, 9);
+            sx = sx + hm_u01(seed, idx, 8, 9);
+            const double gy = (sy - 2.0) * 1.7320508075688772;
+            const double gx = (sx - 2.0) * 1.7320508075688772;
+            la = tab[c] + tab[2 * k + c] * gy;
+            lo = tab[k + c] + tab[2 * k + c] * gx;
+        } else {
+            const double u0 = hm_u01(seed, idx, 0, 3), u1 = hm_u01(seed, idx, 1, 3), u2 = hm_u01(seed, idx, 2, 3);
+            const double w = 360.0 / 262144.0;
+            if (u0 < 0.9) {
+                la = 47.60014 + (u1 - 0.5) * 0.0008;
+                lo = (42015.0 + 0.0625 + u2 * 0.875) * w - 180.0;
+            } else {
+                la = (u1 * 2.0 - 1.0) * 85.0511287798066;
+                lo = u2 * 360.0 - 180.0;
+            }
+        }
+        lat[i] = la;
+        lon[i] = lo;
+    }
+}
+
+void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
+                     const double* tab, int k)
+{
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 256 * 32) blocks = 256 * 32;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(256), 0, s, kind, seed, start, n, lat, lon, tab, k);
+}

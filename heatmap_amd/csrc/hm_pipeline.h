@@ -139,3 +139,5 @@ void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* part
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots);
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);
+void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
+                     const double* tab, int k);

@@ -207,3 +207,27 @@ def count(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, t
     cnt = buf.counts[:m].cpu().numpy()
     z, r, c = decode_keys(keys)
     return Counts(z, r, c, cnt, slow, us)
+
+
+_SYNTH_KIND = {"uniform": 0, "hotspots": 1, "skew": 2}
+
+
+def synth(kind: str, lat, lon, seed: int = 0, start: int = 0, device: int = 0):
+    """Fill torch CUDA tensors lat/lon with points start.. of heatmap_amd.synth's
+    `kind` cloud (bit-identical to the numpy generator)."""
+    torch = _torch()
+    from . import synth as _synth
+
+    ctx = context(device)
+    n = lat.numel()
+    tab = None
+    k = 0
+    if kind == "hotspots":
+        clat, clon, sig, cdf = _synth.hotspot_centres(seed)
+        k = len(cdf)
+        tab = torch.from_numpy(np.concatenate([clat, clon, sig, cdf]).astype(np.float64)).to(lat.device)
+    rc = ctx.L.hm_synth(ctx.ptr, _SYNTH_KIND[kind], int(seed) & ((1 << 64) - 1), int(start), n, _ptr(lat), _ptr(lon),
+                        _ptr(tab), k)
+    if rc != _lib.HM_OK:
+        _lib.raise_for(rc)
+    torch.cuda.current_stream(device).synchronize()

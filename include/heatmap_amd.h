@@ -70,7 +70,7 @@ extern "C" {
 #define HM_KEY_ZOOM(k) ((int)((k) >> 58))
 #define HM_KEY_ROW(k) ((int64_t)(((k) >> 29) & 0x1FFFFFFFull))
 #define HM_KEY_COL(k) ((int64_t)((k) & 0x1FFFFFFFull))
-#define HM_MAX_ZOOM 28   /* largest zmax accepted by hm_count* */
+#define HM_MAX_ZOOM 22   /* largest zmax accepted by hm_count* (level-1 keys fit u32) */
 
 typedef struct hm_ctx hm_ctx;
 
@@ -110,8 +110,21 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
 
 /* Diagnostics of the last hm_project/hm_count call: points resolved by the
  * bit-exact glibc-restating slow path (guard band / out-of-window), and the
- * per-stage device time in microseconds of the last hm_count (0 if unmeasured). */
+ * per-stage device time in microseconds of the last hm_count:
+ *   [0] k_project_partition (projection + level-1 partition, the dominant kernel)
+ *   [1] remaining partition levels, run scans and compactions (incl. host reads)
+ *   [2] k_aggregate (+ merged buckets)   [3] k_pool levels */
 int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_stages);
+
+/* Benchmark/test utility, not part of the reference boundary: fill lat/lon
+ * (device) with points start..start+n-1 of a synthetic cloud, bit-identical
+ * to heatmap_amd/synth.py.  kind: 0 uniform, 1 hotspots (table = device
+ * double[4k]: centre lat, centre lon, sigma, Zipf cdf), 2 skew.  Asynchronous. */
+#define HM_SYNTH_UNIFORM 0
+#define HM_SYNTH_HOTSPOTS 1
+#define HM_SYNTH_SKEW 2
+int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
+             const double* table, int k);
 
 #ifdef __cplusplus
 }

@@ -43,3 +43,16 @@ def test_count_vs_oracle(gpu, kind, n, zmin, zmax):
     assert np.array_equal(got.row, ref["row"])
     assert np.array_equal(got.col, ref["col"])
     assert np.array_equal(got.count, ref["count"])
+
+
+@pytest.mark.parametrize("kind", ["uniform", "hotspots", "skew"])
+def test_synth_bit_exact(gpu, kind):
+    import torch
+
+    n = 300001
+    lat = torch.empty(n, dtype=torch.float64, device="cuda")
+    lon = torch.empty(n, dtype=torch.float64, device="cuda")
+    device.synth(kind, lat, lon, seed=5, start=12345)
+    hl, ho = synth.generate(kind, n, seed=5, start=12345)
+    assert np.array_equal(lat.cpu().numpy().view(np.uint64), hl.view(np.uint64))
+    assert np.array_equal(lon.cpu().numpy().view(np.uint64), ho.view(np.uint64))
