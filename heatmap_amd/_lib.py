@@ -23,7 +23,7 @@ HM_E_ARG = 16
 HM_E_CAPACITY = 17
 HM_E_HIP = 18
 HM_E_NOMEM = 19
-HM_COUNT_MAX_ZOOM = 22
+HM_COUNT_MAX_ZOOM = 21
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
            "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats", "hm_synth"]

@@ -77,7 +77,7 @@ static int hip_fail(hipError_t e, const char* what)
 /* named arena slots */
 enum {
     B_KEYS_A, B_KEYS_B, B_RUNS_A, B_RUNS_B, B_RUNPRE_A, B_RUNPRE_B, B_NRUNS, B_NKEYS, B_VALS, B_PREFIX,
-    B_PARTIAL, B_TOTAL, B_ROOT,
+    B_PARTIAL, B_TOTAL, B_ROOT, B_NRUNS_TOT,
     B_BK0, /* 4 levels x 8 arrays */
     B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
     B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
@@ -262,10 +262,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     int zs[HM_MAX_LEVELS];
     int L = 0;
     {
-        int z = zb < 6 ? zb : 6;
+        int z = zb < HM_Z1 ? zb : HM_Z1;
         zs[L++] = z;
         while (z < zb) {
-            z = std::min(z + 5, zb);
+            z = std::min(z + HM_LEVEL_ZOOMS, zb);
             if (L >= HM_MAX_LEVELS) return HM_E_ARG;
             zs[L++] = z;
         }
@@ -319,6 +319,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         const uint64_t ntiles = (l == 0) ? tiles1 : lv[l - 1].items;
         const uint64_t tile_keys = (l == 0) ? HM_T1 : HM_TN;
         if (V.nchildren > (uint64_t)HM_SCAN_LIMIT) return HM_E_NOMEM;
+        /* run-counter shards: 32 unless the dense child space is large (then
+         * per-child contention is low anyway); keeps counters <= 2^25 */
+        int sb = 5;
+        while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
+        const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
+        if (run_cap >= (1ull << 32)) return HM_E_NOMEM;
 
         /* outputs of the level's partition kernel */
         void* keys_out;
@@ -326,10 +332,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         uint32_t* runpre_out;
         uint32_t* nruns;
         ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, ntiles * tile_keys * (V.out16 ? 2 : 4), keys_out);
-        ENSURE(slot_k ? B_RUNS_B : B_RUNS_A, (ntiles << V.dbits) * sizeof(uint2), runs_out);
-        ENSURE(slot_k ? B_RUNPRE_B : B_RUNPRE_A, (ntiles << V.dbits) * sizeof(uint32_t), runpre_out);
-        ENSURE(B_NRUNS, V.nchildren * sizeof(uint32_t), nruns);
-        HIPCHK(hipMemsetAsync(nruns, 0, V.nchildren * sizeof(uint32_t), s));
+        ENSURE(slot_k ? B_RUNS_B : B_RUNS_A, run_cap * sizeof(uint2), runs_out);
+        ENSURE(slot_k ? B_RUNPRE_B : B_RUNPRE_A, run_cap * sizeof(uint32_t), runpre_out);
+        ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
+        HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
+        uint32_t* nruns_tot;
+        ENSURE(B_NRUNS_TOT, V.nchildren * sizeof(uint32_t), nruns_tot);
 
         if (l == 0) {
             HmPart1Args a;
@@ -344,6 +352,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.dbits = V.dbits;
             a.restbits = restbits;
             a.tiles = tiles1;
+            a.shard_bits = sb;
             a.keys_out = keys_out;
             a.nruns = nruns;
             a.runs = runs_out;
@@ -365,6 +374,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.runpre_in = runpre_cur;
             a.dbits = V.dbits;
             a.restbits = restbits;
+            a.shard_bits = sb;
             a.keys_out = keys_out;
             a.nruns_out = nruns;
             a.runs_out = runs_out;
@@ -383,7 +393,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         HmScanArgs sa;
         sa.nchildren = V.nchildren;
         sa.dbits = V.dbits;
+        sa.shard_bits = sb;
         sa.nruns = nruns;
+        sa.nruns_tot = nruns_tot;
         sa.runs = runs_out;
         sa.runpre = runpre_out;
         sa.parent_item_begin = parent_item_begin;
@@ -409,11 +421,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ca.nchildren = V.nchildren;
         ca.nparents = nparents;
         ca.dbits = V.dbits;
+        ca.shard_bits = sb;
         ca.vals = vals;
         ca.prefix = prefix;
         ca.total = total;
         ca.nkeys = nkeys;
-        ca.nruns = nruns;
+        ca.nruns = nruns_tot;
         ca.parent_item_begin = parent_item_begin;
         ca.parent_morton = parent_morton;
         ca.child_begin = child_begin;

@@ -28,6 +28,23 @@ __device__ __forceinline__ uint32_t hm_compact64(uint64_t v)
     return (uint32_t)v;
 }
 
+/* 16-bit -> even bits of 32 */
+__device__ __forceinline__ uint32_t hm_spread16(uint32_t v)
+{
+    v &= 0xFFFFu;
+    v = (v | (v << 8)) & 0x00FF00FFu;
+    v = (v | (v << 4)) & 0x0F0F0F0Fu;
+    v = (v | (v << 2)) & 0x33333333u;
+    v = (v | (v << 1)) & 0x55555555u;
+    return v;
+}
+
+/* Morton of two values < 2^16 (row bit above col bit) */
+__device__ __forceinline__ uint32_t hm_morton16(uint32_t row, uint32_t col)
+{
+    return (hm_spread16(row) << 1) | hm_spread16(col);
+}
+
 __device__ __forceinline__ uint64_t hm_morton(uint32_t row, uint32_t col)
 {
     return (hm_spread32(row) << 1) | hm_spread32(col);
@@ -101,38 +118,48 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
     return r;
 }
 
-/* LDS histogram increment with wave aggregation of the leading lane's key:
- * lanes holding the same key as the first active lane add once (skew guard,
- * SURVEY.md section 7 hard part 3). */
+/* LDS histogram increment with wave aggregation: up to HM_AGG_ROUNDS times,
+ * the lanes holding the first remaining lane's key add once; the rest add
+ * individually.  One round catches the skewed case (most of a wave on one
+ * key, SURVEY.md section 7 hard part 3); more rounds cost more scalar issue
+ * than the duplicate-address serialisation they save (measured: 4 rounds made
+ * k_project_partition SALU-bound). */
+#define HM_AGG_ROUNDS 1
 __device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t key, bool valid)
 {
-    const uint64_t vm = __ballot(valid);
-    if (vm == 0) return;
-    const int leader = __ffsll((unsigned long long)vm) - 1;
-    const uint32_t kl = __shfl(key, leader, 64);
-    const uint64_t same = __ballot(valid && key == kl);
-    if (hm_lane() == leader) atomicAdd(&hist[kl], (uint32_t)__popcll(same));
-    if (valid && key != kl) atomicAdd(&hist[key], 1u);
+    uint64_t act = __ballot(valid);
+    const int lane = hm_lane();
+#pragma unroll
+    for (int it = 0; it < HM_AGG_ROUNDS; it++) {
+        if (act == 0) return;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
+        const uint64_t same = __ballot(valid && key == kl) & act;
+        if (lane == leader) atomicAdd(&hist[kl], (uint32_t)__popcll(same));
+        act &= ~same;
+    }
+    if ((act >> lane) & 1ull) atomicAdd(&hist[key], 1u);
 }
 
 /* LDS slot reservation with the same aggregation: returns the position of
  * this lane's element in bucket `key` (cursor array `cur`). */
 __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t key, bool valid)
 {
-    const uint64_t vm = __ballot(valid);
-    if (vm == 0) return 0;
-    const int leader = __ffsll((unsigned long long)vm) - 1;
-    const uint32_t kl = __shfl(key, leader, 64);
-    const uint64_t same = __ballot(valid && key == kl);
-    uint32_t base = 0;
-    if (hm_lane() == leader) base = atomicAdd(&cur[kl], (uint32_t)__popcll(same));
-    base = __shfl(base, leader, 64);
+    uint64_t act = __ballot(valid);
+    const int lane = hm_lane();
     uint32_t pos = 0;
-    if (valid) {
-        if (key == kl)
-            pos = base + hm_mbcnt(same);
-        else
-            pos = atomicAdd(&cur[key], 1u);
+#pragma unroll
+    for (int it = 0; it < HM_AGG_ROUNDS; it++) {
+        if (act == 0) return pos;
+        const int leader = __ffsll((unsigned long long)act) - 1;
+        const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
+        const uint64_t same = __ballot(valid && key == kl) & act;
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(&cur[kl], (uint32_t)__popcll(same));
+        base = __builtin_amdgcn_readlane(base, leader);
+        if ((same >> lane) & 1ull) pos = base + hm_mbcnt(same);
+        act &= ~same;
     }
+    if ((act >> lane) & 1ull) pos = atomicAdd(&cur[key], 1u);
     return pos;
 }

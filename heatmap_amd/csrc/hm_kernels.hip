@@ -34,6 +34,13 @@
 #include "hm_project.h"
 #include "hm_pipeline.h"
 
+__constant__ double c_logtab[2 * HM_LOGTAB_N] = HM_LOGTAB_INIT;
+
+__device__ __forceinline__ void hm_load_logtab(double* tab)
+{
+    for (int i = threadIdx.x; i < 2 * HM_LOGTAB_N; i += blockDim.x) tab[i] = c_logtab[i];
+}
+
 /* ------------------------------------------------------------------------ */
 /* projection API kernel (hm_project)                                        */
 /* ------------------------------------------------------------------------ */
@@ -43,11 +50,14 @@ __global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat,
                                                  int64_t* __restrict__ col, uint8_t* __restrict__ status,
                                                  unsigned long long* err_word, unsigned long long* slow_count)
 {
+    __shared__ double tab[2 * HM_LOGTAB_N];
+    hm_load_logtab(tab);
+    __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         int64_t r = 0, c = 0;
         int slow = 0;
-        const int st = hm_project_point(lat[i], lon[i], zoom, &r, &c, &slow);
+        const int st = hm_project_point(lat[i], lon[i], zoom, &r, &c, &slow, tab);
         row[i] = st == HM_OK ? r : 0;
         col[i] = st == HM_OK ? c : 0;
         status[i] = (uint8_t)st;
@@ -67,9 +77,11 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     __shared__ uint32_t cur[HM_MAX_F1];
     __shared__ OutT stage[HM_T1];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
+    __shared__ double tab[2 * HM_LOGTAB_N];
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
+    if (!FROM_TILES) hm_load_logtab(tab);
     __syncthreads();
 
     const int64_t base = (int64_t)blockIdx.x * HM_T1;
@@ -78,6 +90,41 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     uint32_t dig[HM_P1_PPT];
     uint32_t rest[HM_P1_PPT];
     int nslow = 0;
+    /* issue every load of the tile before any arithmetic: 16 points x 16 B per
+     * lane in flight (double2 = two consecutive points of one array) */
+    double2 la[HM_P1_PPT / 2], lo[HM_P1_PPT / 2];
+    uint16_t kp[HM_P1_PPT / 2];
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT / 2; k++) {
+        const int64_t i0 = base + 2 * ((int64_t)k * HM_P1_THREADS + tid);
+        kp[k] = 0x0101;
+        if (i0 + 1 < a.n) {
+            if (FROM_TILES) {
+                la[k].x = __longlong_as_double(a.rows_in[i0]);
+                la[k].y = __longlong_as_double(a.rows_in[i0 + 1]);
+                lo[k].x = __longlong_as_double(a.cols_in[i0]);
+                lo[k].y = __longlong_as_double(a.cols_in[i0 + 1]);
+            } else {
+                la[k] = *(const double2*)(a.lat + i0);
+                lo[k] = *(const double2*)(a.lon + i0);
+            }
+            if (a.keep) kp[k] = (uint16_t)a.keep[i0] | ((uint16_t)a.keep[i0 + 1] << 8);
+        } else if (i0 < a.n) {
+            if (FROM_TILES) {
+                la[k].x = __longlong_as_double(a.rows_in[i0]);
+                lo[k].x = __longlong_as_double(a.cols_in[i0]);
+            } else {
+                la[k].x = a.lat[i0];
+                lo[k].x = a.lon[i0];
+            }
+            la[k].y = 0.0;
+            lo[k].y = 0.0;
+            if (a.keep) kp[k] = (uint16_t)a.keep[i0];
+        } else {
+            la[k] = make_double2(0.0, 0.0);
+            lo[k] = make_double2(0.0, 0.0);
+        }
+    }
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT / 2; k++) {
         const int64_t i0 = base + 2 * ((int64_t)k * HM_P1_THREADS + tid);
@@ -87,28 +134,31 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             dig[2 * k + h] = 0xFFFFFFFFu;
             rest[2 * k + h] = 0;
             if (i >= a.n) continue;
+            const double pa = h ? la[k].y : la[k].x;
+            const double po = h ? lo[k].y : lo[k].x;
             int64_t r = 0, c = 0;
             int st, slow = 0;
             if (FROM_TILES) {
-                r = a.rows_in[i];
-                c = a.cols_in[i];
+                r = __double_as_longlong(pa);
+                c = __double_as_longlong(po);
                 st = HM_OK;
             } else {
-                st = hm_project_point(a.lat[i], a.lon[i], a.Z, &r, &c, &slow);
+                st = hm_project_point(pa, po, a.Z, &r, &c, &slow, tab);
             }
             nslow += slow;
             if (HM_UNLIKELY(st != HM_OK)) {
                 atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
                 continue;
             }
-            if (a.keep && !a.keep[i]) continue;
+            if (!((kp[k] >> (8 * h)) & 0xFF)) continue;
             if (HM_UNLIKELY((uint64_t)r >= lim || (uint64_t)c >= lim)) {
                 atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
                 continue;
             }
-            const uint64_t m = hm_morton((uint32_t)r, (uint32_t)c);
-            dig[2 * k + h] = (uint32_t)(m >> a.restbits);
-            rest[2 * k + h] = (uint32_t)m & restmask;
+            const int sh = a.restbits >> 1;
+            const uint32_t lowm = (1u << sh) - 1u;
+            dig[2 * k + h] = hm_morton16((uint32_t)r >> sh, (uint32_t)c >> sh);
+            rest[2 * k + h] = hm_morton16((uint32_t)r & lowm, (uint32_t)c & lowm) & restmask;
         }
     }
     if (!FROM_TILES) {
@@ -137,8 +187,11 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (d < F) {
             cur[d] = off;
             if (cnt[q]) {
-                const uint32_t idx = atomicAdd(&a.nruns[d], 1u);
-                a.runs[(uint64_t)d * a.tiles + idx] = make_uint2((uint32_t)base + off, cnt[q]);
+                const uint32_t sh = blockIdx.x & ((1u << a.shard_bits) - 1u);
+                const uint32_t idx = atomicAdd(&a.nruns[((uint64_t)d << a.shard_bits) + sh], 1u);
+                const uint64_t cap = ((uint64_t)a.tiles + (1u << a.shard_bits) - 1) >> a.shard_bits;
+                a.runs[hm_run_base(0, a.tiles, 0, d, a.dbits, a.shard_bits) + sh * cap + idx] =
+                    make_uint2((uint32_t)base + off, cnt[q]);
             }
         }
         off += cnt[q];
@@ -196,27 +249,98 @@ __device__ __forceinline__ HmItem hm_locate(const HmBuckets& B, uint32_t g, uint
     return it;
 }
 
-/* Calls f(key, valid) for every key of [a, b); one wave per run. Wave-uniform. */
-template <typename InT, int THREADS, typename F>
-__device__ __forceinline__ void hm_stream_item(const HmItem& it, const InT* keys, const uint2* runs,
-                                               const uint32_t* runpre, F f)
+/* Calls f(key, valid) for every key of the item's logical range [a, b).
+ * Run descriptors are staged in LDS HM_RCHUNK at a time.  Each wave owns a
+ * contiguous span of logical positions and walks it 64 at a time (lane l takes
+ * position q + l, so loads coalesce within a run); each lane keeps a monotone
+ * run cursor that advances linearly (runs hold >= 1 key) and falls back to a
+ * binary search after HM_WALK steps.  HM_SU positions per lane are resolved
+ * before any load is consumed.  Block-uniform; every thread calls. */
+#define HM_RCHUNK 1024
+#define HM_SU 4
+#define HM_WALK 4
+struct HmStreamLds {
+    uint32_t end[HM_RCHUNK];
+    uint32_t src[HM_RCHUNK];
+};
+
+__device__ __forceinline__ uint32_t hm_run_of(const HmStreamLds& L, uint32_t ri, uint32_t rc, uint32_t p)
 {
-    const int w = threadIdx.x >> 6;
-    const int lane = hm_lane();
-    for (uint32_t r = it.r0 + w; r < it.nr; r += THREADS / 64) {
-        const uint2 run = runs[it.rb + r];
-        const uint32_t re = runpre[it.rb + r];
-        const uint32_t rs = re - run.y;
-        if (rs >= it.b) break;
-        const uint32_t s = max(rs, it.a);
-        const uint32_t e = min(re, it.b);
-        const InT* src = keys + run.x + (s - rs);
-        for (uint32_t i0 = 0; i0 < e - s; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const bool v = i < e - s;
-            const uint32_t key = v ? (uint32_t)src[i] : 0u;
-            f(key, v);
+#pragma unroll
+    for (int k = 0; k < HM_WALK; k++) {
+        if (L.end[ri] > p) return ri;
+        ri++;
+    }
+    uint32_t lo = ri, hi = rc - 1;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.end[mid] <= p)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+template <typename InT, int THREADS, typename F>
+__device__ __forceinline__ void hm_stream_item(const HmItem& it, const InT* __restrict__ keys,
+                                               const uint2* __restrict__ runs, const uint32_t* __restrict__ runpre,
+                                               HmStreamLds& L, F f)
+{
+    constexpr int NW = THREADS / 64;
+    const int tid = threadIdx.x;
+    const int w = tid >> 6;
+    const int lane = tid & 63;
+    uint32_t r = it.r0;
+    uint32_t pos = it.a;
+    while (pos < it.b) {
+        const uint32_t rc = min((uint32_t)HM_RCHUNK, it.nr - r);
+        if (rc == 0) break;
+        for (uint32_t i = tid; i < rc; i += THREADS) {
+            const uint2 run = runs[it.rb + r + i];
+            const uint32_t re = runpre[it.rb + r + i];
+            L.end[i] = re;
+            L.src[i] = run.x + run.y - re;     /* key address = src + logical position */
         }
+        __syncthreads();
+        const uint32_t cend = min(L.end[rc - 1], it.b);
+        /* wave spans: multiples of 64*HM_SU positions */
+        const uint32_t n = cend - pos;
+        const uint32_t step = 64 * HM_SU;
+        const uint32_t span = ((n + NW - 1) / NW + step - 1) / step * step;
+        const uint32_t ws = pos + min(n, span * w);
+        const uint32_t we = pos + min(n, span * (w + 1));
+        uint32_t ri = 0;
+        if (ws < we) {
+            uint32_t lo = 0, hi = rc - 1;
+            while (lo < hi) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L.end[mid] <= ws)
+                    lo = mid + 1;
+                else
+                    hi = mid;
+            }
+            ri = lo;
+        }
+        for (uint32_t q = ws; q < we; q += step) {
+            uint32_t key[HM_SU];
+            bool v[HM_SU];
+#pragma unroll
+            for (int u = 0; u < HM_SU; u++) {
+                const uint32_t p = q + u * 64 + lane;
+                v[u] = p < we;
+                key[u] = 0;
+                if (v[u]) {
+                    ri = hm_run_of(L, ri, rc, p);
+                    key[u] = (uint32_t)keys[L.src[ri] + p];
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < HM_SU; u++) f(key[u], v[u]);
+        }
+        __syncthreads();
+        pos = cend;
+        r += rc;
     }
 }
 
@@ -232,6 +356,7 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     __shared__ uint32_t cur[HM_MAX_FN];
     __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
     __shared__ uint32_t scnt;
+    __shared__ HmStreamLds sl;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
@@ -239,7 +364,7 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     __syncthreads();
     const HmItem it = hm_locate(a.parent, blockIdx.x, HM_TN, a.runpre_in);
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
-    hm_stream_item<uint32_t, HM_PN_THREADS>(it, a.keys_in, a.runs_in, a.runpre_in, [&](uint32_t key, bool v) {
+    hm_stream_item<uint32_t, HM_PN_THREADS>(it, a.keys_in, a.runs_in, a.runpre_in, sl, [&](uint32_t key, bool v) {
         const uint32_t d = key >> a.restbits;
         hm_lds_count(cur, d, v);
         const uint64_t vm = __ballot(v);
@@ -270,9 +395,11 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
             cur[d] = off;
             if (cnt[q]) {
                 const uint64_t child = (uint64_t)it.bucket * F + d;
-                const uint32_t idx = atomicAdd(&a.nruns_out[child], 1u);
-                const uint64_t rb = (uint64_t)tile0 * F + (uint64_t)d * it.nitems;
-                a.runs_out[rb + idx] = make_uint2((uint32_t)(gtile * HM_TN) + off, cnt[q]);
+                const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
+                const uint32_t idx = atomicAdd(&a.nruns_out[(child << a.shard_bits) + sh], 1u);
+                const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
+                const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
+                a.runs_out[rb + sh * cap + idx] = make_uint2((uint32_t)(gtile * HM_TN) + off, cnt[q]);
             }
         }
         off += cnt[q];
@@ -297,16 +424,30 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
 
 /* one wave per dense child c = p*F + d: inclusive prefix of its run counts,
  * key total, and the packed scan value (1 << 32 | work items) */
+/* Per dense child c = p*F + d: compact the S run-counter shards into one list,
+ * write the inclusive prefix of its run counts, its key total and the packed
+ * scan value (1 << 32 | work items).  One block per child (BLOCK = true, few
+ * children with up to ~1e5 runs each, i.e. level 1) or one wave per child. */
+template <bool BLOCK>
 __global__ __launch_bounds__(256) void k_runscan(HmScanArgs a)
 {
+    constexpr int NW = 4;
+    __shared__ uint32_t wsum[NW + 1];
     const int lane = hm_lane();
-    const uint64_t nwaves = (uint64_t)gridDim.x * (blockDim.x >> 6);
-    for (uint64_t c = (uint64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6); c < a.nchildren; c += nwaves) {
-        const uint32_t nr = a.nruns[c];
+    const int w = threadIdx.x >> 6;
+    const uint32_t S = 1u << a.shard_bits;
+    const uint64_t first = BLOCK ? blockIdx.x : (uint64_t)blockIdx.x * NW + w;
+    const uint64_t stride = BLOCK ? gridDim.x : (uint64_t)gridDim.x * NW;
+    for (uint64_t c = first; c < a.nchildren; c += stride) {
+        /* shard counts -> exclusive offsets (S <= 64), every wave computes them */
+        const uint32_t ns = lane < (int)S ? a.nruns[(c << a.shard_bits) + lane] : 0u;
+        const uint32_t inc = hm_wave_incl_scan(ns);
+        const uint32_t nr = __shfl(inc, 63, 64);
         if (nr == 0) {
-            if (lane == 0) {
+            if (threadIdx.x == (BLOCK ? 0 : (unsigned)w * 64)) {
                 a.nkeys[c] = 0;
                 a.vals[c] = 0;
+                a.nruns_tot[c] = 0;
             }
             continue;
         }
@@ -314,17 +455,77 @@ __global__ __launch_bounds__(256) void k_runscan(HmScanArgs a)
         const uint64_t d = c & ((1ull << a.dbits) - 1);
         const uint32_t t0 = a.parent_item_begin[p];
         const uint32_t tp = a.parent_item_begin[p + 1] - t0;
-        const uint64_t rb = (uint64_t)t0 * (1ull << a.dbits) + d * tp;
-        uint32_t carry = 0;
-        for (uint32_t i0 = 0; i0 < nr; i0 += 64) {
-            const uint32_t i = i0 + lane;
-            const uint32_t v = i < nr ? a.runs[rb + i].y : 0u;
-            const uint32_t inc = hm_wave_incl_scan(v) + carry;
-            if (i < nr) a.runpre[rb + i] = inc;
-            carry = __shfl(inc, 63, 64);
+        const uint64_t rb = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits);
+        const uint32_t cap = (tp + S - 1) >> a.shard_bits;
+        const uint32_t nthr = BLOCK ? blockDim.x : 64;
+        const uint32_t t = BLOCK ? threadIdx.x : (uint32_t)lane;
+        /* compact shards 1..S-1 down behind shard 0 (in place, forward copy,
+         * shard by shard; a shard's destination never reaches a later shard) */
+        for (uint32_t sh = 1; sh < S; sh++) {
+            const uint32_t n_s = __shfl(ns, sh, 64);
+            const uint32_t o_s = __shfl(inc, sh, 64) - n_s;
+            if (n_s == 0 || o_s == sh * cap) continue;
+            for (uint32_t i0 = 0; i0 < n_s; i0 += nthr) {
+                const uint32_t i = i0 + t;
+                uint2 v = make_uint2(0, 0);
+                if (i < n_s) v = a.runs[rb + (uint64_t)sh * cap + i];
+                if (BLOCK)
+                    __syncthreads();
+                else
+                    __builtin_amdgcn_wave_barrier();
+                if (i < n_s) a.runs[rb + o_s + i] = v;
+            }
+            if (BLOCK) __syncthreads();
         }
-        if (lane == 0) {
+        if (BLOCK) {
+            __threadfence_block();
+            __syncthreads();
+        }
+        /* inclusive prefix of the run counts: 8 consecutive runs per thread */
+        uint32_t carry = 0;
+        for (uint32_t i0 = 0; i0 < nr; i0 += 8 * nthr) {
+            const uint32_t b = i0 + t * 8;
+            uint32_t v[8];
+            uint32_t loc = 0;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                v[q] = (b + q < nr) ? a.runs[rb + b + q].y : 0u;
+                loc += v[q];
+            }
+            uint32_t excl, tot;
+            if (BLOCK) {
+                const uint32_t winc = hm_wave_incl_scan(loc);
+                if (lane == 63) wsum[w] = winc;
+                __syncthreads();
+                if (threadIdx.x == 0) {
+                    uint32_t acc = 0;
+                    for (int k = 0; k < NW; k++) {
+                        const uint32_t x = wsum[k];
+                        wsum[k] = acc;
+                        acc += x;
+                    }
+                    wsum[NW] = acc;
+                }
+                __syncthreads();
+                excl = wsum[w] + winc - loc;
+                tot = wsum[NW];
+                __syncthreads();
+            } else {
+                const uint32_t winc = hm_wave_incl_scan(loc);
+                excl = winc - loc;
+                tot = __shfl(winc, 63, 64);
+            }
+            uint32_t acc = carry + excl;
+#pragma unroll
+            for (int q = 0; q < 8; q++) {
+                acc += v[q];
+                if (b + q < nr) a.runpre[rb + b + q] = acc;
+            }
+            carry += tot;
+        }
+        if (t == 0) {
             a.nkeys[c] = carry;
+            a.nruns_tot[c] = nr;
             const uint64_t items = (carry + a.item_keys - 1) / a.item_keys;
             a.vals[c] = (1ull << 32) | items;
         }
@@ -443,7 +644,7 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
             const uint32_t tp = a.parent_item_begin[p + 1] - t0;
             a.out.nkeys[idx] = a.nkeys[c];
             a.out.nruns[idx] = a.nruns[c];
-            a.out.rbase[idx] = (uint32_t)((uint64_t)t0 * F + d * tp);
+            a.out.rbase[idx] = (uint32_t)hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits);
             a.out.item_begin[idx] = ib;
             a.out.digit[idx] = (uint32_t)d;
             a.out.morton[idx] = (a.parent_morton[p] << a.dbits) | d;
@@ -528,6 +729,87 @@ __device__ void hm_pyramid(T* v, int lg, int z_top, uint64_t prefix, const HmOut
     }
 }
 
+/* Bucket pyramid with two output reservations per block: level z_top (4^lg
+ * cells in v) is emitted first; then levels z_top-1 .. z_top-lg+1 are built as
+ * consecutive regions of v (the first in place), counted together, reserved
+ * with one atomic and emitted.  v[0] ends up holding nothing useful; the
+ * bucket total is returned (block-uniform). */
+template <int THREADS>
+__device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t prefix, const HmOut& o,
+                                      uint32_t* scr, unsigned long long* sbase)
+{
+    const uint32_t n0 = 1u << (2 * lg);
+    if (lg == 0) return v[0];   /* the bucket is the zoom-z_top cell; k_pool emits it */
+    if (z_top >= o.zmin && z_top <= o.zmax) hm_emit_level<uint32_t, THREADS>(v, n0, z_top, prefix, lg, o, scr, sbase);
+    __syncthreads();
+    /* level z_top-1 in place into v[0 .. n0/4) */
+    uint32_t n = n0 >> 2;
+    {
+        constexpr int MAXPER = (HM_AG_CELLS / 4 + THREADS - 1) / THREADS;
+        uint32_t acc[MAXPER];
+#pragma unroll
+        for (int m = 0; m < MAXPER; m++) {
+            const uint32_t i = threadIdx.x + m * THREADS;
+            acc[m] = i < n ? v[4 * i] + v[4 * i + 1] + v[4 * i + 2] + v[4 * i + 3] : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int m = 0; m < MAXPER; m++) {
+            const uint32_t i = threadIdx.x + m * THREADS;
+            if (i < n) v[i] = acc[m];
+        }
+        __syncthreads();
+    }
+    /* remaining levels appended: level k (k = 1 .. lg-1) at off[k], 4^(lg-k) cells */
+    uint32_t off[HM_AG_LG + 1];
+    off[1] = 0;
+    uint32_t end = n;
+    for (int k = 2; k <= lg; k++) {
+        const uint32_t src = off[k - 1];
+        const uint32_t m = n >> 2;
+        off[k] = end;
+        for (uint32_t i = threadIdx.x; i < m; i += THREADS)
+            v[end + i] = v[src + 4 * i] + v[src + 4 * i + 1] + v[src + 4 * i + 2] + v[src + 4 * i + 3];
+        __syncthreads();
+        end += m;
+        n = m;
+    }
+    /* v[off[lg]] is the bucket total (zoom z_top - lg); count levels 1..lg-1 */
+    const uint64_t total = v[off[lg]];
+    const uint32_t per = (end + THREADS - 1) / THREADS;
+    const uint32_t i0 = threadIdx.x * per, i1 = min(i0 + per, off[lg]);
+    uint32_t c = 0;
+    for (uint32_t i = i0; i < i1; i++) {
+        int k = 1;
+        while (k < lg - 1 && i >= off[k + 1]) k++;
+        const int z = z_top - k;
+        c += (v[i] != 0 && z >= o.zmin && z <= o.zmax);
+    }
+    uint32_t tot;
+    uint32_t pos = hm_block_excl_scan<THREADS>(c, scr, &tot);
+    if (tot) {
+        if (threadIdx.x == 0) *sbase = atomicAdd(o.cursor, (unsigned long long)tot);
+        __syncthreads();
+        const uint64_t base = *sbase;
+        for (uint32_t i = i0; i < i1; i++) {
+            int k = 1;
+            while (k < lg - 1 && i >= off[k + 1]) k++;
+            const int z = z_top - k;
+            const uint32_t x = v[i];
+            if (x != 0 && z >= o.zmin && z <= o.zmax) {
+                const uint64_t q = base + pos;
+                if (q < o.capacity) {
+                    o.keys[q] = hm_out_key(z, (prefix << (2 * (lg - k))) | (i - off[k]));
+                    o.counts[q] = x;
+                }
+                pos++;
+            }
+        }
+    }
+    __syncthreads();
+    return total;
+}
+
 /* ------------------------------------------------------------------------ */
 /* final level: dense 128x128 LDS histogram per zoom-zb bucket               */
 /* ------------------------------------------------------------------------ */
@@ -537,17 +819,18 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate(HmAggArgs a)
     __shared__ uint32_t grid[HM_AG_CELLS];
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
+    __shared__ HmStreamLds sl;
     const int tid = threadIdx.x;
     const uint32_t ncell = 1u << (2 * a.lg);
     for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
     const HmItem it = hm_locate(a.B, blockIdx.x, HM_TA, a.runpre);
-    hm_stream_item<uint16_t, HM_AG_THREADS>(it, a.keys, a.runs, a.runpre,
+    hm_stream_item<uint16_t, HM_AG_THREADS>(it, a.keys, a.runs, a.runpre, sl,
                                             [&](uint32_t key, bool v) { hm_lds_count(grid, key, v); });
     __syncthreads();
     if (it.nitems == 1) {
-        hm_pyramid<uint32_t, HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[it.bucket], a.out, scr, &sbase);
-        if (tid == 0) a.totals[it.bucket] = grid[0];
+        const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[it.bucket], a.out, scr, &sbase);
+        if (tid == 0) a.totals[it.bucket] = t;
     } else {
         uint32_t* g = a.gslots + (uint64_t)a.B.slots[it.bucket] * HM_AG_CELLS;
         uint32_t s = 0;
@@ -571,7 +854,7 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
     const uint32_t* g = a.gslots + (uint64_t)blockIdx.x * HM_AG_CELLS;
     for (uint32_t i = threadIdx.x; i < ncell; i += HM_AG_THREADS) grid[i] = g[i];
     __syncthreads();
-    hm_pyramid<uint32_t, HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[b], a.out, scr, &sbase);
+    hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[b], a.out, scr, &sbase);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -580,7 +863,7 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
 
 __global__ __launch_bounds__(HM_POOL_THREADS) void k_pool(HmPoolArgs a)
 {
-    __shared__ unsigned long long v[HM_MAX_F1];
+    __shared__ unsigned long long v[HM_MAX_FN];
     __shared__ uint32_t scr[HM_POOL_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
     const uint32_t p = blockIdx.x;
@@ -646,11 +929,14 @@ void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool o
 
 void hm_launch_runscan(hipStream_t s, const HmScanArgs& a)
 {
-    uint64_t waves = a.nchildren;
-    uint64_t blocks = (waves + 3) / 4;
+    if (a.nchildren <= 8192) {
+        const uint64_t blocks = a.nchildren ? a.nchildren : 1;
+        hipLaunchKernelGGL(k_runscan<true>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+        return;
+    }
+    uint64_t blocks = (a.nchildren + 3) / 4;
     if (blocks > 16384) blocks = 16384;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_runscan, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_runscan<false>, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
 
 void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total)

@@ -5,22 +5,37 @@
 
 /* level 1: projection + partition by the zoom-z1 digit */
 #define HM_P1_THREADS 512
-#define HM_P1_PPT 16
-#define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 8192 points per tile */
-#define HM_MAX_F1 4096                      /* z1 <= 6 */
+#define HM_P1_PPT 8
+#define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 4096 points per tile */
+#define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
+#define HM_MAX_F1 1024
 /* levels >= 2 */
 #define HM_PN_THREADS 512
 #define HM_TN 8192
-#define HM_MAX_FN 1024                      /* <= 5 zooms per level */
+#define HM_LEVEL_ZOOMS 6                    /* <= 6 zooms per level */
+#define HM_MAX_FN 4096
+#define HM_MAX_SHARDS 32                    /* run-counter shards per child */
 /* final aggregation: zoom-zb bucket = 128 x 128 zoom-Z bins */
 #define HM_AG_THREADS 512
 #define HM_AG_CELLS 16384
 #define HM_AG_LG 7
-#define HM_TA (1u << 20)                    /* keys per aggregation work item */
+#define HM_TA (1u << 18)                    /* keys per aggregation work item */
 #define HM_POOL_THREADS 256
 #define HM_MAX_LEVELS 4
-#define HM_COUNT_MAX_ZOOM 22
+#define HM_COUNT_MAX_ZOOM 21                /* level-1 keys 2*(Z-5) bits fit u32 */
 #define HM_SCAN_LIMIT (4096ull * 4096ull)   /* dense children per level */
+
+/* Run region of child (p, d): parent p owns level tiles [t0, t0+tp); its
+ * children's regions start at F*(t0 + S*p), each S*ceil(tp/S) records, shard s
+ * of a child at offset s*ceil(tp/S).  Capacity: F*(tiles + S*parents). */
+__host__ __device__ inline uint64_t hm_run_base(uint64_t t0, uint64_t tp, uint64_t p, uint64_t d, int dbits,
+                                               int shard_bits)
+{
+    const uint64_t S = 1ull << shard_bits;
+    const uint64_t cap = (tp + S - 1) >> shard_bits;
+    return ((t0 + S * p) << dbits) + d * (cap << shard_bits);
+}
+
 
 struct HmBuckets {
     uint32_t count;        /* compact buckets */
@@ -50,8 +65,9 @@ struct HmPart1Args {
     int64_t n;
     int Z, dbits, restbits;
     uint32_t tiles;
+    int shard_bits;
     void* keys_out;
-    uint32_t* nruns;
+    uint32_t* nruns;            /* [F << shard_bits] */
     uint2* runs;
     unsigned long long* err_word;
     unsigned long long* exotic_word;
@@ -63,7 +79,7 @@ struct HmPartNArgs {
     const uint32_t* keys_in;
     const uint2* runs_in;
     const uint32_t* runpre_in;
-    int dbits, restbits;
+    int dbits, restbits, shard_bits;
     void* keys_out;
     uint32_t* nruns_out;
     uint2* runs_out;
@@ -71,9 +87,10 @@ struct HmPartNArgs {
 
 struct HmScanArgs {
     uint64_t nchildren;
-    int dbits;
-    const uint32_t* nruns;
-    const uint2* runs;
+    int dbits, shard_bits;
+    const uint32_t* nruns;      /* sharded counters */
+    uint32_t* nruns_tot;        /* out: runs per child after shard compaction */
+    uint2* runs;
     uint32_t* runpre;
     const uint32_t* parent_item_begin;
     uint32_t item_keys;
@@ -93,7 +110,7 @@ struct HmCompactOut {
 struct HmCompactArgs {
     uint64_t nchildren;
     uint32_t nparents;
-    int dbits;
+    int dbits, shard_bits;
     const uint64_t* vals;
     const uint64_t* prefix;
     const uint64_t* total;

@@ -25,13 +25,14 @@
 #pragma once
 #include "hm_common.h"
 #include "hm_glibc_emul.h"
+#include "hm_logtab.h"
 #include "../../include/heatmap_amd.h"
 
 #define HM_PI 0x1.921fb54442d18p+1          /* math.pi */
 #define HM_DEG2RAD 0x1.1df46a2529d39p-6     /* pi/180 rounded */
 #define HM_INV4PI 0x1.45f306dc9c883p-4      /* 1/(4 pi) rounded */
 #define HM_LN2 0x1.62e42fefa39efp-1
-#define HM_SQRT2 0x1.6a09e667f3bcdp+0
+#define HM_INV360 0x1.6c16c16c16c17p-9      /* RN(1/360) */
 #define HM_LAT_FAST 85.06
 #define HM_Y_EPS 1.5e-13
 
@@ -40,8 +41,31 @@ HM_FN double hm_exp2i(int z)
     return hm_u2d((uint64_t)(1023 + z) << 52);   /* 2^z, 0 <= z <= 1023 */
 }
 
-/* Y(lat) = 0.5 - atanh(sin(lat*pi/180)) / (2 pi), |lat| <= 85.06. */
-HM_FN double hm_fast_Y(double lat)
+/* ln(x), x positive normal: x = 2^e m, m in [1,2); interval i = top 7 mantissa
+ * bits; ln m = -ln(invc_i) + log1p(m*invc_i - 1), |m*invc_i - 1| < 2^-8, log1p
+ * by its Taylor series to r^8 (truncation < 2^-75).  Division-free, so the
+ * host build and gfx950 produce identical bits.  tab = HM_LOGTAB_INIT. */
+HM_FN double hm_fast_ln(double x, const double* tab)
+{
+    const uint64_t b = hm_d2u(x);
+    const int e = (int)(b >> 52) - 1023;
+    const uint32_t i = (uint32_t)(b >> 45) & 127u;
+    const double m = hm_u2d((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
+    const double r = fma(m, tab[2 * i], -1.0);
+    double q = -0x1p-3;
+    q = fma(q, r, 0x1.2492492492492p-3);   /*  1/7 */
+    q = fma(q, r, -0x1.5555555555555p-3);  /* -1/6 */
+    q = fma(q, r, 0x1.999999999999ap-3);   /*  1/5 */
+    q = fma(q, r, -0x1p-2);                /* -1/4 */
+    q = fma(q, r, 0x1.5555555555555p-2);   /*  1/3 */
+    q = fma(q, r, -0x1p-1);                /* -1/2 */
+    const double l1p = fma(r * r, q, r);
+    return fma((double)e, HM_LN2, tab[2 * i + 1] + l1p);
+}
+
+/* Y(lat) = 0.5 - (ln(1+s) - ln(1-s)) / (4 pi), s = sin(lat*pi/180), |lat| <= 85.06.
+ * 1 +- s is exact where it could cancel (Sterbenz), so no division is needed. */
+HM_FN double hm_fast_Y(double lat, const double* tab)
 {
     const double p = lat * HM_DEG2RAD;
     const double p2 = p * p;
@@ -59,29 +83,7 @@ HM_FN double hm_fast_Y(double lat)
     s = fma(s, p2, 0x1.1111111111111p-7);    /*  1/5!  */
     s = fma(s, p2, -0x1.5555555555555p-3);   /* -1/3!  */
     s = fma(p * p2, s, p);
-    /* q = (1+s)/(1-s) > 0;  ln q = e ln2 + 2 atanh(t), t = (m-1)/(m+1) */
-    const double q = (1.0 + s) / (1.0 - s);
-    const uint64_t qb = hm_d2u(q);
-    int e = (int)((qb >> 52) & 0x7ff) - 1023;
-    double m = hm_u2d((qb & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-    if (m > HM_SQRT2) {
-        m = m * 0.5;
-        e = e + 1;
-    }
-    const double t = (m - 1.0) / (m + 1.0);   /* |t| <= 0.1716 */
-    const double t2 = t * t;
-    double a = 0x1.8618618618618p-5;          /* 1/21 */
-    a = fma(a, t2, 0x1.af286bca1af28p-5);     /* 1/19 */
-    a = fma(a, t2, 0x1.e1e1e1e1e1e1ep-5);     /* 1/17 */
-    a = fma(a, t2, 0x1.1111111111111p-4);     /* 1/15 */
-    a = fma(a, t2, 0x1.3b13b13b13b14p-4);     /* 1/13 */
-    a = fma(a, t2, 0x1.745d1745d1746p-4);     /* 1/11 */
-    a = fma(a, t2, 0x1.c71c71c71c71cp-4);     /* 1/9  */
-    a = fma(a, t2, 0x1.2492492492492p-3);     /* 1/7  */
-    a = fma(a, t2, 0x1.999999999999ap-3);     /* 1/5  */
-    a = fma(a, t2, 0x1.5555555555555p-2);     /* 1/3  */
-    const double lnm = 2.0 * fma(t * t2, a, t);
-    const double L = fma((double)e, HM_LN2, lnm);
+    const double L = hm_fast_ln(1.0 + s, tab) - hm_fast_ln(1.0 - s, tab);
     return fma(-L, HM_INV4PI, 0.5);
 }
 
@@ -108,11 +110,11 @@ HM_SLOW_FN int hm_row_exact(double lat, int zoom, int64_t* row)
 }
 
 /* Returns status; *slow = 1 when the exact chain was used. */
-HM_FN int hm_row(double lat, int zoom, int64_t* row, int* slow)
+HM_FN int hm_row(double lat, int zoom, int64_t* row, int* slow, const double* tab)
 {
     if (fabs(lat) <= HM_LAT_FAST) {
         const double scale = hm_exp2i(zoom);
-        const double R = hm_fast_Y(lat) * scale;
+        const double R = hm_fast_Y(lat, tab) * scale;
         const double f = floor(R);
         const double fr = R - f;
         const double g = HM_Y_EPS * scale;
@@ -126,7 +128,11 @@ HM_FN int hm_row(double lat, int zoom, int64_t* row, int* slow)
     return hm_row_exact(lat, zoom, row);
 }
 
-HM_FN int hm_col(double lon, int zoom, int64_t* col)
+/* Column: the reference's (lon + 180.0) / 360.0 * 2^z (tile.py:21).  Fast path
+ * multiplies by RN(1/360) instead of dividing: |y_fast - y_ref| < |y| 2^-51,
+ * so a fraction farther than |y| 2^-49 from an integer floors identically;
+ * anything else (and NaN/inf) takes the literal division. */
+HM_SLOW_FN int hm_col_exact(double lon, int zoom, int64_t* col)
 {
     const double R = (lon + 180.0) / 360.0 * hm_exp2i(zoom);
     if (R != R) return HM_E_NAN;
@@ -137,10 +143,27 @@ HM_FN int hm_col(double lon, int zoom, int64_t* col)
     return HM_OK;
 }
 
-/* tile_id_from_lat_long order: row first, its error wins (tile.py:10-11). */
-HM_FN int hm_project_point(double lat, double lon, int zoom, int64_t* row, int64_t* col, int* slow)
+HM_FN int hm_col(double lon, int zoom, int64_t* col)
 {
-    int st = hm_row(lat, zoom, row, slow);
+    const double y = (lon + 180.0) * HM_INV360 * hm_exp2i(zoom);
+    const double ay = fabs(y);
+    if (ay < 0x1p52) {
+        const double f = floor(y);
+        const double fr = y - f;
+        const double g = ay * 0x1p-49;
+        if (fr > g && fr < 1.0 - g) {
+            *col = (int64_t)f;
+            return HM_OK;
+        }
+    }
+    return hm_col_exact(lon, zoom, col);
+}
+
+/* tile_id_from_lat_long order: row first, its error wins (tile.py:10-11). */
+HM_FN int hm_project_point(double lat, double lon, int zoom, int64_t* row, int64_t* col, int* slow,
+                           const double* tab)
+{
+    int st = hm_row(lat, zoom, row, slow, tab);
     if (st != HM_OK) return st;
     return hm_col(lon, zoom, col);
 }

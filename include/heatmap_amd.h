@@ -70,7 +70,7 @@ extern "C" {
 #define HM_KEY_ZOOM(k) ((int)((k) >> 58))
 #define HM_KEY_ROW(k) ((int64_t)(((k) >> 29) & 0x1FFFFFFFull))
 #define HM_KEY_COL(k) ((int64_t)((k) & 0x1FFFFFFFull))
-#define HM_MAX_ZOOM 22   /* largest zmax accepted by hm_count* (level-1 keys fit u32) */
+#define HM_MAX_ZOOM 21   /* largest zmax accepted by hm_count* (level-1 keys fit u32) */
 
 typedef struct hm_ctx hm_ctx;
 

@@ -10,6 +10,8 @@
 #include <math.h>
 #include "hm_project.h"
 
+static const double TAB[2 * HM_LOGTAB_N] = HM_LOGTAB_INIT;
+
 int hmh_project(const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
                 int64_t* col, uint8_t* st, uint8_t* slow)
 {
@@ -17,7 +19,7 @@ int hmh_project(const double* lat, const double* lon, int64_t n, int zoom, int64
     for (int64_t i = 0; i < n; i++) {
         int64_t r = 0, c = 0;
         int s = 0;
-        int k = hm_project_point(lat[i], lon[i], zoom, &r, &c, &s);
+        int k = hm_project_point(lat[i], lon[i], zoom, &r, &c, &s, TAB);
         row[i] = k == HM_OK ? r : 0;
         col[i] = k == HM_OK ? c : 0;
         st[i] = (uint8_t)k;
@@ -34,7 +36,7 @@ double hmh_fast_Y_maxerr(const double* lat, int64_t n, double* worst_lat)
     for (int64_t i = 0; i < n; i++) {
         double x = lat[i] * M_PI / 180;
         double yr = (1 - log(tan(x) + 1 / cos(x)) / M_PI) / 2;
-        double e = fabs(hm_fast_Y(lat[i]) - yr);
+        double e = fabs(hm_fast_Y(lat[i], TAB) - yr);
         if (e > m) {
             m = e;
             *worst_lat = lat[i];
