@@ -50,8 +50,8 @@ def load() -> ctypes.CDLL:
     with _LOCK:
         if _LIB is not None:
             return _LIB
-        path = _build.LIB
-        if not os.path.exists(path) or _build._stale():
+        path = os.environ.get("HM_LIB_PATH") or _build.LIB
+        if path == _build.LIB and (not os.path.exists(path) or _build._stale()):
             try:
                 _build.build(verbose=False)
             except Exception as e:  # pragma: no cover - surfaced to the caller

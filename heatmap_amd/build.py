@@ -35,25 +35,27 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True) -> str:
-    if not force and not _stale():
+def build(force: bool = False, verbose: bool = True, out: str = None, defines=()) -> str:
+    """Compile the library (out/defines: tools/variants.py builds tuning variants)."""
+    lib = out or LIB
+    if not force and out is None and not _stale():
         return LIB
-    os.makedirs(LIBDIR, exist_ok=True)
+    os.makedirs(os.path.dirname(lib), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
     objs = []
     for src in SOURCES:
-        obj = os.path.join(LIBDIR, src.rsplit(".", 1)[0] + ".o")
-        cmd = [hipcc, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(os.path.dirname(lib), os.path.basename(lib) + "." + src.rsplit(".", 1)[0] + ".o")
+        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(CSRC, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)
         objs.append(obj)
-    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", LIB + ".tmp"]
+    cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
-    os.replace(LIB + ".tmp", LIB)
-    return LIB
+    os.replace(lib + ".tmp", lib)
+    return lib
 
 
 if __name__ == "__main__":

@@ -58,6 +58,8 @@ enum {
     ST_SLOW = 2,
     ST_CURSOR = 3,
     ST_NSLOTS = 4,
+    ST_REDO = 5,
+    ST_REDO_OUT = 6,
     ST_COUNT = 8
 };
 
@@ -77,7 +79,7 @@ static int hip_fail(hipError_t e, const char* what)
 /* named arena slots */
 enum {
     B_KEYS_A, B_KEYS_B, B_RUNS_A, B_RUNS_B, B_RUNPRE_A, B_RUNPRE_B, B_NRUNS, B_NKEYS, B_VALS, B_PREFIX,
-    B_PARTIAL, B_TOTAL, B_ROOT, B_NRUNS_TOT,
+    B_PARTIAL, B_TOTAL, B_ROOT, B_NRUNS_TOT, B_REDO_IDX, B_REDO_ROWS, B_REDO_COLS,
     B_BK0, /* 4 levels x 8 arrays */
     B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
     B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
@@ -279,8 +281,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     int nev = 0;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
 
-    /* root bucket list B_0: one bucket (the zoom-0 tile) */
-    const uint32_t tiles1 = (uint32_t)((n + HM_T1 - 1) / HM_T1);
+    /* level-1 tiles: the input tiles, then (lat/lon input only) tiles of the
+     * points the fast path deferred to k_redo, at most redo_cap of them */
+    const uint32_t tiles_in = (uint32_t)((n + HM_T1 - 1) / HM_T1);
+    const bool from_tiles = rows != nullptr;
+    uint64_t redo_cap = from_tiles ? 0 : std::max<uint64_t>(1u << 20, (uint64_t)n / 256);
+    if (redo_cap > (uint64_t)n) redo_cap = (uint64_t)n;
+    uint32_t tiles1 = tiles_in + (uint32_t)((redo_cap + HM_T1 - 1) / HM_T1);
     uint32_t* root = nullptr;
     ENSURE(B_ROOT, 4 * sizeof(uint32_t) + 2 * sizeof(uint64_t), root);
     {
@@ -340,6 +347,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_NRUNS_TOT, V.nchildren * sizeof(uint32_t), nruns_tot);
 
         if (l == 0) {
+            uint32_t* redo_idx = nullptr;
+            int64_t *redo_rows = nullptr, *redo_cols = nullptr;
+            if (!from_tiles) {
+                ENSURE(B_REDO_IDX, redo_cap * sizeof(uint32_t), redo_idx);
+                ENSURE(B_REDO_ROWS, redo_cap * sizeof(int64_t), redo_rows);
+                ENSURE(B_REDO_COLS, redo_cap * sizeof(int64_t), redo_cols);
+            }
             HmPart1Args a;
             memset(&a, 0, sizeof(a));
             a.lat = lat;
@@ -352,6 +366,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.dbits = V.dbits;
             a.restbits = restbits;
             a.tiles = tiles1;
+            a.tile0 = 0;
             a.shard_bits = sb;
             a.keys_out = keys_out;
             a.nruns = nruns;
@@ -359,12 +374,61 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.err_word = ctx->state + ST_ERR;
             a.exotic_word = ctx->state + ST_EXOTIC;
             a.slow_count = ctx->state + ST_SLOW;
+            a.redo_idx = redo_idx;
+            a.redo_count = ctx->state + ST_REDO;
+            a.redo_cap = redo_cap;
             HIPCHK(hipEventRecord(ev[nev++], s));
-            hm_launch_part1(s, a, V.out16, rows != nullptr);
+            hm_launch_part1(s, a, tiles_in, V.out16, from_tiles ? 1 : 0);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[nev++], s));
+            if (!from_tiles) {
+                HmRedoArgs ra;
+                ra.lat = lat;
+                ra.lon = lon;
+                ra.keep = keep;
+                ra.Z = Z;
+                ra.redo_idx = redo_idx;
+                ra.redo_count = ctx->state + ST_REDO;
+                ra.rows_out = redo_rows;
+                ra.cols_out = redo_cols;
+                ra.out_count = ctx->state + ST_REDO_OUT;
+                ra.err_word = ctx->state + ST_ERR;
+                ra.exotic_word = ctx->state + ST_EXOTIC;
+                hm_launch_redo(s, ra, redo_cap);
+                HIPCHK(hipGetLastError());
+            }
             if ((st = read_state(ctx))) return st;
             if ((st = take_error(ctx))) return st;
+            const uint64_t nredo = ctx->host_state[ST_REDO];
+            if (!from_tiles && nredo > redo_cap) {
+                /* adversarial input (mostly polar / guard band): redo the
+                 * level with the exact chain fused into the kernel */
+                HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
+                a.tiles = tiles1 = tiles_in;
+                hm_launch_part1(s, a, tiles_in, V.out16, 2);
+                HIPCHK(hipGetLastError());
+                if ((st = read_state(ctx))) return st;
+                if ((st = take_error(ctx))) return st;
+                unsigned long long* up = ctx->host_state + ST_COUNT;
+                up[0] = (unsigned long long)tiles1 << 32;
+                up[1] = up[2] = up[3] = 0;
+                HIPCHK(hipMemcpyAsync(root, up, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
+            } else if (!from_tiles) {
+                const uint64_t nres = ctx->host_state[ST_REDO_OUT];
+                if (nres) {
+                    HmPart1Args b = a;
+                    b.lat = nullptr;
+                    b.lon = nullptr;
+                    b.rows_in = redo_rows;
+                    b.cols_in = redo_cols;
+                    b.keep = nullptr;
+                    b.n = (int64_t)nres;
+                    b.tile0 = tiles_in;
+                    hm_launch_part1(s, b, (uint32_t)((nres + HM_T1 - 1) / HM_T1), V.out16, 1);
+                    HIPCHK(hipGetLastError());
+                }
+            }
+            ctx->last_slow = (int64_t)nredo;
         } else {
             HmPartNArgs a;
             memset(&a, 0, sizeof(a));

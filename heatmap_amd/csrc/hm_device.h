@@ -118,48 +118,39 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
     return r;
 }
 
-/* LDS histogram increment with wave aggregation: up to HM_AGG_ROUNDS times,
- * the lanes holding the first remaining lane's key add once; the rest add
- * individually.  One round catches the skewed case (most of a wave on one
- * key, SURVEY.md section 7 hard part 3); more rounds cost more scalar issue
- * than the duplicate-address serialisation they save (measured: 4 rounds made
- * k_project_partition SALU-bound). */
-#define HM_AGG_ROUNDS 1
+/* LDS histogram increment.  Duplicate addresses within one ds_add are
+ * serialised by the LDS unit, which is cheaper than software aggregation for
+ * the usual mix; only a wave whose valid lanes ALL share one key (the skew
+ * case, SURVEY.md section 7 hard part 3) is collapsed into a single add.
+ * (Measured: 4 rounds of leader aggregation made k_project_partition
+ * SALU-bound.) */
 __device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t key, bool valid)
 {
-    uint64_t act = __ballot(valid);
-    const int lane = hm_lane();
-#pragma unroll
-    for (int it = 0; it < HM_AGG_ROUNDS; it++) {
-        if (act == 0) return;
-        const int leader = __ffsll((unsigned long long)act) - 1;
-        const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
-        const uint64_t same = __ballot(valid && key == kl) & act;
-        if (lane == leader) atomicAdd(&hist[kl], (uint32_t)__popcll(same));
-        act &= ~same;
+    const uint64_t vm = __ballot(valid);
+    if (vm == 0) return;
+    const int leader = __ffsll((unsigned long long)vm) - 1;
+    const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
+    if (__ballot(valid && key == kl) == vm) {
+        if (hm_lane() == leader) atomicAdd(&hist[kl], (uint32_t)__popcll(vm));
+    } else if (valid) {
+        atomicAdd(&hist[key], 1u);
     }
-    if ((act >> lane) & 1ull) atomicAdd(&hist[key], 1u);
 }
 
-/* LDS slot reservation with the same aggregation: returns the position of
- * this lane's element in bucket `key` (cursor array `cur`). */
+/* Slot reservation in bucket `key` (cursor array `cur`), same policy. */
 __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t key, bool valid)
 {
-    uint64_t act = __ballot(valid);
-    const int lane = hm_lane();
+    const uint64_t vm = __ballot(valid);
+    if (vm == 0) return 0;
+    const int leader = __ffsll((unsigned long long)vm) - 1;
+    const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
     uint32_t pos = 0;
-#pragma unroll
-    for (int it = 0; it < HM_AGG_ROUNDS; it++) {
-        if (act == 0) return pos;
-        const int leader = __ffsll((unsigned long long)act) - 1;
-        const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
-        const uint64_t same = __ballot(valid && key == kl) & act;
+    if (__ballot(valid && key == kl) == vm) {
         uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(&cur[kl], (uint32_t)__popcll(same));
-        base = __builtin_amdgcn_readlane(base, leader);
-        if ((same >> lane) & 1ull) pos = base + hm_mbcnt(same);
-        act &= ~same;
+        if (hm_lane() == leader) base = atomicAdd(&cur[kl], (uint32_t)__popcll(vm));
+        pos = __builtin_amdgcn_readlane(base, leader) + hm_mbcnt(vm);
+    } else if (valid) {
+        pos = atomicAdd(&cur[key], 1u);
     }
-    if ((act >> lane) & 1ull) pos = atomicAdd(&cur[key], 1u);
     return pos;
 }

@@ -71,20 +71,22 @@ __global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat,
 /* level 1: projection fused with the first partition                        */
 /* ------------------------------------------------------------------------ */
 
-template <typename OutT, bool FROM_TILES>
+template <typename OutT, int MODE>
 __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args a)
 {
     __shared__ uint32_t cur[HM_MAX_F1];
     __shared__ OutT stage[HM_T1];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
     __shared__ double tab[2 * HM_LOGTAB_N];
+    constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
     if (!FROM_TILES) hm_load_logtab(tab);
     __syncthreads();
 
-    const int64_t base = (int64_t)blockIdx.x * HM_T1;
+    const uint32_t tile = a.tile0 + blockIdx.x;          /* tile slot in the run layout */
+    const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
     const uint32_t lim = 1u << a.Z;
     uint32_t dig[HM_P1_PPT];
@@ -125,40 +127,83 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             lo[k] = make_double2(0.0, 0.0);
         }
     }
+    /* fast path for every point, branch-free; points the fast path cannot
+     * settle (guard band, polar/out-of-range/non-finite input) are marked in
+     * `redo` and resolved afterwards in one ballot-guarded pass */
+    const int hb = a.restbits >> 1;
+    const uint32_t lowm = (1u << hb) - 1u;
+    uint32_t redo = 0;
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT / 2; k++) {
-        const int64_t i0 = base + 2 * ((int64_t)k * HM_P1_THREADS + tid);
+    for (int k = 0; k < HM_P1_PPT; k++) {
+        const int64_t i = base + 2 * ((int64_t)(k >> 1) * HM_P1_THREADS + tid) + (k & 1);
+        const double pa = (k & 1) ? la[k >> 1].y : la[k >> 1].x;
+        const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
+        int64_t r, c;
+        int ok;
+        if (FROM_TILES) {
+            r = __double_as_longlong(pa);
+            c = __double_as_longlong(po);
+            ok = 1;
+        } else {
+            ok = hm_project_fast(pa, po, a.Z, &r, &c, tab);
+        }
+        const bool inb = i < a.n;
+        const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
+        const bool dom = ((uint64_t)r < lim) & ((uint64_t)c < lim);
+        redo |= (uint32_t)(inb & !(ok & dom)) << k;
+        const bool v = inb & ok & dom & kept;
+        dig[k] = v ? hm_morton16((uint32_t)r >> hb, (uint32_t)c >> hb) : 0xFFFFFFFFu;
+        rest[k] = hm_morton16((uint32_t)r & lowm, (uint32_t)c & lowm) & restmask;
+        /* one point at a time: interleaving all eight projections would need
+         * ~200 VGPRs and halve occupancy */
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if (MODE == 0) {
+        /* defer: k_redo resolves these with the exact chain and feeds them
+         * back as extra tiles (keeps the exact path out of this kernel's
+         * register allocation) */
 #pragma unroll
-        for (int h = 0; h < 2; h++) {
-            const int64_t i = i0 + h;
-            dig[2 * k + h] = 0xFFFFFFFFu;
-            rest[2 * k + h] = 0;
-            if (i >= a.n) continue;
-            const double pa = h ? la[k].y : la[k].x;
-            const double po = h ? lo[k].y : lo[k].x;
+        for (int k = 0; k < HM_P1_PPT; k++) {
+            const bool rd = (redo >> k) & 1u;
+            const uint64_t m = __ballot(rd);
+            if (m) {
+                uint64_t b = 0;
+                if (hm_lane() == __ffsll((unsigned long long)m) - 1) b = atomicAdd(a.redo_count, (unsigned long long)__popcll(m));
+                b = __shfl(b, __ffsll((unsigned long long)m) - 1, 64);
+                const uint64_t q = b + hm_mbcnt(m);
+                if (rd && q < a.redo_cap)
+                    a.redo_idx[q] = (uint32_t)(base + 2 * ((int64_t)(k >> 1) * HM_P1_THREADS + tid) + (k & 1));
+            }
+        }
+        nslow = __popc(redo);
+    } else if (__ballot(redo != 0)) {
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT; k++) {
+            if (!((redo >> k) & 1u)) continue;
+            const int64_t i = base + 2 * ((int64_t)(k >> 1) * HM_P1_THREADS + tid) + (k & 1);
+            const double pa = (k & 1) ? la[k >> 1].y : la[k >> 1].x;
+            const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
             int64_t r = 0, c = 0;
-            int st, slow = 0;
+            int st = HM_OK, slow = 0;
             if (FROM_TILES) {
                 r = __double_as_longlong(pa);
                 c = __double_as_longlong(po);
-                st = HM_OK;
             } else {
-                st = hm_project_point(pa, po, a.Z, &r, &c, &slow, tab);
+                /* the literal reference chain (tile.py:17,21), row before column */
+                st = hm_row_exact(pa, a.Z, &r);
+                if (st == HM_OK) st = hm_col_exact(po, a.Z, &c);
+                nslow++;
             }
-            nslow += slow;
-            if (HM_UNLIKELY(st != HM_OK)) {
+            (void)slow;
+            const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
+            if (st != HM_OK) {
                 atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
-                continue;
-            }
-            if (!((kp[k] >> (8 * h)) & 0xFF)) continue;
-            if (HM_UNLIKELY((uint64_t)r >= lim || (uint64_t)c >= lim)) {
+            } else if (kept && ((uint64_t)r >= lim || (uint64_t)c >= lim)) {
                 atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
-                continue;
+            } else if (kept) {
+                dig[k] = hm_morton16((uint32_t)r >> hb, (uint32_t)c >> hb);
+                rest[k] = hm_morton16((uint32_t)r & lowm, (uint32_t)c & lowm) & restmask;
             }
-            const int sh = a.restbits >> 1;
-            const uint32_t lowm = (1u << sh) - 1u;
-            dig[2 * k + h] = hm_morton16((uint32_t)r >> sh, (uint32_t)c >> sh);
-            rest[2 * k + h] = hm_morton16((uint32_t)r & lowm, (uint32_t)c & lowm) & restmask;
         }
     }
     if (!FROM_TILES) {
@@ -181,20 +226,29 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     }
     uint32_t total;
     uint32_t off = hm_block_excl_scan<HM_P1_THREADS>(s, scr, &total);
+    /* run records: issue every slot atomic before consuming any result, so a
+     * tile pays one atomic latency, not PER of them */
+    const uint32_t sh = tile & ((1u << a.shard_bits) - 1u);
+    const uint64_t cap = ((uint64_t)a.tiles + (1u << a.shard_bits) - 1) >> a.shard_bits;
+    uint32_t idx[PER];
+    uint32_t offq[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        offq[q] = off;
+        idx[q] = 0;
+        if (d < F && cnt[q]) idx[q] = atomicAdd(&a.nruns[((uint64_t)d << a.shard_bits) + sh], 1u);
+        off += cnt[q];
+    }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
         if (d < F) {
-            cur[d] = off;
-            if (cnt[q]) {
-                const uint32_t sh = blockIdx.x & ((1u << a.shard_bits) - 1u);
-                const uint32_t idx = atomicAdd(&a.nruns[((uint64_t)d << a.shard_bits) + sh], 1u);
-                const uint64_t cap = ((uint64_t)a.tiles + (1u << a.shard_bits) - 1) >> a.shard_bits;
-                a.runs[hm_run_base(0, a.tiles, 0, d, a.dbits, a.shard_bits) + sh * cap + idx] =
-                    make_uint2((uint32_t)base + off, cnt[q]);
-            }
+            cur[d] = offq[q];
+            if (cnt[q])
+                a.runs[hm_run_base(0, a.tiles, 0, d, a.dbits, a.shard_bits) + sh * cap + idx[q]] =
+                    make_uint2(tile * HM_T1 + offq[q], cnt[q]);
         }
-        off += cnt[q];
     }
     __syncthreads();
 #pragma unroll
@@ -204,7 +258,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (v) stage[pos] = (OutT)rest[k];
     }
     __syncthreads();
-    OutT* out = (OutT*)a.keys_out + base;
+    OutT* out = (OutT*)a.keys_out + (uint64_t)tile * HM_T1;
     for (uint32_t i = tid; i < total; i += HM_P1_THREADS) out[i] = stage[i];
 }
 
@@ -257,7 +311,9 @@ __device__ __forceinline__ HmItem hm_locate(const HmBuckets& B, uint32_t g, uint
  * binary search after HM_WALK steps.  HM_SU positions per lane are resolved
  * before any load is consumed.  Block-uniform; every thread calls. */
 #define HM_RCHUNK 1024
+#ifndef HM_SU
 #define HM_SU 4
+#endif
 #define HM_WALK 4
 struct HmStreamLds {
     uint32_t end[HM_RCHUNK];
@@ -388,25 +444,35 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     uint32_t off = hm_block_excl_scan<HM_PN_THREADS>(s, scr, &tot2);
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
     const uint64_t gtile = blockIdx.x;
+    const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
+    const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
+    uint32_t idx[PER];
+    uint32_t offq[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        offq[q] = off;
+        idx[q] = 0;
+        if (d < F && cnt[q])
+            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
+        off += cnt[q];
+    }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
         if (d < F) {
-            cur[d] = off;
+            cur[d] = offq[q];
             if (cnt[q]) {
-                const uint64_t child = (uint64_t)it.bucket * F + d;
-                const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
-                const uint32_t idx = atomicAdd(&a.nruns_out[(child << a.shard_bits) + sh], 1u);
-                const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
                 const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
-                a.runs_out[rb + sh * cap + idx] = make_uint2((uint32_t)(gtile * HM_TN) + off, cnt[q]);
+                a.runs_out[rb + sh * cap + idx[q]] = make_uint2((uint32_t)(gtile * HM_TN) + offq[q], cnt[q]);
             }
         }
-        off += cnt[q];
     }
     __syncthreads();
-    for (uint32_t i0 = 0; i0 < total; i0 += HM_PN_THREADS) {
-        const uint32_t i = i0 + tid;
+    constexpr int KPT = HM_TN / HM_PN_THREADS;
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+        const uint32_t i = k * HM_PN_THREADS + tid;
         const bool v = i < total;
         const uint32_t key = v ? stage_in[i] : 0u;
         const uint32_t d = key >> a.restbits;
@@ -901,21 +967,53 @@ void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int6
                        err_word, slow);
 }
 
-void hm_launch_part1(hipStream_t s, const HmPart1Args& a, bool out16, bool from_tiles)
+void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool out16, int mode)
 {
-    if (a.tiles == 0) return;
-    dim3 g(a.tiles), b(HM_P1_THREADS);
-    if (from_tiles) {
-        if (out16)
-            hipLaunchKernelGGL((k_project_partition<uint16_t, true>), g, b, 0, s, a);
-        else
-            hipLaunchKernelGGL((k_project_partition<uint32_t, true>), g, b, 0, s, a);
+    if (grid == 0) return;
+    dim3 g(grid), b(HM_P1_THREADS);
+#define HM_P1_CASE(T, M) hipLaunchKernelGGL((k_project_partition<T, M>), g, b, 0, s, a)
+    if (out16) {
+        if (mode == 0) HM_P1_CASE(uint16_t, 0);
+        else if (mode == 1) HM_P1_CASE(uint16_t, 1);
+        else HM_P1_CASE(uint16_t, 2);
     } else {
-        if (out16)
-            hipLaunchKernelGGL((k_project_partition<uint16_t, false>), g, b, 0, s, a);
-        else
-            hipLaunchKernelGGL((k_project_partition<uint32_t, false>), g, b, 0, s, a);
+        if (mode == 0) HM_P1_CASE(uint32_t, 0);
+        else if (mode == 1) HM_P1_CASE(uint32_t, 1);
+        else HM_P1_CASE(uint32_t, 2);
     }
+#undef HM_P1_CASE
+}
+
+/* exact resolution of the points k_project_partition (mode 0) deferred */
+__global__ __launch_bounds__(256) void k_redo(HmRedoArgs a)
+{
+    const uint64_t n = *a.redo_count;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
+        const uint32_t i = a.redo_idx[q];
+        int64_t r = 0, c = 0;
+        int st = hm_row_exact(a.lat[i], a.Z, &r);
+        if (st == HM_OK) st = hm_col_exact(a.lon[i], a.Z, &c);
+        const bool kept = !a.keep || a.keep[i];
+        const uint64_t lim = 1ull << a.Z;
+        if (st != HM_OK) {
+            atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+        } else if (kept && ((uint64_t)r >= lim || (uint64_t)c >= lim)) {
+            atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
+        } else if (kept) {
+            const unsigned long long o = atomicAdd(a.out_count, 1ull);
+            a.rows_out[o] = r;
+            a.cols_out[o] = c;
+        }
+    }
+}
+
+void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n)
+{
+    uint64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_redo, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
 
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool out16)

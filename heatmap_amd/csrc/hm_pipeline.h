@@ -4,14 +4,22 @@
 #include <stdint.h>
 
 /* level 1: projection + partition by the zoom-z1 digit */
+#ifndef HM_P1_THREADS
 #define HM_P1_THREADS 512
+#endif
+#ifndef HM_P1_PPT
 #define HM_P1_PPT 8
+#endif
 #define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 4096 points per tile */
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
 /* levels >= 2 */
+#ifndef HM_PN_THREADS
 #define HM_PN_THREADS 512
+#endif
+#ifndef HM_TN
 #define HM_TN 8192
+#endif
 #define HM_LEVEL_ZOOMS 6                    /* <= 6 zooms per level */
 #define HM_MAX_FN 4096
 #define HM_MAX_SHARDS 32                    /* run-counter shards per child */
@@ -19,7 +27,9 @@
 #define HM_AG_THREADS 512
 #define HM_AG_CELLS 16384
 #define HM_AG_LG 7
+#ifndef HM_TA
 #define HM_TA (1u << 18)                    /* keys per aggregation work item */
+#endif
 #define HM_POOL_THREADS 256
 #define HM_MAX_LEVELS 4
 #define HM_COUNT_MAX_ZOOM 21                /* level-1 keys 2*(Z-5) bits fit u32 */
@@ -59,13 +69,17 @@ struct HmOut {
 struct HmPart1Args {
     const double* lat;
     const double* lon;
-    const int64_t* rows_in;   /* hm_count_tiles */
+    const int64_t* rows_in;   /* hm_count_tiles, and resolved redo points */
     const int64_t* cols_in;
     const uint8_t* keep;
     int64_t n;
     int Z, dbits, restbits;
-    uint32_t tiles;
+    uint32_t tiles;           /* level-1 tile slots of the run layout (incl. redo tiles) */
+    uint32_t tile0;           /* index of this launch's first tile */
     int shard_bits;
+    uint32_t* redo_idx;       /* fast mode: points the fast path could not settle */
+    unsigned long long* redo_count;
+    uint64_t redo_cap;
     void* keys_out;
     uint32_t* nruns;            /* [F << shard_bits] */
     uint2* runs;
@@ -149,7 +163,22 @@ struct HmPoolArgs {
 
 void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
                        int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow);
-void hm_launch_part1(hipStream_t s, const HmPart1Args& a, bool out16, bool from_tiles);
+/* mode: 0 fast path + redo list, 1 tile input (exact row/col given), 2 fused exact (fallback) */
+void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool out16, int mode);
+struct HmRedoArgs {
+    const double* lat;
+    const double* lon;
+    const uint8_t* keep;
+    int Z;
+    const uint32_t* redo_idx;
+    const unsigned long long* redo_count;
+    int64_t* rows_out;
+    int64_t* cols_out;
+    unsigned long long* out_count;
+    unsigned long long* err_word;
+    unsigned long long* exotic_word;
+};
+void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n);
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool out16);
 void hm_launch_runscan(hipStream_t s, const HmScanArgs& a);
 void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total);

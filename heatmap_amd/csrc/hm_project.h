@@ -159,6 +159,29 @@ HM_FN int hm_col(double lon, int zoom, int64_t* col)
     return hm_col_exact(lon, zoom, col);
 }
 
+/* Branch-free fast projection for the streaming kernels: returns 1 and the
+ * tile when both fast paths are conclusive; 0 means "resolve this point with
+ * hm_project_point" (guard band, |lat| > 85.06, non-finite input, huge lon).
+ * Identical results to hm_project_point whenever it returns 1. */
+HM_FN int hm_project_fast(double lat, double lon, int zoom, int64_t* row, int64_t* col, const double* tab)
+{
+    const double scale = hm_exp2i(zoom);
+    const double R = hm_fast_Y(lat, tab) * scale;
+    const double f = floor(R);
+    const double fr = R - f;
+    const double g = HM_Y_EPS * scale;
+    const double y = (lon + 180.0) * HM_INV360 * scale;
+    const double ay = fabs(y);
+    const double f2 = floor(y);
+    const double fr2 = y - f2;
+    const double g2 = ay * 0x1p-49;
+    const int ok = (fabs(lat) <= HM_LAT_FAST) & (fr > g) & (fr < 1.0 - g) & (ay < 0x1p52) & (fr2 > g2) &
+                   (fr2 < 1.0 - g2);
+    *row = (int64_t)(ok ? f : 0.0);
+    *col = (int64_t)(ok ? f2 : 0.0);
+    return ok;
+}
+
 /* tile_id_from_lat_long order: row first, its error wins (tile.py:10-11). */
 HM_FN int hm_project_point(double lat, double lon, int zoom, int64_t* row, int64_t* col, int* slow,
                            const double* tab)

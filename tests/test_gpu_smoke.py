@@ -56,3 +56,51 @@ def test_synth_bit_exact(gpu, kind):
     hl, ho = synth.generate(kind, n, seed=5, start=12345)
     assert np.array_equal(lat.cpu().numpy().view(np.uint64), hl.view(np.uint64))
     assert np.array_equal(lon.cpu().numpy().view(np.uint64), ho.view(np.uint64))
+
+
+def test_count_guard_band_points(gpu):
+    """Boundary-adjacent latitudes take the deferred exact path (k_redo)."""
+    d = np.load(os.path.join(GOLDEN, "projection_kat.npz"))
+    ok = (d["row_err"] == 0) & (d["col_err"] == 0) & (np.abs(d["lat"]) < 85.05) & (np.abs(d["lon"]) < 179.9)
+    lat, lon = d["lat"][ok], d["lon"][ok]
+    for zmax in (14, 21):
+        got = device.count(lat, lon, None, 0, zmax).sorted()
+        ref = oracle.count(lat, lon, None, 0, zmax)
+        assert got.slow_points > 0
+        assert np.array_equal(got.count, ref["count"]) and np.array_equal(got.row, ref["row"])
+        assert np.array_equal(got.col, ref["col"]) and np.array_equal(got.zoom, ref["zoom"])
+
+
+def test_count_redo_overflow_fallback(gpu):
+    """More deferred points than the redo list holds -> fused exact fallback."""
+    n = 3_000_000
+    lat, lon = synth.uniform(n, seed=9)
+    polar = (np.arange(n) % 5) < 2
+    lat = np.where(polar, 86.0 + (lat % 3.0), lat)       # 40% beyond the fast window
+    keep = (~polar).astype(np.uint8)                      # polar rows would be exotic: drop them
+    got = device.count(lat, lon, keep, 0, 16).sorted()
+    ref = oracle.count(lat, lon, keep, 0, 16)
+    assert got.slow_points > (1 << 20)
+    assert np.array_equal(got.count, ref["count"]) and np.array_equal(got.row, ref["row"])
+    assert np.array_equal(got.col, ref["col"])
+
+
+def test_count_errors_and_exotic(gpu):
+    lat, lon = synth.uniform(50000, seed=4)
+    lat = lat.copy()
+    lat[31337] = np.nan
+    lat[40000] = 95.0
+    with pytest.raises(ValueError, match="NaN"):
+        device.count(lat, lon, None, 0, 14)
+    lat[31337] = 10.0
+    with pytest.raises(ValueError, match="domain"):
+        device.count(lat, lon, None, 0, 14)
+    lat[40000] = 89.0          # valid, but outside the tile domain -> exotic
+    from heatmap_amd._lib import DevicePathUnsupported
+    with pytest.raises(DevicePathUnsupported):
+        device.count(lat, lon, None, 0, 14)
+    keep = np.ones(50000, np.uint8)
+    keep[40000] = 0            # background rows are projected, not binned
+    got = device.count(lat, lon, keep, 0, 14).sorted()
+    ref = oracle.count(lat, lon, keep, 0, 14)
+    assert np.array_equal(got.count, ref["count"])

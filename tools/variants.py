@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""Build and time compile-time tuning variants of the library on one GPU.
+
+    python tools/variants.py build            # here (hipcc), into heatmap_amd/_lib/variants/
+    python tools/variants.py run [names...]   # on the GPU box: one process per variant
+
+Each run times hm_count over the same resident cloud (1e9 hotspot points,
+zooms 0-18 by default) and prints one JSON line per variant.
+"""
+import json
+import os
+import subprocess
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
+
+VARIANTS = {
+    "base": [],
+    "p1_1024x4": ["HM_P1_THREADS=1024", "HM_P1_PPT=4"],
+    "p1_256x16": ["HM_P1_THREADS=256", "HM_P1_PPT=16"],
+    "p1_512x16": ["HM_P1_PPT=16"],
+    "su8": ["HM_SU=8"],
+    "ta64k": ["HM_TA=65536"],
+    "tn4k": ["HM_TN=4096"],
+}
+
+
+def build(names):
+    from heatmap_amd import build as b
+
+    for n in names:
+        out = os.path.join(VDIR, "lib_%s.so" % n)
+        b.build(force=True, verbose=False, out=out, defines=VARIANTS[n])
+        print("built", out, flush=True)
+
+
+def one(name, points, steps, zmax):
+    if name != "main":     # "main": the in-tree library heatmap_amd/_lib/libheatmap_amd.so
+        os.environ["HM_LIB_PATH"] = os.path.join(VDIR, "lib_%s.so" % name)
+    import numpy as np
+    import torch
+
+    from heatmap_amd import device
+
+    lat = torch.empty(points, dtype=torch.float64, device="cuda")
+    lon = torch.empty(points, dtype=torch.float64, device="cuda")
+    device.synth("hotspots", lat, lon)
+    bufs = device.CountBuffers(64 << 20)
+    ctx = device.context(0)
+    m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
+    torch.cuda.synchronize()
+    st = []
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
+        st.append(ctx.last_stats()[1][:4])
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    tot = int(bufs.counts[:m].sum().item())
+    print(json.dumps({"variant": name, "ms": dt * 1e3, "gpts": points / dt / 1e9, "cells": m,
+                      "check": tot == points * (zmax + 1),
+                      "stage_us": [round(x, 1) for x in np.mean(np.array(st), axis=0)]}), flush=True)
+
+
+def main():
+    cmd = sys.argv[1]
+    names = sys.argv[2:] or list(VARIANTS)
+    if cmd == "build":
+        build(names)
+    elif cmd == "run":
+        for n in names:
+            r = subprocess.run([sys.executable, __file__, "one", n], timeout=300)
+            if r.returncode != 0:
+                print(json.dumps({"variant": n, "error": r.returncode}), flush=True)
+                break
+    elif cmd == "one":
+        one(names[0], int(float(os.environ.get("HM_POINTS", "1e9"))), 3, int(os.environ.get("HM_ZMAX", "18")))
+
+
+if __name__ == "__main__":
+    main()
