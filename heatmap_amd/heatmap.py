@@ -126,32 +126,40 @@ def _group_plan(user_ids, keep):
     return keep, lit_all, others, masks
 
 
-def _cells(lat, lon, mask, zmin, zmax, tiles):
-    c = device.count(lat, lon, None if mask is None else mask.astype(np.uint8), zmin, zmax, tiles=tiles)
-    out = defaultdict(dict)
-    for z, r, cc, k in zip(c.zoom.tolist(), c.row.tolist(), c.col.tolist(), c.count.tolist()):
-        out[z][(r, cc)] = k
-    return out
+def _device_counter(lat, lon, zmin, zmax, tiles):
+    """counter(mask) -> {zoom: {(row, col): count}} on the device (hm_count)."""
+
+    def counter(mask):
+        c = device.count(lat, lon, None if mask is None else mask.astype(np.uint8), zmin, zmax, tiles=tiles)
+        out = defaultdict(dict)
+        for z, r, cc, k in zip(c.zoom.tolist(), c.row.tolist(), c.col.tolist(), c.count.tolist()):
+            out[z][(r, cc)] = k
+        return out
+
+    return counter
 
 
-def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None, tiles=False):
-    """Rows {row_id: {bin_id: float}} of build_heatmaps for columnar input.
+def assemble_rows(counter, user_id, keep=None, max_zoom_level=None, delta=None):
+    """Heatmap rows of build_heatmaps from per-group cell counts.
 
-    lat/lon: float64 arrays (or, with tiles=True, int64 row/col at the detail
-    zoom); user_id: sequence of str; keep: mask of non-background rows."""
+    counter(mask) returns {zoom: {(row, col): count}} of the points selected by
+    `mask` (None = all points) for zooms delta+1 .. max_zoom_level+delta; it is
+    the only place points are touched (the device in the product, the oracle
+    in the CPU tests).  Row layout: heatmap.py:55,85-90,120-126; 'all'
+    weighting: heatmap.py:64-70 applied level by level (module docstring)."""
     mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
     d = DETAIL_ZOOM_DELTA if delta is None else delta
     zmax = mz + d
-    zmin = d + 1
     keep, lit_all, others, groups = _group_plan(user_id, keep)
     # every point is projected (and may raise) even when not kept, as
-    # dataframe_loader does (heatmap.py:27-29): hm_count checks all points
-    n_cells = _cells(lat, lon, keep, zmin, zmax, tiles)
-    a_cells = _cells(lat, lon, lit_all, zmin, zmax, tiles) if lit_all.any() else {}
-    u_cells = _cells(lat, lon, others, zmin, zmax, tiles) if others.any() else {}
+    # dataframe_loader does (heatmap.py:27-29): the counter checks all points
+    n_cells = counter(keep)
+    a_cells = counter(lit_all) if lit_all.any() else {}
+    u_cells = counter(others) if others.any() else {}
     rows = {}
 
     def put(group, z, r, c, v):
+        # row tile = re-projected centre at z - d == arithmetic shift (SURVEY a-4)
         rid = "%s|alltime|%d_%d_%d" % (group, z - d, r >> d, c >> d)
         rows.setdefault(rid, {})["%d_%d_%d" % (z, r, c)] = float(v)
 
@@ -163,11 +171,22 @@ def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, d
         for (r, c), cnt in nz.items():
             put("all", z, r, c, (cnt + az.get((r, c), 0)) * (1 << k) + ((1 << k) - 1) * uz.get((r, c), 0))
     for g, m in groups.items():
-        gc = _cells(lat, lon, m, zmin, zmax, tiles)
+        gc = counter(m)
         for z in range(zmax, d, -1):
             for (r, c), cnt in gc.get(z, {}).items():
                 put(g, z, r, c, cnt)
     return rows
+
+
+def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None, tiles=False):
+    """Rows {row_id: {bin_id: float}} of build_heatmaps for columnar input.
+
+    lat/lon: float64 arrays (or, with tiles=True, int64 row/col at the detail
+    zoom); user_id: sequence of str; keep: mask of non-background rows."""
+    mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
+    d = DETAIL_ZOOM_DELTA if delta is None else delta
+    counter = _device_counter(lat, lon, d + 1, mz + d, tiles)
+    return assemble_rows(counter, user_id, keep, mz, d)
 
 
 def build_heatmaps(locations):
