@@ -84,7 +84,7 @@ enum {
     B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
     B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
     B_SLOTS = B_TOT0 + HM_MAX_LEVELS + 1,
-    B_SLOTBKT, B_GSLOTS, B_COUNT
+    B_SLOTBKT, B_GSLOTS, B_DESC0, B_COUNT = B_DESC0 + HM_MAX_LEVELS
 };
 
 static int ensure(hm_ctx* c, int slot, size_t bytes, void** out)
@@ -520,6 +520,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         b.digit = ca.out.digit;
         b.morton = ca.out.morton;
         b.slots = (l == L - 1) ? slots : nullptr;
+        {
+            uint4* desc;
+            ENSURE(B_DESC0 + l, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
+            b.desc = desc;
+            hm_launch_items(s, b, runpre_out, V.items, (l == L - 1) ? HM_TA : HM_TN, desc);
+            HIPCHK(hipGetLastError());
+        }
 
         keys_cur = keys_out;
         runs_cur = runs_out;

@@ -34,11 +34,12 @@
 #include "hm_project.h"
 #include "hm_pipeline.h"
 
-__constant__ double c_logtab[2 * HM_LOGTAB_N] = HM_LOGTAB_INIT;
+#define HM_YTAB_N (HM_YTAB_ROWS * HM_YTAB_STRIDE)
+__constant__ double c_ytab[HM_YTAB_N] = HM_YTAB_INIT;
 
-__device__ __forceinline__ void hm_load_logtab(double* tab)
+__device__ __forceinline__ void hm_load_ytab(double* tab)
 {
-    for (int i = threadIdx.x; i < 2 * HM_LOGTAB_N; i += blockDim.x) tab[i] = c_logtab[i];
+    for (int i = threadIdx.x; i < HM_YTAB_N; i += blockDim.x) tab[i] = c_ytab[i];
 }
 
 /* ------------------------------------------------------------------------ */
@@ -50,8 +51,8 @@ __global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat,
                                                  int64_t* __restrict__ col, uint8_t* __restrict__ status,
                                                  unsigned long long* err_word, unsigned long long* slow_count)
 {
-    __shared__ double tab[2 * HM_LOGTAB_N];
-    hm_load_logtab(tab);
+    __shared__ double tab[HM_YTAB_N];
+    hm_load_ytab(tab);
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
@@ -77,18 +78,20 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     __shared__ uint32_t cur[HM_MAX_F1];
     __shared__ OutT stage[HM_T1];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
-    __shared__ double tab[2 * HM_LOGTAB_N];
+    __shared__ double tab[HM_YTAB_N];
     constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
-    if (!FROM_TILES) hm_load_logtab(tab);
+    if (!FROM_TILES) hm_load_ytab(tab);
     __syncthreads();
 
     const uint32_t tile = a.tile0 + blockIdx.x;          /* tile slot in the run layout */
     const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
     const uint32_t lim = 1u << a.Z;
+    const double scale = hm_exp2i(a.Z);
+    const double kz = HM_INV360 * scale;
     uint32_t dig[HM_P1_PPT];
     uint32_t rest[HM_P1_PPT];
     int nslow = 0;
@@ -145,7 +148,10 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             c = __double_as_longlong(po);
             ok = 1;
         } else {
-            ok = hm_project_fast(pa, po, a.Z, &r, &c, tab);
+            int32_t r32, c32;
+            ok = hm_project_fast(pa, po, scale, kz, &r32, &c32, tab);
+            r = r32;
+            c = c32;
         }
         const bool inb = i < a.n;
         const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
@@ -303,6 +309,39 @@ __device__ __forceinline__ HmItem hm_locate(const HmBuckets& B, uint32_t g, uint
     return it;
 }
 
+/* one 32-B descriptor load (written by k_items) instead of hm_locate's
+ * dependent binary searches */
+__device__ __forceinline__ HmItem hm_item(const HmBuckets& B, uint32_t g)
+{
+    const uint4 d0 = B.desc[2 * g], d1 = B.desc[2 * g + 1];
+    HmItem it;
+    it.bucket = d0.x;
+    it.j = d0.y;
+    it.nitems = d0.z;
+    it.r0 = d0.w;
+    it.rb = d1.x;
+    it.nr = d1.y;
+    it.a = d1.z;
+    it.b = d1.w;
+    return it;
+}
+
+__global__ __launch_bounds__(256) void k_items(HmBuckets B, const uint32_t* runpre, uint32_t items, uint32_t T,
+                                               uint4* desc)
+{
+    const uint32_t g = blockIdx.x * 256 + threadIdx.x;
+    if (g >= items) return;
+    const HmItem it = hm_locate(B, g, T, runpre);
+    desc[2 * g] = make_uint4(it.bucket, it.j, it.nitems, it.r0);
+    desc[2 * g + 1] = make_uint4(it.rb, it.nr, it.a, it.b);
+}
+
+void hm_launch_items(hipStream_t s, const HmBuckets& B, const uint32_t* runpre, uint32_t items, uint32_t T,
+                     uint4* desc)
+{
+    if (items) hipLaunchKernelGGL(k_items, dim3((items + 255) / 256), dim3(256), 0, s, B, runpre, items, T, desc);
+}
+
 /* Calls f(key, valid) for every key of the item's logical range [a, b).
  * Run descriptors are staged in LDS HM_RCHUNK at a time.  Each wave owns a
  * contiguous span of logical positions and walks it 64 at a time (lane l takes
@@ -418,7 +457,7 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
     if (tid == 0) scnt = 0;
     __syncthreads();
-    const HmItem it = hm_locate(a.parent, blockIdx.x, HM_TN, a.runpre_in);
+    const HmItem it = hm_item(a.parent, blockIdx.x);
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
     hm_stream_item<uint32_t, HM_PN_THREADS>(it, a.keys_in, a.runs_in, a.runpre_in, sl, [&](uint32_t key, bool v) {
         const uint32_t d = key >> a.restbits;
@@ -890,7 +929,7 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate(HmAggArgs a)
     const uint32_t ncell = 1u << (2 * a.lg);
     for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
-    const HmItem it = hm_locate(a.B, blockIdx.x, HM_TA, a.runpre);
+    const HmItem it = hm_item(a.B, blockIdx.x);
     hm_stream_item<uint16_t, HM_AG_THREADS>(it, a.keys, a.runs, a.runpre, sl,
                                             [&](uint32_t key, bool v) { hm_lds_count(grid, key, v); });
     __syncthreads();

@@ -56,6 +56,7 @@ struct HmBuckets {
     const uint32_t* digit;
     const uint64_t* morton;     /* Morton index of the bucket at its zoom */
     const int32_t* slots;       /* last level: merge slot or -1 */
+    const uint4* desc;          /* [2*items] work-item descriptors (k_items) */
 };
 
 struct HmOut {
@@ -185,5 +186,10 @@ void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* part
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots);
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);
+/* per work item g of B (item size T keys): desc[2g] = (bucket, j, nitems, r0),
+ * desc[2g+1] = (rbase, nruns, first key, end key) -- replaces two dependent
+ * global binary searches per block with one 32-B load */
+void hm_launch_items(hipStream_t s, const HmBuckets& B, const uint32_t* runpre, uint32_t items, uint32_t T,
+                     uint4* desc);
 void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
                      const double* tab, int k);

@@ -7,12 +7,14 @@
  * two scale) -- reproduced exactly by construction.
  *
  * Row: two paths.
- *   fast  |lat| <= HM_LAT_FAST: Y = 0.5 - ln((1+s)/(1-s)) / (4 pi), s = sin(x),
- *         with sin and ln as fixed polynomials (no table, no libm).  |Y_fast -
- *         Y_ref| is bounded by HM_Y_EPS (calibrated on the CPU against the
- *         reference arithmetic by tests/test_math_host.py with a >= 8x margin),
- *         so if Y_fast * 2^z is more than HM_Y_EPS * 2^z away from an integer
- *         the floor is the reference's floor.
+ *   fast  |lat| <= HM_LAT_FAST: Y = 0.5 - sign(lat) g(90 - |lat|), g a
+ *         piecewise degree-5 polynomial on log-spaced intervals of the polar
+ *         distance (hm_ytab.h, tools/gen_ytab.py): ~20 VALU per point, no
+ *         transcendental.  |Y_fast - Y_ref| is bounded by HM_Y_EPS
+ *         (calibrated on the CPU against the reference arithmetic by
+ *         tests/test_math_host.py with a >= 8x margin), so if Y_fast * 2^z is
+ *         more than HM_Y_EPS * 2^z away from an integer the floor is the
+ *         reference's floor.
  *   exact everything else (guard band, |lat| > 85.06, non-finite input):
  *         the reference's literal evaluation chain, with tan/cos/log replaced
  *         by hm_glibc_{tan,cos,log}, a restatement of glibc 2.35's own
@@ -25,13 +27,10 @@
 #pragma once
 #include "hm_common.h"
 #include "hm_glibc_emul.h"
-#include "hm_logtab.h"
+#include "hm_ytab.h"
 #include "../../include/heatmap_amd.h"
 
 #define HM_PI 0x1.921fb54442d18p+1          /* math.pi */
-#define HM_DEG2RAD 0x1.1df46a2529d39p-6     /* pi/180 rounded */
-#define HM_INV4PI 0x1.45f306dc9c883p-4      /* 1/(4 pi) rounded */
-#define HM_LN2 0x1.62e42fefa39efp-1
 #define HM_INV360 0x1.6c16c16c16c17p-9      /* RN(1/360) */
 #define HM_LAT_FAST 85.06
 #define HM_Y_EPS 1.5e-13
@@ -41,50 +40,37 @@ HM_FN double hm_exp2i(int z)
     return hm_u2d((uint64_t)(1023 + z) << 52);   /* 2^z, 0 <= z <= 1023 */
 }
 
-/* ln(x), x positive normal: x = 2^e m, m in [1,2); interval i = top 7 mantissa
- * bits; ln m = -ln(invc_i) + log1p(m*invc_i - 1), |m*invc_i - 1| < 2^-8, log1p
- * by its Taylor series to r^8 (truncation < 2^-75).  Division-free, so the
- * host build and gfx950 produce identical bits.  tab = HM_LOGTAB_INIT. */
-HM_FN double hm_fast_ln(double x, const double* tab)
+/* g(90 - |lat|) = ln(tan(x) + sec(x)) / (2 pi) for |lat| <= HM_LAT_FAST
+ * (tab = HM_YTAB_INIT).  Interval = exponent and top HM_YTAB_K mantissa bits
+ * of d = 90 - |lat|; t = d - d_lo is exact.  The index is clamped, so any
+ * input (NaN, |lat| > 90) reads inside the table; callers reject those. */
+HM_FN double hm_fast_g(double lat, const double* tab)
 {
-    const uint64_t b = hm_d2u(x);
-    const int e = (int)(b >> 52) - 1023;
-    const uint32_t i = (uint32_t)(b >> 45) & 127u;
-    const double m = hm_u2d((b & 0x000fffffffffffffull) | 0x3ff0000000000000ull);
-    const double r = fma(m, tab[2 * i], -1.0);
-    double q = -0x1p-3;
-    q = fma(q, r, 0x1.2492492492492p-3);   /*  1/7 */
-    q = fma(q, r, -0x1.5555555555555p-3);  /* -1/6 */
-    q = fma(q, r, 0x1.999999999999ap-3);   /*  1/5 */
-    q = fma(q, r, -0x1p-2);                /* -1/4 */
-    q = fma(q, r, 0x1.5555555555555p-2);   /*  1/3 */
-    q = fma(q, r, -0x1p-1);                /* -1/2 */
-    const double l1p = fma(r * r, q, r);
-    return fma((double)e, HM_LN2, tab[2 * i + 1] + l1p);
+    const double d = 90.0 - fabs(lat);
+    const uint32_t hi = (uint32_t)(hm_d2u(d) >> 32);
+    uint32_t idx = (hi >> (20 - HM_YTAB_K)) - ((1023u + HM_YTAB_E0) << HM_YTAB_K);
+    idx = idx < (uint32_t)HM_YTAB_ROWS ? idx : (uint32_t)HM_YTAB_ROWS - 1u;
+    const double dlo = hm_u2d((uint64_t)(hi & ~((1u << (20 - HM_YTAB_K)) - 1u)) << 32);
+    const double t = d - dlo;
+    const double* c = tab + idx * HM_YTAB_STRIDE;
+    double p = c[5];
+    p = fma(p, t, c[4]);
+    p = fma(p, t, c[3]);
+    p = fma(p, t, c[2]);
+    p = fma(p, t, c[1]);
+    return fma(p, t, c[0]);
 }
 
-/* Y(lat) = 0.5 - (ln(1+s) - ln(1-s)) / (4 pi), s = sin(lat*pi/180), |lat| <= 85.06.
- * 1 +- s is exact where it could cancel (Sterbenz), so no division is needed. */
+/* Y(lat) of the fast path (for the CPU error-bound test). */
 HM_FN double hm_fast_Y(double lat, const double* tab)
 {
-    const double p = lat * HM_DEG2RAD;
-    const double p2 = p * p;
-    /* sin p = p + p^3 * S(p^2): Taylor to p^25 (|p| <= 1.4846: truncation < 1e-20) */
-    double s = 0x1.3f3ccdd165fa9p-84;        /*  1/25! */
-    s = fma(s, p2, -0x1.761b41316381ap-75);  /* -1/23! */
-    s = fma(s, p2, 0x1.71b8ef6dcf572p-66);   /*  1/21! */
-    s = fma(s, p2, -0x1.2f49b46814157p-57);  /* -1/19! */
-    s = fma(s, p2, 0x1.952c77030ad4ap-49);   /*  1/17! */
-    s = fma(s, p2, -0x1.ae7f3e733b81fp-41);  /* -1/15! */
-    s = fma(s, p2, 0x1.6124613a86d09p-33);   /*  1/13! */
-    s = fma(s, p2, -0x1.ae64567f544e4p-26);  /* -1/11! */
-    s = fma(s, p2, 0x1.71de3a556c734p-19);   /*  1/9!  */
-    s = fma(s, p2, -0x1.a01a01a01a01ap-13);  /* -1/7!  */
-    s = fma(s, p2, 0x1.1111111111111p-7);    /*  1/5!  */
-    s = fma(s, p2, -0x1.5555555555555p-3);   /* -1/3!  */
-    s = fma(p * p2, s, p);
-    const double L = hm_fast_ln(1.0 + s, tab) - hm_fast_ln(1.0 - s, tab);
-    return fma(-L, HM_INV4PI, 0.5);
+    return 0.5 - copysign(hm_fast_g(lat, tab), lat);
+}
+
+/* R = Y * 2^z, rounded once */
+HM_FN double hm_fast_R(double lat, double scale, const double* tab)
+{
+    return fma(-copysign(hm_fast_g(lat, tab), lat), scale, 0.5 * scale);
 }
 
 /* Reference chain, literally: tile.py:17 with CPython error semantics. */
@@ -114,7 +100,7 @@ HM_FN int hm_row(double lat, int zoom, int64_t* row, int* slow, const double* ta
 {
     if (fabs(lat) <= HM_LAT_FAST) {
         const double scale = hm_exp2i(zoom);
-        const double R = hm_fast_Y(lat, tab) * scale;
+        const double R = hm_fast_R(lat, scale, tab);
         const double f = floor(R);
         const double fr = R - f;
         const double g = HM_Y_EPS * scale;
@@ -160,25 +146,23 @@ HM_FN int hm_col(double lon, int zoom, int64_t* col)
 }
 
 /* Branch-free fast projection for the streaming kernels: returns 1 and the
- * tile when both fast paths are conclusive; 0 means "resolve this point with
- * hm_project_point" (guard band, |lat| > 85.06, non-finite input, huge lon).
- * Identical results to hm_project_point whenever it returns 1. */
-HM_FN int hm_project_fast(double lat, double lon, int zoom, int64_t* row, int64_t* col, const double* tab)
+ * tile (int32) when both fast paths are conclusive; 0 means "resolve this
+ * point with the exact chain" (guard band, |lat| > 85.06, non-finite input,
+ * |column| >= 2^31).  Identical results to hm_project_point whenever it
+ * returns 1.  Per-launch constants: scale = 2^z, kz = RN(1/360) 2^z (exact). */
+HM_FN int hm_project_fast(double lat, double lon, double scale, double kz, int32_t* row, int32_t* col,
+                          const double* tab)
 {
-    const double scale = hm_exp2i(zoom);
-    const double R = hm_fast_Y(lat, tab) * scale;
+    const double R = hm_fast_R(lat, scale, tab);
     const double f = floor(R);
-    const double fr = R - f;
     const double g = HM_Y_EPS * scale;
-    const double y = (lon + 180.0) * HM_INV360 * scale;
-    const double ay = fabs(y);
+    const double y = (lon + 180.0) * kz;
     const double f2 = floor(y);
-    const double fr2 = y - f2;
-    const double g2 = ay * 0x1p-49;
-    const int ok = (fabs(lat) <= HM_LAT_FAST) & (fr > g) & (fr < 1.0 - g) & (ay < 0x1p52) & (fr2 > g2) &
-                   (fr2 < 1.0 - g2);
-    *row = (int64_t)(ok ? f : 0.0);
-    *col = (int64_t)(ok ? f2 : 0.0);
+    const double g2 = scale * 0x1p-49;   /* >= |y| 2^-49 on the accepted range |y| < 2^z */
+    const int ok = (fabs(lat) <= HM_LAT_FAST) & (fabs((R - f) - 0.5) < 0.5 - g) & (fabs(y) < scale) &
+                   (fabs((y - f2) - 0.5) < 0.5 - g2);
+    *row = (int32_t)(ok ? f : 0.0);
+    *col = (int32_t)(ok ? f2 : 0.0);
     return ok;
 }
 

@@ -24,7 +24,7 @@ def host_math():
     out_dir = os.path.join(REPO, "tests", "host_math", "_build")
     out = os.path.join(out_dir, "libhm_host_math.so")
     deps = [src] + [os.path.join(REPO, "heatmap_amd", "csrc", f) for f in
-                    ("hm_project.h", "hm_glibc_emul.h", "hm_common.h")]
+                    ("hm_project.h", "hm_glibc_emul.h", "hm_common.h", "hm_ytab.h")]
     if not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps):
         os.makedirs(out_dir, exist_ok=True)
         subprocess.check_call(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fPIC", "-shared", "-w",
@@ -37,6 +37,9 @@ def host_math():
     L.hmh_fast_Y_maxerr.restype = ctypes.c_double
     L.hmh_glibc_check.argtypes = [ctypes.c_int, P(ctypes.c_double), ctypes.c_int64, P(ctypes.c_int64)]
     L.hmh_glibc_check.restype = ctypes.c_int64
+    L.hmh_project_fast.argtypes = [P(ctypes.c_double), P(ctypes.c_double), ctypes.c_int64, ctypes.c_int,
+                                   P(ctypes.c_int32), P(ctypes.c_int32), P(ctypes.c_uint8)]
+    L.hmh_project_fast.restype = ctypes.c_int64
     return L
 
 

@@ -10,7 +10,7 @@
 #include <math.h>
 #include "hm_project.h"
 
-static const double TAB[2 * HM_LOGTAB_N] = HM_LOGTAB_INIT;
+static const double TAB[HM_YTAB_ROWS * HM_YTAB_STRIDE] = HM_YTAB_INIT;
 
 int hmh_project(const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
                 int64_t* col, uint8_t* st, uint8_t* slow)
@@ -68,4 +68,18 @@ int64_t hmh_glibc_check(int fn, const double* x, int64_t n, int64_t* unsupported
     }
     *unsupported_count = un;
     return bad;
+}
+
+/* the streaming kernels' branch-free fast path (ok[i] = 1 where conclusive) */
+int64_t hmh_project_fast(const double* lat, const double* lon, int64_t n, int zoom, int32_t* row, int32_t* col,
+                         uint8_t* ok)
+{
+    const double scale = hm_exp2i(zoom);
+    const double kz = HM_INV360 * scale;
+    int64_t m = 0;
+    for (int64_t i = 0; i < n; i++) {
+        ok[i] = (uint8_t)hm_project_fast(lat[i], lon[i], scale, kz, &row[i], &col[i], TAB);
+        m += ok[i];
+    }
+    return m;
 }

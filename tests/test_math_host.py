@@ -74,6 +74,33 @@ def test_product_math_vs_oracle_random(host_math, kind):
             assert slow.mean() < 1e-4
 
 
+@pytest.mark.parametrize("kind", ["uniform", "hotspots", "skew", "kat"])
+def test_streaming_fast_path_vs_oracle(host_math, kind):
+    """hm_project_fast (k_project_partition's branch-free path): wherever it
+    claims a result, the result is the reference's; it declines only rarely."""
+    if kind == "kat":
+        d = np.load(os.path.join(GOLDEN, "projection_kat.npz"))
+        lat, lon, zs = d["lat"], d["lon"], sorted(set(int(z) for z in d["zoom"]) & set(range(0, 22)))
+    else:
+        lat, lon = synth.generate(kind, 1_000_000, seed=8)
+        zs = (0, 3, 11, 14, 18, 21)
+    P = ctypes.POINTER
+    for z in zs:
+        n = lat.size
+        row = np.zeros(n, np.int32)
+        col = np.zeros(n, np.int32)
+        ok = np.zeros(n, np.uint8)
+        m = host_math.hmh_project_fast(_dp(np.ascontiguousarray(lat)), _dp(np.ascontiguousarray(lon)), n, z,
+                                       row.ctypes.data_as(P(ctypes.c_int32)), col.ctypes.data_as(P(ctypes.c_int32)),
+                                       ok.ctypes.data_as(P(ctypes.c_uint8)))
+        ro, co, so, _ = oracle.project(lat, lon, z)
+        k = ok.astype(bool)
+        assert np.all(so[k] == 0)
+        assert np.array_equal(row[k], ro[k]) and np.array_equal(col[k], co[k]), z
+        if kind != "kat":
+            assert m >= n - max(50, n // 10000), (z, n - m)
+
+
 def test_fast_Y_error_bound(host_math):
     """HM_Y_EPS carries a >= 8x margin over the worst fast-path error seen."""
     rng = np.random.default_rng(1)
