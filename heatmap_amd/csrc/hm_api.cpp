@@ -78,9 +78,10 @@ static int hip_fail(hipError_t e, const char* what)
 
 /* named arena slots */
 enum {
-    B_KEYS_A, B_KEYS_B, B_RUNS_A, B_RUNS_B, B_RUNPRE_A, B_RUNPRE_B, B_NRUNS, B_NKEYS, B_VALS, B_PREFIX,
-    B_PARTIAL, B_TOTAL, B_ROOT, B_NRUNS_TOT, B_REDO_IDX, B_REDO_ROWS, B_REDO_COLS,
-    B_BK0, /* 4 levels x 8 arrays */
+    B_KEYS_A, B_KEYS_B, B_RUNS_SH, B_FLAT_A, B_FLAT_B, B_EXCL_A, B_EXCL_B, B_CNT, B_SHOFF, B_NR, B_NRUNS,
+    B_NKEYS, B_KEYBASE, B_VALS, B_PREFIX, B_PARTIAL, B_TOTAL, B_ROOT, B_REDO_IDX, B_REDO_ROWS, B_REDO_COLS,
+    B_RUNBASE0,
+    B_BK0 = B_RUNBASE0 + HM_MAX_LEVELS, /* 4 levels x 8 arrays */
     B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
     B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
     B_SLOTS = B_TOT0 + HM_MAX_LEVELS + 1,
@@ -308,12 +309,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     HmBuckets B[HM_MAX_LEVELS];
     memset(B, 0, sizeof(B));
     void* keys_cur = nullptr;
-    uint2* runs_cur = nullptr;
-    uint32_t* runpre_cur = nullptr;
+    HmRuns runs_cur = {nullptr, nullptr};
     int slot_k = 0; /* ping-pong A/B */
     uint32_t nslots = 0;
     int32_t* slots = nullptr;
     uint32_t* slot_bucket = nullptr;
+    uint64_t level_keys = 0;    /* keys entering level l >= 2 (global positions) */
 
     for (int l = 0; l < L; l++) {
         Level& V = lv[l];
@@ -324,7 +325,6 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         V.out16 = (l == L - 1);
         const int restbits = 2 * (Z - zs[l]);
         const uint64_t ntiles = (l == 0) ? tiles1 : lv[l - 1].items;
-        const uint64_t tile_keys = (l == 0) ? HM_T1 : HM_TN;
         if (V.nchildren > (uint64_t)HM_SCAN_LIMIT) return HM_E_NOMEM;
         /* run-counter shards: 32 unless the dense child space is large (then
          * per-child contention is low anyway); keeps counters <= 2^25 */
@@ -333,18 +333,16 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
         if (run_cap >= (1ull << 32)) return HM_E_NOMEM;
 
-        /* outputs of the level's partition kernel */
-        void* keys_out;
-        uint2* runs_out;
-        uint32_t* runpre_out;
+        /* outputs of the level's partition kernel: keys (level 1: per tile;
+         * levels >= 2: at the item's global positions) and sharded runs */
+        void* kout;
+        uint2* runs_sh;
         uint32_t* nruns;
-        ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, ntiles * tile_keys * (V.out16 ? 2 : 4), keys_out);
-        ENSURE(slot_k ? B_RUNS_B : B_RUNS_A, run_cap * sizeof(uint2), runs_out);
-        ENSURE(slot_k ? B_RUNPRE_B : B_RUNPRE_A, run_cap * sizeof(uint32_t), runpre_out);
+        const uint64_t nkeys_out = (l == 0) ? ntiles * (uint64_t)HM_T1 : level_keys;
+        ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
+        ENSURE(B_RUNS_SH, run_cap * sizeof(uint2), runs_sh);
         ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
         HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
-        uint32_t* nruns_tot;
-        ENSURE(B_NRUNS_TOT, V.nchildren * sizeof(uint32_t), nruns_tot);
 
         if (l == 0) {
             uint32_t* redo_idx = nullptr;
@@ -368,9 +366,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.tiles = tiles1;
             a.tile0 = 0;
             a.shard_bits = sb;
-            a.keys_out = keys_out;
+            a.keys_out = kout;
             a.nruns = nruns;
-            a.runs = runs_out;
+            a.runs = runs_sh;
             a.err_word = ctx->state + ST_ERR;
             a.exotic_word = ctx->state + ST_EXOTIC;
             a.slow_count = ctx->state + ST_SLOW;
@@ -434,40 +432,65 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             memset(&a, 0, sizeof(a));
             a.parent = B[l - 1];
             a.keys_in = (const uint32_t*)keys_cur;
-            a.runs_in = runs_cur;
-            a.runpre_in = runpre_cur;
+            a.in = runs_cur;
             a.dbits = V.dbits;
             a.restbits = restbits;
             a.shard_bits = sb;
-            a.keys_out = keys_out;
+            a.keys_out = kout;
             a.nruns_out = nruns;
-            a.runs_out = runs_out;
+            a.runs_out = runs_sh;
             hm_launch_partN(s, a, lv[l - 1].items, V.out16);
             HIPCHK(hipGetLastError());
         }
 
-        /* run scan + compaction into B_l */
-        uint32_t* nkeys;
-        uint64_t *vals, *prefix, *partial, *total;
-        ENSURE(B_NKEYS, V.nchildren * sizeof(uint32_t), nkeys);
+        /* run scan: sharded counters -> flat child-ordered runs + key prefix */
+        HmRsArgs ra;
+        memset(&ra, 0, sizeof(ra));
+        ra.nchildren = V.nchildren;
+        ra.dbits = V.dbits;
+        ra.shard_bits = sb;
+        ra.nruns = nruns;
+        ra.runs = runs_sh;
+        ra.parent_item_begin = parent_item_begin;
+        ra.item_keys = (l == L - 1) ? HM_TA : HM_TN;
+        uint64_t *partial, *tot;
+        ENSURE(B_SHOFF, (V.nchildren << sb) * sizeof(uint32_t), ra.shoff);
+        ENSURE(B_NR, V.nchildren * sizeof(uint64_t), ra.nr);
+        uint64_t* runbase;
+        ENSURE(B_RUNBASE0 + l, V.nchildren * sizeof(uint64_t), runbase);
+        ra.runbase = runbase;
+        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+        ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+        hm_launch_rs_count(s, ra);
+        hm_launch_scan(s, ra.nr, V.nchildren, partial, runbase, tot + 0);
+        HIPCHK(hipGetLastError());
+        unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+        HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const uint64_t nflat = down[0];
+        ra.nflat = nflat;
+        uint2* flat;
+        uint64_t* excl;
+        ENSURE(slot_k ? B_FLAT_B : B_FLAT_A, (nflat + 1) * sizeof(uint2), flat);
+        ENSURE(slot_k ? B_EXCL_B : B_EXCL_A, (nflat + 1) * sizeof(uint64_t), excl);
+        ENSURE(B_CNT, (nflat + 1) * sizeof(uint64_t), ra.cnt);
+        ra.flat = flat;
+        ra.excl = excl;
+        hm_launch_rs_copy(s, ra);
+        hm_launch_scan(s, ra.cnt, nflat, partial, excl, tot + 1);
+        ra.total_keys = tot + 1;
+        uint32_t* cnkeys;
+        uint32_t* ckeybase;
+        uint64_t *vals, *prefix;
+        ENSURE(B_NKEYS, V.nchildren * sizeof(uint32_t), cnkeys);
+        ENSURE(B_KEYBASE, V.nchildren * sizeof(uint32_t), ckeybase);
         ENSURE(B_VALS, V.nchildren * sizeof(uint64_t), vals);
         ENSURE(B_PREFIX, V.nchildren * sizeof(uint64_t), prefix);
-        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
-        ENSURE(B_TOTAL, sizeof(uint64_t), total);
-        HmScanArgs sa;
-        sa.nchildren = V.nchildren;
-        sa.dbits = V.dbits;
-        sa.shard_bits = sb;
-        sa.nruns = nruns;
-        sa.nruns_tot = nruns_tot;
-        sa.runs = runs_out;
-        sa.runpre = runpre_out;
-        sa.parent_item_begin = parent_item_begin;
-        sa.item_keys = (l == L - 1) ? HM_TA : HM_TN;
-        sa.nkeys = nkeys;
-        sa.vals = vals;
-        hm_launch_runscan(s, sa);
-        hm_launch_scan(s, vals, V.nchildren, partial, prefix, total);
+        ra.nkeys = cnkeys;
+        ra.keybase = ckeybase;
+        ra.vals = vals;
+        hm_launch_rs_keys(s, ra);
+        hm_launch_scan(s, vals, V.nchildren, partial, prefix, tot + 2);
         HIPCHK(hipGetLastError());
 
         /* B_l arrays: sized by nchildren (upper bound of |B_l|) */
@@ -480,18 +503,19 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_BK0 + l * 8 + 3, cap * 4, ca.out.item_begin);
         ENSURE(B_BK0 + l * 8 + 4, cap * 4, ca.out.digit);
         ENSURE(B_BK0 + l * 8 + 5, cap * 8, ca.out.morton);
+        ENSURE(B_BK0 + l * 8 + 6, cap * 4, ca.out.keybase);
         uint32_t* child_begin;
         ENSURE(B_CHILD0 + l, ((uint64_t)nparents + 1) * 4, child_begin);
         ca.nchildren = V.nchildren;
         ca.nparents = nparents;
         ca.dbits = V.dbits;
-        ca.shard_bits = sb;
         ca.vals = vals;
         ca.prefix = prefix;
-        ca.total = total;
-        ca.nkeys = nkeys;
-        ca.nruns = nruns_tot;
-        ca.parent_item_begin = parent_item_begin;
+        ca.total = tot + 2;
+        ca.nkeys = cnkeys;
+        ca.nr = ra.nr;
+        ca.runbase = runbase;
+        ca.keybase = ckeybase;
         ca.parent_morton = parent_morton;
         ca.child_begin = child_begin;
         if (l == L - 1) {
@@ -503,10 +527,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         }
         hm_launch_compact(s, ca);
         HIPCHK(hipGetLastError());
-        unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
-        HIPCHK(hipMemcpyAsync(down, total, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipMemcpyAsync(down, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
         if ((st = read_state(ctx))) return st;
-        const uint64_t tot_h = down[0];
+        level_keys = down[1];
+        const uint64_t tot_h = down[2];
         V.count = (uint32_t)(tot_h >> 32);
         V.items = (uint32_t)(tot_h & 0xFFFFFFFFull);
         if (l == L - 1) nslots = (uint32_t)(ctx->host_state[ST_NSLOTS] & 0xFFFFFFFFull);
@@ -516,21 +540,22 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         b.nkeys = ca.out.nkeys;
         b.nruns = ca.out.nruns;
         b.rbase = ca.out.rbase;
+        b.keybase = ca.out.keybase;
         b.item_begin = ca.out.item_begin;
         b.digit = ca.out.digit;
         b.morton = ca.out.morton;
         b.slots = (l == L - 1) ? slots : nullptr;
+        runs_cur.run = flat;
+        runs_cur.excl = excl;
         {
             uint4* desc;
             ENSURE(B_DESC0 + l, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
             b.desc = desc;
-            hm_launch_items(s, b, runpre_out, V.items, (l == L - 1) ? HM_TA : HM_TN, desc);
+            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? HM_TA : HM_TN, desc);
             HIPCHK(hipGetLastError());
         }
 
-        keys_cur = keys_out;
-        runs_cur = runs_out;
-        runpre_cur = runpre_out;
+        keys_cur = kout;
         parent_item_begin = ca.out.item_begin;
         parent_morton = ca.out.morton;
         nparents = V.count;
@@ -558,8 +583,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         memset(&a, 0, sizeof(a));
         a.B = B[l];
         a.keys = (const uint16_t*)keys_cur;
-        a.runs = runs_cur;
-        a.runpre = runpre_cur;
+        a.in = runs_cur;
         a.Z = Z;
         a.lg = Z - zb;
         a.totals = totals[l];
@@ -591,7 +615,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     if ((st = read_state(ctx))) return st;
     for (int i = 0; i + 1 < nev; i++) {
         float ms = 0;
-        hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
+        (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
         ctx->stage_us[i] = ms * 1000.0;
     }
     const unsigned long long nc = ctx->host_state[ST_CURSOR];

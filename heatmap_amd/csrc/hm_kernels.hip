@@ -269,10 +269,11 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 }
 
 /* ------------------------------------------------------------------------ */
-/* shared: locate a work item and stream its keys                            */
+/* work items and run streaming                                              */
 /* ------------------------------------------------------------------------ */
 
-__device__ __forceinline__ uint32_t hm_upper_bound(const uint32_t* a, uint32_t n, uint32_t v)
+template <typename T>
+__device__ __forceinline__ uint32_t hm_upper_bound(const T* a, uint32_t n, T v)
 {
     uint32_t lo = 0, hi = n;
     while (lo < hi) {
@@ -285,32 +286,21 @@ __device__ __forceinline__ uint32_t hm_upper_bound(const uint32_t* a, uint32_t n
     return lo;
 }
 
-struct HmItem {
-    uint32_t bucket;   /* compact parent bucket */
-    uint32_t j;        /* work item within the bucket */
-    uint32_t nitems;   /* work items of the bucket */
-    uint32_t a, b;     /* logical key range */
-    uint32_t rb, nr;   /* run list */
-    uint32_t r0;       /* first run overlapping [a, b) */
-};
-
-__device__ __forceinline__ HmItem hm_locate(const HmBuckets& B, uint32_t g, uint32_t T, const uint32_t* runpre)
+template <typename T>
+__device__ __forceinline__ uint32_t hm_lower_bound(const T* a, uint32_t n, T v)
 {
-    HmItem it;
-    it.bucket = hm_upper_bound(B.item_begin, B.count + 1, g) - 1;
-    it.j = g - B.item_begin[it.bucket];
-    it.nitems = B.item_begin[it.bucket + 1] - B.item_begin[it.bucket];
-    const uint32_t nk = B.nkeys[it.bucket];
-    it.a = it.j * T;
-    it.b = min(it.a + T, nk);
-    it.rb = B.rbase[it.bucket];
-    it.nr = B.nruns[it.bucket];
-    it.r0 = hm_upper_bound(runpre + it.rb, it.nr, it.a);
-    return it;
+    uint32_t lo = 0, hi = n;
+    while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (a[mid] < v)
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
 }
 
-/* one 32-B descriptor load (written by k_items) instead of hm_locate's
- * dependent binary searches */
+/* one 32-B descriptor load (written by k_items) per block */
 __device__ __forceinline__ HmItem hm_item(const HmBuckets& B, uint32_t g)
 {
     const uint4 d0 = B.desc[2 * g], d1 = B.desc[2 * g + 1];
@@ -319,139 +309,192 @@ __device__ __forceinline__ HmItem hm_item(const HmBuckets& B, uint32_t g)
     it.j = d0.y;
     it.nitems = d0.z;
     it.r0 = d0.w;
-    it.rb = d1.x;
-    it.nr = d1.y;
+    it.r1 = d1.x;
     it.a = d1.z;
     it.b = d1.w;
     return it;
 }
 
-__global__ __launch_bounds__(256) void k_items(HmBuckets B, const uint32_t* runpre, uint32_t items, uint32_t T,
-                                               uint4* desc)
+/* Descriptor of work item g (T keys per item): its bucket (binary search over
+ * item_begin), its logical positions [a, b) and the runs [r0, r1) that
+ * overlap them.  One thread per item; the searches of all items overlap. */
+__global__ __launch_bounds__(256) void k_items(HmBuckets B, HmRuns in, uint32_t items, uint32_t T, uint4* desc)
 {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= items) return;
-    const HmItem it = hm_locate(B, g, T, runpre);
-    desc[2 * g] = make_uint4(it.bucket, it.j, it.nitems, it.r0);
-    desc[2 * g + 1] = make_uint4(it.rb, it.nr, it.a, it.b);
+    const uint32_t bk = hm_upper_bound(B.item_begin, B.count + 1, g) - 1;
+    const uint32_t j = g - B.item_begin[bk];
+    const uint32_t nitems = B.item_begin[bk + 1] - B.item_begin[bk];
+    const uint64_t kb = B.keybase[bk], nk = B.nkeys[bk];
+    const uint64_t a = kb + (uint64_t)j * T;
+    const uint64_t b = kb + min((uint64_t)(j + 1) * T, nk);
+    const uint32_t rb = B.rbase[bk], nr = B.nruns[bk];
+    const uint32_t r0 = rb + hm_upper_bound(in.excl + rb, nr, a) - 1;   /* last run starting <= a */
+    const uint32_t r1 = rb + hm_lower_bound(in.excl + rb, nr, b);       /* first run starting >= b */
+    desc[2 * g] = make_uint4(bk, j, nitems, r0);
+    desc[2 * g + 1] = make_uint4(r1, 0u, (uint32_t)a, (uint32_t)b);
 }
 
-void hm_launch_items(hipStream_t s, const HmBuckets& B, const uint32_t* runpre, uint32_t items, uint32_t T,
-                     uint4* desc)
+void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc)
 {
-    if (items) hipLaunchKernelGGL(k_items, dim3((items + 255) / 256), dim3(256), 0, s, B, runpre, items, T, desc);
+    if (items) hipLaunchKernelGGL(k_items, dim3((items + 255) / 256), dim3(256), 0, s, B, in, items, T, desc);
 }
 
-/* Calls f(key, valid) for every key of the item's logical range [a, b).
- * Run descriptors are staged in LDS HM_RCHUNK at a time.  Each wave owns a
- * contiguous span of logical positions and walks it 64 at a time (lane l takes
- * position q + l, so loads coalesce within a run); each lane keeps a monotone
- * run cursor that advances linearly (runs hold >= 1 key) and falls back to a
- * binary search after HM_WALK steps.  HM_SU positions per lane are resolved
- * before any load is consumed.  Block-uniform; every thread calls. */
-#define HM_RCHUNK 1024
+/* Run chunk staged in LDS: long runs' aligned bodies (in 16-B vectors) and
+ * their exclusive prefix, short pieces (short runs, heads and tails). */
+template <int RCH>
+struct HmRunLds {
+    uint2 body[RCH];            /* (first vector index, vectors) */
+    uint32_t pre[RCH + 1];      /* exclusive prefix of body vectors */
+    uint2 piece[2 * RCH];       /* (first key index, keys), < HM_LONG_RUN keys each */
+    uint32_t nbody, npiece;
+};
+
+template <typename InT, typename F>
+__device__ __forceinline__ void hm_apply_vec(const uint4& x, bool v, F& f)
+{
+    if (sizeof(InT) == 4) {
+        f(x.x, v);
+        f(x.y, v);
+        f(x.z, v);
+        f(x.w, v);
+    } else {
+        f(x.x & 0xFFFFu, v);
+        f(x.x >> 16, v);
+        f(x.y & 0xFFFFu, v);
+        f(x.y >> 16, v);
+        f(x.z & 0xFFFFu, v);
+        f(x.z >> 16, v);
+        f(x.w & 0xFFFFu, v);
+        f(x.w >> 16, v);
+    }
+}
+
+/* wave-aggregated append of one entry per flagged lane to list[base + n++] */
+__device__ __forceinline__ void hm_lds_append(uint2* list, uint32_t* n, bool flag, uint2 e)
+{
+    const uint64_t m = __ballot(flag);
+    if (m == 0) return;
+    const int leader = __ffsll((unsigned long long)m) - 1;
+    uint32_t b = 0;
+    if (hm_lane() == leader) b = atomicAdd(n, (uint32_t)__popcll(m));
+    b = __builtin_amdgcn_readlane(b, leader);
+    if (flag) list[b + hm_mbcnt(m)] = e;
+}
+
+/* Calls f(key, valid) for every key at the item's logical positions [a, b),
+ * in no particular order (the consumers count or re-sort).  The item's runs
+ * are staged RCH at a time and clipped to [a, b).  The 16-B-aligned bodies of
+ * runs with >= HM_LONG_RUN keys form one flat vector space, split into
+ * contiguous per-wave spans; a lane keeps HM_SU 16-B loads in flight and
+ * finds each vector's run by walking a monotone cursor over the body prefix.
+ * Short runs and the bodies' unaligned heads and tails go one lane each (8
+ * loads in flight).  Block-uniform: every thread calls; f is also called
+ * under divergence and must use ballots of the active lanes only. */
 #ifndef HM_SU
 #define HM_SU 4
 #endif
-#define HM_WALK 4
-struct HmStreamLds {
-    uint32_t end[HM_RCHUNK];
-    uint32_t src[HM_RCHUNK];
-};
-
-__device__ __forceinline__ uint32_t hm_run_of(const HmStreamLds& L, uint32_t ri, uint32_t rc, uint32_t p)
-{
-#pragma unroll
-    for (int k = 0; k < HM_WALK; k++) {
-        if (L.end[ri] > p) return ri;
-        ri++;
-    }
-    uint32_t lo = ri, hi = rc - 1;
-    while (lo < hi) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (L.end[mid] <= p)
-            lo = mid + 1;
-        else
-            hi = mid;
-    }
-    return lo;
-}
-
-template <typename InT, int THREADS, typename F>
-__device__ __forceinline__ void hm_stream_item(const HmItem& it, const InT* __restrict__ keys,
-                                               const uint2* __restrict__ runs, const uint32_t* __restrict__ runpre,
-                                               HmStreamLds& L, F f)
+template <typename InT, int THREADS, int RCH, typename F>
+__device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __restrict__ keys, const HmRuns& in,
+                                               HmRunLds<RCH>& L, uint32_t* scr, F f)
 {
     constexpr int NW = THREADS / 64;
+    constexpr uint32_t V = 16 / sizeof(InT);   /* keys per 16-B vector */
     const int tid = threadIdx.x;
-    const int w = tid >> 6;
     const int lane = tid & 63;
-    uint32_t r = it.r0;
-    uint32_t pos = it.a;
-    while (pos < it.b) {
-        const uint32_t rc = min((uint32_t)HM_RCHUNK, it.nr - r);
-        if (rc == 0) break;
-        for (uint32_t i = tid; i < rc; i += THREADS) {
-            const uint2 run = runs[it.rb + r + i];
-            const uint32_t re = runpre[it.rb + r + i];
-            L.end[i] = re;
-            L.src[i] = run.x + run.y - re;     /* key address = src + logical position */
+    const int w = tid >> 6;
+    const uint4* kv = (const uint4*)keys;
+    for (uint32_t rc = it.r0; rc < it.r1; rc += RCH) {
+        const uint32_t m = min((uint32_t)RCH, it.r1 - rc);
+        if (tid == 0) {
+            L.nbody = 0;
+            L.npiece = 0;
         }
         __syncthreads();
-        const uint32_t cend = min(L.end[rc - 1], it.b);
-        /* wave spans: multiples of 64*HM_SU positions */
-        const uint32_t n = cend - pos;
-        const uint32_t step = 64 * HM_SU;
-        const uint32_t span = ((n + NW - 1) / NW + step - 1) / step * step;
-        const uint32_t ws = pos + min(n, span * w);
-        const uint32_t we = pos + min(n, span * (w + 1));
-        uint32_t ri = 0;
-        if (ws < we) {
-            uint32_t lo = 0, hi = rc - 1;
-            while (lo < hi) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (L.end[mid] <= ws)
-                    lo = mid + 1;
-                else
-                    hi = mid;
+        for (uint32_t i0 = 0; i0 < m; i0 += THREADS) {
+            const uint32_t i = i0 + tid;
+            uint32_t cnt = 0, src = 0;
+            if (i < m) {
+                const uint2 run = in.run[rc + i];
+                const uint64_t s = in.excl[rc + i];
+                const uint64_t e = s + run.y;
+                const uint64_t s2 = max(s, (uint64_t)it.a), e2 = min(e, (uint64_t)it.b);
+                cnt = e2 > s2 ? (uint32_t)(e2 - s2) : 0u;
+                src = run.x + (uint32_t)(s2 - s);
             }
-            ri = lo;
+            const uint32_t head = min(cnt, (V - (src & (V - 1))) & (V - 1));
+            const uint32_t nv = (cnt - head) / V;
+            const bool lg = cnt >= HM_LONG_RUN && nv > 0;
+            const uint32_t tail = lg ? cnt - head - nv * V : 0u;
+            hm_lds_append(L.body, &L.nbody, lg, make_uint2((src + head) / V, nv));
+            hm_lds_append(L.piece, &L.npiece, lg ? head > 0 : cnt > 0, make_uint2(src, lg ? head : cnt));
+            hm_lds_append(L.piece, &L.npiece, tail > 0, make_uint2(src + head + nv * V, tail));
         }
-        for (uint32_t q = ws; q < we; q += step) {
-            uint32_t key[HM_SU];
-            bool v[HM_SU];
+        __syncthreads();
+        const uint32_t nb = L.nbody, np = L.npiece;
+        /* exclusive prefix of the body lengths */
+        for (uint32_t i0 = 0; i0 < nb; i0 += THREADS) {
+            const uint32_t i = i0 + tid;
+            const uint32_t x = i < nb ? L.body[i].y : 0u;
+            uint32_t tot;
+            const uint32_t ex = hm_block_excl_scan<THREADS>(x, scr, &tot);
+            const uint32_t carry = i0 ? L.pre[i0] : 0u;
+            if (i < nb) L.pre[i] = carry + ex;
+            if (tid == 0) L.pre[min(i0 + THREADS, nb)] = carry + tot;
+            __syncthreads();
+        }
+        if (nb == 0 && tid == 0) L.pre[0] = 0;
+        __syncthreads();
+        const uint32_t total = L.pre[nb];
+        /* bodies: contiguous wave spans of the flat vector space */
+        const uint32_t span = ((total + NW - 1) / NW + 63) & ~63u;
+        const uint32_t vb = min(total, span * w), ve = min(total, vb + span);
+        if (vb < ve) {
+            uint32_t r = hm_upper_bound(L.pre, nb + 1, vb) - 1;
+            for (uint32_t v0 = vb; v0 < ve; v0 += 64 * HM_SU) {
+                uint4 x[HM_SU];
+                bool ok[HM_SU];
 #pragma unroll
-            for (int u = 0; u < HM_SU; u++) {
-                const uint32_t p = q + u * 64 + lane;
-                v[u] = p < we;
-                key[u] = 0;
-                if (v[u]) {
-                    ri = hm_run_of(L, ri, rc, p);
-                    key[u] = (uint32_t)keys[L.src[ri] + p];
+                for (int u = 0; u < HM_SU; u++) {
+                    const uint32_t v = v0 + u * 64 + lane;
+                    ok[u] = v < ve;
+                    x[u] = make_uint4(0, 0, 0, 0);
+                    if (ok[u]) {
+                        while (L.pre[r + 1] <= v) r++;
+                        x[u] = kv[L.body[r].x + (v - L.pre[r])];
+                    }
                 }
-            }
 #pragma unroll
-            for (int u = 0; u < HM_SU; u++) f(key[u], v[u]);
+                for (int u = 0; u < HM_SU; u++) hm_apply_vec<InT>(x[u], ok[u], f);
+            }
+        }
+        /* pieces: one lane each */
+        for (uint32_t q = tid; q < np; q += THREADS) {
+            const uint2 r = L.piece[q];
+            for (uint32_t k0 = 0; k0 < r.y; k0 += 8) {
+                uint32_t kk[8];
+#pragma unroll
+                for (int u = 0; u < 8; u++) kk[u] = (k0 + u < r.y) ? (uint32_t)keys[r.x + k0 + u] : 0u;
+#pragma unroll
+                for (int u = 0; u < 8; u++) f(kk[u], k0 + u < r.y);
+            }
         }
         __syncthreads();
-        pos = cend;
-        r += rc;
     }
 }
 
 /* ------------------------------------------------------------------------ */
-/* levels >= 2: gather a parent's runs, counting sort by the next digit      */
+/* levels >= 2: stream a parent item's runs, counting sort by the next digit */
 /* ------------------------------------------------------------------------ */
 
 template <typename OutT>
 __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
 {
-    __shared__ uint32_t stage_in[HM_TN];
-    __shared__ OutT stage_out[HM_TN];
+    __shared__ uint32_t stage[HM_TN];      /* streamed keys, then the sorted output (OutT) */
     __shared__ uint32_t cur[HM_MAX_FN];
     __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
     __shared__ uint32_t scnt;
-    __shared__ HmStreamLds sl;
+    __shared__ HmRunLds<512> L;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
@@ -459,17 +502,19 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     __syncthreads();
     const HmItem it = hm_item(a.parent, blockIdx.x);
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
-    hm_stream_item<uint32_t, HM_PN_THREADS>(it, a.keys_in, a.runs_in, a.runpre_in, sl, [&](uint32_t key, bool v) {
-        const uint32_t d = key >> a.restbits;
-        hm_lds_count(cur, d, v);
+    hm_stream_runs<uint32_t, HM_PN_THREADS, 512>(it, a.keys_in, a.in, L, scr, [&](uint32_t key, bool v) {
+        hm_lds_count(cur, key >> a.restbits, v);
         const uint64_t vm = __ballot(v);
-        uint32_t wp = 0;
-        if (hm_lane() == 0) wp = atomicAdd(&scnt, (uint32_t)__popcll(vm));
-        wp = __shfl(wp, 0, 64);
-        if (v) stage_in[wp + hm_mbcnt(vm)] = key;
+        if (vm) {
+            const int leader = __ffsll((unsigned long long)vm) - 1;
+            uint32_t wp = 0;
+            if (hm_lane() == leader) wp = atomicAdd(&scnt, (uint32_t)__popcll(vm));
+            wp = __builtin_amdgcn_readlane(wp, leader);
+            if (v) stage[wp + hm_mbcnt(vm)] = key;
+        }
     });
     __syncthreads();
-    const uint32_t total = scnt;
+    const uint32_t total = it.b - it.a;
     constexpr int PER = HM_MAX_FN / HM_PN_THREADS;
     uint32_t cnt[PER];
     uint32_t s = 0;
@@ -482,7 +527,6 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     uint32_t tot2;
     uint32_t off = hm_block_excl_scan<HM_PN_THREADS>(s, scr, &tot2);
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
-    const uint64_t gtile = blockIdx.x;
     const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
     const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
     uint32_t idx[PER];
@@ -503,152 +547,128 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
             cur[d] = offq[q];
             if (cnt[q]) {
                 const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
-                a.runs_out[rb + sh * cap + idx[q]] = make_uint2((uint32_t)(gtile * HM_TN) + offq[q], cnt[q]);
+                a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);
             }
         }
     }
-    __syncthreads();
     constexpr int KPT = HM_TN / HM_PN_THREADS;
+    uint32_t kv[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+        const uint32_t i = k * HM_PN_THREADS + tid;
+        kv[k] = i < total ? stage[i] : 0u;
+    }
+    __syncthreads();
+    OutT* so = (OutT*)stage;
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
         const uint32_t i = k * HM_PN_THREADS + tid;
         const bool v = i < total;
-        const uint32_t key = v ? stage_in[i] : 0u;
-        const uint32_t d = key >> a.restbits;
-        const uint32_t pos = hm_lds_claim(cur, d, v);
-        if (v) stage_out[pos] = (OutT)(key & restmask);
+        const uint32_t pos = hm_lds_claim(cur, kv[k] >> a.restbits, v);
+        if (v) so[pos] = (OutT)(kv[k] & restmask);
     }
     __syncthreads();
-    OutT* out = (OutT*)a.keys_out + gtile * HM_TN;
-    for (uint32_t i = tid; i < total; i += HM_PN_THREADS) out[i] = stage_out[i];
+    OutT* out = (OutT*)a.keys_out + it.a;
+    for (uint32_t i = tid; i < total; i += HM_PN_THREADS) out[i] = so[i];
 }
 
 /* ------------------------------------------------------------------------ */
-/* run scan + compaction of dense children into a Morton-ordered bucket list */
+/* run scan: sharded run counters -> one flat, child-ordered run list        */
 /* ------------------------------------------------------------------------ */
 
-/* one wave per dense child c = p*F + d: inclusive prefix of its run counts,
- * key total, and the packed scan value (1 << 32 | work items) */
-/* Per dense child c = p*F + d: compact the S run-counter shards into one list,
- * write the inclusive prefix of its run counts, its key total and the packed
- * scan value (1 << 32 | work items).  One block per child (BLOCK = true, few
- * children with up to ~1e5 runs each, i.e. level 1) or one wave per child. */
-template <bool BLOCK>
-__global__ __launch_bounds__(256) void k_runscan(HmScanArgs a)
+/* per child: exclusive shard offsets within the child, and its run total */
+__global__ __launch_bounds__(256) void k_rs_count(HmRsArgs a)
 {
-    constexpr int NW = 4;
-    __shared__ uint32_t wsum[NW + 1];
-    const int lane = hm_lane();
-    const int w = threadIdx.x >> 6;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
     const uint32_t S = 1u << a.shard_bits;
-    const uint64_t first = BLOCK ? blockIdx.x : (uint64_t)blockIdx.x * NW + w;
-    const uint64_t stride = BLOCK ? gridDim.x : (uint64_t)gridDim.x * NW;
-    for (uint64_t c = first; c < a.nchildren; c += stride) {
-        /* shard counts -> exclusive offsets (S <= 64), every wave computes them */
-        const uint32_t ns = lane < (int)S ? a.nruns[(c << a.shard_bits) + lane] : 0u;
-        const uint32_t inc = hm_wave_incl_scan(ns);
-        const uint32_t nr = __shfl(inc, 63, 64);
-        if (nr == 0) {
-            if (threadIdx.x == (BLOCK ? 0 : (unsigned)w * 64)) {
-                a.nkeys[c] = 0;
-                a.vals[c] = 0;
-                a.nruns_tot[c] = 0;
-            }
-            continue;
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < a.nchildren; c += stride) {
+        uint32_t acc = 0;
+        for (uint32_t s = 0; s < S; s++) {
+            const uint64_t k = (c << a.shard_bits) + s;
+            const uint32_t n = a.nruns[k];
+            a.shoff[k] = acc;
+            acc += n;
         }
-        const uint64_t p = c >> a.dbits;
-        const uint64_t d = c & ((1ull << a.dbits) - 1);
-        const uint32_t t0 = a.parent_item_begin[p];
-        const uint32_t tp = a.parent_item_begin[p + 1] - t0;
-        const uint64_t rb = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits);
-        const uint32_t cap = (tp + S - 1) >> a.shard_bits;
-        const uint32_t nthr = BLOCK ? blockDim.x : 64;
-        const uint32_t t = BLOCK ? threadIdx.x : (uint32_t)lane;
-        /* compact shards 1..S-1 down behind shard 0 (in place, forward copy,
-         * shard by shard; a shard's destination never reaches a later shard) */
-        for (uint32_t sh = 1; sh < S; sh++) {
-            const uint32_t n_s = __shfl(ns, sh, 64);
-            const uint32_t o_s = __shfl(inc, sh, 64) - n_s;
-            if (n_s == 0 || o_s == sh * cap) continue;
-            for (uint32_t i0 = 0; i0 < n_s; i0 += nthr) {
-                const uint32_t i = i0 + t;
-                uint2 v = make_uint2(0, 0);
-                if (i < n_s) v = a.runs[rb + (uint64_t)sh * cap + i];
-                if (BLOCK)
-                    __syncthreads();
-                else
-                    __builtin_amdgcn_wave_barrier();
-                if (i < n_s) a.runs[rb + o_s + i] = v;
-            }
-            if (BLOCK) __syncthreads();
-        }
-        if (BLOCK) {
-            __threadfence_block();
-            __syncthreads();
-        }
-        /* inclusive prefix of the run counts: 8 consecutive runs per thread */
-        uint32_t carry = 0;
-        for (uint32_t i0 = 0; i0 < nr; i0 += 8 * nthr) {
-            const uint32_t b = i0 + t * 8;
-            uint32_t v[8];
-            uint32_t loc = 0;
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                v[q] = (b + q < nr) ? a.runs[rb + b + q].y : 0u;
-                loc += v[q];
-            }
-            uint32_t excl, tot;
-            if (BLOCK) {
-                const uint32_t winc = hm_wave_incl_scan(loc);
-                if (lane == 63) wsum[w] = winc;
-                __syncthreads();
-                if (threadIdx.x == 0) {
-                    uint32_t acc = 0;
-                    for (int k = 0; k < NW; k++) {
-                        const uint32_t x = wsum[k];
-                        wsum[k] = acc;
-                        acc += x;
-                    }
-                    wsum[NW] = acc;
-                }
-                __syncthreads();
-                excl = wsum[w] + winc - loc;
-                tot = wsum[NW];
-                __syncthreads();
-            } else {
-                const uint32_t winc = hm_wave_incl_scan(loc);
-                excl = winc - loc;
-                tot = __shfl(winc, 63, 64);
-            }
-            uint32_t acc = carry + excl;
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                acc += v[q];
-                if (b + q < nr) a.runpre[rb + b + q] = acc;
-            }
-            carry += tot;
-        }
-        if (t == 0) {
-            a.nkeys[c] = carry;
-            a.nruns_tot[c] = nr;
-            const uint64_t items = (carry + a.item_keys - 1) / a.item_keys;
-            a.vals[c] = (1ull << 32) | items;
-        }
+        a.nr[c] = acc;
     }
 }
+
+/* copy shard (c, s) of the sharded layout to flat[runbase[c] + shoff .. ) */
+__device__ __forceinline__ void hm_rs_copy_shard(const HmRsArgs& a, uint64_t c, uint32_t s, uint32_t t, uint32_t nt)
+{
+    const uint64_t k = (c << a.shard_bits) + s;
+    const uint32_t n = a.nruns[k];
+    if (n == 0) return;
+    const uint64_t p = c >> a.dbits;
+    const uint64_t d = c & ((1ull << a.dbits) - 1);
+    const uint32_t t0 = a.parent_item_begin[p];
+    const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+    const uint32_t cap = (tp + (1u << a.shard_bits) - 1) >> a.shard_bits;
+    const uint64_t src = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits) + (uint64_t)s * cap;
+    const uint64_t dst = a.runbase[c] + a.shoff[k];
+    for (uint32_t i = t; i < n; i += nt) {
+        const uint2 r = a.runs[src + i];
+        a.flat[dst + i] = r;
+        a.cnt[dst + i] = r.y;
+    }
+}
+
+/* few children (level 1): one block per (child, shard) */
+__global__ __launch_bounds__(256) void k_rs_copy_pairs(HmRsArgs a)
+{
+    const uint64_t pair = blockIdx.x;
+    hm_rs_copy_shard(a, pair >> a.shard_bits, (uint32_t)(pair & ((1u << a.shard_bits) - 1)), threadIdx.x, 256);
+}
+
+/* many children: one wave per child */
+__global__ __launch_bounds__(256) void k_rs_copy_children(HmRsArgs a)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 4;
+    const uint32_t S = 1u << a.shard_bits;
+    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < a.nchildren; c += stride) {
+        if (a.nr[c] == 0) continue;
+        for (uint32_t s = 0; s < S; s++) hm_rs_copy_shard(a, c, s, threadIdx.x & 63, 64);
+    }
+}
+
+/* per child: global key range of its runs and work items of the next stage */
+__global__ __launch_bounds__(256) void k_rs_keys(HmRsArgs a)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < a.nchildren; c += stride) {
+        const uint64_t nr = a.nr[c];
+        if (nr == 0) {
+            a.nkeys[c] = 0;
+            a.keybase[c] = 0;
+            a.vals[c] = 0;
+            continue;
+        }
+        const uint64_t rb = a.runbase[c];
+        const uint64_t kb = a.excl[rb];
+        const uint64_t ke = (rb + nr < a.nflat) ? a.excl[rb + nr] : *a.total_keys;
+        const uint32_t nk = (uint32_t)(ke - kb);
+        a.nkeys[c] = nk;
+        a.keybase[c] = (uint32_t)kb;
+        a.vals[c] = (1ull << 32) | (uint64_t)((nk + a.item_keys - 1) / a.item_keys);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* device-wide exclusive scan of u64 (any length)                            */
+/* ------------------------------------------------------------------------ */
 
 #define HM_SCAN_ITEMS 4096
 #define HM_SCAN_THREADS 256
+#define HM_SCAN_MAXB 4096
 
-__global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_reduce(const uint64_t* v, uint64_t n, uint64_t* partial)
+__global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_reduce(const uint64_t* v, uint64_t n, uint64_t chunk,
+                                                                 uint64_t* partial)
 {
     __shared__ uint64_t red[HM_SCAN_THREADS / 64];
-    const uint64_t b0 = (uint64_t)blockIdx.x * HM_SCAN_ITEMS;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t b1 = min(b0 + chunk, n);
     uint64_t s = 0;
-    for (int k = threadIdx.x; k < HM_SCAN_ITEMS; k += HM_SCAN_THREADS) {
-        const uint64_t i = b0 + k;
-        if (i < n) s += v[i];
-    }
+    for (uint64_t i = b0 + threadIdx.x; i < b1; i += HM_SCAN_THREADS) s += v[i];
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
     if (hm_lane() == 0) red[threadIdx.x >> 6] = s;
@@ -697,40 +717,50 @@ __global__ __launch_bounds__(1024) void k_scan_partials(uint64_t* partial, uint3
     if (tid == 0) *total = ws[16];
 }
 
-__global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v, uint64_t n, const uint64_t* partial,
-                                                               uint64_t* out)
+/* block b: its chunk in sub-chunks of HM_SCAN_ITEMS, carrying the prefix */
+__global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v, uint64_t n, uint64_t chunk,
+                                                               const uint64_t* partial, uint64_t* out)
 {
     __shared__ uint64_t ws[HM_SCAN_THREADS / 64 + 1];
     constexpr int PER = HM_SCAN_ITEMS / HM_SCAN_THREADS;
-    const uint64_t b0 = (uint64_t)blockIdx.x * HM_SCAN_ITEMS + (uint64_t)threadIdx.x * PER;
-    uint64_t x[PER];
-    uint64_t s = 0;
+    const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
+    const uint64_t c1 = min(c0 + chunk, n);
+    uint64_t carry = partial[blockIdx.x];
+    for (uint64_t s0 = c0; s0 < c1; s0 += HM_SCAN_ITEMS) {
+        const uint64_t b0 = s0 + (uint64_t)threadIdx.x * PER;
+        uint64_t x[PER];
+        uint64_t s = 0;
 #pragma unroll
-    for (int q = 0; q < PER; q++) {
-        x[q] = (b0 + q < n) ? v[b0 + q] : 0;
-        s += x[q];
-    }
-    const uint64_t inc = hm_wave_incl_scan64(s);
-    const int w = threadIdx.x >> 6;
-    if (hm_lane() == 63) ws[w] = inc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        uint64_t acc = 0;
-        for (int k = 0; k < HM_SCAN_THREADS / 64; k++) {
-            const uint64_t t = ws[k];
-            ws[k] = acc;
-            acc += t;
+        for (int q = 0; q < PER; q++) {
+            x[q] = (b0 + q < c1) ? v[b0 + q] : 0;
+            s += x[q];
         }
-    }
-    __syncthreads();
-    uint64_t off = partial[blockIdx.x] + ws[w] + inc - s;
+        const uint64_t inc = hm_wave_incl_scan64(s);
+        const int w = threadIdx.x >> 6;
+        if (hm_lane() == 63) ws[w] = inc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint64_t acc = 0;
+            for (int k = 0; k < HM_SCAN_THREADS / 64; k++) {
+                const uint64_t t = ws[k];
+                ws[k] = acc;
+                acc += t;
+            }
+            ws[HM_SCAN_THREADS / 64] = acc;
+        }
+        __syncthreads();
+        uint64_t off = carry + ws[w] + inc - s;
 #pragma unroll
-    for (int q = 0; q < PER; q++) {
-        if (b0 + q < n) out[b0 + q] = off;
-        off += x[q];
+        for (int q = 0; q < PER; q++) {
+            if (b0 + q < c1) out[b0 + q] = off;
+            off += x[q];
+        }
+        carry += ws[HM_SCAN_THREADS / 64];
+        __syncthreads();
     }
 }
 
+/* compaction of non-empty children into the Morton-ordered bucket list B_l */
 __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -745,11 +775,10 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
         const uint64_t d = c & (F - 1);
         if (d == 0) a.child_begin[p] = idx;
         if (a.vals[c] >> 32) {
-            const uint32_t t0 = a.parent_item_begin[p];
-            const uint32_t tp = a.parent_item_begin[p + 1] - t0;
             a.out.nkeys[idx] = a.nkeys[c];
-            a.out.nruns[idx] = a.nruns[c];
-            a.out.rbase[idx] = (uint32_t)hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits);
+            a.out.nruns[idx] = (uint32_t)a.nr[c];
+            a.out.rbase[idx] = (uint32_t)a.runbase[c];
+            a.out.keybase[idx] = a.keybase[c];
             a.out.item_begin[idx] = ib;
             a.out.digit[idx] = (uint32_t)d;
             a.out.morton[idx] = (a.parent_morton[p] << a.dbits) | d;
@@ -769,7 +798,6 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
         a.child_begin[a.nparents] = count;
     }
 }
-
 /* ------------------------------------------------------------------------ */
 /* emission helpers                                                          */
 /* ------------------------------------------------------------------------ */
@@ -924,14 +952,14 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate(HmAggArgs a)
     __shared__ uint32_t grid[HM_AG_CELLS];
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
-    __shared__ HmStreamLds sl;
+    __shared__ HmRunLds<512> L;
     const int tid = threadIdx.x;
     const uint32_t ncell = 1u << (2 * a.lg);
     for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
     const HmItem it = hm_item(a.B, blockIdx.x);
-    hm_stream_item<uint16_t, HM_AG_THREADS>(it, a.keys, a.runs, a.runpre, sl,
-                                            [&](uint32_t key, bool v) { hm_lds_count(grid, key, v); });
+    hm_stream_runs<uint16_t, HM_AG_THREADS, 512>(it, a.keys, a.in, L, scr,
+                                                 [&](uint32_t key, bool v) { hm_lds_count(grid, key, v); });
     __syncthreads();
     if (it.nitems == 1) {
         const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[it.bucket], a.out, scr, &sbase);
@@ -948,7 +976,6 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate(HmAggArgs a)
         if (hm_lane() == 0 && s) atomicAdd(&a.totals[it.bucket], (unsigned long long)s);
     }
 }
-
 __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
 {
     __shared__ uint32_t grid[HM_AG_CELLS];
@@ -1055,42 +1082,55 @@ void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n)
     hipLaunchKernelGGL(k_redo, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }
 
-void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool out16)
+void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16)
 {
-    if (tiles == 0) return;
+    if (items == 0) return;
     if (out16)
-        hipLaunchKernelGGL(k_partition<uint16_t>, dim3(tiles), dim3(HM_PN_THREADS), 0, s, a);
+        hipLaunchKernelGGL(k_partition<uint16_t>, dim3(items), dim3(HM_PN_THREADS), 0, s, a);
     else
-        hipLaunchKernelGGL(k_partition<uint32_t>, dim3(tiles), dim3(HM_PN_THREADS), 0, s, a);
+        hipLaunchKernelGGL(k_partition<uint32_t>, dim3(items), dim3(HM_PN_THREADS), 0, s, a);
 }
 
-void hm_launch_runscan(hipStream_t s, const HmScanArgs& a)
+static unsigned hm_grid(uint64_t n, unsigned per, unsigned cap)
 {
-    if (a.nchildren <= 8192) {
-        const uint64_t blocks = a.nchildren ? a.nchildren : 1;
-        hipLaunchKernelGGL(k_runscan<true>, dim3((unsigned)blocks), dim3(256), 0, s, a);
-        return;
-    }
-    uint64_t blocks = (a.nchildren + 3) / 4;
-    if (blocks > 16384) blocks = 16384;
-    hipLaunchKernelGGL(k_runscan<false>, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    uint64_t b = (n + per - 1) / per;
+    if (b > cap) b = cap;
+    return (unsigned)(b ? b : 1);
+}
+
+void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a)
+{
+    hipLaunchKernelGGL(k_rs_count, dim3(hm_grid(a.nchildren, 256, 16384)), dim3(256), 0, s, a);
+}
+
+void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a)
+{
+    const uint64_t pairs = a.nchildren << a.shard_bits;
+    if (a.nchildren <= 8192 && pairs <= (1u << 20))
+        hipLaunchKernelGGL(k_rs_copy_pairs, dim3((unsigned)pairs), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_rs_copy_children, dim3(hm_grid(a.nchildren, 4, 16384)), dim3(256), 0, s, a);
+}
+
+void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a)
+{
+    hipLaunchKernelGGL(k_rs_keys, dim3(hm_grid(a.nchildren, 256, 16384)), dim3(256), 0, s, a);
 }
 
 void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total)
 {
-    const uint32_t nb = (uint32_t)((n + HM_SCAN_ITEMS - 1) / HM_SCAN_ITEMS);
+    uint64_t chunk = HM_SCAN_ITEMS;
+    while ((n + chunk - 1) / chunk > HM_SCAN_MAXB) chunk += HM_SCAN_ITEMS;
+    const uint32_t nb = (uint32_t)((n + chunk - 1) / chunk);
     const uint32_t g = nb ? nb : 1;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, partial);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial);
     hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, partial, g, total);
-    hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, partial, out);
+    hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out);
 }
 
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a)
 {
-    uint64_t blocks = (a.nchildren + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
-    if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_compact, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_compact, dim3(hm_grid(a.nchildren, 256, 8192)), dim3(256), 0, s, a);
 }
 
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots)
@@ -1098,7 +1138,6 @@ void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint
     if (items) hipLaunchKernelGGL(k_aggregate, dim3(items), dim3(HM_AG_THREADS), 0, s, a);
     if (nslots) hipLaunchKernelGGL(k_aggregate_merged, dim3(nslots), dim3(HM_AG_THREADS), 0, s, a);
 }
-
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {
     if (nparents) hipLaunchKernelGGL(k_pool, dim3(nparents), dim3(HM_POOL_THREADS), 0, s, a);

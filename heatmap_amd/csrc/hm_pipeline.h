@@ -14,17 +14,13 @@
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
 /* levels >= 2 */
-#ifndef HM_PN_THREADS
-#define HM_PN_THREADS 512
-#endif
-#ifndef HM_TN
-#define HM_TN 8192
-#endif
+#define HM_PN_THREADS 1024
+#define HM_TN 8192                          /* keys per partition work item */
 #define HM_LEVEL_ZOOMS 6                    /* <= 6 zooms per level */
 #define HM_MAX_FN 4096
 #define HM_MAX_SHARDS 32                    /* run-counter shards per child */
 /* final aggregation: zoom-zb bucket = 128 x 128 zoom-Z bins */
-#define HM_AG_THREADS 512
+#define HM_AG_THREADS 1024
 #define HM_AG_CELLS 16384
 #define HM_AG_LG 7
 #ifndef HM_TA
@@ -34,10 +30,16 @@
 #define HM_MAX_LEVELS 4
 #define HM_COUNT_MAX_ZOOM 21                /* level-1 keys 2*(Z-5) bits fit u32 */
 #define HM_SCAN_LIMIT (4096ull * 4096ull)   /* dense children per level */
+/* run streaming: runs staged per chunk; runs of >= HM_LONG_RUN keys are read
+ * by a whole wave with 16-B loads, shorter ones by one lane each */
+#define HM_RCH 1024
+#define HM_LONG_RUN 32
 
-/* Run region of child (p, d): parent p owns level tiles [t0, t0+tp); its
- * children's regions start at F*(t0 + S*p), each S*ceil(tp/S) records, shard s
- * of a child at offset s*ceil(tp/S).  Capacity: F*(tiles + S*parents). */
+/* Sharded run region of child (p, d) as the partition kernels write it:
+ * parent p owns level tiles [t0, t0+tp); its children's regions start at
+ * F*(t0 + S*p), each S*ceil(tp/S) records, shard s of a child at offset
+ * s*ceil(tp/S).  Capacity: F*(tiles + S*parents).  The run scan copies every
+ * child's shards into one flat, child-ordered list (HmRuns). */
 __host__ __device__ inline uint64_t hm_run_base(uint64_t t0, uint64_t tp, uint64_t p, uint64_t d, int dbits,
                                                int shard_bits)
 {
@@ -46,17 +48,34 @@ __host__ __device__ inline uint64_t hm_run_base(uint64_t t0, uint64_t tp, uint64
     return ((t0 + S * p) << dbits) + d * (cap << shard_bits);
 }
 
+/* Flat run list of a level: run j holds cnt = run[j].y keys starting at key
+ * index run[j].x of the level's key array; its keys are the global logical
+ * positions [excl[j], excl[j] + cnt) (exclusive prefix over all runs).  The
+ * runs of one bucket are consecutive, so a bucket is a position range. */
+struct HmRuns {
+    const uint2* run;
+    const uint64_t* excl;
+};
 
 struct HmBuckets {
-    uint32_t count;        /* compact buckets */
+    uint32_t count;             /* compact buckets */
     const uint32_t* nkeys;
     const uint32_t* nruns;
-    const uint32_t* rbase;      /* first run record */
+    const uint32_t* rbase;      /* first run (flat index) */
+    const uint32_t* keybase;    /* first global logical key position */
     const uint32_t* item_begin; /* [count+1] work-item prefix for the next stage */
     const uint32_t* digit;
     const uint64_t* morton;     /* Morton index of the bucket at its zoom */
     const int32_t* slots;       /* last level: merge slot or -1 */
     const uint4* desc;          /* [2*items] work-item descriptors (k_items) */
+};
+
+/* work item g: desc[2g] = (bucket, j, nitems, r0), desc[2g+1] = (r1, -, a, b):
+ * logical positions [a, b) of the bucket, runs [r0, r1) overlap them */
+struct HmItem {
+    uint32_t bucket, j, nitems;
+    uint32_t r0, r1;
+    uint32_t a, b;
 };
 
 struct HmOut {
@@ -92,31 +111,39 @@ struct HmPart1Args {
 struct HmPartNArgs {
     HmBuckets parent;
     const uint32_t* keys_in;
-    const uint2* runs_in;
-    const uint32_t* runpre_in;
+    HmRuns in;
     int dbits, restbits, shard_bits;
-    void* keys_out;
+    void* keys_out;             /* item g writes its keys at its positions [a, b) */
     uint32_t* nruns_out;
     uint2* runs_out;
 };
 
-struct HmScanArgs {
+/* run scan of one level (sharded counters -> flat child-ordered runs) */
+struct HmRsArgs {
     uint64_t nchildren;
     int dbits, shard_bits;
-    const uint32_t* nruns;      /* sharded counters */
-    uint32_t* nruns_tot;        /* out: runs per child after shard compaction */
-    uint2* runs;
-    uint32_t* runpre;
+    const uint32_t* nruns;      /* [nchildren << shard_bits] sharded counters */
+    const uint2* runs;          /* sharded layout */
     const uint32_t* parent_item_begin;
+    uint32_t* shoff;            /* [nchildren << shard_bits] shard offset within child */
+    uint64_t* nr;               /* [nchildren] runs per child (scan input) */
+    const uint64_t* runbase;    /* [nchildren] exclusive scan of nr */
+    uint2* flat;                /* flat runs */
+    uint64_t* cnt;              /* flat run key counts (scan input) */
+    const uint64_t* excl;       /* exclusive scan of cnt */
+    uint64_t nflat;             /* total runs */
+    const uint64_t* total_keys;
     uint32_t item_keys;
-    uint32_t* nkeys;
-    uint64_t* vals;
+    uint32_t* nkeys;            /* [nchildren] */
+    uint32_t* keybase;          /* [nchildren] */
+    uint64_t* vals;             /* [nchildren] (1 << 32 | items) for non-empty children */
 };
 
 struct HmCompactOut {
     uint32_t* nkeys;
     uint32_t* nruns;
     uint32_t* rbase;
+    uint32_t* keybase;
     uint32_t* item_begin;
     uint32_t* digit;
     uint64_t* morton;
@@ -125,13 +152,14 @@ struct HmCompactOut {
 struct HmCompactArgs {
     uint64_t nchildren;
     uint32_t nparents;
-    int dbits, shard_bits;
+    int dbits;
     const uint64_t* vals;
     const uint64_t* prefix;
     const uint64_t* total;
     const uint32_t* nkeys;
-    const uint32_t* nruns;
-    const uint32_t* parent_item_begin;
+    const uint64_t* nr;
+    const uint64_t* runbase;
+    const uint32_t* keybase;
     const uint64_t* parent_morton;
     HmCompactOut out;
     uint32_t* child_begin;
@@ -143,8 +171,7 @@ struct HmCompactArgs {
 struct HmAggArgs {
     HmBuckets B;
     const uint16_t* keys;
-    const uint2* runs;
-    const uint32_t* runpre;
+    HmRuns in;
     int Z, lg;
     unsigned long long* totals;
     uint32_t* gslots;
@@ -180,16 +207,16 @@ struct HmRedoArgs {
     unsigned long long* exotic_word;
 };
 void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n);
-void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t tiles, bool out16);
-void hm_launch_runscan(hipStream_t s, const HmScanArgs& a);
+void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16);
+/* run scan steps: per-child shard offsets + run totals; flat copy; per-child keys */
+void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a);
+void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a);
+void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a);
+/* exclusive scan of v[0..n) into out (any n), total into *total; partial: 4096 u64 */
 void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total);
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
+void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc);
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots);
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);
-/* per work item g of B (item size T keys): desc[2g] = (bucket, j, nitems, r0),
- * desc[2g+1] = (rbase, nruns, first key, end key) -- replaces two dependent
- * global binary searches per block with one 32-B load */
-void hm_launch_items(hipStream_t s, const HmBuckets& B, const uint32_t* runpre, uint32_t items, uint32_t T,
-                     uint4* desc);
 void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
                      const double* tab, int k);
