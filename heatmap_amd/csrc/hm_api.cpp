@@ -292,7 +292,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     uint32_t* root = nullptr;
     ENSURE(B_ROOT, 4 * sizeof(uint32_t) + 2 * sizeof(uint64_t), root);
     {
-        /* staged through the pinned scratch: [0, tiles1, 0, 0 | morton 0, 0] */
+        /* staged through the pinned scratch: [0, tiles1, 0, 0 | coord 0, 0] */
         unsigned long long* up = ctx->host_state + ST_COUNT;
         HIPCHK(hipStreamSynchronize(s));
         up[0] = (unsigned long long)tiles1 << 32;
@@ -302,7 +302,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         HIPCHK(hipMemcpyAsync(root, up, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
     }
     const uint32_t* parent_item_begin = root;
-    const uint64_t* parent_morton = (const uint64_t*)(root + 4);
+    const uint64_t* parent_coord = (const uint64_t*)(root + 4);
     uint32_t nparents = 1;
 
     Level lv[HM_MAX_LEVELS];
@@ -502,7 +502,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_BK0 + l * 8 + 2, cap * 4, ca.out.rbase);
         ENSURE(B_BK0 + l * 8 + 3, cap * 4, ca.out.item_begin);
         ENSURE(B_BK0 + l * 8 + 4, cap * 4, ca.out.digit);
-        ENSURE(B_BK0 + l * 8 + 5, cap * 8, ca.out.morton);
+        ENSURE(B_BK0 + l * 8 + 5, cap * 8, ca.out.coord);
         ENSURE(B_BK0 + l * 8 + 6, cap * 4, ca.out.keybase);
         uint32_t* child_begin;
         ENSURE(B_CHILD0 + l, ((uint64_t)nparents + 1) * 4, child_begin);
@@ -516,7 +516,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ca.nr = ra.nr;
         ca.runbase = runbase;
         ca.keybase = ckeybase;
-        ca.parent_morton = parent_morton;
+        ca.parent_coord = parent_coord;
         ca.child_begin = child_begin;
         if (l == L - 1) {
             ENSURE(B_SLOTS, cap * 4, slots);
@@ -543,7 +543,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         b.keybase = ca.out.keybase;
         b.item_begin = ca.out.item_begin;
         b.digit = ca.out.digit;
-        b.morton = ca.out.morton;
+        b.coord = ca.out.coord;
         b.slots = (l == L - 1) ? slots : nullptr;
         runs_cur.run = flat;
         runs_cur.excl = excl;
@@ -557,7 +557,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
 
         keys_cur = kout;
         parent_item_begin = ca.out.item_begin;
-        parent_morton = ca.out.morton;
+        parent_coord = ca.out.coord;
         nparents = V.count;
         slot_k ^= 1;
     }
@@ -605,7 +605,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         pa.child_begin = (const uint32_t*)cb;
         pa.child_digit = B[l].digit;
         pa.child_totals = totals[l];
-        pa.parent_morton = l ? B[l - 1].morton : nullptr;
+        pa.parent_coord = l ? B[l - 1].coord : nullptr;
         pa.parent_totals = l ? totals[l - 1] : nullptr;
         pa.out = o;
         hm_launch_pool(s, pa, lv[l].nparents);

@@ -1,59 +1,40 @@
-/* Device-side helpers for gfx950 (wave64): Morton codes, wave aggregation,
+/* Device-side helpers for gfx950 (wave64): tile keys, wave aggregation,
  * block scans.  Wave width is hard-coded to 64 (CDNA). */
 #pragma once
 #include "hm_common.h"
 
 #define HM_WAVE 64
 
-/* ---- Morton (row bit above col bit) ---- */
-__device__ __forceinline__ uint64_t hm_spread32(uint64_t v)
+/* ---- tile keys ----
+ * Keys are row-major: a level's key holds the (row, col) offsets of a point's
+ * tile inside its bucket as (row << s) | col, s bits each; a digit is the
+ * top w bits of both, (row >> s' << w) | (col >> s').  Buckets carry their
+ * tile as coord = (row << 32) | col. */
+
+/* output cell key (include/heatmap_amd.h HM_KEY) */
+__device__ __forceinline__ uint64_t hm_key(int z, uint64_t row, uint64_t col)
 {
-    v &= 0xFFFFFFFFull;
-    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
-    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
-    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    v = (v | (v << 2)) & 0x3333333333333333ull;
-    v = (v | (v << 1)) & 0x5555555555555555ull;
-    return v;
+    return ((uint64_t)z << 58) | (row << 29) | col;
 }
 
-__device__ __forceinline__ uint32_t hm_compact64(uint64_t v)
+/* cell i of the row-major (2^lg)^2 block of zoom z whose corner tile at zoom
+ * z - lg is `coord` */
+__device__ __forceinline__ uint64_t hm_cell_key(int z, uint64_t coord, int lg, uint32_t i)
 {
-    v &= 0x5555555555555555ull;
-    v = (v | (v >> 1)) & 0x3333333333333333ull;
-    v = (v | (v >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-    v = (v | (v >> 4)) & 0x00FF00FF00FF00FFull;
-    v = (v | (v >> 8)) & 0x0000FFFF0000FFFFull;
-    v = (v | (v >> 16)) & 0x00000000FFFFFFFFull;
-    return (uint32_t)v;
+    const uint64_t row = ((coord >> 32) << lg) | (i >> lg);
+    const uint64_t col = ((coord & 0xFFFFFFFFull) << lg) | (i & ((1u << lg) - 1u));
+    return hm_key(z, row, col);
 }
 
-/* 16-bit -> even bits of 32 */
-__device__ __forceinline__ uint32_t hm_spread16(uint32_t v)
+/* sum of the 4 children of cell i of the next (coarser) level: the child
+ * block is row-major with side 2^(lgn+1) at v */
+template <typename T>
+__device__ __forceinline__ T hm_sum4(const T* v, uint32_t i, int lgn)
 {
-    v &= 0xFFFFu;
-    v = (v | (v << 8)) & 0x00FF00FFu;
-    v = (v | (v << 4)) & 0x0F0F0F0Fu;
-    v = (v | (v << 2)) & 0x33333333u;
-    v = (v | (v << 1)) & 0x55555555u;
-    return v;
-}
-
-/* Morton of two values < 2^16 (row bit above col bit) */
-__device__ __forceinline__ uint32_t hm_morton16(uint32_t row, uint32_t col)
-{
-    return (hm_spread16(row) << 1) | hm_spread16(col);
-}
-
-__device__ __forceinline__ uint64_t hm_morton(uint32_t row, uint32_t col)
-{
-    return (hm_spread32(row) << 1) | hm_spread32(col);
-}
-
-/* output key of cell `m` (Morton index at zoom z) */
-__device__ __forceinline__ uint64_t hm_out_key(int z, uint64_t m)
-{
-    return ((uint64_t)z << 58) | ((uint64_t)hm_compact64(m >> 1) << 29) | (uint64_t)hm_compact64(m);
+    const uint32_t r = i >> lgn, c = i & ((1u << lgn) - 1u);
+    const uint32_t side = 2u << lgn;
+    const uint32_t j = (r << (lgn + 2)) | (c << 1);
+    return (T)(v[j] + v[j + 1] + v[j + side] + v[j + side + 1]);
 }
 
 /* ---- wave helpers ---- */
@@ -118,13 +99,15 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
     return r;
 }
 
-/* LDS histogram increment.  Duplicate addresses within one ds_add are
- * serialised by the LDS unit, which is cheaper than software aggregation for
- * the usual mix; only a wave whose valid lanes ALL share one key (the skew
- * case, SURVEY.md section 7 hard part 3) is collapsed into a single add.
- * (Measured: 4 rounds of leader aggregation made k_project_partition
- * SALU-bound.) */
-__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t key, bool valid)
+/* LDS histogram increment / slot reservation, branch-free.  The lanes whose
+ * key equals the first active lane's are added by one atomic of their first
+ * lane (the skew case, SURVEY.md section 7 hard part 3: a wave of one key
+ * costs one atomic, not 64 serialised ones); every other valid lane adds 1 to
+ * its own key; lanes with nothing to add hit a private dummy slot, so no
+ * branch, leader election loop or exec-mask juggling is needed -- those made
+ * the partition kernels scalar-issue bound.  `dummy` is 64 words of LDS. */
+#ifdef HM_OLD_LDS
+__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t*, uint32_t key, bool valid)
 {
     const uint64_t vm = __ballot(valid);
     if (vm == 0) return;
@@ -137,8 +120,7 @@ __device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t key, bool 
     }
 }
 
-/* Slot reservation in bucket `key` (cursor array `cur`), same policy. */
-__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t key, bool valid)
+__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t*, uint32_t key, bool valid)
 {
     const uint64_t vm = __ballot(valid);
     if (vm == 0) return 0;
@@ -154,3 +136,31 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t key, bo
     }
     return pos;
 }
+#else
+__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t* dummy, uint32_t key, bool valid)
+{
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    const bool same = valid && key == k0;
+    const uint64_t m = __ballot(same);
+    const bool lead = same && hm_mbcnt(m) == 0;
+    const bool own = valid && !same;
+    uint32_t* p = lead ? &hist[k0] : (own ? &hist[key] : &dummy[hm_lane()]);
+    const uint32_t inc = lead ? (uint32_t)__popcll(m) : (uint32_t)own;
+    atomicAdd(p, inc);
+}
+
+__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t* dummy, uint32_t key, bool valid)
+{
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    const bool same = valid && key == k0;
+    const uint64_t m = __ballot(same);
+    const uint32_t r = hm_mbcnt(m);
+    const bool lead = same && r == 0;
+    const bool own = valid && !same;
+    uint32_t* p = lead ? &cur[k0] : (own ? &cur[key] : &dummy[hm_lane()]);
+    const uint32_t inc = lead ? (uint32_t)__popcll(m) : (uint32_t)own;
+    const uint32_t old = atomicAdd(p, inc);
+    const uint32_t base = __builtin_amdgcn_readlane(old, m ? __ffsll((unsigned long long)m) - 1 : 0);
+    return same ? base + r : old;
+}
+#endif

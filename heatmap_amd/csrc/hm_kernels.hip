@@ -3,7 +3,7 @@
  * Path (SURVEY.md section 8a, a-1 .. a-11), one hm_count() call:
  *
  *   k_project_partition   fp64 lat/lon SoA -> tile row/col at zoom Z (exact,
- *                         hm_project.h) -> Morton key -> LDS counting sort of an
+ *                         hm_project.h) -> row-major key -> LDS counting sort of an
  *                         8192-point tile by the key's top digit (zoom z1
  *                         tile); writes the tile's keys (u32/u16, top digit
  *                         dropped) contiguously and one run record per
@@ -22,11 +22,11 @@
  *                         totals -> 4:1 pyramid -> zooms z_l .. z_{l-1}+1; the
  *                         root emits zooms z1 .. 0.
  *   k_runscan / scans / k_compact: turn per-digit run counters into compact,
- *                         Morton-ordered bucket lists and work-item prefixes.
+ *                         parent-major bucket lists and work-item prefixes.
  *
- * The Morton key makes every parent a right shift (key >> 2), which is the
- * reference's tile-centre re-projection on the shift window
- * and the direct projection at every zoom (a-1).  Counts are integers (u32
+ * Every coarser tile is a right shift of the zoom-Z row and column, which is
+ * the reference's tile-centre re-projection on the shift window (SURVEY.md
+ * a-4) and the direct projection at every zoom (a-1).  Counts are integers (u32
  * per call, u64 out): the reference's float sums of 1.0 are exact below 2^53.
  */
 #include <hip/hip_runtime.h>
@@ -76,7 +76,8 @@ template <typename OutT, int MODE>
 __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args a)
 {
     __shared__ uint32_t cur[HM_MAX_F1];
-    __shared__ OutT stage[HM_T1];
+    __shared__ uint32_t dummy[64];
+    __shared__ OutT stage[HM_T1 + 64];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
     __shared__ double tab[HM_YTAB_N];
     constexpr bool FROM_TILES = MODE == 1;
@@ -88,7 +89,6 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 
     const uint32_t tile = a.tile0 + blockIdx.x;          /* tile slot in the run layout */
     const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
-    const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
     const uint32_t lim = 1u << a.Z;
     const double scale = hm_exp2i(a.Z);
     const double kz = HM_INV360 * scale;
@@ -133,7 +133,8 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     /* fast path for every point, branch-free; points the fast path cannot
      * settle (guard band, polar/out-of-range/non-finite input) are marked in
      * `redo` and resolved afterwards in one ballot-guarded pass */
-    const int hb = a.restbits >> 1;
+    const int hb = a.restbits >> 1;      /* offset bits per coordinate in rest */
+    const int wd = a.dbits >> 1;         /* digit bits per coordinate */
     const uint32_t lowm = (1u << hb) - 1u;
     uint32_t redo = 0;
 #pragma unroll
@@ -158,8 +159,11 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         const bool dom = ((uint64_t)r < lim) & ((uint64_t)c < lim);
         redo |= (uint32_t)(inb & !(ok & dom)) << k;
         const bool v = inb & ok & dom & kept;
-        dig[k] = v ? hm_morton16((uint32_t)r >> hb, (uint32_t)c >> hb) : 0xFFFFFFFFu;
-        rest[k] = hm_morton16((uint32_t)r & lowm, (uint32_t)c & lowm) & restmask;
+        dig[k] = v ? ((((uint32_t)r >> hb) << wd) | ((uint32_t)c >> hb)) : 0xFFFFFFFFu;
+        rest[k] = (((uint32_t)r & lowm) << hb) | ((uint32_t)c & lowm);
+        /* pin the key: without it the compiler keeps every point's
+         * projection temporaries alive past this point (158 VGPRs, 1 block/CU) */
+        asm volatile("" : "+v"(dig[k]), "+v"(rest[k]));
         /* one point at a time: interleaving all eight projections would need
          * ~200 VGPRs and halve occupancy */
         __builtin_amdgcn_sched_barrier(0);
@@ -207,8 +211,8 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             } else if (kept && ((uint64_t)r >= lim || (uint64_t)c >= lim)) {
                 atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
             } else if (kept) {
-                dig[k] = hm_morton16((uint32_t)r >> hb, (uint32_t)c >> hb);
-                rest[k] = hm_morton16((uint32_t)r & lowm, (uint32_t)c & lowm) & restmask;
+                dig[k] = (((uint32_t)r >> hb) << wd) | ((uint32_t)c >> hb);
+                rest[k] = (((uint32_t)r & lowm) << hb) | ((uint32_t)c & lowm);
             }
         }
     }
@@ -217,7 +221,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, dig[k], dig[k] != 0xFFFFFFFFu);
+    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, dummy, dig[k], dig[k] != 0xFFFFFFFFu);
     __syncthreads();
 
     /* exclusive scan of the digit histogram; one run record per digit */
@@ -260,8 +264,8 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT; k++) {
         const bool v = dig[k] != 0xFFFFFFFFu;
-        const uint32_t pos = hm_lds_claim(cur, dig[k], v);
-        if (v) stage[pos] = (OutT)rest[k];
+        const uint32_t pos = hm_lds_claim(cur, dummy, dig[k], v);
+        stage[v ? pos : HM_T1 + hm_lane()] = (OutT)rest[k];
     }
     __syncthreads();
     OutT* out = (OutT*)a.keys_out + (uint64_t)tile * HM_T1;
@@ -341,36 +345,32 @@ void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t item
 }
 
 /* Run chunk staged in LDS: long runs' aligned bodies (in 16-B vectors) and
- * their exclusive prefix, short pieces (short runs, heads and tails). */
+ * short pieces (short runs, heads and tails), each with its exclusive prefix. */
 template <int RCH>
 struct HmRunLds {
     uint2 body[RCH];            /* (first vector index, vectors) */
     uint32_t pre[RCH + 1];      /* exclusive prefix of body vectors */
     uint2 piece[2 * RCH];       /* (first key index, keys), < HM_LONG_RUN keys each */
+    uint32_t ppre[2 * RCH + 1]; /* exclusive prefix of piece keys */
     uint32_t nbody, npiece;
 };
 
-template <typename InT, typename F>
-__device__ __forceinline__ void hm_apply_vec(const uint4& x, bool v, F& f)
+/* LDS slot of cell (r, c) = (r << w) | c of a row-major 2^w x 2^w histogram:
+ * the column is rotated by 8 r, so a 2-D cluster of cells spreads over the 64
+ * LDS banks instead of piling up on the few banks of its columns */
+__device__ __forceinline__ uint32_t hm_skew(uint32_t d, int w)
 {
-    if (sizeof(InT) == 4) {
-        f(x.x, v);
-        f(x.y, v);
-        f(x.z, v);
-        f(x.w, v);
-    } else {
-        f(x.x & 0xFFFFu, v);
-        f(x.x >> 16, v);
-        f(x.y & 0xFFFFu, v);
-        f(x.y >> 16, v);
-        f(x.z & 0xFFFFu, v);
-        f(x.z >> 16, v);
-        f(x.w & 0xFFFFu, v);
-        f(x.w >> 16, v);
-    }
+    const uint32_t m = (1u << w) - 1u;
+    return (d & ~m) | ((d + ((d >> w) << 3)) & m);
 }
 
-/* wave-aggregated append of one entry per flagged lane to list[base + n++] */
+__device__ __forceinline__ uint32_t hm_unskew(uint32_t j, int w)
+{
+    const uint32_t m = (1u << w) - 1u;
+    return (j & ~m) | ((j - ((j >> w) << 3)) & m);
+}
+
+/* wave-aggregated append of one entry per flagged lane to list[n++] */
 __device__ __forceinline__ void hm_lds_append(uint2* list, uint32_t* n, bool flag, uint2 e)
 {
     const uint64_t m = __ballot(flag);
@@ -382,21 +382,40 @@ __device__ __forceinline__ void hm_lds_append(uint2* list, uint32_t* n, bool fla
     if (flag) list[b + hm_mbcnt(m)] = e;
 }
 
-/* Calls f(key, valid) for every key at the item's logical positions [a, b),
- * in no particular order (the consumers count or re-sort).  The item's runs
- * are staged RCH at a time and clipped to [a, b).  The 16-B-aligned bodies of
- * runs with >= HM_LONG_RUN keys form one flat vector space, split into
- * contiguous per-wave spans; a lane keeps HM_SU 16-B loads in flight and
- * finds each vector's run by walking a monotone cursor over the body prefix.
- * Short runs and the bodies' unaligned heads and tails go one lane each (8
- * loads in flight).  Block-uniform: every thread calls; f is also called
- * under divergence and must use ballots of the active lanes only. */
+/* pre[0..n] = exclusive prefix of list[i].y, pre[n] = total (block-uniform) */
+template <int THREADS>
+__device__ __forceinline__ void hm_block_prefix(const uint2* list, uint32_t n, uint32_t* pre, uint32_t* scr)
+{
+    uint32_t carry = 0;
+    for (uint32_t i0 = 0; i0 < n; i0 += THREADS) {
+        const uint32_t i = i0 + threadIdx.x;
+        const uint32_t x = i < n ? list[i].y : 0u;
+        uint32_t tot;
+        const uint32_t ex = hm_block_excl_scan<THREADS>(x, scr, &tot);
+        if (i < n) pre[i] = carry + ex;
+        carry += tot;
+    }
+    if (threadIdx.x == 0) pre[n] = carry;
+    __syncthreads();
+}
+
 #ifndef HM_SU
 #define HM_SU 4
 #endif
+
+/* Calls f.vec(uint4 x, valid, pos) / f.key(key, valid, pos) for every key at
+ * the item's logical positions [a, b): the keys of vector x are staged order
+ * positions pos..pos+V-1, single keys pos; together the positions are a
+ * permutation of [0, b - a) (deterministic: no append atomics).  The item's
+ * runs are staged RCH at a time and clipped to [a, b).  The 16-B-aligned
+ * bodies of runs with >= HM_LONG_RUN keys form one flat vector space, split
+ * into contiguous per-wave spans; a lane keeps HM_SU 16-B loads in flight and
+ * finds each vector's run by walking a monotone cursor over the body prefix.
+ * Short runs and the bodies' unaligned heads and tails go one lane each (8
+ * loads in flight).  Block-uniform: every thread calls. */
 template <typename InT, int THREADS, int RCH, typename F>
 __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __restrict__ keys, const HmRuns& in,
-                                               HmRunLds<RCH>& L, uint32_t* scr, F f)
+                                               HmRunLds<RCH>& L, uint32_t* scr, F& f)
 {
     constexpr int NW = THREADS / 64;
     constexpr uint32_t V = 16 / sizeof(InT);   /* keys per 16-B vector */
@@ -404,6 +423,7 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
     const int lane = tid & 63;
     const int w = tid >> 6;
     const uint4* kv = (const uint4*)keys;
+    uint32_t carry = 0;                        /* keys staged by earlier chunks */
     for (uint32_t rc = it.r0; rc < it.r1; rc += RCH) {
         const uint32_t m = min((uint32_t)RCH, it.r1 - rc);
         if (tid == 0) {
@@ -432,20 +452,10 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
         }
         __syncthreads();
         const uint32_t nb = L.nbody, np = L.npiece;
-        /* exclusive prefix of the body lengths */
-        for (uint32_t i0 = 0; i0 < nb; i0 += THREADS) {
-            const uint32_t i = i0 + tid;
-            const uint32_t x = i < nb ? L.body[i].y : 0u;
-            uint32_t tot;
-            const uint32_t ex = hm_block_excl_scan<THREADS>(x, scr, &tot);
-            const uint32_t carry = i0 ? L.pre[i0] : 0u;
-            if (i < nb) L.pre[i] = carry + ex;
-            if (tid == 0) L.pre[min(i0 + THREADS, nb)] = carry + tot;
-            __syncthreads();
-        }
-        if (nb == 0 && tid == 0) L.pre[0] = 0;
-        __syncthreads();
+        hm_block_prefix<THREADS>(L.body, nb, L.pre, scr);
+        hm_block_prefix<THREADS>(L.piece, np, L.ppre, scr);
         const uint32_t total = L.pre[nb];
+        const uint32_t pbase = carry + V * total;
         /* bodies: contiguous wave spans of the flat vector space */
         const uint32_t span = ((total + NW - 1) / NW + 63) & ~63u;
         const uint32_t vb = min(total, span * w), ve = min(total, vb + span);
@@ -465,20 +475,22 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
                     }
                 }
 #pragma unroll
-                for (int u = 0; u < HM_SU; u++) hm_apply_vec<InT>(x[u], ok[u], f);
+                for (int u = 0; u < HM_SU; u++) f.vec(x[u], ok[u], carry + V * (v0 + u * 64 + lane));
             }
         }
         /* pieces: one lane each */
         for (uint32_t q = tid; q < np; q += THREADS) {
             const uint2 r = L.piece[q];
+            const uint32_t pq = pbase + L.ppre[q];
             for (uint32_t k0 = 0; k0 < r.y; k0 += 8) {
                 uint32_t kk[8];
 #pragma unroll
                 for (int u = 0; u < 8; u++) kk[u] = (k0 + u < r.y) ? (uint32_t)keys[r.x + k0 + u] : 0u;
 #pragma unroll
-                for (int u = 0; u < 8; u++) f(kk[u], k0 + u < r.y);
+                for (int u = 0; u < 8; u++) f.key(kk[u], k0 + u < r.y, pq + k0 + u);
             }
         }
+        carry = pbase + L.ppre[np];
         __syncthreads();
     }
 }
@@ -488,32 +500,49 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
 /* ------------------------------------------------------------------------ */
 
 template <typename OutT>
-__global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
+__global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
 {
-    __shared__ uint32_t stage[HM_TN];      /* streamed keys, then the sorted output (OutT) */
+    /* streamed keys in staged order, then the digit-sorted output (OutT);
+     * words [HM_TN, HM_TN + 64) absorb the writes of idle lanes */
+    __shared__ __attribute__((aligned(16))) uint32_t stage[HM_TN + 64];
     __shared__ uint32_t cur[HM_MAX_FN];
+    __shared__ uint32_t dummy[64];
     __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
-    __shared__ uint32_t scnt;
     __shared__ HmRunLds<512> L;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
-    if (tid == 0) scnt = 0;
     __syncthreads();
     const HmItem it = hm_item(a.parent, blockIdx.x);
-    const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
-    hm_stream_runs<uint32_t, HM_PN_THREADS, 512>(it, a.keys_in, a.in, L, scr, [&](uint32_t key, bool v) {
-        hm_lds_count(cur, key >> a.restbits, v);
-        const uint64_t vm = __ballot(v);
-        if (vm) {
-            const int leader = __ffsll((unsigned long long)vm) - 1;
-            uint32_t wp = 0;
-            if (hm_lane() == leader) wp = atomicAdd(&scnt, (uint32_t)__popcll(vm));
-            wp = __builtin_amdgcn_readlane(wp, leader);
-            if (v) stage[wp + hm_mbcnt(vm)] = key;
+    /* parent key: (row << sp) | col, sp = s + w bits each; digit = top w bits
+     * of both, rest = low s bits of both */
+    const int sw = a.restbits >> 1, ww = a.dbits >> 1, sp = sw + ww;
+    const uint32_t lowm = (1u << sw) - 1u;
+    struct {
+        uint32_t* cur;
+        uint32_t* dummy;
+        uint32_t* stage;
+        int s, w, sp;
+        /* skewed LDS slot of the key's digit */
+        __device__ __forceinline__ uint32_t digit(uint32_t k) const
+        {
+            return hm_skew(((k >> (sp + s)) << w) | ((k & ((1u << sp) - 1u)) >> s), w);
         }
-    });
-    __syncthreads();
+        __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t pos)
+        {
+            hm_lds_count(cur, dummy, digit(k), v);
+            stage[v ? pos : HM_TN + hm_lane()] = k;
+        }
+        __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t pos)
+        {
+            hm_lds_count(cur, dummy, digit(x.x), v);
+            hm_lds_count(cur, dummy, digit(x.y), v);
+            hm_lds_count(cur, dummy, digit(x.z), v);
+            hm_lds_count(cur, dummy, digit(x.w), v);
+            *(uint4*)&stage[v ? pos : HM_TN] = x;
+        }
+    } f{cur, dummy, stage, sw, ww, sp};
+    hm_stream_runs<uint32_t, HM_PN_THREADS, 512>(it, a.keys_in, a.in, L, scr, f);
     const uint32_t total = it.b - it.a;
     constexpr int PER = HM_MAX_FN / HM_PN_THREADS;
     uint32_t cnt[PER];
@@ -526,6 +555,8 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     }
     uint32_t tot2;
     uint32_t off = hm_block_excl_scan<HM_PN_THREADS>(s, scr, &tot2);
+    /* cur[] slots are skewed digits (hm_skew): the run records and counters
+     * use the digit itself */
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
     const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
     const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
@@ -537,7 +568,8 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
         offq[q] = off;
         idx[q] = 0;
         if (d < F && cnt[q])
-            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
+            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + hm_unskew(d, ww)) << a.shard_bits) + sh],
+                               1u);
         off += cnt[q];
     }
 #pragma unroll
@@ -546,7 +578,7 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
         if (d < F) {
             cur[d] = offq[q];
             if (cnt[q]) {
-                const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
+                const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, hm_unskew(d, ww), a.dbits, a.shard_bits);
                 a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);
             }
         }
@@ -564,8 +596,9 @@ __global__ __launch_bounds__(HM_PN_THREADS) void k_partition(HmPartNArgs a)
     for (int k = 0; k < KPT; k++) {
         const uint32_t i = k * HM_PN_THREADS + tid;
         const bool v = i < total;
-        const uint32_t pos = hm_lds_claim(cur, kv[k] >> a.restbits, v);
-        if (v) so[pos] = (OutT)(kv[k] & restmask);
+        const uint32_t pos = hm_lds_claim(cur, dummy, f.digit(kv[k]), v);
+        const uint32_t rr = kv[k] >> sp, cc = kv[k] & ((1u << sp) - 1u);
+        so[v ? pos : HM_TN + tid % 64] = (OutT)(((rr & lowm) << sw) | (cc & lowm));
     }
     __syncthreads();
     OutT* out = (OutT*)a.keys_out + it.a;
@@ -760,7 +793,7 @@ __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v
     }
 }
 
-/* compaction of non-empty children into the Morton-ordered bucket list B_l */
+/* compaction of non-empty children into the bucket list B_l (parent-major) */
 __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
 {
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -781,7 +814,11 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
             a.out.keybase[idx] = a.keybase[c];
             a.out.item_begin[idx] = ib;
             a.out.digit[idx] = (uint32_t)d;
-            a.out.morton[idx] = (a.parent_morton[p] << a.dbits) | d;
+            const uint64_t pc = a.parent_coord[p];
+            const int wd = a.dbits >> 1;
+            const uint64_t rr = ((pc >> 32) << wd) | (d >> wd);
+            const uint64_t cc = ((pc & 0xFFFFFFFFull) << wd) | (d & ((1ull << wd) - 1));
+            a.out.coord[idx] = (rr << 32) | cc;
             if (a.slots) {
                 const uint32_t nit = (uint32_t)(a.vals[c] & 0xFFFFFFFFull);
                 int32_t sl = -1;
@@ -802,8 +839,9 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
 /* emission helpers                                                          */
 /* ------------------------------------------------------------------------ */
 
-/* Emit the non-zero cells v[0..n) of zoom z whose Morton index is
- * (prefix << (2*lg)) | i.  All threads of the block must call. */
+/* Emit the non-zero cells v[0..n) of zoom z: the row-major (2^lg)^2 block
+ * whose corner tile at zoom z - lg is `prefix` (a coord).  All threads of the
+ * block must call. */
 template <typename T, int THREADS>
 __device__ void hm_emit_level(const T* v, uint32_t n, int z, uint64_t prefix, int lg, const HmOut& o,
                               uint32_t* scr, unsigned long long* sbase)
@@ -825,7 +863,7 @@ __device__ void hm_emit_level(const T* v, uint32_t n, int z, uint64_t prefix, in
         if (x != 0) {
             const uint64_t pos = base + off;
             if (pos < o.capacity) {
-                o.keys[pos] = hm_out_key(z, (prefix << (2 * lg)) | i);
+                o.keys[pos] = hm_cell_key(z, prefix, lg, i);
                 o.counts[pos] = (uint64_t)x;
             }
             off++;
@@ -833,8 +871,8 @@ __device__ void hm_emit_level(const T* v, uint32_t n, int z, uint64_t prefix, in
     }
 }
 
-/* In-LDS 4:1 pyramid over v[0..4^lg): emits zooms z_top .. z_top-lg+1 (those in
- * [zmin, zmax]) and leaves the total in v[0]. */
+/* In-LDS 4:1 pyramid over the row-major v[0..4^lg): emits zooms z_top ..
+ * z_top-lg+1 (those in [zmin, zmax]) and leaves the total in v[0]. */
 template <typename T, int THREADS>
 __device__ void hm_pyramid(T* v, int lg, int z_top, uint64_t prefix, const HmOut& o, uint32_t* scr,
                            unsigned long long* sbase)
@@ -850,7 +888,7 @@ __device__ void hm_pyramid(T* v, int lg, int z_top, uint64_t prefix, const HmOut
 #pragma unroll
         for (int m = 0; m < MAXPER; m++) {
             const uint32_t i = threadIdx.x + m * THREADS;
-            acc[m] = i < n ? (T)(v[4 * i] + v[4 * i + 1] + v[4 * i + 2] + v[4 * i + 3]) : (T)0;
+            acc[m] = i < n ? hm_sum4<T>(v, i, lg - k - 1) : (T)0;
         }
         __syncthreads();
 #pragma unroll
@@ -883,7 +921,7 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
 #pragma unroll
         for (int m = 0; m < MAXPER; m++) {
             const uint32_t i = threadIdx.x + m * THREADS;
-            acc[m] = i < n ? v[4 * i] + v[4 * i + 1] + v[4 * i + 2] + v[4 * i + 3] : 0u;
+            acc[m] = i < n ? hm_sum4<uint32_t>(v, i, lg - 1) : 0u;
         }
         __syncthreads();
 #pragma unroll
@@ -902,7 +940,7 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
         const uint32_t m = n >> 2;
         off[k] = end;
         for (uint32_t i = threadIdx.x; i < m; i += THREADS)
-            v[end + i] = v[src + 4 * i] + v[src + 4 * i + 1] + v[src + 4 * i + 2] + v[src + 4 * i + 3];
+            v[end + i] = hm_sum4<uint32_t>(v + src, i, lg - k);
         __syncthreads();
         end += m;
         n = m;
@@ -932,7 +970,7 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
             if (x != 0 && z >= o.zmin && z <= o.zmax) {
                 const uint64_t q = base + pos;
                 if (q < o.capacity) {
-                    o.keys[q] = hm_out_key(z, (prefix << (2 * (lg - k))) | (i - off[k]));
+                    o.keys[q] = hm_cell_key(z, prefix, lg - k, i - off[k]);
                     o.counts[q] = x;
                 }
                 pos++;
@@ -947,22 +985,55 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
 /* final level: dense 128x128 LDS histogram per zoom-zb bucket               */
 /* ------------------------------------------------------------------------ */
 
-__global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate(HmAggArgs a)
+__global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
 {
     __shared__ uint32_t grid[HM_AG_CELLS];
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
-    __shared__ HmRunLds<512> L;
+    __shared__ uint32_t dummy[64];
+    __shared__ HmRunLds<256> L;
     const int tid = threadIdx.x;
     const uint32_t ncell = 1u << (2 * a.lg);
     for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
     const HmItem it = hm_item(a.B, blockIdx.x);
-    hm_stream_runs<uint16_t, HM_AG_THREADS, 512>(it, a.keys, a.in, L, scr,
-                                                 [&](uint32_t key, bool v) { hm_lds_count(grid, key, v); });
+    /* counted at skewed slots (hm_skew), un-skewed before the pyramid */
+    struct {
+        uint32_t* grid;
+        uint32_t* dummy;
+        int lg;
+        __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { hm_lds_count(grid, dummy, hm_skew(k, lg), v); }
+        __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t)
+        {
+            hm_lds_count(grid, dummy, hm_skew(x.x & 0xFFFFu, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.x >> 16, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.y & 0xFFFFu, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.y >> 16, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.z & 0xFFFFu, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.z >> 16, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.w & 0xFFFFu, lg), v);
+            hm_lds_count(grid, dummy, hm_skew(x.w >> 16, lg), v);
+        }
+    } f{grid, dummy, a.lg};
+    hm_stream_runs<uint16_t, HM_AG_THREADS, 256>(it, a.keys, a.in, L, scr, f);
+    {
+        constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;
+        uint32_t x[CPT];
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            const uint32_t i = k * HM_AG_THREADS + tid;
+            x[k] = i < ncell ? grid[hm_skew(i, a.lg)] : 0u;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            const uint32_t i = k * HM_AG_THREADS + tid;
+            if (i < ncell) grid[i] = x[k];
+        }
+    }
     __syncthreads();
     if (it.nitems == 1) {
-        const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[it.bucket], a.out, scr, &sbase);
+        const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[it.bucket], a.out, scr, &sbase);
         if (tid == 0) a.totals[it.bucket] = t;
     } else {
         uint32_t* g = a.gslots + (uint64_t)a.B.slots[it.bucket] * HM_AG_CELLS;
@@ -986,7 +1057,7 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
     const uint32_t* g = a.gslots + (uint64_t)blockIdx.x * HM_AG_CELLS;
     for (uint32_t i = threadIdx.x; i < ncell; i += HM_AG_THREADS) grid[i] = g[i];
     __syncthreads();
-    hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.morton[b], a.out, scr, &sbase);
+    hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[b], a.out, scr, &sbase);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -1005,14 +1076,14 @@ __global__ __launch_bounds__(HM_POOL_THREADS) void k_pool(HmPoolArgs a)
     const uint32_t c0 = a.child_begin[p], c1 = a.child_begin[p + 1];
     for (uint32_t c = c0 + threadIdx.x; c < c1; c += HM_POOL_THREADS) v[a.child_digit[c]] = a.child_totals[c];
     __syncthreads();
-    const uint64_t pm = a.parent_morton ? a.parent_morton[p] : 0ull;
+    const uint64_t pm = a.parent_coord ? a.parent_coord[p] : 0ull;
     hm_pyramid<unsigned long long, HM_POOL_THREADS>(v, a.dbits / 2, a.z_child, pm, a.out, scr, &sbase);
     if (threadIdx.x == 0) {
         if (a.parent_totals) a.parent_totals[p] = v[0];
         if (a.emit_root && v[0] && a.out.zmin == 0) {
             const uint64_t pos = atomicAdd(a.out.cursor, 1ull);
             if (pos < a.out.capacity) {
-                a.out.keys[pos] = hm_out_key(0, 0);
+                a.out.keys[pos] = hm_key(0, 0, 0);
                 a.out.counts[pos] = v[0];
             }
         }

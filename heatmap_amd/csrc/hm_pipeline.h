@@ -65,7 +65,7 @@ struct HmBuckets {
     const uint32_t* keybase;    /* first global logical key position */
     const uint32_t* item_begin; /* [count+1] work-item prefix for the next stage */
     const uint32_t* digit;
-    const uint64_t* morton;     /* Morton index of the bucket at its zoom */
+    const uint64_t* coord;      /* (row << 32) | col of the bucket tile at its zoom */
     const int32_t* slots;       /* last level: merge slot or -1 */
     const uint4* desc;          /* [2*items] work-item descriptors (k_items) */
 };
@@ -146,7 +146,7 @@ struct HmCompactOut {
     uint32_t* keybase;
     uint32_t* item_begin;
     uint32_t* digit;
-    uint64_t* morton;
+    uint64_t* coord;
 };
 
 struct HmCompactArgs {
@@ -160,7 +160,7 @@ struct HmCompactArgs {
     const uint64_t* nr;
     const uint64_t* runbase;
     const uint32_t* keybase;
-    const uint64_t* parent_morton;
+    const uint64_t* parent_coord;
     HmCompactOut out;
     uint32_t* child_begin;
     int32_t* slots;         /* last level only */
@@ -184,7 +184,7 @@ struct HmPoolArgs {
     const uint32_t* child_begin;
     const uint32_t* child_digit;
     const unsigned long long* child_totals;
-    const uint64_t* parent_morton;
+    const uint64_t* parent_coord;
     unsigned long long* parent_totals;
     HmOut out;
 };

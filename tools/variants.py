@@ -19,12 +19,7 @@ VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
 
 VARIANTS = {
     "base": [],
-    "p1_1024x4": ["HM_P1_THREADS=1024", "HM_P1_PPT=4"],
-    "p1_256x16": ["HM_P1_THREADS=256", "HM_P1_PPT=16"],
-    "p1_512x16": ["HM_P1_PPT=16"],
-    "su8": ["HM_SU=8"],
-    "ta64k": ["HM_TA=65536"],
-    "tn4k": ["HM_TN=4096"],
+    "oldlds": ["HM_OLD_LDS=1"],
 }
 
 
