@@ -164,3 +164,12 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t* dummy,
     return same ? base + r : old;
 }
 #endif
+
+/* LDS slot of cell (r, c) = (r << w) | c of a row-major 2^w x 2^w histogram:
+ * the column is rotated by 8 r, so a 2-D cluster of cells spreads over more
+ * LDS banks than the few of its columns */
+__device__ __forceinline__ uint32_t hm_skew(uint32_t d, int w)
+{
+    const uint32_t m = (1u << w) - 1u;
+    return (d & ~m) | ((d + ((d >> w) << 3)) & m);
+}

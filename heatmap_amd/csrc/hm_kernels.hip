@@ -34,6 +34,24 @@
 #include "hm_project.h"
 #include "hm_pipeline.h"
 
+#ifdef HM_STAMPS
+/* phase timing (profiling builds only, tools/stamps.py): thread 0 of the first
+ * HM_STAMP_BLOCKS blocks of k_partition records s_memtime at 12 points */
+#define HM_STAMP_BLOCKS 65536
+__device__ unsigned long long g_stamps[HM_STAMP_BLOCKS * 12];
+#define HM_STAMP(k)                                                                            \
+    do {                                                                                       \
+        if (threadIdx.x == 0 && blockIdx.x < HM_STAMP_BLOCKS)                                  \
+            g_stamps[blockIdx.x * 12 + (k)] = __builtin_amdgcn_s_memtime();                    \
+    } while (0)
+extern "C" int hm_debug_stamps(void* host, size_t bytes)
+{
+    return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
+}
+#else
+#define HM_STAMP(k) do { } while (0)
+#endif
+
 #define HM_YTAB_N (HM_YTAB_ROWS * HM_YTAB_STRIDE)
 __constant__ double c_ytab[HM_YTAB_N] = HM_YTAB_INIT;
 
@@ -253,12 +271,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F) {
-            cur[d] = offq[q];
-            if (cnt[q])
-                a.runs[hm_run_base(0, a.tiles, 0, d, a.dbits, a.shard_bits) + sh * cap + idx[q]] =
-                    make_uint2(tile * HM_T1 + offq[q], cnt[q]);
-        }
+        if (d < F) cur[d] = offq[q];
     }
     __syncthreads();
 #pragma unroll
@@ -270,6 +283,14 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     __syncthreads();
     OutT* out = (OutT*)a.keys_out + (uint64_t)tile * HM_T1;
     for (uint32_t i = tid; i < total; i += HM_P1_THREADS) out[i] = stage[i];
+    /* run records last: the slot atomics' latency hid behind the scatter */
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F && cnt[q])
+            a.runs[hm_run_base(0, a.tiles, 0, d, a.dbits, a.shard_bits) + sh * cap + idx[q]] =
+                make_uint2(tile * HM_T1 + offq[q], cnt[q]);
+    }
 }
 
 /* ------------------------------------------------------------------------ */
@@ -344,59 +365,31 @@ void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t item
     if (items) hipLaunchKernelGGL(k_items, dim3((items + 255) / 256), dim3(256), 0, s, B, in, items, T, desc);
 }
 
-/* Run chunk staged in LDS: long runs' aligned bodies (in 16-B vectors) and
- * short pieces (short runs, heads and tails), each with its exclusive prefix. */
+/* Run chunk staged in LDS, dense per run i of the chunk: its 16-B-aligned
+ * body (first vector, vectors; zero unless long) and two pieces (head and
+ * tail of a long run, or the whole short run), each with an exclusive prefix. */
 template <int RCH>
 struct HmRunLds {
-    uint2 body[RCH];            /* (first vector index, vectors) */
-    uint32_t pre[RCH + 1];      /* exclusive prefix of body vectors */
-    uint2 piece[2 * RCH];       /* (first key index, keys), < HM_LONG_RUN keys each */
-    uint32_t ppre[2 * RCH + 1]; /* exclusive prefix of piece keys */
-    uint32_t nbody, npiece;
+    uint32_t bv[RCH], bn[RCH], pre[RCH + 1];
+    uint32_t ps[2 * RCH], pn[2 * RCH], ppre[2 * RCH + 1];
 };
 
-/* LDS slot of cell (r, c) = (r << w) | c of a row-major 2^w x 2^w histogram:
- * the column is rotated by 8 r, so a 2-D cluster of cells spreads over the 64
- * LDS banks instead of piling up on the few banks of its columns */
-__device__ __forceinline__ uint32_t hm_skew(uint32_t d, int w)
+/* one wave: pre[0..n] = exclusive prefix of in[0..n), pre[n] = total */
+__device__ __forceinline__ void hm_wave_prefix(const uint32_t* in, uint32_t n, uint32_t* pre)
 {
-    const uint32_t m = (1u << w) - 1u;
-    return (d & ~m) | ((d + ((d >> w) << 3)) & m);
-}
-
-__device__ __forceinline__ uint32_t hm_unskew(uint32_t j, int w)
-{
-    const uint32_t m = (1u << w) - 1u;
-    return (j & ~m) | ((j - ((j >> w) << 3)) & m);
-}
-
-/* wave-aggregated append of one entry per flagged lane to list[n++] */
-__device__ __forceinline__ void hm_lds_append(uint2* list, uint32_t* n, bool flag, uint2 e)
-{
-    const uint64_t m = __ballot(flag);
-    if (m == 0) return;
-    const int leader = __ffsll((unsigned long long)m) - 1;
-    uint32_t b = 0;
-    if (hm_lane() == leader) b = atomicAdd(n, (uint32_t)__popcll(m));
-    b = __builtin_amdgcn_readlane(b, leader);
-    if (flag) list[b + hm_mbcnt(m)] = e;
-}
-
-/* pre[0..n] = exclusive prefix of list[i].y, pre[n] = total (block-uniform) */
-template <int THREADS>
-__device__ __forceinline__ void hm_block_prefix(const uint2* list, uint32_t n, uint32_t* pre, uint32_t* scr)
-{
-    uint32_t carry = 0;
-    for (uint32_t i0 = 0; i0 < n; i0 += THREADS) {
-        const uint32_t i = i0 + threadIdx.x;
-        const uint32_t x = i < n ? list[i].y : 0u;
-        uint32_t tot;
-        const uint32_t ex = hm_block_excl_scan<THREADS>(x, scr, &tot);
-        if (i < n) pre[i] = carry + ex;
-        carry += tot;
+    const uint32_t lane = hm_lane();
+    const uint32_t per = (n + 63) / 64;
+    const uint32_t i0 = min(n, lane * per), i1 = min(n, i0 + per);
+    uint32_t sum = 0;
+    for (uint32_t i = i0; i < i1; i++) sum += in[i];
+    const uint32_t incl = hm_wave_incl_scan(sum);
+    uint32_t acc = incl - sum;
+    for (uint32_t i = i0; i < i1; i++) {
+        const uint32_t x = in[i];
+        pre[i] = acc;
+        acc += x;
     }
-    if (threadIdx.x == 0) pre[n] = carry;
-    __syncthreads();
+    if (lane == 63) pre[n] = incl;
 }
 
 #ifndef HM_SU
@@ -411,9 +404,10 @@ __device__ __forceinline__ void hm_block_prefix(const uint2* list, uint32_t n, u
  * bodies of runs with >= HM_LONG_RUN keys form one flat vector space, split
  * into contiguous per-wave spans; a lane keeps HM_SU 16-B loads in flight and
  * finds each vector's run by walking a monotone cursor over the body prefix.
- * Short runs and the bodies' unaligned heads and tails go one lane each (8
- * loads in flight).  Block-uniform: every thread calls. */
-template <typename InT, int THREADS, int RCH, typename F>
+ * Short runs and the bodies' unaligned heads and tails ("pieces") go either
+ * one lane each (8 loads in flight) or, COOP, 64 pieces per wave expanded
+ * into consecutive keys per lane.  Block-uniform: every thread calls. */
+template <typename InT, int THREADS, int RCH, bool COOP, typename F>
 __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __restrict__ keys, const HmRuns& in,
                                                HmRunLds<RCH>& L, uint32_t* scr, F& f)
 {
@@ -426,34 +420,28 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
     uint32_t carry = 0;                        /* keys staged by earlier chunks */
     for (uint32_t rc = it.r0; rc < it.r1; rc += RCH) {
         const uint32_t m = min((uint32_t)RCH, it.r1 - rc);
-        if (tid == 0) {
-            L.nbody = 0;
-            L.npiece = 0;
-        }
-        __syncthreads();
-        for (uint32_t i0 = 0; i0 < m; i0 += THREADS) {
-            const uint32_t i = i0 + tid;
-            uint32_t cnt = 0, src = 0;
-            if (i < m) {
-                const uint2 run = in.run[rc + i];
-                const uint64_t s = in.excl[rc + i];
-                const uint64_t e = s + run.y;
-                const uint64_t s2 = max(s, (uint64_t)it.a), e2 = min(e, (uint64_t)it.b);
-                cnt = e2 > s2 ? (uint32_t)(e2 - s2) : 0u;
-                src = run.x + (uint32_t)(s2 - s);
-            }
+        for (uint32_t i = tid; i < m; i += THREADS) {
+            const uint2 run = in.run[rc + i];
+            const uint64_t s = in.excl[rc + i];
+            const uint64_t e = s + run.y;
+            const uint64_t s2 = max(s, (uint64_t)it.a), e2 = min(e, (uint64_t)it.b);
+            const uint32_t cnt = e2 > s2 ? (uint32_t)(e2 - s2) : 0u;
+            const uint32_t src = run.x + (uint32_t)(s2 - s);
             const uint32_t head = min(cnt, (V - (src & (V - 1))) & (V - 1));
             const uint32_t nv = (cnt - head) / V;
             const bool lg = cnt >= HM_LONG_RUN && nv > 0;
-            const uint32_t tail = lg ? cnt - head - nv * V : 0u;
-            hm_lds_append(L.body, &L.nbody, lg, make_uint2((src + head) / V, nv));
-            hm_lds_append(L.piece, &L.npiece, lg ? head > 0 : cnt > 0, make_uint2(src, lg ? head : cnt));
-            hm_lds_append(L.piece, &L.npiece, tail > 0, make_uint2(src + head + nv * V, tail));
+            L.bv[i] = (src + head) / V;
+            L.bn[i] = lg ? nv : 0u;
+            L.ps[2 * i] = src;
+            L.pn[2 * i] = lg ? head : cnt;
+            L.ps[2 * i + 1] = src + head + nv * V;
+            L.pn[2 * i + 1] = lg ? cnt - head - nv * V : 0u;
         }
         __syncthreads();
-        const uint32_t nb = L.nbody, np = L.npiece;
-        hm_block_prefix<THREADS>(L.body, nb, L.pre, scr);
-        hm_block_prefix<THREADS>(L.piece, np, L.ppre, scr);
+        if (w == 0) hm_wave_prefix(L.bn, m, L.pre);
+        if (w == 1 || NW == 1) hm_wave_prefix(L.pn, 2 * m, L.ppre);
+        __syncthreads();
+        const uint32_t nb = m, np = 2 * m;
         const uint32_t total = L.pre[nb];
         const uint32_t pbase = carry + V * total;
         /* bodies: contiguous wave spans of the flat vector space */
@@ -471,25 +459,65 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
                     x[u] = make_uint4(0, 0, 0, 0);
                     if (ok[u]) {
                         while (L.pre[r + 1] <= v) r++;
-                        x[u] = kv[L.body[r].x + (v - L.pre[r])];
+#ifdef HM_EXP_NOLOAD
+                        x[u] = make_uint4(v, v * 3u, v * 5u, v * 7u);   /* timing experiment only */
+#else
+                        x[u] = kv[L.bv[r] + (v - L.pre[r])];
+#endif
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < HM_SU; u++) f.vec(x[u], ok[u], carry + V * (v0 + u * 64 + lane));
             }
         }
-        /* pieces: one lane each */
-        for (uint32_t q = tid; q < np; q += THREADS) {
-            const uint2 r = L.piece[q];
-            const uint32_t pq = pbase + L.ppre[q];
-            for (uint32_t k0 = 0; k0 < r.y; k0 += 8) {
-                uint32_t kk[8];
+        if (sizeof(InT) == 4 && rc == it.r0) HM_STAMP(5);
+        /* pieces: a wave takes 64 at a time, scans their lengths and hands
+         * consecutive keys to consecutive lanes (piece found by a 6-step
+         * shuffle search), 4 loads per lane in flight */
+        if (COOP) {
+        for (uint32_t q0 = (uint32_t)w * 64; q0 < np; q0 += NW * 64) {
+            const uint32_t q = q0 + lane;
+            const uint2 pc = q < np ? make_uint2(L.ps[q], L.pn[q]) : make_uint2(0, 0);
+            const uint32_t pp = q < np ? pbase + L.ppre[q] : 0u;
+            const uint32_t incl = hm_wave_incl_scan(pc.y);
+            const uint32_t tot = __shfl(incl, 63, 64);
+            for (uint32_t j0 = 0; j0 < tot; j0 += 256) {
+                uint32_t kk[4], at[4];
+                bool ok[4];
 #pragma unroll
-                for (int u = 0; u < 8; u++) kk[u] = (k0 + u < r.y) ? (uint32_t)keys[r.x + k0 + u] : 0u;
+                for (int u = 0; u < 4; u++) {
+                    const uint32_t j = j0 + u * 64 + lane;
+                    uint32_t lo = 0;
 #pragma unroll
-                for (int u = 0; u < 8; u++) f.key(kk[u], k0 + u < r.y, pq + k0 + u);
+                    for (int st = 32; st > 0; st >>= 1)
+                        if (__shfl(incl, lo + st - 1, 64) <= j) lo += st;
+                    lo = min(lo, 63u);
+                    const uint32_t cnt = __shfl(pc.y, lo, 64);
+                    const uint32_t off = j - (__shfl(incl, lo, 64) - cnt);
+                    ok[u] = j < tot;
+                    at[u] = __shfl(pp, lo, 64) + off;
+                    /* every shuffle outside the ok-branch: a shuffle under a
+                     * partial exec mask reads garbage from inactive lanes */
+                    const uint32_t src = __shfl(pc.x, lo, 64) + off;
+                    kk[u] = ok[u] ? (uint32_t)keys[src] : 0u;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; u++) f.key(kk[u], ok[u], at[u]);
             }
         }
+        } else {
+            for (uint32_t q = tid; q < np; q += THREADS) {
+                const uint32_t cnt = L.pn[q], src = L.ps[q], pq = pbase + L.ppre[q];
+                for (uint32_t k0 = 0; k0 < cnt; k0 += 8) {
+                    uint32_t kk[8];
+#pragma unroll
+                    for (int u = 0; u < 8; u++) kk[u] = (k0 + u < cnt) ? (uint32_t)keys[src + k0 + u] : 0u;
+#pragma unroll
+                    for (int u = 0; u < 8; u++) f.key(kk[u], k0 + u < cnt, pq + k0 + u);
+                }
+            }
+        }
+        if (sizeof(InT) == 4 && rc == it.r0) HM_STAMP(6);
         carry = pbase + L.ppre[np];
         __syncthreads();
     }
@@ -509,40 +537,50 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     __shared__ uint32_t dummy[64];
     __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
     __shared__ HmRunLds<512> L;
+    HM_STAMP(0);
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
     __syncthreads();
+    HM_STAMP(1);
     const HmItem it = hm_item(a.parent, blockIdx.x);
     /* parent key: (row << sp) | col, sp = s + w bits each; digit = top w bits
-     * of both, rest = low s bits of both */
+     * of both, rest = low s bits of both.  Streaming re-encodes every key as
+     * (digit << 2s) | rest (still <= 32 bits), so the scatter only shifts. */
     const int sw = a.restbits >> 1, ww = a.dbits >> 1, sp = sw + ww;
-    const uint32_t lowm = (1u << sw) - 1u;
+    const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
     struct {
         uint32_t* cur;
         uint32_t* dummy;
         uint32_t* stage;
         int s, w, sp;
-        /* skewed LDS slot of the key's digit */
-        __device__ __forceinline__ uint32_t digit(uint32_t k) const
+        __device__ __forceinline__ uint32_t pack(uint32_t k) const
         {
-            return hm_skew(((k >> (sp + s)) << w) | ((k & ((1u << sp) - 1u)) >> s), w);
+            const uint32_t r = k >> sp, c = k & ((1u << sp) - 1u), m = (1u << s) - 1u;
+            const uint32_t d = ((r >> s) << w) | (c >> s);
+            return (d << (2 * s)) | ((r & m) << s) | (c & m);
         }
         __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t pos)
         {
-            hm_lds_count(cur, dummy, digit(k), v);
-            stage[v ? pos : HM_TN + hm_lane()] = k;
+            const uint32_t x = pack(k);
+            hm_lds_count(cur, dummy, x >> (2 * s), v);
+            stage[v ? pos : HM_TN + hm_lane()] = x;
         }
-        __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t pos)
+        __device__ __forceinline__ void vec(const uint4& k, bool v, uint32_t pos)
         {
-            hm_lds_count(cur, dummy, digit(x.x), v);
-            hm_lds_count(cur, dummy, digit(x.y), v);
-            hm_lds_count(cur, dummy, digit(x.z), v);
-            hm_lds_count(cur, dummy, digit(x.w), v);
+            const uint4 x = make_uint4(pack(k.x), pack(k.y), pack(k.z), pack(k.w));
+#ifndef HM_EXP_NOCOUNT
+            hm_lds_count(cur, dummy, x.x >> (2 * s), v);
+            hm_lds_count(cur, dummy, x.y >> (2 * s), v);
+            hm_lds_count(cur, dummy, x.z >> (2 * s), v);
+            hm_lds_count(cur, dummy, x.w >> (2 * s), v);
+#endif
             *(uint4*)&stage[v ? pos : HM_TN] = x;
         }
     } f{cur, dummy, stage, sw, ww, sp};
-    hm_stream_runs<uint32_t, HM_PN_THREADS, 512>(it, a.keys_in, a.in, L, scr, f);
+    HM_STAMP(2);
+    hm_stream_runs<uint32_t, HM_PN_THREADS, 512, true>(it, a.keys_in, a.in, L, scr, f);
+    HM_STAMP(7);
     const uint32_t total = it.b - it.a;
     constexpr int PER = HM_MAX_FN / HM_PN_THREADS;
     uint32_t cnt[PER];
@@ -555,11 +593,12 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     }
     uint32_t tot2;
     uint32_t off = hm_block_excl_scan<HM_PN_THREADS>(s, scr, &tot2);
-    /* cur[] slots are skewed digits (hm_skew): the run records and counters
-     * use the digit itself */
+    HM_STAMP(8);
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
     const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
     const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
+    /* run-slot atomics are issued here and their results consumed only after
+     * the scatter, so their latency hides behind it */
     uint32_t idx[PER];
     uint32_t offq[PER];
 #pragma unroll
@@ -567,21 +606,18 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         const int d = tid * PER + q;
         offq[q] = off;
         idx[q] = 0;
+#ifdef HM_EXP_NOATOM
+        idx[q] = it.j >> a.shard_bits;   /* timing experiment only: counters stay 0 */
+#else
         if (d < F && cnt[q])
-            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + hm_unskew(d, ww)) << a.shard_bits) + sh],
-                               1u);
+            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
+#endif
         off += cnt[q];
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F) {
-            cur[d] = offq[q];
-            if (cnt[q]) {
-                const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, hm_unskew(d, ww), a.dbits, a.shard_bits);
-                a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);
-            }
-        }
+        if (d < F) cur[d] = offq[q];
     }
     constexpr int KPT = HM_TN / HM_PN_THREADS;
     uint32_t kv[KPT];
@@ -591,18 +627,48 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         kv[k] = i < total ? stage[i] : 0u;
     }
     __syncthreads();
+    HM_STAMP(9);
     OutT* so = (OutT*)stage;
+    /* claim: every slot atomic issued before any result is consumed (the
+     * helper's logic of hm_lds_claim, unrolled over the KPT keys) */
+    {
+        uint32_t old[KPT], rk[KPT];
+        uint64_t mk[KPT];
+        bool same[KPT], v[KPT];
 #pragma unroll
-    for (int k = 0; k < KPT; k++) {
-        const uint32_t i = k * HM_PN_THREADS + tid;
-        const bool v = i < total;
-        const uint32_t pos = hm_lds_claim(cur, dummy, f.digit(kv[k]), v);
-        const uint32_t rr = kv[k] >> sp, cc = kv[k] & ((1u << sp) - 1u);
-        so[v ? pos : HM_TN + tid % 64] = (OutT)(((rr & lowm) << sw) | (cc & lowm));
+        for (int k = 0; k < KPT; k++) {
+            v[k] = k * HM_PN_THREADS + tid < total;
+            const uint32_t d = kv[k] >> a.restbits;
+            const uint32_t k0 = __builtin_amdgcn_readfirstlane(d);
+            same[k] = v[k] && d == k0;
+            mk[k] = __ballot(same[k]);
+            rk[k] = hm_mbcnt(mk[k]);
+            const bool lead = same[k] && rk[k] == 0;
+            const bool own = v[k] && !same[k];
+            uint32_t* p = lead ? &cur[k0] : (own ? &cur[d] : &dummy[hm_lane()]);
+            old[k] = atomicAdd(p, lead ? (uint32_t)__popcll(mk[k]) : (uint32_t)own);
+        }
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            const uint32_t base =
+                __builtin_amdgcn_readlane(old[k], mk[k] ? __ffsll((unsigned long long)mk[k]) - 1 : 0);
+            const uint32_t pos = same[k] ? base + rk[k] : old[k];
+            so[v[k] ? pos : HM_TN + tid % 64] = (OutT)(kv[k] & restmask);
+        }
     }
     __syncthreads();
+    HM_STAMP(10);
     OutT* out = (OutT*)a.keys_out + it.a;
     for (uint32_t i = tid; i < total; i += HM_PN_THREADS) out[i] = so[i];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F && cnt[q]) {
+            const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
+            a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);
+        }
+    }
+    HM_STAMP(11);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -997,7 +1063,8 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
     for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
     const HmItem it = hm_item(a.B, blockIdx.x);
-    /* counted at skewed slots (hm_skew), un-skewed before the pyramid */
+    /* counted at skewed slots (hm_skew), un-skewed before the pyramid
+     * (measured neutral on hotspot data; kept for the column-clustered case) */
     struct {
         uint32_t* grid;
         uint32_t* dummy;
@@ -1015,7 +1082,7 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
             hm_lds_count(grid, dummy, hm_skew(x.w >> 16, lg), v);
         }
     } f{grid, dummy, a.lg};
-    hm_stream_runs<uint16_t, HM_AG_THREADS, 256>(it, a.keys, a.in, L, scr, f);
+    hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);
     {
         constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;
         uint32_t x[CPT];

@@ -14,8 +14,12 @@
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
 /* levels >= 2 */
+#ifndef HM_PN_THREADS
 #define HM_PN_THREADS 1024
+#endif
+#ifndef HM_TN
 #define HM_TN 8192                          /* keys per partition work item */
+#endif
 #define HM_LEVEL_ZOOMS 6                    /* <= 6 zooms per level */
 #define HM_MAX_FN 4096
 #define HM_MAX_SHARDS 32                    /* run-counter shards per child */

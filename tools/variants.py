@@ -19,7 +19,7 @@ VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
 
 VARIANTS = {
     "base": [],
-    "oldlds": ["HM_OLD_LDS=1"],
+    "stamps": ["HM_STAMPS=1"],
 }
 
 
