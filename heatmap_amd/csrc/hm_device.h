@@ -105,9 +105,12 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
  * costs one atomic, not 64 serialised ones); every other valid lane adds 1 to
  * its own key; lanes with nothing to add hit a private dummy slot, so no
  * branch, leader election loop or exec-mask juggling is needed -- those made
- * the partition kernels scalar-issue bound.  `dummy` is 64 words of LDS. */
+ * the partition kernels scalar-issue bound.  `dummy` is the index of 64
+ * spare words at the end of the same array (an index select, not a pointer
+ * select, and non-short-circuit logic: either of those makes the compiler
+ * emit exec-mask branches). */
 #ifdef HM_OLD_LDS
-__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t*, uint32_t key, bool valid)
+__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t, uint32_t key, bool valid)
 {
     const uint64_t vm = __ballot(valid);
     if (vm == 0) return;
@@ -120,7 +123,7 @@ __device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t*, uint32_t
     }
 }
 
-__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t*, uint32_t key, bool valid)
+__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t, uint32_t key, bool valid)
 {
     const uint64_t vm = __ballot(valid);
     if (vm == 0) return 0;
@@ -137,29 +140,30 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t*, uint3
     return pos;
 }
 #else
-__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t* dummy, uint32_t key, bool valid)
+__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t dummy, uint32_t key, bool valid)
 {
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
-    const bool same = valid && key == k0;
-    const uint64_t m = __ballot(same);
-    const bool lead = same && hm_mbcnt(m) == 0;
-    const bool own = valid && !same;
-    uint32_t* p = lead ? &hist[k0] : (own ? &hist[key] : &dummy[hm_lane()]);
-    const uint32_t inc = lead ? (uint32_t)__popcll(m) : (uint32_t)own;
-    atomicAdd(p, inc);
-}
-
-__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t* dummy, uint32_t key, bool valid)
-{
-    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
-    const bool same = valid && key == k0;
+    const bool same = valid & (key == k0);
     const uint64_t m = __ballot(same);
     const uint32_t r = hm_mbcnt(m);
-    const bool lead = same && r == 0;
-    const bool own = valid && !same;
-    uint32_t* p = lead ? &cur[k0] : (own ? &cur[key] : &dummy[hm_lane()]);
+    const bool lead = same & (r == 0);
+    const bool own = valid & !same;
+    const uint32_t i = lead ? k0 : (own ? key : dummy + (uint32_t)hm_lane());
     const uint32_t inc = lead ? (uint32_t)__popcll(m) : (uint32_t)own;
-    const uint32_t old = atomicAdd(p, inc);
+    atomicAdd(&hist[i], inc);
+}
+
+__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t dummy, uint32_t key, bool valid)
+{
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    const bool same = valid & (key == k0);
+    const uint64_t m = __ballot(same);
+    const uint32_t r = hm_mbcnt(m);
+    const bool lead = same & (r == 0);
+    const bool own = valid & !same;
+    const uint32_t i = lead ? k0 : (own ? key : dummy + (uint32_t)hm_lane());
+    const uint32_t inc = lead ? (uint32_t)__popcll(m) : (uint32_t)own;
+    const uint32_t old = atomicAdd(&cur[i], inc);
     const uint32_t base = __builtin_amdgcn_readlane(old, m ? __ffsll((unsigned long long)m) - 1 : 0);
     return same ? base + r : old;
 }

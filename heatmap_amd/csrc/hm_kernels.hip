@@ -93,8 +93,7 @@ __global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat,
 template <typename OutT, int MODE>
 __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args a)
 {
-    __shared__ uint32_t cur[HM_MAX_F1];
-    __shared__ uint32_t dummy[64];
+    __shared__ uint32_t cur[HM_MAX_F1 + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ OutT stage[HM_T1 + 64];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
     __shared__ double tab[HM_YTAB_N];
@@ -239,7 +238,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, dummy, dig[k], dig[k] != 0xFFFFFFFFu);
+    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, HM_MAX_F1, dig[k], dig[k] != 0xFFFFFFFFu);
     __syncthreads();
 
     /* exclusive scan of the digit histogram; one run record per digit */
@@ -277,7 +276,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT; k++) {
         const bool v = dig[k] != 0xFFFFFFFFu;
-        const uint32_t pos = hm_lds_claim(cur, dummy, dig[k], v);
+        const uint32_t pos = hm_lds_claim(cur, HM_MAX_F1, dig[k], v);
         stage[v ? pos : HM_T1 + hm_lane()] = (OutT)rest[k];
     }
     __syncthreads();
@@ -533,8 +532,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     /* streamed keys in staged order, then the digit-sorted output (OutT);
      * words [HM_TN, HM_TN + 64) absorb the writes of idle lanes */
     __shared__ __attribute__((aligned(16))) uint32_t stage[HM_TN + 64];
-    __shared__ uint32_t cur[HM_MAX_FN];
-    __shared__ uint32_t dummy[64];
+    __shared__ uint32_t cur[HM_MAX_FN + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
     __shared__ HmRunLds<512> L;
     HM_STAMP(0);
@@ -551,7 +549,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
     struct {
         uint32_t* cur;
-        uint32_t* dummy;
+        uint32_t dummy;
         uint32_t* stage;
         int s, w, sp;
         __device__ __forceinline__ uint32_t pack(uint32_t k) const
@@ -568,7 +566,14 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         }
         __device__ __forceinline__ void vec(const uint4& k, bool v, uint32_t pos)
         {
+#ifdef HM_EXP_NOCONFLICT
+            /* timing experiment only: digit's low 6 bits replaced by the lane id */
+            const uint32_t sm = 2 * s, lm = ((uint32_t)hm_lane()) << sm, hm = ~(63u << sm);
+            const uint4 x = make_uint4((pack(k.x) & hm) | lm, (pack(k.y) & hm) | lm, (pack(k.z) & hm) | lm,
+                                       (pack(k.w) & hm) | lm);
+#else
             const uint4 x = make_uint4(pack(k.x), pack(k.y), pack(k.z), pack(k.w));
+#endif
 #ifndef HM_EXP_NOCOUNT
             hm_lds_count(cur, dummy, x.x >> (2 * s), v);
             hm_lds_count(cur, dummy, x.y >> (2 * s), v);
@@ -577,7 +582,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
 #endif
             *(uint4*)&stage[v ? pos : HM_TN] = x;
         }
-    } f{cur, dummy, stage, sw, ww, sp};
+    } f{cur, HM_MAX_FN, stage, sw, ww, sp};
     HM_STAMP(2);
     hm_stream_runs<uint32_t, HM_PN_THREADS, 512, true>(it, a.keys_in, a.in, L, scr, f);
     HM_STAMP(7);
@@ -640,13 +645,13 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
             v[k] = k * HM_PN_THREADS + tid < total;
             const uint32_t d = kv[k] >> a.restbits;
             const uint32_t k0 = __builtin_amdgcn_readfirstlane(d);
-            same[k] = v[k] && d == k0;
+            same[k] = v[k] & (d == k0);
             mk[k] = __ballot(same[k]);
             rk[k] = hm_mbcnt(mk[k]);
-            const bool lead = same[k] && rk[k] == 0;
-            const bool own = v[k] && !same[k];
-            uint32_t* p = lead ? &cur[k0] : (own ? &cur[d] : &dummy[hm_lane()]);
-            old[k] = atomicAdd(p, lead ? (uint32_t)__popcll(mk[k]) : (uint32_t)own);
+            const bool lead = same[k] & (rk[k] == 0);
+            const bool own = v[k] & !same[k];
+            const uint32_t ci = lead ? k0 : (own ? d : HM_MAX_FN + (uint32_t)hm_lane());
+            old[k] = atomicAdd(&cur[ci], lead ? (uint32_t)__popcll(mk[k]) : (uint32_t)own);
         }
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
@@ -1053,10 +1058,9 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
 
 __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
 {
-    __shared__ uint32_t grid[HM_AG_CELLS];
+    __shared__ uint32_t grid[HM_AG_CELLS + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
-    __shared__ uint32_t dummy[64];
     __shared__ HmRunLds<256> L;
     const int tid = threadIdx.x;
     const uint32_t ncell = 1u << (2 * a.lg);
@@ -1067,7 +1071,7 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
      * (measured neutral on hotspot data; kept for the column-clustered case) */
     struct {
         uint32_t* grid;
-        uint32_t* dummy;
+        uint32_t dummy;
         int lg;
         __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { hm_lds_count(grid, dummy, hm_skew(k, lg), v); }
         __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t)
@@ -1081,7 +1085,7 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
             hm_lds_count(grid, dummy, hm_skew(x.w & 0xFFFFu, lg), v);
             hm_lds_count(grid, dummy, hm_skew(x.w >> 16, lg), v);
         }
-    } f{grid, dummy, a.lg};
+    } f{grid, HM_AG_CELLS, a.lg};
     hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);
     {
         constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;

@@ -19,7 +19,17 @@ VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
 
 VARIANTS = {
     "base": [],
-    "stamps": ["HM_STAMPS=1"],
+    "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py
+    # timing-only experiments (results wrong, every access stays in bounds)
+    "noload": ["HM_EXP_NOLOAD=1"],
+    "noatom": ["HM_EXP_NOATOM=1"],
+    "noclaim": ["HM_EXP_NOCLAIM=1"],
+    "nocount": ["HM_EXP_NOCOUNT=1"],
+    "noconflict": ["HM_EXP_NOCONFLICT=1"],
+    # tuning
+    "t512_8k": ["HM_PN_THREADS=512"],
+    "su2": ["HM_SU=2"],
+    "su8": ["HM_SU=8"],
 }
 
 
@@ -62,7 +72,7 @@ def one(name, points, steps, zmax):
 
 def main():
     cmd = sys.argv[1]
-    names = sys.argv[2:] or list(VARIANTS)
+    names = sys.argv[2:] or ["base"]
     if cmd == "build":
         build(names)
     elif cmd == "run":
