@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=float, default=2e8,
                     help="points timed on the CPU oracle, ~10-30 s of host work (0 = skip)")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the RCCL merge path even with one rank (rehearsal of the N>1 code)")
     return ap.parse_args()
 
 
@@ -58,7 +60,8 @@ def dist_init(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if ws > 1:
+    args.dist = ws > 1 or args.force_dist
+    if args.dist:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -67,7 +70,9 @@ def dist_init(args):
 
 
 def barrier(ws):
-    if ws > 1:
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
         import torch.distributed as dist
 
         dist.barrier()
@@ -133,7 +138,7 @@ def main():
 
     def step():
         m, b = device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=bufs)
-        if ws > 1:
+        if args.dist:
             m = multigpu.merge_cells(b, m, ws, rank)
         return m, b
 
@@ -151,7 +156,7 @@ def main():
     torch.cuda.synchronize()
     barrier(ws)
     dt = time.perf_counter() - t0
-    if ws > 1:
+    if args.dist:
         import torch.distributed as dist
 
         t = torch.tensor([dt, float(m)], dtype=torch.float64, device="cuda")
@@ -161,10 +166,15 @@ def main():
     else:
         cells = int(m)
     check = None
-    if not args.no_check and ws == 1:
-        # every zoom's counts sum to the number of points
-        tot = int(bufs.counts[:m].sum().item())
-        check = "ok" if tot == per * (args.zmax - args.zmin + 1) else "FAIL sum %d" % tot
+    if not args.no_check:
+        # every zoom's counts sum to the number of points (over all ranks' owned cells)
+        tot_t = bufs.counts[:m].sum().reshape(1)
+        if args.dist:
+            import torch.distributed as dist
+
+            dist.all_reduce(tot_t)
+        tot = int(tot_t.item())
+        check = "ok" if tot == per * ws * (args.zmax - args.zmin + 1) else "FAIL sum %d" % tot
     ms = dt / args.steps * 1e3
     total_points = per * ws
     k1_us = float(np.mean(k1))

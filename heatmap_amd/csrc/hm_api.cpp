@@ -439,6 +439,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.keys_out = kout;
             a.nruns_out = nruns;
             a.runs_out = runs_sh;
+            a.items = lv[l - 1].items;
             hm_launch_partN(s, a, lv[l - 1].items, V.out16);
             HIPCHK(hipGetLastError());
         }
@@ -590,6 +591,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         a.gslots = gslots;
         a.slot_bucket = slot_bucket;
         a.out = o;
+        a.items = lv[l].items;
+        a.nslots = nslots;
         hm_launch_aggregate(s, a, lv[l].items, nslots);
         HIPCHK(hipGetLastError());
     }
@@ -608,6 +611,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         pa.parent_coord = l ? B[l - 1].coord : nullptr;
         pa.parent_totals = l ? totals[l - 1] : nullptr;
         pa.out = o;
+        pa.nparents = lv[l].nparents;
         hm_launch_pool(s, pa, lv[l].nparents);
         HIPCHK(hipGetLastError());
     }

@@ -37,6 +37,9 @@ __device__ __forceinline__ T hm_sum4(const T* v, uint32_t i, int lgn)
     return (T)(v[j] + v[j + 1] + v[j + side] + v[j + side + 1]);
 }
 
+/* linear block id of a 2-D grid (hm_grid2) */
+__device__ __forceinline__ uint32_t hm_block_id() { return blockIdx.y * gridDim.x + blockIdx.x; }
+
 /* ---- wave helpers ---- */
 __device__ __forceinline__ int hm_lane() { return (int)__lane_id(); }
 

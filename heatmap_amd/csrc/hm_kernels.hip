@@ -41,8 +41,8 @@
 __device__ unsigned long long g_stamps[HM_STAMP_BLOCKS * 12];
 #define HM_STAMP(k)                                                                            \
     do {                                                                                       \
-        if (threadIdx.x == 0 && blockIdx.x < HM_STAMP_BLOCKS)                                  \
-            g_stamps[blockIdx.x * 12 + (k)] = __builtin_amdgcn_s_memtime();                    \
+        if (threadIdx.x == 0 && hm_block_id() < HM_STAMP_BLOCKS)                               \
+            g_stamps[hm_block_id() * 12 + (k)] = __builtin_amdgcn_s_memtime();                 \
     } while (0)
 extern "C" int hm_debug_stamps(void* host, size_t bytes)
 {
@@ -541,7 +541,8 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     for (int i = tid; i < F; i += HM_PN_THREADS) cur[i] = 0;
     __syncthreads();
     HM_STAMP(1);
-    const HmItem it = hm_item(a.parent, blockIdx.x);
+    if (hm_block_id() >= a.items) return;
+    const HmItem it = hm_item(a.parent, hm_block_id());
     /* parent key: (row << sp) | col, sp = s + w bits each; digit = top w bits
      * of both, rest = low s bits of both.  Streaming re-encodes every key as
      * (digit << 2s) | rest (still <= 32 bits), so the scatter only shifts. */
@@ -1066,7 +1067,8 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
     const uint32_t ncell = 1u << (2 * a.lg);
     for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
-    const HmItem it = hm_item(a.B, blockIdx.x);
+    if (hm_block_id() >= a.items) return;   /* block-uniform */
+    const HmItem it = hm_item(a.B, hm_block_id());
     /* counted at skewed slots (hm_skew), un-skewed before the pyramid
      * (measured neutral on hotspot data; kept for the column-clustered case) */
     struct {
@@ -1124,8 +1126,9 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
     const uint32_t ncell = 1u << (2 * a.lg);
-    const uint32_t b = a.slot_bucket[blockIdx.x];
-    const uint32_t* g = a.gslots + (uint64_t)blockIdx.x * HM_AG_CELLS;
+    if (hm_block_id() >= a.nslots) return;
+    const uint32_t b = a.slot_bucket[hm_block_id()];
+    const uint32_t* g = a.gslots + (uint64_t)hm_block_id() * HM_AG_CELLS;
     for (uint32_t i = threadIdx.x; i < ncell; i += HM_AG_THREADS) grid[i] = g[i];
     __syncthreads();
     hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[b], a.out, scr, &sbase);
@@ -1140,7 +1143,8 @@ __global__ __launch_bounds__(HM_POOL_THREADS) void k_pool(HmPoolArgs a)
     __shared__ unsigned long long v[HM_MAX_FN];
     __shared__ uint32_t scr[HM_POOL_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
-    const uint32_t p = blockIdx.x;
+    const uint32_t p = hm_block_id();
+    if (p >= a.nparents) return;
     const uint32_t F = 1u << a.dbits;
     for (uint32_t i = threadIdx.x; i < F; i += HM_POOL_THREADS) v[i] = 0;
     __syncthreads();
@@ -1228,9 +1232,9 @@ void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool o
 {
     if (items == 0) return;
     if (out16)
-        hipLaunchKernelGGL(k_partition<uint16_t>, dim3(items), dim3(HM_PN_THREADS), 0, s, a);
+        hipLaunchKernelGGL(k_partition<uint16_t>, hm_grid2(items), dim3(HM_PN_THREADS), 0, s, a);
     else
-        hipLaunchKernelGGL(k_partition<uint32_t>, dim3(items), dim3(HM_PN_THREADS), 0, s, a);
+        hipLaunchKernelGGL(k_partition<uint32_t>, hm_grid2(items), dim3(HM_PN_THREADS), 0, s, a);
 }
 
 static unsigned hm_grid(uint64_t n, unsigned per, unsigned cap)
@@ -1277,12 +1281,12 @@ void hm_launch_compact(hipStream_t s, const HmCompactArgs& a)
 
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots)
 {
-    if (items) hipLaunchKernelGGL(k_aggregate, dim3(items), dim3(HM_AG_THREADS), 0, s, a);
-    if (nslots) hipLaunchKernelGGL(k_aggregate_merged, dim3(nslots), dim3(HM_AG_THREADS), 0, s, a);
+    if (items) hipLaunchKernelGGL(k_aggregate, hm_grid2(items), dim3(HM_AG_THREADS), 0, s, a);
+    if (nslots) hipLaunchKernelGGL(k_aggregate_merged, hm_grid2(nslots), dim3(HM_AG_THREADS), 0, s, a);
 }
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {
-    if (nparents) hipLaunchKernelGGL(k_pool, dim3(nparents), dim3(HM_POOL_THREADS), 0, s, a);
+    if (nparents) hipLaunchKernelGGL(k_pool, hm_grid2(nparents), dim3(HM_POOL_THREADS), 0, s, a);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -52,6 +52,15 @@ __host__ __device__ inline uint64_t hm_run_base(uint64_t t0, uint64_t tp, uint64
     return ((t0 + S * p) << dbits) + d * (cap << shard_bits);
 }
 
+/* Grids with one block per item can exceed the 2^32 work-items a 1-D
+ * dispatch allows (4M buckets x 1024 threads): they are 2-D, <= 65536 blocks
+ * in x; kernels read their linear block id with hm_block_id(). */
+inline dim3 hm_grid2(uint32_t nblocks)
+{
+    const uint32_t x = nblocks < 65536u ? (nblocks ? nblocks : 1u) : 65536u;
+    return dim3(x, (nblocks + x - 1) / x);
+}
+
 /* Flat run list of a level: run j holds cnt = run[j].y keys starting at key
  * index run[j].x of the level's key array; its keys are the global logical
  * positions [excl[j], excl[j] + cnt) (exclusive prefix over all runs).  The
@@ -117,6 +126,7 @@ struct HmPartNArgs {
     const uint32_t* keys_in;
     HmRuns in;
     int dbits, restbits, shard_bits;
+    uint32_t items;             /* blocks of the (2-D) grid that have an item */
     void* keys_out;             /* item g writes its keys at its positions [a, b) */
     uint32_t* nruns_out;
     uint2* runs_out;
@@ -177,6 +187,7 @@ struct HmAggArgs {
     const uint16_t* keys;
     HmRuns in;
     int Z, lg;
+    uint32_t items, nslots;     /* blocks with work in the (2-D) grids */
     unsigned long long* totals;
     uint32_t* gslots;
     const uint32_t* slot_bucket;
@@ -185,6 +196,7 @@ struct HmAggArgs {
 
 struct HmPoolArgs {
     int dbits, z_child, emit_root;
+    uint32_t nparents;
     const uint32_t* child_begin;
     const uint32_t* child_digit;
     const unsigned long long* child_totals;
