@@ -454,6 +454,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ra.runs = runs_sh;
         ra.parent_item_begin = parent_item_begin;
         ra.item_keys = (l == L - 1) ? HM_TA : HM_TN;
+        ra.sparse_max = (l == L - 1) ? HM_SP_MAX : 0u;
         uint64_t *partial, *tot;
         ENSURE(B_SHOFF, (V.nchildren << sb) * sizeof(uint32_t), ra.shoff);
         ENSURE(B_NR, V.nchildren * sizeof(uint64_t), ra.nr);

@@ -30,6 +30,13 @@
 #ifndef HM_TA
 #define HM_TA (1u << 18)                    /* keys per aggregation work item */
 #endif
+/* sparse final buckets (k_aggregate_sparse): u16 level grids, 2 cells/word */
+#define HM_SP_THREADS 512
+#ifndef HM_SP_MAX
+#define HM_SP_MAX 2048
+#endif
+#define HM_SP_WORDS ((HM_AG_CELLS / 3 * 4 + 1) / 2 + 1)   /* 4^7 + ... + 4 cells */
+#define HM_SP_GRID (256 * 3 * 4)
 #define HM_POOL_THREADS 256
 #define HM_MAX_LEVELS 4
 #define HM_COUNT_MAX_ZOOM 21                /* level-1 keys 2*(Z-5) bits fit u32 */
@@ -148,6 +155,7 @@ struct HmRsArgs {
     uint64_t nflat;             /* total runs */
     const uint64_t* total_keys;
     uint32_t item_keys;
+    uint32_t sparse_max;        /* last level: buckets of <= this many keys get no work items */
     uint32_t* nkeys;            /* [nchildren] */
     uint32_t* keybase;          /* [nchildren] */
     uint64_t* vals;             /* [nchildren] (1 << 32 | items) for non-empty children */
