@@ -85,7 +85,7 @@ enum {
     B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
     B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
     B_SLOTS = B_TOT0 + HM_MAX_LEVELS + 1,
-    B_SLOTBKT, B_GSLOTS, B_DESC0, B_COUNT = B_DESC0 + HM_MAX_LEVELS
+    B_SLOTBKT, B_GSLOTS, B_SPCODES, B_DESC0, B_COUNT = B_DESC0 + HM_MAX_LEVELS
 };
 
 static int ensure(hm_ctx* c, int slot, size_t bytes, void** out)
@@ -594,7 +594,19 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         a.out = o;
         a.items = lv[l].items;
         a.nslots = nslots;
+        const uint64_t cnt = (uint64_t)lv[l].count + 1;
+        uint64_t *spcnt, *spoff, *sptot, *partial;
+        ENSURE(B_VALS, cnt * 8, spcnt);
+        ENSURE(B_PREFIX, cnt * 8, spoff);
+        ENSURE(B_TOTAL, 4 * sizeof(uint64_t), sptot);
+        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+        ENSURE(B_SPCODES, (level_keys + 8) * 2, a.codes);
+        a.spcnt = spcnt;
+        a.spoff = spoff;
+        a.sptotal = sptot;
+        a.spbase = (unsigned long long*)(sptot + 1);
         hm_launch_aggregate(s, a, lv[l].items, nslots);
+        hm_launch_small(s, a, partial);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(ev[nev++], s));

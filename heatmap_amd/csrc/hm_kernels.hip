@@ -1177,7 +1177,7 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
     const uint32_t nblk = gridDim.x * gridDim.y;
     for (uint32_t b = hm_block_id(); b < a.B.count; b += nblk) {
         const uint32_t nk = a.B.nkeys[b];
-        if (nk > HM_SP_MAX) continue;   /* block-uniform: a dense bucket */
+        if (nk > HM_SP_MAX || nk <= HM_SPW_MAX) continue;   /* block-uniform: dense or small */
         HmItem it;
         it.bucket = b;
         it.j = 0;
@@ -1239,10 +1239,17 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
         uint32_t cnt = 0;
 #pragma unroll
         for (int m = 0; m < KPT; m++) cnt += __popc(own[m] & zmask);
+#ifdef HM_EXP_SPNOEMIT
+        cnt = 0;   /* timing experiment only */
+#endif
         uint32_t tot;
         uint32_t pos = hm_block_excl_scan<HM_SP_THREADS>(cnt, scr, &tot);
         if (tot) {
+#ifdef HM_EXP_SPNOATOM
+            if (tid == 0) sbase = ((uint64_t)b * 1024u) % (a.out.capacity > 16384 ? a.out.capacity - 16384 : 1);
+#else
             if (tid == 0) sbase = atomicAdd(a.out.cursor, (unsigned long long)tot);
+#endif
             __syncthreads();
             const uint64_t base = sbase;
             const uint64_t coord = a.B.coord[b];
@@ -1277,6 +1284,286 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
     }
 }
 
+/* ------------------------------------------------------------------------ */
+/* final level, small buckets (<= HM_SPW_MAX keys): one wavefront per bucket  */
+/* ------------------------------------------------------------------------ */
+
+__device__ __forceinline__ uint32_t hm_spread7(uint32_t x)
+{
+    x = (x | (x << 4)) & 0x0F0Fu;
+    x = (x | (x << 2)) & 0x3333u;
+    return (x | (x << 1)) & 0x5555u;
+}
+__device__ __forceinline__ uint32_t hm_compact7(uint32_t x)
+{
+    x &= 0x5555u;
+    x = (x | (x >> 1)) & 0x3333u;
+    x = (x | (x >> 2)) & 0x0F0Fu;
+    return (x | (x >> 4)) & 0x00FFu;
+}
+
+/* Ascending bitonic sort of the wave's 64*K values, element e = lane*K + u in
+ * v[u]: distances < K swap registers, larger ones exchange across lanes. */
+template <int K>
+__device__ __forceinline__ void hm_wave_bitonic(uint32_t (&v)[K])
+{
+    const uint32_t lane = hm_lane();
+#pragma unroll
+    for (uint32_t size = 2; size <= 64u * K; size <<= 1) {
+#pragma unroll
+        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
+            if (stride >= (uint32_t)K) {
+#pragma unroll
+                for (int u = 0; u < K; u++) {
+                    const uint32_t e = lane * K + u;
+                    const uint32_t o = __shfl_xor(v[u], (int)(stride / K), 64);
+                    const bool take_min = ((e & stride) == 0) == ((e & size) == 0);
+                    v[u] = take_min ? min(v[u], o) : max(v[u], o);
+                }
+            } else {
+#pragma unroll
+                for (int u = 0; u < K; u++) {
+                    if ((u & stride) == 0) {
+                        const int w = u | (int)stride;
+                        const bool up = ((lane * K + u) & size) == 0;
+                        const uint32_t lo = min(v[u], v[w]), hi = max(v[u], v[w]);
+                        v[u] = up ? lo : hi;
+                        v[w] = up ? hi : lo;
+                    }
+                }
+            }
+        }
+    }
+}
+
+/* Small buckets run in two passes so that the output needs no per-bucket
+ * cursor atomic (4M buckets would serialise on it at ~12 ns each):
+ *   pass 1 (k_small_sort): a wave gathers a bucket's keys, re-codes them in
+ *     Morton order inside the bucket, sorts them (Morton parents preserve the
+ *     order, so the cells of level l are the runs of equal code >> 2l), stores
+ *     the sorted codes at the bucket's own key range and counts its cells;
+ *   an exclusive scan of the counts places every bucket's cells;
+ *   pass 2 (k_small_emit): re-reads the sorted codes (coalesced) and writes
+ *     each cell at its place; a cell is written by its last element, its count
+ *     is that position minus the segment start (a wave max-scan). */
+
+template <int K>
+__device__ __forceinline__ void hm_small_load(const uint16_t* src, uint32_t nk, uint32_t (&v)[K])
+{
+    const uint32_t lane = hm_lane();
+#pragma unroll
+    for (int u = 0; u < K; u++) {
+        const uint32_t e = lane * K + u;
+        v[u] = e < nk ? (uint32_t)src[e] : 0xFFFFFFFFu;
+    }
+}
+
+/* last element of its level-l cell (valid elements only) */
+template <int K>
+__device__ __forceinline__ void hm_small_ends(const uint32_t (&v)[K], uint32_t nk, int l, bool (&end)[K])
+{
+    const uint32_t lane = hm_lane();
+    const uint32_t nx = __shfl_down(v[0], 1, 64);
+#pragma unroll
+    for (int u = 0; u < K; u++) {
+        const uint32_t e = lane * K + u;
+        const uint32_t next = (u + 1 < K) ? v[u + 1] : nx;
+        end[u] = (e < nk) & ((e + 1 == nk) | ((next >> (2 * l)) != (v[u] >> (2 * l))));
+    }
+}
+
+template <int K>
+__device__ __forceinline__ void hm_small_sort(const HmAggArgs& a, const uint16_t* ks, uint32_t nk, uint32_t kb,
+                                              uint32_t zmask, uint32_t b)
+{
+    const uint32_t lane = hm_lane();
+    const int lg = a.lg;
+    const uint32_t cm = (1u << lg) - 1;
+    uint32_t v[K];
+    hm_small_load<K>(ks, nk, v);
+#pragma unroll
+    for (int u = 0; u < K; u++)
+        if (v[u] != 0xFFFFFFFFu) v[u] = hm_spread7(v[u] & cm) | (hm_spread7(v[u] >> lg) << 1);
+    hm_wave_bitonic<K>(v);
+#pragma unroll
+    for (int u = 0; u < K; u++) {
+        const uint32_t e = lane * K + u;
+        if (e < nk) a.codes[kb + e] = (uint16_t)v[u];
+    }
+    uint32_t total = 0;
+    for (int l = 0; l < lg; l++) {
+        if (!((zmask >> l) & 1u)) continue;
+        bool end[K];
+        hm_small_ends<K>(v, nk, l, end);
+#pragma unroll
+        for (int u = 0; u < K; u++) total += __popcll(__ballot(end[u]));
+    }
+    if (lane == 0) a.spcnt[b] = total;
+}
+
+template <int K>
+__device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, uint32_t kb, uint64_t coord,
+                                              uint32_t zmask, uint64_t base)
+{
+    const uint32_t lane = hm_lane();
+    const int lg = a.lg;
+    uint32_t v[K];
+    hm_small_load<K>(a.codes + kb, nk, v);
+    for (int l = 0; l < lg; l++) {
+        if (!((zmask >> l) & 1u)) continue;
+        bool end[K];
+        hm_small_ends<K>(v, nk, l, end);
+        /* segment start of every element: running max of head positions */
+        const uint32_t pv = __shfl_up(v[K - 1], 1, 64);
+        uint32_t hs[K];
+        uint32_t run = 0;
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+            const uint32_t e = lane * K + u;
+            const uint32_t prev = u > 0 ? v[u - 1] : pv;
+            run = ((e == 0) | ((prev >> (2 * l)) != (v[u] >> (2 * l)))) ? e : run;
+            hs[u] = run;
+        }
+        uint32_t x = run;   /* inclusive max-scan over lanes */
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const uint32_t y = __shfl_up(x, d, 64);
+            if (lane >= (uint32_t)d) x = max(x, y);
+        }
+        uint32_t ex = __shfl_up(x, 1, 64);
+        ex = lane ? ex : 0u;
+        const int zl = a.Z - l;
+        const int s = lg - l;
+#pragma unroll
+        for (int u = 0; u < K; u++) {
+            const uint64_t bal = __ballot(end[u]);
+            if (end[u]) {
+                const uint32_t e = lane * K + u;
+                const uint32_t code = v[u] >> (2 * l);
+                const uint32_t idx = (hm_compact7(code >> 1) << s) | hm_compact7(code);
+                const uint64_t q = base + hm_mbcnt(bal);
+                if (q < a.out.capacity) {
+                    a.out.keys[q] = hm_cell_key(zl, coord, s, idx);
+                    a.out.counts[q] = (uint64_t)(e - max(hs[u], ex) + 1);
+                }
+            }
+            base += __popcll(bal);
+        }
+    }
+}
+
+__device__ __forceinline__ uint32_t hm_small_zmask(const HmAggArgs& a)
+{
+    uint32_t zmask = 0;
+    for (int l = 0; l < a.lg; l++) {
+        const int z = a.Z - l;
+        zmask |= (uint32_t)(z >= a.out.zmin && z <= a.out.zmax) << l;
+    }
+    return zmask;
+}
+
+/* Persistent: wave w takes the 64-bucket batches w, w + waves, ...; buckets of
+ * more than HM_SPW_MAX keys are left to k_aggregate_sparse / k_aggregate
+ * (their count stays 0). */
+__global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
+{
+    __shared__ uint16_t kss[HM_SPW_THREADS / 64][HM_SPW_MAX];
+    const uint32_t lane = hm_lane();
+    uint16_t* ks = kss[threadIdx.x >> 6];
+    const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
+    const uint32_t zmask = hm_small_zmask(a);
+    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * 64; b0 < a.B.count;
+         b0 += nw * 64) {
+        const uint32_t bl = b0 + lane;
+        const bool in = bl < a.B.count;
+        const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
+        const bool small = in & (nkl <= HM_SPW_MAX);
+        const uint32_t rbl = small ? a.B.rbase[bl] : 0u, nrl = small ? a.B.nruns[bl] : 0u;
+        const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
+        if (in) {
+            a.spcnt[bl] = 0;
+            if (small) a.totals[bl] = nkl;
+        }
+        uint64_t m = __ballot(small);
+        while (m) {
+            const int i = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t b = b0 + i;
+            const uint32_t nk = __shfl(nkl, i, 64), r0 = __shfl(rbl, i, 64), nr = __shfl(nrl, i, 64);
+            const uint32_t kb = __shfl(kbl, i, 64);
+            /* gather: runs 64 at a time, consecutive keys to consecutive lanes */
+            uint32_t fill = 0;
+            for (uint32_t c0 = 0; c0 < nr; c0 += 64) {
+                const uint32_t q = c0 + lane;
+                const uint2 run = q < nr ? a.in.run[r0 + q] : make_uint2(0, 0);
+                const uint32_t incl = hm_wave_incl_scan(run.y);
+                const uint32_t tot = __shfl(incl, 63, 64);
+                for (uint32_t j0 = 0; j0 < tot; j0 += 64) {
+                    const uint32_t j = j0 + lane;
+                    uint32_t lo = 0;
+#pragma unroll
+                    for (int st = 32; st > 0; st >>= 1)
+                        if (__shfl(incl, lo + st - 1, 64) <= j) lo += st;
+                    lo = min(lo, 63u);
+                    const uint32_t cnt = __shfl(run.y, lo, 64);
+                    const uint32_t off = j - (__shfl(incl, lo, 64) - cnt);
+                    const uint32_t src = __shfl(run.x, lo, 64) + off;
+                    if (j < tot) ks[fill + j] = a.keys[src];
+                }
+                fill += tot;
+            }
+            __builtin_amdgcn_wave_barrier();
+            if (nk <= 64)
+                hm_small_sort<1>(a, ks, nk, kb, zmask, b);
+            else if (nk <= 128)
+                hm_small_sort<2>(a, ks, nk, kb, zmask, b);
+            else if (nk <= 256)
+                hm_small_sort<4>(a, ks, nk, kb, zmask, b);
+            else
+                hm_small_sort<8>(a, ks, nk, kb, zmask, b);
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+}
+
+/* one reservation for every small bucket's cells */
+__global__ void k_small_reserve(HmAggArgs a)
+{
+    if (threadIdx.x == 0) *a.spbase = atomicAdd(a.out.cursor, (unsigned long long)*a.sptotal);
+}
+
+__global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
+{
+    const uint32_t lane = hm_lane();
+    const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
+    const uint32_t zmask = hm_small_zmask(a);
+    const uint64_t base = *a.spbase;
+    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * 64; b0 < a.B.count;
+         b0 += nw * 64) {
+        const uint32_t bl = b0 + lane;
+        const bool in = bl < a.B.count;
+        const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
+        const bool small = in & (nkl <= HM_SPW_MAX);
+        const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
+        const uint64_t cl = small ? a.B.coord[bl] : 0ull;
+        const uint64_t ol = small ? a.spoff[bl] : 0ull;
+        uint64_t m = __ballot(small);
+        while (m) {
+            const int i = __builtin_ctzll(m);
+            m &= m - 1;
+            const uint32_t nk = __shfl(nkl, i, 64), kb = __shfl(kbl, i, 64);
+            const uint64_t coord = __shfl(cl, i, 64), q = base + __shfl(ol, i, 64);
+            if (nk <= 64)
+                hm_small_emit<1>(a, nk, kb, coord, zmask, q);
+            else if (nk <= 128)
+                hm_small_emit<2>(a, nk, kb, coord, zmask, q);
+            else if (nk <= 256)
+                hm_small_emit<4>(a, nk, kb, coord, zmask, q);
+            else
+                hm_small_emit<8>(a, nk, kb, coord, zmask, q);
+        }
+    }
+}
 /* ------------------------------------------------------------------------ */
 /* pooling of bucket totals: zooms z_l .. z_{l-1}+1 (root: down to 0)        */
 /* ------------------------------------------------------------------------ */
@@ -1430,6 +1717,16 @@ void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint
         hipLaunchKernelGGL(k_aggregate_sparse, dim3(blocks), dim3(HM_SP_THREADS), 0, s, a);
     }
     if (nslots) hipLaunchKernelGGL(k_aggregate_merged, hm_grid2(nslots), dim3(HM_AG_THREADS), 0, s, a);
+}
+void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
+{
+    if (!a.B.count) return;
+    const uint32_t wb = (a.B.count + HM_SPW_THREADS - 1) / HM_SPW_THREADS;   /* 64-bucket batches per wave */
+    const dim3 g(wb < HM_SPW_GRID ? wb : HM_SPW_GRID);
+    hipLaunchKernelGGL(k_small_sort, g, dim3(HM_SPW_THREADS), 0, s, a);
+    hm_launch_scan(s, a.spcnt, a.B.count, partial, (uint64_t*)a.spoff, a.sptotal);
+    hipLaunchKernelGGL(k_small_reserve, dim3(1), dim3(64), 0, s, a);
+    hipLaunchKernelGGL(k_small_emit, g, dim3(HM_SPW_THREADS), 0, s, a);
 }
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {

@@ -36,7 +36,13 @@
 #define HM_SP_MAX 2048
 #endif
 #define HM_SP_WORDS ((HM_AG_CELLS / 3 * 4 + 1) / 2 + 1)   /* 4^7 + ... + 4 cells */
-#define HM_SP_GRID (256 * 3 * 4)
+#define HM_SP_GRID (256 * 3)
+/* small final buckets (k_small_sort / k_small_emit): one wavefront per bucket */
+#ifndef HM_SPW_MAX
+#define HM_SPW_MAX 512
+#endif
+#define HM_SPW_THREADS 256
+#define HM_SPW_GRID (256 * 8)
 #define HM_POOL_THREADS 256
 #define HM_MAX_LEVELS 4
 #define HM_COUNT_MAX_ZOOM 21                /* level-1 keys 2*(Z-5) bits fit u32 */
@@ -196,6 +202,12 @@ struct HmAggArgs {
     HmRuns in;
     int Z, lg;
     uint32_t items, nslots;     /* blocks with work in the (2-D) grids */
+    /* small buckets (k_small_sort / k_small_emit) */
+    uint16_t* codes;            /* sorted in-bucket Morton codes at each bucket's key range */
+    uint64_t* spcnt;            /* [count] cells per small bucket (0 otherwise) */
+    const uint64_t* spoff;      /* exclusive scan of spcnt */
+    uint64_t* sptotal;
+    unsigned long long* spbase; /* output position of the small buckets' region */
     unsigned long long* totals;
     uint32_t* gslots;
     const uint32_t* slot_bucket;
@@ -241,6 +253,8 @@ void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* part
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
 void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc);
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots);
+/* small buckets: sort pass, scan, one reservation, emit pass (partial: 4096 u64) */
+void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial);
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);
 void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
                      const double* tab, int k);

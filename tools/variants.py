@@ -30,6 +30,8 @@ VARIANTS = {
     "t512_8k": ["HM_PN_THREADS=512"],
     "su2": ["HM_SU=2"],
     "su8": ["HM_SU=8"],
+    "spnoatom": ["HM_EXP_SPNOATOM=1"],      # sparse buckets: no output cursor atomic
+    "spnoemit": ["HM_EXP_SPNOEMIT=1"],      # sparse buckets: no output at all
 }
 
 
@@ -52,7 +54,7 @@ def one(name, points, steps, zmax):
 
     lat = torch.empty(points, dtype=torch.float64, device="cuda")
     lon = torch.empty(points, dtype=torch.float64, device="cuda")
-    device.synth("hotspots", lat, lon)
+    device.synth(os.environ.get("HM_KIND", "hotspots"), lat, lon)
     bufs = device.CountBuffers(64 << 20)
     ctx = device.context(0)
     m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
@@ -66,7 +68,7 @@ def one(name, points, steps, zmax):
     dt = (time.perf_counter() - t0) / steps
     tot = int(bufs.counts[:m].sum().item())
     print(json.dumps({"variant": name, "ms": dt * 1e3, "gpts": points / dt / 1e9, "cells": m,
-                      "check": tot == points * (zmax + 1),
+                      "check": tot == points * (zmax + 1), "kind": os.environ.get("HM_KIND", "hotspots"),
                       "stage_us": [round(x, 1) for x in np.mean(np.array(st), axis=0)]}), flush=True)
 
 
