@@ -1175,9 +1175,23 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
     for (uint32_t i = tid; i < HM_SP_WORDS; i += HM_SP_THREADS) g[i] = 0;
     __syncthreads();
     const uint32_t nblk = gridDim.x * gridDim.y;
-    for (uint32_t b = hm_block_id(); b < a.B.count; b += nblk) {
-        const uint32_t nk = a.B.nkeys[b];
-        if (nk > HM_SP_MAX || nk <= HM_SPW_MAX) continue;   /* block-uniform: dense or small */
+    const uint32_t lane = hm_lane();
+    /* buckets are screened 64 per step (one load per lane; every wave ballots
+     * the same mask, so the loop stays block-uniform) */
+    uint32_t b0 = hm_block_id() * 64, bs = 0, nkl = 0;
+    uint64_t msk = 0;
+    for (;;) {
+        while (msk == 0 && b0 < a.B.count) {
+            const uint32_t bl = b0 + lane;
+            nkl = bl < a.B.count ? a.B.nkeys[bl] : 0u;
+            msk = __ballot((nkl > HM_SPW_MAX) & (nkl <= HM_SP_MAX));
+            bs = b0;
+            b0 += nblk * 64;
+        }
+        if (msk == 0) break;
+        const uint32_t b = bs + (uint32_t)__builtin_ctzll(msk);
+        msk &= msk - 1;
+        const uint32_t nk = __shfl(nkl, (int)(b - bs), 64);
         HmItem it;
         it.bucket = b;
         it.j = 0;
@@ -1472,10 +1486,10 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
     uint16_t* ks = kss[threadIdx.x >> 6];
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
     const uint32_t zmask = hm_small_zmask(a);
-    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * 64; b0 < a.B.count;
-         b0 += nw * 64) {
+    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * a.spbatch; b0 < a.B.count;
+         b0 += nw * a.spbatch) {
         const uint32_t bl = b0 + lane;
-        const bool in = bl < a.B.count;
+        const bool in = (lane < a.spbatch) & (bl < a.B.count);
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
         const bool small = in & (nkl <= HM_SPW_MAX);
         const uint32_t rbl = small ? a.B.rbase[bl] : 0u, nrl = small ? a.B.nruns[bl] : 0u;
@@ -1538,10 +1552,10 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
     const uint32_t zmask = hm_small_zmask(a);
     const uint64_t base = *a.spbase;
-    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * 64; b0 < a.B.count;
-         b0 += nw * 64) {
+    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * a.spbatch; b0 < a.B.count;
+         b0 += nw * a.spbatch) {
         const uint32_t bl = b0 + lane;
-        const bool in = bl < a.B.count;
+        const bool in = (lane < a.spbatch) & (bl < a.B.count);
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
         const bool small = in & (nkl <= HM_SPW_MAX);
         const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
@@ -1721,12 +1735,20 @@ void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint
 void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
 {
     if (!a.B.count) return;
-    const uint32_t wb = (a.B.count + HM_SPW_THREADS - 1) / HM_SPW_THREADS;   /* 64-bucket batches per wave */
+    /* batches of <= 64 consecutive buckets per wave, small enough that every
+     * wave of the grid gets one when buckets are few (a wave walks its batch
+     * serially) */
+    HmAggArgs b = a;
+    const uint32_t waves = HM_SPW_GRID * (HM_SPW_THREADS / 64);
+    b.spbatch = 1;
+    while (b.spbatch < 64 && (uint64_t)b.spbatch * waves < a.B.count) b.spbatch <<= 1;
+    const uint32_t per_block = b.spbatch * (HM_SPW_THREADS / 64);
+    const uint32_t wb = (a.B.count + per_block - 1) / per_block;
     const dim3 g(wb < HM_SPW_GRID ? wb : HM_SPW_GRID);
-    hipLaunchKernelGGL(k_small_sort, g, dim3(HM_SPW_THREADS), 0, s, a);
-    hm_launch_scan(s, a.spcnt, a.B.count, partial, (uint64_t*)a.spoff, a.sptotal);
-    hipLaunchKernelGGL(k_small_reserve, dim3(1), dim3(64), 0, s, a);
-    hipLaunchKernelGGL(k_small_emit, g, dim3(HM_SPW_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_small_sort, g, dim3(HM_SPW_THREADS), 0, s, b);
+    hm_launch_scan(s, b.spcnt, b.B.count, partial, (uint64_t*)b.spoff, b.sptotal);
+    hipLaunchKernelGGL(k_small_reserve, dim3(1), dim3(64), 0, s, b);
+    hipLaunchKernelGGL(k_small_emit, g, dim3(HM_SPW_THREADS), 0, s, b);
 }
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {

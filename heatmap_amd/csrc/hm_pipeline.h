@@ -208,6 +208,7 @@ struct HmAggArgs {
     const uint64_t* spoff;      /* exclusive scan of spcnt */
     uint64_t* sptotal;
     unsigned long long* spbase; /* output position of the small buckets' region */
+    uint32_t spbatch;           /* consecutive buckets per wave step (power of 2, <= 64) */
     unsigned long long* totals;
     uint32_t* gslots;
     const uint32_t* slot_bucket;

@@ -159,3 +159,16 @@ def test_config1_heatmap_digest():
     assert _digest(items) == h["sha256"]
     for k, v in h["sample_rows"].items():
         assert got[k] == v
+
+
+def test_count_tiles_matches_count():
+    """oracle.count_tiles (tile input) == oracle.count on the same points' tiles."""
+    from heatmap_amd import synth
+
+    lat, lon = synth.generate("hotspots", 20000, seed=8)
+    r, c, st, _ = oracle.project(lat, lon, 14)
+    assert (st == 0).all()
+    a = oracle.count_tiles(r, c, 0, 14)
+    b = oracle.count(lat, lon, None, 0, 14)
+    for k in ("zoom", "row", "col", "count"):
+        assert np.array_equal(a[k], b[k]), k
