@@ -100,10 +100,6 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
-    for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
-    if (!FROM_TILES) hm_load_ytab(tab);
-    __syncthreads();
-
     const uint32_t tile = a.tile0 + blockIdx.x;          /* tile slot in the run layout */
     const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
     const uint32_t lim = 1u << a.Z;
@@ -116,6 +112,27 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
      * lane in flight (double2 = two consecutive points of one array) */
     double2 la[HM_P1_PPT / 2], lo[HM_P1_PPT / 2];
     uint16_t kp[HM_P1_PPT / 2];
+    /* Full tiles (block-uniform branch) load unconditionally.  The per-lane
+     * tail code below writes the same registers in its other branches, which
+     * makes the compiler wait for each load pair before the next one: one
+     * 32-B pair per lane in flight instead of all of them. */
+    if (!FROM_TILES && base + HM_T1 <= a.n) {
+        const double2* lat2 = (const double2*)(a.lat + base);
+        const double2* lon2 = (const double2*)(a.lon + base);
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT / 2; k++) {
+            la[k] = lat2[k * HM_P1_THREADS + tid];
+            lo[k] = lon2[k * HM_P1_THREADS + tid];
+        }
+        if (a.keep) {
+            const uint16_t* kp2 = (const uint16_t*)(a.keep + base);
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = kp2[k * HM_P1_THREADS + tid];
+        } else {
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = 0x0101;
+        }
+    } else
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT / 2; k++) {
         const int64_t i0 = base + 2 * ((int64_t)k * HM_P1_THREADS + tid);
@@ -147,6 +164,10 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             lo[k] = make_double2(0.0, 0.0);
         }
     }
+    /* LDS set-up after the loads are issued: the table's latency overlaps theirs */
+    for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
+    if (!FROM_TILES) hm_load_ytab(tab);
+    __syncthreads();
     /* fast path for every point, branch-free; points the fast path cannot
      * settle (guard band, polar/out-of-range/non-finite input) are marked in
      * `redo` and resolved afterwards in one ballot-guarded pass */
