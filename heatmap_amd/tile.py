@@ -7,14 +7,20 @@ with the reference's glibc arithmetic -- so every call needs the GPU; the
 vectorised forms (rows_from_latitudes, ...) are what callers should use in
 bulk.  Pure string helpers (ids) are plain Python, as in the reference.
 
-Not provided on the device path yet ("next"):
-latitude_from_row / tile_from_tile_id / parent / children /
-tile_ids_for_all_zoom_levels, which need the reference's exp/atan inverse
-projection.  The count pyramid does not need them: the reference's re-projection
-of tile centres equals a right shift on the tile domain, which
-is what the device uses.
+Tile utility API: tile_from_tile_id, parent_id,
+parent, children and tile_ids_for_all_zoom_levels (tile.py:33-98).  Their
+forward projections (the centre / quarter points re-projected one zoom up or
+down) go through the same device hm_project call, batched per zoom.  The inverse
+projection latitude_from_row (tile.py:23-26) is a per-tile scalar with exp/atan
+that the device does not restate; it is evaluated on the host in the
+reference's own operation order with the same libm, so it is bit-identical
+(tests/golden/tile_utils.json).  The count pyramid never needs it: the
+reference's re-projection of tile centres equals a right shift on the tile
+domain, which is what the device uses.
 """
 from __future__ import annotations
+
+import math
 
 import numpy as np
 
@@ -98,10 +104,57 @@ class Tile:
 
     @classmethod
     def latitude_from_row(cls, row, zoom):
-        raise NotImplementedError("inverse projection (tile.py:23-26) is not on the device path yet; "
-                                  "see DESIGN.md 'Next'")
+        """tile.py:23-26, same operation order: n = pi - 2*pi*row / 2^z, then
+        180/pi * atan(sinh(n)) written as 0.5*(e^n - e^-n)."""
+        n = math.pi - 2.0 * math.pi * row / (2 ** zoom)
+        return 180.0 / math.pi * math.atan(0.5 * (math.exp(n) - math.exp(-n)))
 
     @classmethod
     def tile_from_tile_id(cls, tile_id):
-        raise NotImplementedError("tile_from_tile_id needs the inverse projection (tile.py:33-54); "
-                                  "see DESIGN.md 'Next'")
+        """tile.py:33-54: a Tile with its bounds and centre, or None for an id
+        that does not split into three parts."""
+        d = cls.decode_tile_id(tile_id)
+        if d is None:
+            return None
+        t = Tile()
+        t.tile_id = tile_id
+        t.zoom, t.row, t.column = d["zoom"], d["row"], d["column"]
+        t.latitude_north = Tile.latitude_from_row(t.row, t.zoom)
+        t.latitude_south = Tile.latitude_from_row(t.row + 1, t.zoom)
+        t.longitude_west = Tile.longitude_from_column(t.column, t.zoom)
+        t.longitude_east = Tile.longitude_from_column(t.column + 1, t.zoom)
+        t.center_latitude = (t.latitude_north + t.latitude_south) / 2.0
+        t.center_longitude = (t.longitude_east + t.longitude_west) / 2.0
+        return t
+
+    # --- hierarchy (forward projections on the device) -------------------------
+    def parent_id(self):
+        """tile.py:60-61: the tile holding this tile's centre one zoom up."""
+        if self.zoom < 1:
+            raise _lib.DevicePathUnsupported("parent of a zoom-0 tile (zoom -1) is not projected on the device")
+        return Tile.tile_id_from_lat_long(self.center_latitude, self.center_longitude, self.zoom - 1)
+
+    def parent(self):
+        """tile.py:63-64."""
+        return Tile.tile_from_tile_id(self.parent_id())
+
+    def children(self):
+        """tile.py:88-98: ids of the tiles holding the four quarter centres one
+        zoom down, in the reference's order NE, NW, SE, SW (one device call)."""
+        north = (self.center_latitude + self.latitude_north) / 2
+        south = (self.center_latitude + self.latitude_south) / 2
+        east = (self.center_longitude + self.longitude_east) / 2
+        west = (self.center_longitude + self.longitude_west) / 2
+        return Tile.tile_ids_from_lat_longs([north, north, south, south], [east, west, east, west], self.zoom + 1)
+
+    @classmethod
+    def tile_ids_for_all_zoom_levels(cls, tileId):
+        """tile.py:79-86: the tiles holding this tile's centre at zooms
+        MAX_ZOOM down to MIN_ZOOM + 1 (range(16, 0, -1) leaves out zoom 0)."""
+        t = Tile.tile_from_tile_id(tileId)
+        lat, lon = np.array([t.center_latitude]), np.array([t.center_longitude])
+        out = []
+        for z in range(Tile.MAX_ZOOM, Tile.MIN_ZOOM, -1):
+            p = device.project(lat, lon, z, raise_errors=True)
+            out.append(Tile.tile_id_from_row_column(int(p.row[0]), int(p.col[0]), z))
+        return out

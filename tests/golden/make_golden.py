@@ -334,6 +334,37 @@ def hotspot_zoom_digest(Tile):
     print("hotspot zoom digests done")
 
 
+def tile_utils_golden(Tile, rng):
+    """Tile utility API (tile.py:23-98): inverse projection, tile_from_tile_id,
+    parent_id, children, tile_ids_for_all_zoom_levels.  Floats are stored as
+    repr() strings so the fixture is bit-exact."""
+    ids = ["0_0_0", "1_0_0", "1_1_1", "16_0_0", "16_65535_65535", "16_22894_10501", "12_1430_656",
+           "5_12_3", "9_511_0", "14_5724_2625", "2_3_0", "16_32768_32768", "7_0_127"]
+    for _ in range(60):
+        z = int(rng.integers(1, 17))
+        ids.append("%d_%d_%d" % (z, int(rng.integers(0, 2 ** z)), int(rng.integers(0, 2 ** z))))
+    cases = []
+    for tid in ids:
+        t = Tile.tile_from_tile_id(tid)
+        rec = {"id": tid,
+               "fields": {k: repr(getattr(t, k)) for k in
+                          ("latitude_north", "latitude_south", "longitude_west", "longitude_east",
+                           "center_latitude", "center_longitude")},
+               "children": t.children(),
+               "all_zooms": Tile.tile_ids_for_all_zoom_levels(tid)}
+        rec["parent_id"] = t.parent_id() if t.zoom > 0 else None
+        cases.append(rec)
+    lat_rows = []
+    for _ in range(200):
+        z = int(rng.integers(0, 25))
+        r = int(rng.integers(-2, 2 ** z + 3))
+        lat_rows.append([r, z, repr(Tile.latitude_from_row(r, z))])
+    with open(os.path.join(HERE, "tile_utils.json"), "w") as f:
+        json.dump({"generator": "tests/golden/make_golden.py --only utils", "tiles": cases,
+                   "latitude_from_row": lat_rows, "malformed": ["1_2", "a_b_c_d", "", "3__4_5"]}, f)
+    print("tile utils done: %d tiles" % len(cases))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--quick", action="store_true")
@@ -348,6 +379,8 @@ def main():
         heatmap_goldens(hm, rng)
     if "hot" in todo:
         hotspot_zoom_digest(Tile)
+    if "utils" in todo or not a.only:
+        tile_utils_golden(Tile, np.random.default_rng(20261016))
     if "c1" in todo and not a.quick:
         config1_digest(Tile, hm)
 
