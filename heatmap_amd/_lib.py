@@ -26,7 +26,8 @@ HM_E_NOMEM = 19
 HM_COUNT_MAX_ZOOM = 21
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
-           "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats", "hm_synth"]
+           "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
+           "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_extract", "hm_stream_destroy"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -72,6 +73,11 @@ def load() -> ctypes.CDLL:
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
         L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]
+        L.hm_stream_create.argtypes = [vp, c.c_int, c.c_int, c.c_uint32, c.c_int64, P(vp)]
+        L.hm_stream_add.argtypes = [vp, vp, vp, vp, vp, c.c_int64]
+        L.hm_stream_cells.argtypes = [vp, P(c.c_int64), P(c.c_int64)]
+        L.hm_stream_extract.argtypes = [vp, c.c_int64, vp, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_stream_destroy.argtypes = [vp]
         for name in EXPORTS:
             getattr(L, name).restype = getattr(L, name).restype or c.c_int
         L.hm_status_string.restype = c.c_char_p

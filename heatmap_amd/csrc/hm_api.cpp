@@ -666,3 +666,227 @@ extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int
     HIPCHK(hipGetLastError());
     return HM_OK;
 }
+
+/* ------------------------------------------------------------------------ */
+/* streaming: resident multi-zoom heatmap (kernels in hm_stream.hip)          */
+/* ------------------------------------------------------------------------ */
+
+struct hm_stream {
+    hm_ctx* ctx = nullptr;
+    int zmin = 0, zmax = 0;
+    uint32_t base = 0;
+    HmsTable t{};
+    uint64_t occupied = 0;
+    unsigned long long* hstate = nullptr; /* pinned mirror of t.state (8 words) */
+    Buf bkeys, bcounts, mask, present;    /* per-batch scratch */
+    int64_t bcap = 0;                     /* cells bkeys/bcounts hold */
+};
+
+static int stream_sync_state(hm_stream* s)
+{
+    HIPCHK(hipMemcpyAsync(s->hstate, s->t.state, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+                          s->ctx->stream));
+    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    s->occupied = s->hstate[HMS_ST_OCCUPIED];
+    return s->hstate[HMS_ST_OVERFLOW] ? HM_E_CAPACITY : HM_OK;
+}
+
+static int stream_alloc_table(hm_stream* s, uint64_t cap, HmsTable* t)
+{
+    t->mask = cap - 1;
+    t->state = s->t.state;
+    if (hipMalloc((void**)&t->keys, cap * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        return HM_E_NOMEM;
+    }
+    if (hipMalloc((void**)&t->counts, cap * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipFree(t->keys);
+        return HM_E_NOMEM;
+    }
+    HIPCHK(hipMemsetAsync(t->keys, 0xFF, cap * 8, s->ctx->stream));
+    HIPCHK(hipMemsetAsync(t->counts, 0, cap * 8, s->ctx->stream));
+    return HM_OK;
+}
+
+/* keep the load factor <= 5/8 after inserting `incoming` more cells */
+static int stream_reserve(hm_stream* s, uint64_t incoming)
+{
+    uint64_t cap = s->t.mask + 1;
+    const uint64_t need = s->occupied + incoming;
+    if (need * 8 <= cap * 5) return HM_OK;
+    while (need * 8 > cap * 5) cap <<= 1;
+    HmsTable nt;
+    int st = stream_alloc_table(s, cap, &nt);
+    if (st) return st;
+    HIPCHK(hipMemsetAsync(s->t.state, 0, 2 * sizeof(unsigned long long), s->ctx->stream));
+    hm_launch_stream_rehash(s->ctx->stream, s->t, nt);
+    HIPCHK(hipGetLastError());
+    st = stream_sync_state(s);
+    HIPCHK(hipFree(s->t.keys));
+    HIPCHK(hipFree(s->t.counts));
+    s->t = nt;
+    return st;
+}
+
+static int stream_buf(hm_stream* s, Buf& b, size_t bytes)
+{
+    if (b.cap >= bytes) return HM_OK;
+    if (b.p) HIPCHK(hipFree(b.p));
+    b.p = nullptr;
+    b.cap = 0;
+    if (hipMalloc(&b.p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        return HM_E_NOMEM;
+    }
+    b.cap = bytes;
+    return HM_OK;
+}
+
+/* one count pyramid over the batch (mask = kept points of one hour), folded in */
+static int stream_fold(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
+                       uint64_t tag_a, uint64_t tag_b)
+{
+    int64_t m = 0;
+    int st;
+    if (s->bcap < 2 * n + 1024) { /* typical batches: fewer cells than 2 per point */
+        const int64_t want = 2 * n + 1024;
+        if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))
+            return st;
+        s->bcap = want;
+    }
+    for (;;) {
+        st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, (uint64_t*)s->bkeys.p, (uint64_t*)s->bcounts.p,
+                      s->bcap, &m);
+        if (st != HM_E_CAPACITY) break;
+        const int64_t want = m + m / 4 + 1024;
+        if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))
+            return st;
+        s->bcap = want;
+    }
+    if (st) return st;
+    if ((st = stream_reserve(s, (uint64_t)m * (tag_b ? 2 : 1)))) return st;
+    hm_launch_stream_insert(s->ctx->stream, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m,
+                            tag_a, tag_b, s->t);
+    HIPCHK(hipGetLastError());
+    return stream_sync_state(s);
+}
+
+extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_t initial_cells,
+                                hm_stream** out)
+{
+    if (!ctx || !out || zmin < 0 || zmax < zmin || zmax > HM_MAX_ZOOM || initial_cells < 0) return HM_E_ARG;
+    *out = nullptr;
+    HIPCHK(hipSetDevice(ctx->device));
+    hm_stream* s = new hm_stream();
+    s->ctx = ctx;
+    s->zmin = zmin;
+    s->zmax = zmax;
+    s->base = base_hour;
+    uint64_t cap = 1024;
+    while (cap * 5 < (uint64_t)initial_cells * 8) cap <<= 1;
+    if (hipMalloc((void**)&s->t.state, 8 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc((void**)&s->hstate, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        (void)hipGetLastError();
+        hm_stream_destroy(s);
+        return HM_E_NOMEM;
+    }
+    int st = stream_alloc_table(s, cap, &s->t);
+    if (st == HM_OK) {
+        st = hip_fail(hipMemsetAsync(s->t.state, 0, 8 * sizeof(unsigned long long), ctx->stream), "memset");
+    }
+    if (st == HM_OK) st = stream_sync_state(s);
+    if (st) {
+        hm_stream_destroy(s);
+        return st;
+    }
+    *out = s;
+    return HM_OK;
+}
+
+extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep,
+                             const uint32_t* hour, int64_t n)
+{
+    if (!s || n < 0 || (n > 0 && (!lat || !lon))) return HM_E_ARG;
+    HIPCHK(hipSetDevice(s->ctx->device));
+    hipStream_t q = s->ctx->stream;
+    int st;
+    if (!hour || n == 0) return stream_fold(s, lat, lon, keep, n, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT, 0);
+    /* hour range of the kept points */
+    unsigned int* mm = (unsigned int*)(s->t.state + HMS_ST_HOURS);
+    const unsigned int init[2] = {0xFFFFFFFFu, 0u};
+    HIPCHK(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, q));
+    hm_launch_stream_hour_range(q, hour, keep, (uint64_t)n, mm);
+    HIPCHK(hipGetLastError());
+    if ((st = stream_sync_state(s))) return st;
+    const unsigned int lo = ((unsigned int*)(s->hstate + HMS_ST_HOURS))[0];
+    const unsigned int hi = ((unsigned int*)(s->hstate + HMS_ST_HOURS))[1];
+    if (lo > hi) /* nothing kept: still project every point (errors), fold nothing */
+        return stream_fold(s, lat, lon, keep, n, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT, 0);
+    if (lo < s->base || (uint64_t)hi - s->base >= HM_STREAM_MAX_HOURS) return HM_E_RANGE;
+    if ((uint64_t)hi - lo >= HM_STREAM_MAX_SPAN) return HM_E_ARG;
+    const uint32_t span = hi - lo + 1;
+    if ((st = stream_buf(s, s->present, span)) || (st = stream_buf(s, s->mask, (size_t)n))) return st;
+    HIPCHK(hipMemsetAsync(s->present.p, 0, span, q));
+    hm_launch_stream_hour_presence(q, hour, keep, (uint64_t)n, lo, (uint8_t*)s->present.p);
+    HIPCHK(hipGetLastError());
+    std::vector<uint8_t> present(span);
+    HIPCHK(hipMemcpyAsync(present.data(), s->present.p, span, hipMemcpyDeviceToHost, q));
+    HIPCHK(hipStreamSynchronize(q));
+    for (uint32_t d = 0; d < span; d++) {
+        if (!present[d]) continue;
+        hm_launch_stream_hour_mask(q, hour, keep, (uint64_t)n, lo + d, (uint8_t*)s->mask.p);
+        HIPCHK(hipGetLastError());
+        const uint64_t tag = (uint64_t)(lo + d - s->base) << HMS_TAG_SHIFT;
+        if ((st = stream_fold(s, lat, lon, (const uint8_t*)s->mask.p, n, tag, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT)))
+            return st;
+    }
+    return HM_OK;
+}
+
+extern "C" int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity)
+{
+    if (!s) return HM_E_ARG;
+    if (cells) *cells = (int64_t)s->occupied;
+    if (capacity) *capacity = (int64_t)(s->t.mask + 1);
+    return HM_OK;
+}
+
+extern "C" int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out, uint64_t* counts_out,
+                                 uint32_t* hours_out, int64_t capacity, int64_t* n_out)
+{
+    if (!s || !n_out || capacity < 0 || (capacity > 0 && (!keys_out || !counts_out))) return HM_E_ARG;
+    uint64_t sel;
+    if (hour == HM_STREAM_ALLTIME)
+        sel = HM_STREAM_ALLTIME_TAG;
+    else if (hour == HM_STREAM_EACH_HOUR)
+        sel = HMS_SEL_EVERY_HOUR;
+    else if (hour >= (int64_t)s->base && hour - (int64_t)s->base < HM_STREAM_MAX_HOURS)
+        sel = (uint64_t)(hour - s->base);
+    else
+        return HM_E_ARG;
+    *n_out = 0;
+    HIPCHK(hipSetDevice(s->ctx->device));
+    hipStream_t q = s->ctx->stream;
+    unsigned long long* cursor = s->t.state + HMS_ST_CURSOR;
+    HIPCHK(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), q));
+    hm_launch_stream_extract(q, s->t, sel, keys_out, counts_out, hours_out, s->base, (uint64_t)capacity, cursor);
+    HIPCHK(hipGetLastError());
+    int st = stream_sync_state(s);
+    if (st) return st;
+    *n_out = (int64_t)s->hstate[HMS_ST_CURSOR];
+    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+}
+
+extern "C" int hm_stream_destroy(hm_stream* s)
+{
+    if (!s) return HM_OK;
+    if (s->ctx) (void)hipSetDevice(s->ctx->device);
+    if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
+    for (void* p : {(void*)s->t.keys, (void*)s->t.counts, (void*)s->t.state, s->bkeys.p, s->bcounts.p, s->mask.p,
+                    s->present.p})
+        if (p) (void)hipFree(p);
+    if (s->hstate) (void)hipHostFree(s->hstate);
+    delete s;
+    return HM_OK;
+}

@@ -259,3 +259,27 @@ void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial);
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);
 void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
                      const double* tab, int k);
+
+/* resident streaming heatmap (hm_stream.hip) */
+#define HMS_TAG_SHIFT 47                    /* table key = tag<<47 | zoom<<42 | row<<21 | col */
+#define HM_STREAM_ALLTIME_TAG 0x1FFFFull    /* hour bucket of the alltime heatmap */
+#define HMS_SEL_EVERY_HOUR (1ull << 20)     /* extract selector: every hour bucket */
+enum { HMS_ST_OCCUPIED = 0, HMS_ST_OVERFLOW = 1, HMS_ST_CURSOR = 2, HMS_ST_HOURS = 4 /* min, max as u32 */ };
+struct HmsTable {
+    uint64_t* keys;
+    uint64_t* counts;
+    uint64_t mask; /* capacity - 1 (power of two) */
+    unsigned long long* state;
+};
+void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, uint64_t tag_a,
+                             uint64_t tag_b, const HmsTable& t);
+void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to);
+void hm_launch_stream_hour_range(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
+                                 unsigned int* mm);
+void hm_launch_stream_hour_presence(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
+                                    uint32_t lo, uint8_t* present);
+void hm_launch_stream_hour_mask(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n, uint32_t h,
+                                uint8_t* mask);
+void hm_launch_stream_extract(hipStream_t s, const HmsTable& t, uint64_t sel, uint64_t* keys_out,
+                              uint64_t* counts_out, uint32_t* hours_out, uint32_t base, uint64_t cap,
+                              unsigned long long* cursor);

@@ -1,0 +1,239 @@
+/* Resident multi-zoom heatmap for streaming micro-batches (BASELINE config 5,
+ * SURVEY.md 8f item 2).
+ *
+ * The reference recomputes its whole pyramid per Spark job (heatmap.py:152-158);
+ * a streaming caller instead folds each micro-batch's hm_count cells into a
+ * heatmap that stays in HBM.  The resident heatmap is an open-addressing hash
+ * table (SoA: u64 keys, u64 counts, linear probing, EMPTY = all ones):
+ *   - merge cost is O(cells of the batch), independent of the resident size
+ *     (a sorted resident set would re-stream every resident cell per batch);
+ *   - a batch cell is one probe sequence + one 64-bit atomic add, so the
+ *     kernel is bound by random 64-B HBM transactions, not by arithmetic.
+ * Table key = hour bucket (17 bits) | zoom (5) | row (21) | col (21); the hour
+ * bucket HM_STREAM_ALLTIME_TAG holds the alltime heatmap, every other value
+ * an epoch hour relative to the stream's base hour.
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hm_pipeline.h"
+
+#define HMS_EMPTY 0xFFFFFFFFFFFFFFFFull
+
+__device__ __forceinline__ uint64_t hms_hash(uint64_t k)
+{
+    /* 64-bit finaliser (MurmurHash3 fmix64) */
+    k ^= k >> 33;
+    k *= 0xFF51AFD7ED558CCDull;
+    k ^= k >> 33;
+    k *= 0xC4CEB9FE1A85EC53ull;
+    k ^= k >> 33;
+    return k;
+}
+
+/* hm_count key (zoom<<58 | row<<29 | col) -> 42-bit cell field of a table key */
+__device__ __forceinline__ uint64_t hms_pack(uint64_t k)
+{
+    const uint64_t z = k >> 58, r = (k >> 29) & 0x1FFFFFFFull, c = k & 0x1FFFFFFFull;
+    return (z << 42) | (r << 21) | c;
+}
+
+__device__ __forceinline__ uint64_t hms_unpack(uint64_t p)
+{
+    const uint64_t z = (p >> 42) & 31ull, r = (p >> 21) & 0x1FFFFFull, c = p & 0x1FFFFFull;
+    return (z << 58) | (r << 29) | c;
+}
+
+__device__ __forceinline__ uint64_t hms_wave_sum(uint64_t v)
+{
+    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o, 64);
+    return v;
+}
+
+/* Insert-or-add; returns 1 if this call claimed a new slot. */
+__device__ __forceinline__ uint32_t hms_insert(const HmsTable& t, uint64_t k, uint64_t c, uint32_t* overflow)
+{
+    uint64_t h = hms_hash(k) & t.mask;
+    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+        uint64_t cur = __atomic_load_n(&t.keys[h], __ATOMIC_RELAXED);
+        uint32_t claimed = 0;
+        if (cur == HMS_EMPTY) {
+            const unsigned long long prev =
+                atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
+            claimed = prev == HMS_EMPTY;
+            cur = claimed ? k : prev;
+        }
+        if (cur == k) {
+            atomicAdd((unsigned long long*)&t.counts[h], (unsigned long long)c);
+            return claimed;
+        }
+        h = (h + 1) & t.mask;
+    }
+    *overflow = 1;
+    return 0;
+}
+
+/* Fold n cells (hm_count layout) into the table under tag_a and, if
+ * tag_b != 0, again under tag_b (the alltime bucket). */
+__global__ __launch_bounds__(256) void k_stream_insert(const uint64_t* __restrict__ keys,
+                                                       const uint64_t* __restrict__ counts, uint64_t n,
+                                                       uint64_t tag_a, uint64_t tag_b, HmsTable t)
+{
+    uint64_t claimed = 0;
+    uint32_t overflow = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t p = hms_pack(keys[i]);
+        const uint64_t c = counts[i];
+        claimed += hms_insert(t, tag_a | p, c, &overflow);
+        if (tag_b) claimed += hms_insert(t, tag_b | p, c, &overflow);
+    }
+    claimed = hms_wave_sum(claimed);
+    const uint64_t of = hms_wave_sum(overflow);
+    if ((threadIdx.x & 63) == 0) {
+        if (claimed) atomicAdd(&t.state[HMS_ST_OCCUPIED], (unsigned long long)claimed);
+        if (of) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)of);
+    }
+}
+
+/* Re-insert every occupied slot of `from` into `to` (table growth). */
+__global__ __launch_bounds__(256) void k_stream_rehash(HmsTable from, HmsTable to)
+{
+    uint64_t claimed = 0;
+    uint32_t overflow = 0;
+    const uint64_t n = from.mask + 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        const uint64_t k = from.keys[i];
+        if (k != HMS_EMPTY) claimed += hms_insert(to, k, from.counts[i], &overflow);
+    }
+    claimed = hms_wave_sum(claimed);
+    const uint64_t of = hms_wave_sum(overflow);
+    if ((threadIdx.x & 63) == 0) {
+        if (claimed) atomicAdd(&to.state[HMS_ST_OCCUPIED], (unsigned long long)claimed);
+        if (of) atomicAdd(&to.state[HMS_ST_OVERFLOW], (unsigned long long)of);
+    }
+}
+
+/* Min / max epoch hour over the kept points of a batch. */
+__global__ __launch_bounds__(256) void k_stream_hour_range(const uint32_t* __restrict__ hour,
+                                                           const uint8_t* __restrict__ keep, uint64_t n,
+                                                           unsigned int* mm)
+{
+    uint32_t lo = 0xFFFFFFFFu, hi = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (keep && !keep[i]) continue;
+        const uint32_t h = hour[i];
+        lo = h < lo ? h : lo;
+        hi = h > hi ? h : hi;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        const uint32_t a = __shfl_xor(lo, o, 64), b = __shfl_xor(hi, o, 64);
+        lo = a < lo ? a : lo;
+        hi = b > hi ? b : hi;
+    }
+    if ((threadIdx.x & 63) == 0 && lo <= hi) {
+        atomicMin(&mm[0], lo);
+        atomicMax(&mm[1], hi);
+    }
+}
+
+/* present[h - lo] = 1 for every hour of a kept point (benign same-value races). */
+__global__ __launch_bounds__(256) void k_stream_hour_presence(const uint32_t* __restrict__ hour,
+                                                              const uint8_t* __restrict__ keep, uint64_t n,
+                                                              uint32_t lo, uint8_t* present)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        if (keep && !keep[i]) continue;
+        present[hour[i] - lo] = 1;
+    }
+}
+
+/* mask[i] = keep[i] && hour[i] == h */
+__global__ __launch_bounds__(256) void k_stream_hour_mask(const uint32_t* __restrict__ hour,
+                                                          const uint8_t* __restrict__ keep, uint64_t n, uint32_t h,
+                                                          uint8_t* __restrict__ mask)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        mask[i] = (uint8_t)((!keep || keep[i]) && hour[i] == h);
+}
+
+/* Dump the slots whose hour bucket matches `sel` (sel == HMS_SEL_EVERY_HOUR:
+ * every bucket but alltime) as hm_count keys + counts (+ absolute epoch hour).
+ * Wave-aggregated cursor; slots past `cap` are counted but not written. */
+__global__ __launch_bounds__(256) void k_stream_extract(HmsTable t, uint64_t sel, uint64_t* __restrict__ keys_out,
+                                                        uint64_t* __restrict__ counts_out,
+                                                        uint32_t* __restrict__ hours_out, uint32_t base_hour,
+                                                        uint64_t cap, unsigned long long* cursor)
+{
+    const uint64_t n = t.mask + 1;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
+        const uint64_t i = i0 + lane;
+        uint64_t k = i < n ? t.keys[i] : HMS_EMPTY;
+        const uint64_t tag = k >> HMS_TAG_SHIFT;
+        const bool m = k != HMS_EMPTY &&
+                       (sel == HMS_SEL_EVERY_HOUR ? tag != HM_STREAM_ALLTIME_TAG : tag == sel);
+        const uint64_t bal = __ballot(m);
+        if (!bal) continue;
+        unsigned long long first = 0;
+        if (lane == 0) first = atomicAdd(cursor, (unsigned long long)__popcll(bal));
+        first = __shfl(first, 0, 64);
+        if (m) {
+            const uint64_t pos = first + __popcll(bal & ((1ull << lane) - 1));
+            if (pos < cap) {
+                keys_out[pos] = hms_unpack(k);
+                counts_out[pos] = t.counts[i];
+                if (hours_out) hours_out[pos] = base_hour + (uint32_t)tag;
+            }
+        }
+    }
+}
+
+static dim3 hms_grid(uint64_t n)
+{
+    uint64_t b = (n + 255) / 256;
+    if (b > 8192) b = 8192;
+    return dim3((unsigned)(b ? b : 1));
+}
+
+void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, uint64_t tag_a,
+                             uint64_t tag_b, const HmsTable& t)
+{
+    if (n) hipLaunchKernelGGL(k_stream_insert, hms_grid(n), dim3(256), 0, s, keys, counts, n, tag_a, tag_b, t);
+}
+
+void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to)
+{
+    hipLaunchKernelGGL(k_stream_rehash, hms_grid(from.mask + 1), dim3(256), 0, s, from, to);
+}
+
+void hm_launch_stream_hour_range(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
+                                 unsigned int* mm)
+{
+    if (n) hipLaunchKernelGGL(k_stream_hour_range, hms_grid(n), dim3(256), 0, s, hour, keep, n, mm);
+}
+
+void hm_launch_stream_hour_presence(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
+                                    uint32_t lo, uint8_t* present)
+{
+    if (n) hipLaunchKernelGGL(k_stream_hour_presence, hms_grid(n), dim3(256), 0, s, hour, keep, n, lo, present);
+}
+
+void hm_launch_stream_hour_mask(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n, uint32_t h,
+                                uint8_t* mask)
+{
+    if (n) hipLaunchKernelGGL(k_stream_hour_mask, hms_grid(n), dim3(256), 0, s, hour, keep, n, h, mask);
+}
+
+void hm_launch_stream_extract(hipStream_t s, const HmsTable& t, uint64_t sel, uint64_t* keys_out,
+                              uint64_t* counts_out, uint32_t* hours_out, uint32_t base, uint64_t cap,
+                              unsigned long long* cursor)
+{
+    hipLaunchKernelGGL(k_stream_extract, hms_grid(t.mask + 1), dim3(256), 0, s, t, sel, keys_out, counts_out,
+                       hours_out, base, cap, cursor);
+}

@@ -116,6 +116,37 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
  *   [2] k_aggregate (+ merged buckets)   [3] k_pool levels */
 int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_stages);
 
+/* Streaming: micro-batches folded into a heatmap resident in HBM (BASELINE
+ * config 5).  The reference recomputes the pyramid per
+ * Spark job (heatmap.py:152-158) under the single timespan label 'alltime'
+ * (heatmap.py:62-63); a stream keeps that alltime heatmap plus one bucket per
+ * epoch hour (uint32 hours since 1970, hour = unix_seconds / 3600).
+ *   hm_stream_create  zooms [zmin, zmax] (zmax <= HM_MAX_ZOOM); hours
+ *                     base_hour .. base_hour + HM_STREAM_MAX_HOURS - 1;
+ *                     initial_cells sizes the table (it grows as needed).
+ *   hm_stream_add     hm_count semantics per point (projection errors, keep);
+ *                     hour: uint32[n] (device) or NULL (alltime only).  The
+ *                     kept points of one batch may span at most
+ *                     HM_STREAM_MAX_SPAN hours; each distinct hour costs one
+ *                     count pyramid over the batch (batches are time-ordered).
+ *   hm_stream_extract hour = HM_STREAM_ALLTIME, HM_STREAM_EACH_HOUR (hours_out
+ *                     receives each cell's hour) or one epoch hour; keys in
+ *                     hm_count's layout, unspecified order.  HM_E_CAPACITY
+ *                     with *n_out = cells needed when capacity is too small. */
+#define HM_STREAM_ALLTIME (-1)
+#define HM_STREAM_EACH_HOUR (-2)
+#define HM_STREAM_MAX_HOURS 131071
+#define HM_STREAM_MAX_SPAN 65536
+typedef struct hm_stream hm_stream;
+int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_t initial_cells, hm_stream** out);
+int hm_stream_add(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, const uint32_t* hour,
+                  int64_t n);
+/* occupied table slots over all buckets, and the table capacity */
+int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity);
+int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out, uint64_t* counts_out, uint32_t* hours_out,
+                      int64_t capacity, int64_t* n_out);
+int hm_stream_destroy(hm_stream* s);
+
 /* Benchmark/test utility, not part of the reference boundary: fill lat/lon
  * (device) with points start..start+n-1 of a synthetic cloud, bit-identical
  * to heatmap_amd/synth.py.  kind: 0 uniform, 1 hotspots (table = device
