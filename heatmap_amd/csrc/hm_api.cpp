@@ -695,17 +695,13 @@ static int stream_alloc_table(hm_stream* s, uint64_t cap, HmsTable* t)
 {
     t->mask = cap - 1;
     t->state = s->t.state;
-    if (hipMalloc((void**)&t->keys, cap * 8) != hipSuccess) {
+    if (hipMalloc((void**)&t->slots, cap * 16) != hipSuccess) {
         (void)hipGetLastError();
+        t->slots = nullptr;
         return HM_E_NOMEM;
     }
-    if (hipMalloc((void**)&t->counts, cap * 8) != hipSuccess) {
-        (void)hipGetLastError();
-        (void)hipFree(t->keys);
-        return HM_E_NOMEM;
-    }
-    HIPCHK(hipMemsetAsync(t->keys, 0xFF, cap * 8, s->ctx->stream));
-    HIPCHK(hipMemsetAsync(t->counts, 0, cap * 8, s->ctx->stream));
+    hm_launch_stream_init(s->ctx->stream, *t);
+    HIPCHK(hipGetLastError());
     return HM_OK;
 }
 
@@ -723,8 +719,7 @@ static int stream_reserve(hm_stream* s, uint64_t incoming)
     hm_launch_stream_rehash(s->ctx->stream, s->t, nt);
     HIPCHK(hipGetLastError());
     st = stream_sync_state(s);
-    HIPCHK(hipFree(s->t.keys));
-    HIPCHK(hipFree(s->t.counts));
+    HIPCHK(hipFree(s->t.slots));
     s->t = nt;
     return st;
 }
@@ -883,7 +878,7 @@ extern "C" int hm_stream_destroy(hm_stream* s)
     if (!s) return HM_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
-    for (void* p : {(void*)s->t.keys, (void*)s->t.counts, (void*)s->t.state, s->bkeys.p, s->bcounts.p, s->mask.p,
+    for (void* p : {(void*)s->t.slots, (void*)s->t.state, s->bkeys.p, s->bcounts.p, s->mask.p,
                     s->present.p})
         if (p) (void)hipFree(p);
     if (s->hstate) (void)hipHostFree(s->hstate);

@@ -266,13 +266,13 @@ void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int6
 #define HMS_SEL_EVERY_HOUR (1ull << 20)     /* extract selector: every hour bucket */
 enum { HMS_ST_OCCUPIED = 0, HMS_ST_OVERFLOW = 1, HMS_ST_CURSOR = 2, HMS_ST_HOURS = 4 /* min, max as u32 */ };
 struct HmsTable {
-    uint64_t* keys;
-    uint64_t* counts;
-    uint64_t mask; /* capacity - 1 (power of two) */
+    uint64_t* slots; /* capacity x {key, count} */
+    uint64_t mask;   /* capacity - 1 (power of two) */
     unsigned long long* state;
 };
 void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, uint64_t tag_a,
                              uint64_t tag_b, const HmsTable& t);
+void hm_launch_stream_init(hipStream_t s, const HmsTable& t);
 void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to);
 void hm_launch_stream_hour_range(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
                                  unsigned int* mm);

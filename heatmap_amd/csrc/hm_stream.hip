@@ -4,7 +4,8 @@
  * The reference recomputes its whole pyramid per Spark job (heatmap.py:152-158);
  * a streaming caller instead folds each micro-batch's hm_count cells into a
  * heatmap that stays in HBM.  The resident heatmap is an open-addressing hash
- * table (SoA: u64 keys, u64 counts, linear probing, EMPTY = all ones):
+ * table of 16-B slots (u64 key, u64 count in one slot, so a probe hit and its
+ * count add touch one cache line; linear probing, EMPTY key = all ones):
  *   - merge cost is O(cells of the batch), independent of the resident size
  *     (a sorted resident set would re-stream every resident cell per batch);
  *   - a batch cell is one probe sequence + one 64-bit atomic add, so the
@@ -55,16 +56,16 @@ __device__ __forceinline__ uint32_t hms_insert(const HmsTable& t, uint64_t k, ui
 {
     uint64_t h = hms_hash(k) & t.mask;
     for (uint64_t probe = 0; probe <= t.mask; probe++) {
-        uint64_t cur = __atomic_load_n(&t.keys[h], __ATOMIC_RELAXED);
+        uint64_t cur = __atomic_load_n(&t.slots[2 * h], __ATOMIC_RELAXED);
         uint32_t claimed = 0;
         if (cur == HMS_EMPTY) {
             const unsigned long long prev =
-                atomicCAS((unsigned long long*)&t.keys[h], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
+                atomicCAS((unsigned long long*)&t.slots[2 * h], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
             claimed = prev == HMS_EMPTY;
             cur = claimed ? k : prev;
         }
         if (cur == k) {
-            atomicAdd((unsigned long long*)&t.counts[h], (unsigned long long)c);
+            atomicAdd((unsigned long long*)&t.slots[2 * h + 1], (unsigned long long)c);
             return claimed;
         }
         h = (h + 1) & t.mask;
@@ -104,8 +105,8 @@ __global__ __launch_bounds__(256) void k_stream_rehash(HmsTable from, HmsTable t
     const uint64_t n = from.mask + 1;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t k = from.keys[i];
-        if (k != HMS_EMPTY) claimed += hms_insert(to, k, from.counts[i], &overflow);
+        const ulonglong2 sl = ((const ulonglong2*)from.slots)[i];
+        if (sl.x != HMS_EMPTY) claimed += hms_insert(to, sl.x, sl.y, &overflow);
     }
     claimed = hms_wave_sum(claimed);
     const uint64_t of = hms_wave_sum(overflow);
@@ -113,6 +114,14 @@ __global__ __launch_bounds__(256) void k_stream_rehash(HmsTable from, HmsTable t
         if (claimed) atomicAdd(&to.state[HMS_ST_OCCUPIED], (unsigned long long)claimed);
         if (of) atomicAdd(&to.state[HMS_ST_OVERFLOW], (unsigned long long)of);
     }
+}
+
+__global__ __launch_bounds__(256) void k_stream_init(HmsTable t)
+{
+    const uint64_t n = t.mask + 1;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        ((ulonglong2*)t.slots)[i] = make_ulonglong2(HMS_EMPTY, 0ull);
 }
 
 /* Min / max epoch hour over the kept points of a batch. */
@@ -133,9 +142,21 @@ __global__ __launch_bounds__(256) void k_stream_hour_range(const uint32_t* __res
         lo = a < lo ? a : lo;
         hi = b > hi ? b : hi;
     }
-    if ((threadIdx.x & 63) == 0 && lo <= hi) {
-        atomicMin(&mm[0], lo);
-        atomicMax(&mm[1], hi);
+    __shared__ uint32_t wlo[4], whi[4];
+    if ((threadIdx.x & 63) == 0) {
+        wlo[threadIdx.x >> 6] = lo;
+        whi[threadIdx.x >> 6] = hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; w++) {
+            lo = wlo[w] < lo ? wlo[w] : lo;
+            hi = whi[w] > hi ? whi[w] : hi;
+        }
+        if (lo <= hi) { /* one pair of atomics per block */
+            atomicMin(&mm[0], lo);
+            atomicMax(&mm[1], hi);
+        }
     }
 }
 
@@ -163,33 +184,50 @@ __global__ __launch_bounds__(256) void k_stream_hour_mask(const uint32_t* __rest
 
 /* Dump the slots whose hour bucket matches `sel` (sel == HMS_SEL_EVERY_HOUR:
  * every bucket but alltime) as hm_count keys + counts (+ absolute epoch hour).
- * Wave-aggregated cursor; slots past `cap` are counted but not written. */
+ * Each wave owns chunks of HMS_XCHUNK slots: it counts its matches (ballots),
+ * reserves output with ONE atomic per chunk, then re-reads the (cache-hot)
+ * chunk and writes in slot order.  Matches past `cap` are counted, not written. */
+#define HMS_XCHUNK (64 * 64)
+__device__ __forceinline__ bool hms_sel(uint64_t k, uint64_t sel)
+{
+    const uint64_t tag = k >> HMS_TAG_SHIFT;
+    return k != HMS_EMPTY && (sel == HMS_SEL_EVERY_HOUR ? tag != HM_STREAM_ALLTIME_TAG : tag == sel);
+}
+
 __global__ __launch_bounds__(256) void k_stream_extract(HmsTable t, uint64_t sel, uint64_t* __restrict__ keys_out,
                                                         uint64_t* __restrict__ counts_out,
                                                         uint32_t* __restrict__ hours_out, uint32_t base_hour,
                                                         uint64_t cap, unsigned long long* cursor)
 {
-    const uint64_t n = t.mask + 1;
+    const uint64_t n = t.mask + 1; /* power of two >= 1024 */
     const uint32_t lane = threadIdx.x & 63;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i0 = (uint64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63u); i0 < n; i0 += stride) {
-        const uint64_t i = i0 + lane;
-        uint64_t k = i < n ? t.keys[i] : HMS_EMPTY;
-        const uint64_t tag = k >> HMS_TAG_SHIFT;
-        const bool m = k != HMS_EMPTY &&
-                       (sel == HMS_SEL_EVERY_HOUR ? tag != HM_STREAM_ALLTIME_TAG : tag == sel);
-        const uint64_t bal = __ballot(m);
-        if (!bal) continue;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const ulonglong2* slots = (const ulonglong2*)t.slots;
+    for (uint64_t c0 = wave * HMS_XCHUNK; c0 < n; c0 += waves * HMS_XCHUNK) {
+        const uint64_t c1 = c0 + HMS_XCHUNK < n ? c0 + HMS_XCHUNK : n;
+        uint64_t cnt = 0;
+        for (uint64_t i = c0 + lane; i < c1; i += 64) cnt += hms_sel(slots[i].x, sel);
+        cnt = hms_wave_sum(cnt);
+        if (!cnt) continue;
         unsigned long long first = 0;
-        if (lane == 0) first = atomicAdd(cursor, (unsigned long long)__popcll(bal));
+        if (lane == 0) first = atomicAdd(cursor, (unsigned long long)cnt);
         first = __shfl(first, 0, 64);
-        if (m) {
-            const uint64_t pos = first + __popcll(bal & ((1ull << lane) - 1));
-            if (pos < cap) {
-                keys_out[pos] = hms_unpack(k);
-                counts_out[pos] = t.counts[i];
-                if (hours_out) hours_out[pos] = base_hour + (uint32_t)tag;
+        for (uint64_t j0 = c0; j0 < c1; j0 += 64) {
+            const uint64_t i = j0 + lane;
+            ulonglong2 sl = make_ulonglong2(HMS_EMPTY, 0ull);
+            if (i < c1) sl = slots[i];
+            const bool m = hms_sel(sl.x, sel);
+            const uint64_t bal = __ballot(m);
+            if (m) {
+                const uint64_t pos = first + __popcll(bal & ((1ull << lane) - 1));
+                if (pos < cap) {
+                    keys_out[pos] = hms_unpack(sl.x);
+                    counts_out[pos] = sl.y;
+                    if (hours_out) hours_out[pos] = base_hour + (uint32_t)(sl.x >> HMS_TAG_SHIFT);
+                }
             }
+            first += __popcll(bal);
         }
     }
 }
@@ -207,6 +245,11 @@ void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t
     if (n) hipLaunchKernelGGL(k_stream_insert, hms_grid(n), dim3(256), 0, s, keys, counts, n, tag_a, tag_b, t);
 }
 
+void hm_launch_stream_init(hipStream_t s, const HmsTable& t)
+{
+    hipLaunchKernelGGL(k_stream_init, hms_grid(t.mask + 1), dim3(256), 0, s, t);
+}
+
 void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to)
 {
     hipLaunchKernelGGL(k_stream_rehash, hms_grid(from.mask + 1), dim3(256), 0, s, from, to);
@@ -215,7 +258,8 @@ void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable
 void hm_launch_stream_hour_range(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
                                  unsigned int* mm)
 {
-    if (n) hipLaunchKernelGGL(k_stream_hour_range, hms_grid(n), dim3(256), 0, s, hour, keep, n, mm);
+    const uint64_t b = (n + 255) / 256;
+    if (n) hipLaunchKernelGGL(k_stream_hour_range, dim3((unsigned)(b < 1024 ? b : 1024)), dim3(256), 0, s, hour, keep, n, mm);
 }
 
 void hm_launch_stream_hour_presence(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
@@ -234,6 +278,7 @@ void hm_launch_stream_extract(hipStream_t s, const HmsTable& t, uint64_t sel, ui
                               uint64_t* counts_out, uint32_t* hours_out, uint32_t base, uint64_t cap,
                               unsigned long long* cursor)
 {
-    hipLaunchKernelGGL(k_stream_extract, hms_grid(t.mask + 1), dim3(256), 0, s, t, sel, keys_out, counts_out,
+    const uint64_t chunks = (t.mask + HMS_XCHUNK) / HMS_XCHUNK, blocks = (chunks + 3) / 4;
+    hipLaunchKernelGGL(k_stream_extract, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, t, sel, keys_out, counts_out,
                        hours_out, base, cap, cursor);
 }
