@@ -820,6 +820,9 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
         return stream_fold(s, lat, lon, keep, n, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT, 0);
     if (lo < s->base || (uint64_t)hi - s->base >= HM_STREAM_MAX_HOURS) return HM_E_RANGE;
     if ((uint64_t)hi - lo >= HM_STREAM_MAX_SPAN) return HM_E_ARG;
+    if (lo == hi) /* one hour (the usual time-ordered batch): the kept points are that hour's */
+        return stream_fold(s, lat, lon, keep, n, (uint64_t)(lo - s->base) << HMS_TAG_SHIFT,
+                           HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT);
     const uint32_t span = hi - lo + 1;
     if ((st = stream_buf(s, s->present, span)) || (st = stream_buf(s, s->mask, (size_t)n))) return st;
     HIPCHK(hipMemsetAsync(s->present.p, 0, span, q));

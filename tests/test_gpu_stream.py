@@ -85,3 +85,22 @@ def test_stream_empty_and_unkept(gpu):
     assert s.counts().count.size == 0
     assert s.cells()[0] == 0
     s.close()
+
+
+def test_stream_single_hour_batches(gpu):
+    """Time-ordered batches, one hour each (the fast path that folds `keep` directly)."""
+    lat, lon = synth.generate("hotspots", 60000, seed=9)
+    rng = np.random.default_rng(9)
+    keep = (rng.random(60000) > 0.2).astype(np.uint8)
+    hour = (BASE + np.arange(60000) // 20000).astype(np.uint32)  # 3 batches, 1 hour each
+    s = StreamingHeatmap(2, 17, base_hour=BASE, initial_cells=2000)
+    for b in range(3):
+        sl = slice(b * 20000, (b + 1) * 20000)
+        s.add(lat[sl], lon[sl], keep[sl], hour[sl])
+    s.add(lat[:5000], lon[:5000], keep[:5000], hour[:5000])  # a late batch for an older hour
+    lat2, lon2 = np.concatenate([lat, lat[:5000]]), np.concatenate([lon, lon[:5000]])
+    keep2, hour2 = np.concatenate([keep, keep[:5000]]), np.concatenate([hour, hour[:5000]])
+    _same(s.counts(ALLTIME), oracle.count(lat2, lon2, keep2, 2, 17))
+    for h, c in s.hourly().items():
+        _same(c, oracle.count(lat2, lon2, keep2 & (hour2 == h).astype(np.uint8), 2, 17))
+    s.close()
