@@ -65,16 +65,24 @@ try:
     device.project([1.0], [2.0], 3)
 except _lib.DeviceUnavailable as e:
     print("RAISED", e)
+from heatmap_amd.stream import StreamingHeatmap
+try:
+    StreamingHeatmap(0, 18)
+except _lib.DeviceUnavailable as e:
+    print("STREAM RAISED", e)
 L = _lib.load()
 p = ctypes.c_void_p()
 st = L.hm_ctx_create(ctypes.byref(p), 0, None)
 print("CTX", st)
+print("STREAM ARG", L.hm_stream_create(None, 0, 18, 0, 0, ctypes.byref(p)))
 """
     r = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=300)
     if "SKIP" in r.stdout:
         pytest.skip("a GPU is present")
     assert "RAISED" in r.stdout, r.stdout + r.stderr
     assert "CTX 18" in r.stdout, r.stdout + r.stderr     # HM_E_HIP
+    assert "STREAM RAISED" in r.stdout, r.stdout + r.stderr
+    assert "STREAM ARG 16" in r.stdout, r.stdout + r.stderr  # HM_E_ARG: no context
 
 
 def test_product_does_not_import_the_oracle():
