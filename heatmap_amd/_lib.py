@@ -24,9 +24,10 @@ HM_E_CAPACITY = 17
 HM_E_HIP = 18
 HM_E_NOMEM = 19
 HM_COUNT_MAX_ZOOM = 21
+HM_ABI_VERSION = 2
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
-           "hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
+           "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_last_error", "hm_last_stats", "hm_synth",
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_extract", "hm_stream_destroy"]
 
 _LIB = None
@@ -58,6 +59,9 @@ def load() -> ctypes.CDLL:
             except Exception as e:  # pragma: no cover - surfaced to the caller
                 raise DeviceUnavailable("heatmap_amd: cannot build %s: %s" % (path, e)) from e
         L = ctypes.CDLL(path)
+        if L.hm_abi_version() != HM_ABI_VERSION:
+            raise DeviceUnavailable("heatmap_amd: %s has ABI %d, this binding needs %d"
+                                    % (path, L.hm_abi_version(), HM_ABI_VERSION))
         c = ctypes
         P = c.POINTER
         vp = c.c_void_p
@@ -68,8 +72,12 @@ def load() -> ctypes.CDLL:
         L.hm_ctx_set_stream.argtypes = [vp, vp]
         L.hm_ctx_destroy.argtypes = [vp]
         L.hm_project.argtypes = [vp, vp, vp, c.c_int64, c.c_int, vp, vp, vp]
-        L.hm_count.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
-        L.hm_count_tiles.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_count.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64),
+                               vp, c.c_int64, P(c.c_int64)]
+        L.hm_count_tiles.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64),
+                                     vp, c.c_int64, P(c.c_int64)]
+        L.hm_count_grouped.argtypes = [vp, vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, c.c_int64,
+                                       P(c.c_int64)]
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
         L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]

@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libheatmap_amd.so")
-SOURCES = ["hm_kernels.hip", "hm_stream.hip", "hm_api.cpp"]
+SOURCES = ["hm_kernels.hip", "hm_general.hip", "hm_stream.hip", "hm_api.cpp"]
 HEADERS = ["hm_common.h", "hm_device.h", "hm_glibc_emul.h", "hm_project.h", "hm_pipeline.h", "hm_ytab.h"]
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=" + ARCH,

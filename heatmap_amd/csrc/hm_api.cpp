@@ -43,7 +43,7 @@ struct hm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     std::vector<Buf> bufs;
-    unsigned long long* state = nullptr;      /* device: err, exotic, slow, cursor, nslots */
+    unsigned long long* state = nullptr;      /* device: err, exotic count, slow, cursor, nslots, ... */
     unsigned long long* host_state = nullptr; /* pinned mirror */
     int64_t last_err_index = -1;
     int last_err_kind = 0;
@@ -54,7 +54,7 @@ struct hm_ctx {
 
 enum {
     ST_ERR = 0,
-    ST_EXOTIC = 1,
+    ST_XCOUNT = 1,
     ST_SLOW = 2,
     ST_CURSOR = 3,
     ST_NSLOTS = 4,
@@ -85,7 +85,11 @@ enum {
     B_CHILD0 = B_BK0 + HM_MAX_LEVELS * 8,
     B_TOT0 = B_CHILD0 + HM_MAX_LEVELS,
     B_SLOTS = B_TOT0 + HM_MAX_LEVELS + 1,
-    B_SLOTBKT, B_GSLOTS, B_SPCODES, B_DESC0, B_COUNT = B_DESC0 + HM_MAX_LEVELS
+    B_SLOTBKT, B_GSLOTS, B_SPCODES, B_DESC0,
+    /* exotic list and the general path (hm_general.hip) */
+    B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
+    B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
+    B_COUNT
 };
 
 static int ensure(hm_ctx* c, int slot, size_t bytes, void** out)
@@ -128,7 +132,7 @@ const char* hm_status_string(int s)
     case HM_E_DOMAIN: return "math domain error";
     case HM_E_INF: return "cannot convert float infinity to integer";
     case HM_E_RANGE: return "value outside the range supported by the device path";
-    case HM_E_EXOTIC: return "tile outside [0, 2^zmax)^2 is not binned by the device path";
+    case HM_E_EXOTIC: return "the streaming heatmap holds tiles inside [0, 2^zmax)^2 only";
     case HM_E_ARG: return "invalid argument";
     case HM_E_CAPACITY: return "output capacity too small";
     case HM_E_HIP: return "HIP runtime error";
@@ -152,12 +156,25 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     c->device = device;
     c->stream = (hipStream_t)stream;
     c->bufs.resize(B_COUNT);
-    if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc(&c->host_state, 4 * ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
-        delete c;
-        return HM_E_NOMEM;
+    for (int i = 0; i < 10; i++) c->ev[i] = nullptr;
+    int st = HM_OK;
+    if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
+        c->state = nullptr;
+        st = HM_E_NOMEM;
+    } else if (hipHostMalloc(&c->host_state, 4 * ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
+        c->host_state = nullptr;
+        st = HM_E_NOMEM;
     }
-    for (int i = 0; i < 10; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    for (int i = 0; i < 10 && st == HM_OK; i++)
+        if (hipEventCreate(&c->ev[i]) != hipSuccess) {
+            c->ev[i] = nullptr;
+            st = HM_E_HIP;
+        }
+    if (st != HM_OK) {
+        (void)hipGetLastError();
+        hm_ctx_destroy(c);
+        return st;
+    }
     *out = c;
     return HM_OK;
 }
@@ -172,12 +189,13 @@ int hm_ctx_set_stream(hm_ctx* c, void* stream)
 int hm_ctx_destroy(hm_ctx* c)
 {
     if (!c) return HM_OK;
-    hipSetDevice(c->device);
+    (void)hipSetDevice(c->device);
     for (auto& b : c->bufs)
-        if (b.p) hipFree(b.p);
-    if (c->state) hipFree(c->state);
-    if (c->host_state) hipHostFree(c->host_state);
-    for (int i = 0; i < 10; i++) hipEventDestroy(c->ev[i]);
+        if (b.p) (void)hipFree(b.p);
+    if (c->state) (void)hipFree(c->state);
+    if (c->host_state) (void)hipHostFree(c->host_state);
+    for (int i = 0; i < 10; i++)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     delete c;
     return HM_OK;
 }
@@ -203,7 +221,7 @@ int hm_last_stats(hm_ctx* c, int64_t* slow_points, double* stage_us, int n_stage
 static int reset_state(hm_ctx* ctx)
 {
     HIPCHK(hipMemsetAsync(ctx->state, 0, ST_COUNT * sizeof(unsigned long long), ctx->stream));
-    HIPCHK(hipMemsetAsync(ctx->state + ST_ERR, 0xFF, 2 * sizeof(unsigned long long), ctx->stream));
+    HIPCHK(hipMemsetAsync(ctx->state + ST_ERR, 0xFF, sizeof(unsigned long long), ctx->stream));
     return HM_OK;
 }
 
@@ -218,18 +236,15 @@ static int read_state(hm_ctx* ctx)
 static int take_error(hm_ctx* ctx)
 {
     const unsigned long long e = ctx->host_state[ST_ERR];
-    const unsigned long long x = ctx->host_state[ST_EXOTIC];
     ctx->last_slow = (int64_t)ctx->host_state[ST_SLOW];
-    /* the first failing point in input order wins; a projection error at a
-     * smaller index than an exotic point is reported first */
-    const unsigned long long w = e < x ? e : x;
-    if (w == ~0ull) {
+    /* the first failing point in input order (atomicMin of index << 8 | kind) */
+    if (e == ~0ull) {
         ctx->last_err_index = -1;
         ctx->last_err_kind = HM_OK;
         return HM_OK;
     }
-    ctx->last_err_index = (int64_t)(w >> 8);
-    ctx->last_err_kind = (int)(w & 0xFF);
+    ctx->last_err_index = (int64_t)(e >> 8);
+    ctx->last_err_kind = (int)(e & 0xFF);
     return ctx->last_err_kind;
 }
 
@@ -250,14 +265,109 @@ extern "C" int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int
 
 /* ------------------------------------------------------------------------ */
 
+/* ------------------------------------------------------------------------ */
+/* general path: n exact zoom-Z tiles (device lists) -> records of zooms       */
+/* [zmin, Z] (hm_general.hip).  *total = records (all of them, even past the   */
+/* capacity).  Errors (tiles beyond the key's range) go to the error word.      */
+/* ------------------------------------------------------------------------ */
+static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint32_t* group, const int64_t* index,
+                     uint64_t n, int Z, int zmin, int64_t* cells, int width, int64_t capacity, uint64_t* total)
+{
+    *total = 0;
+    if (n == 0) return HM_OK;
+    if (n >= (1ull << 32)) return HM_E_ARG;   /* radix ranks are u32 */
+    hipStream_t s = ctx->stream;
+    ulonglong2 *ka, *kb;
+    uint64_t *flag, *idx, *c, *S, *end, *cnt0, *cnt1, *partial, *tot, *hist, *off;
+    unsigned long long* orand;
+    ENSURE(B_GEN_KA, n * 16, ka);
+    ENSURE(B_GEN_KB, n * 16, kb);
+    ENSURE(B_GEN_ORAND, 4 * 8, orand);
+    ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+    ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+    unsigned long long* up = ctx->host_state + ST_COUNT;
+    HIPCHK(hipStreamSynchronize(s));
+    up[0] = 0;
+    up[1] = 0;
+    up[2] = ~0ull;
+    up[3] = ~0ull;
+    HIPCHK(hipMemcpyAsync(orand, up, 4 * 8, hipMemcpyHostToDevice, s));
+    HmGenArgs ga;
+    ga.row = row;
+    ga.col = col;
+    ga.group = group;
+    ga.index = index;
+    ga.n = n;
+    ga.Z = Z;
+    ga.keys = ka;
+    ga.orand = orand;
+    ga.err_word = ctx->state + ST_ERR;
+    hm_launch_gen_keys(s, ga);
+    HIPCHK(hipGetLastError());
+    unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+    HIPCHK(hipMemcpyAsync(down, orand, 4 * 8, hipMemcpyDeviceToHost, s));
+    int st;
+    if ((st = read_state(ctx))) return st;
+    if ((st = take_error(ctx))) return st;
+    /* LSD passes over the digits that differ between keys */
+    const unsigned __int128 var = ((((unsigned __int128)down[1]) << 64) | down[0]) ^
+                                  ((((unsigned __int128)down[3]) << 64) | down[2]);
+    const uint64_t nt = hm_rx_tiles(n);
+    ENSURE(B_GEN_HIST, nt * 256 * 8, hist);
+    ENSURE(B_GEN_OFF, nt * 256 * 8, off);
+    ulonglong2 *cur = ka, *oth = kb;
+    for (int sh = 0; sh < 128; sh += 8) {
+        if (!(uint64_t)((var >> sh) & 0xFF)) continue;
+        hm_launch_rx_pass(s, cur, oth, n, sh, hist, off, partial, tot);
+        HIPCHK(hipGetLastError());
+        std::swap(cur, oth);
+    }
+    /* zoom cascade: level z = Z, Z-1, ..., zmin; cur holds the sorted keys */
+    ENSURE(B_GEN_FLAG, n * 8, flag);
+    ENSURE(B_GEN_IDX, n * 8, idx);
+    ENSURE(B_GEN_C, n * 8, c);
+    ENSURE(B_GEN_S, n * 8, S);
+    ENSURE(B_GEN_END, n * 8, end);
+    ENSURE(B_GEN_CNT0, n * 8, cnt0);
+    ENSURE(B_GEN_CNT1, n * 8, cnt1);
+    HmGenEmit e;
+    e.cells = cells;
+    e.capacity = (uint64_t)capacity;
+    e.width = width;
+    const uint64_t* cin = nullptr;
+    uint64_t m = n, emitted = 0;
+    for (int z = Z; z >= zmin; z--) {
+        const int sh = z == Z ? 0 : 2;
+        hm_launch_rle_prep(s, cur, cin, m, sh, flag, c);
+        hm_launch_scan(s, flag, m, partial, idx, tot + 0);
+        hm_launch_scan(s, c, m, partial, S, tot + 1);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        const uint64_t u = down[0];
+        uint64_t* cout = (cin == cnt0) ? cnt1 : cnt0;
+        hm_launch_rle_scatter(s, cur, m, sh, flag, idx, S, c, oth, end);
+        hm_launch_rle_emit(s, e, oth, end, u, z, cout, emitted, 1);
+        HIPCHK(hipGetLastError());
+        emitted += u;
+        std::swap(cur, oth);
+        cin = cout;
+        m = u;
+    }
+    *total = emitted;
+    return HM_OK;
+}
+
 static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows, const int64_t* cols,
                       const uint8_t* keep, int64_t n, int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out,
-                      int64_t capacity, int64_t* n_out)
+                      int64_t capacity, int64_t* n_out, int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
-    if (!ctx || !n_out || n < 0 || n >= (int64_t)0xFFFFFFF0ll || zmin < 0 || zmax < zmin ||
-        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && (!keys_out || !counts_out)))
+    if (!ctx || !n_out || !nx_out || n < 0 || n >= (int64_t)0xFFFFFFF0ll || zmin < 0 || zmax < zmin ||
+        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && (!keys_out || !counts_out)) || xcapacity < 0 ||
+        (xcapacity > 0 && !xcells_out))
         return HM_E_ARG;
     *n_out = 0;
+    *nx_out = 0;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const int Z = zmax;
@@ -289,6 +399,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     uint64_t redo_cap = from_tiles ? 0 : std::max<uint64_t>(1u << 20, (uint64_t)n / 256);
     if (redo_cap > (uint64_t)n) redo_cap = (uint64_t)n;
     uint32_t tiles1 = tiles_in + (uint32_t)((redo_cap + HM_T1 - 1) / HM_T1);
+    /* exotic list: first capacity like the redo list's; rebuilt if it overflows */
+    HmExotic xl;
+    xl.cap = std::min<uint64_t>((uint64_t)n, std::max<uint64_t>(1u << 20, (uint64_t)n / 256));
+    ENSURE(B_X_ROW, xl.cap * 8 + 8, xl.row);
+    ENSURE(B_X_COL, xl.cap * 8 + 8, xl.col);
+    ENSURE(B_X_IDX, xl.cap * 8 + 8, xl.idx);
+    xl.count = ctx->state + ST_XCOUNT;
     uint32_t* root = nullptr;
     ENSURE(B_ROOT, 4 * sizeof(uint32_t) + 2 * sizeof(uint64_t), root);
     {
@@ -315,6 +432,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     int32_t* slots = nullptr;
     uint32_t* slot_bucket = nullptr;
     uint64_t level_keys = 0;    /* keys entering level l >= 2 (global positions) */
+    uint64_t nx = 0;            /* kept points outside [0, 2^Z)^2 */
 
     for (int l = 0; l < L; l++) {
         Level& V = lv[l];
@@ -370,7 +488,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.nruns = nruns;
             a.runs = runs_sh;
             a.err_word = ctx->state + ST_ERR;
-            a.exotic_word = ctx->state + ST_EXOTIC;
+            a.x = xl;
             a.slow_count = ctx->state + ST_SLOW;
             a.redo_idx = redo_idx;
             a.redo_count = ctx->state + ST_REDO;
@@ -391,7 +509,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 ra.cols_out = redo_cols;
                 ra.out_count = ctx->state + ST_REDO_OUT;
                 ra.err_word = ctx->state + ST_ERR;
-                ra.exotic_word = ctx->state + ST_EXOTIC;
+                ra.x = xl;
+                ra.cap = redo_cap;
                 hm_launch_redo(s, ra, redo_cap);
                 HIPCHK(hipGetLastError());
             }
@@ -402,6 +521,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 /* adversarial input (mostly polar / guard band): redo the
                  * level with the exact chain fused into the kernel */
                 HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
+                HIPCHK(hipMemsetAsync(xl.count, 0, sizeof(unsigned long long), s));
                 a.tiles = tiles1 = tiles_in;
                 hm_launch_part1(s, a, tiles_in, V.out16, 2);
                 HIPCHK(hipGetLastError());
@@ -427,6 +547,21 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 }
             }
             ctx->last_slow = (int64_t)nredo;
+            if ((st = read_state(ctx))) return st;
+            nx = ctx->host_state[ST_XCOUNT];
+            if (nx > xl.cap) {
+                /* more kept out-of-square points than the list held: rebuild it */
+                xl.cap = nx;
+                ENSURE(B_X_ROW, xl.cap * 8, xl.row);
+                ENSURE(B_X_COL, xl.cap * 8, xl.col);
+                ENSURE(B_X_IDX, xl.cap * 8, xl.idx);
+                HIPCHK(hipMemsetAsync(xl.count, 0, sizeof(unsigned long long), s));
+                hm_launch_collect_exotic(s, lat, lon, rows, cols, keep, n, Z, xl);
+                HIPCHK(hipGetLastError());
+                if ((st = read_state(ctx))) return st;
+                nx = ctx->host_state[ST_XCOUNT];
+                if (nx > xl.cap) return HM_E_HIP;   /* cannot happen: the same points */
+            }
         } else {
             HmPartNArgs a;
             memset(&a, 0, sizeof(a));
@@ -637,23 +772,65 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     }
     const unsigned long long nc = ctx->host_state[ST_CURSOR];
     *n_out = (int64_t)nc;
-    if (nc > (unsigned long long)capacity) return HM_E_CAPACITY;
+    /* cells outside the square: the general path over the exotic list */
+    uint64_t xt = 0;
+    if (nx) {
+        if ((st = gen_count(ctx, xl.row, xl.col, nullptr, xl.idx, nx, Z, zmin, xcells_out, 4, xcapacity, &xt)))
+            return st;
+        if ((st = read_state(ctx))) return st;
+    }
+    *nx_out = (int64_t)xt;
+    if (nc > (unsigned long long)capacity || xt > (uint64_t)xcapacity) return HM_E_CAPACITY;
     return HM_OK;
 }
 
 extern "C" int hm_count(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep, int64_t n, int zmin,
-                        int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+                        int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out,
+                        int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
     if (n > 0 && (!lat || !lon)) return HM_E_ARG;
-    return count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out);
+    return count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
+                      xcells_out, xcapacity, nx_out);
 }
 
 extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep, int64_t n,
                               int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
-                              int64_t* n_out)
+                              int64_t* n_out, int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
     if (n > 0 && (!row || !col)) return HM_E_ARG;
-    return count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out);
+    return count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
+                      xcells_out, xcapacity, nx_out);
+}
+
+extern "C" int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
+                                const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
+                                int64_t capacity, int64_t* n_out)
+{
+    if (!ctx || !n_out || n < 0 || n >= (int64_t)0xFFFFFFF0ll || zmin < 0 || zmax < zmin ||
+        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && !cells_out) || (n > 0 && (!lat || !lon)))
+        return HM_E_ARG;
+    *n_out = 0;
+    HIPCHK(hipSetDevice(ctx->device));
+    int st = reset_state(ctx);
+    if (st) return st;
+    if (n == 0) return HM_OK;
+    int64_t *row, *col, *idx;
+    uint32_t* grp;
+    ENSURE(B_X_ROW, (uint64_t)n * 8, row);
+    ENSURE(B_X_COL, (uint64_t)n * 8, col);
+    ENSURE(B_X_IDX, (uint64_t)n * 8, idx);
+    ENSURE(B_GL_GRP, (uint64_t)n * 4, grp);
+    hm_launch_project_list(ctx->stream, lat, lon, keep, group, n, zmax, row, col, grp, idx, ctx->state + ST_XCOUNT,
+                           ctx->state + ST_ERR);
+    HIPCHK(hipGetLastError());
+    if ((st = read_state(ctx))) return st;
+    if ((st = take_error(ctx))) return st;
+    const uint64_t m = ctx->host_state[ST_XCOUNT];
+    uint64_t total = 0;
+    if ((st = gen_count(ctx, row, col, grp, idx, m, zmax, zmin, cells_out, 5, capacity, &total))) return st;
+    if ((st = read_state(ctx))) return st;
+    *n_out = (int64_t)total;
+    return total > (uint64_t)capacity ? HM_E_CAPACITY : HM_OK;
 }
 
 extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
@@ -751,8 +928,11 @@ static int stream_fold(hm_stream* s, const double* lat, const double* lon, const
         s->bcap = want;
     }
     for (;;) {
+        int64_t nx = 0;
         st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, (uint64_t*)s->bkeys.p, (uint64_t*)s->bcounts.p,
-                      s->bcap, &m);
+                      s->bcap, &m, nullptr, 0, &nx);
+        /* the resident table's keys hold tiles inside [0, 2^z)^2 only */
+        if (nx > 0) return HM_E_EXOTIC;
         if (st != HM_E_CAPACITY) break;
         const int64_t want = m + m / 4 + 1024;
         if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))

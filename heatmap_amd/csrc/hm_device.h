@@ -180,3 +180,11 @@ __device__ __forceinline__ uint32_t hm_skew(uint32_t d, int w)
     const uint32_t m = (1u << w) - 1u;
     return (d & ~m) | ((d + ((d >> w) << 3)) & m);
 }
+
+/* LDS slot of digit d in the partition kernels' digit counters (cur[]): the
+ * hm_skew rotation, so that a hotspot's 2-D cluster of digits (same columns,
+ * consecutive rows) does not pile onto the few banks of its columns */
+#ifndef HM_SKEW_CUR
+#define HM_SKEW_CUR 1
+#endif
+__device__ __forceinline__ uint32_t hm_cur_slot(uint32_t d, int w) { return HM_SKEW_CUR ? hm_skew(d, w) : d; }

@@ -86,6 +86,23 @@ __global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat,
     }
 }
 
+/* wave-aggregated append to the exotic list (every lane of the wave calls) */
+__device__ __forceinline__ void hm_exotic_append(const HmExotic& x, bool p, int64_t r, int64_t c, int64_t i)
+{
+    const uint64_t m = __ballot(p);
+    if (!m) return;
+    const int lead = __ffsll((unsigned long long)m) - 1;
+    unsigned long long b = 0;
+    if (hm_lane() == lead) b = atomicAdd(x.count, (unsigned long long)__popcll(m));
+    b = __shfl(b, lead, 64);
+    const uint64_t q = b + hm_mbcnt(m);
+    if (p && q < x.cap) {
+        x.row[q] = r;
+        x.col[q] = c;
+        x.idx[q] = i;
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* level 1: projection fused with the first partition                        */
 /* ------------------------------------------------------------------------ */
@@ -225,30 +242,32 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         }
         nslow = __popc(redo);
     } else if (__ballot(redo != 0)) {
+        /* every lane runs each step (the exotic append is a wave operation) */
 #pragma unroll
         for (int k = 0; k < HM_P1_PPT; k++) {
-            if (!((redo >> k) & 1u)) continue;
+            const bool rd = (redo >> k) & 1u;
             const int64_t i = base + 2 * ((int64_t)(k >> 1) * HM_P1_THREADS + tid) + (k & 1);
-            const double pa = (k & 1) ? la[k >> 1].y : la[k >> 1].x;
-            const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
             int64_t r = 0, c = 0;
-            int st = HM_OK, slow = 0;
-            if (FROM_TILES) {
-                r = __double_as_longlong(pa);
-                c = __double_as_longlong(po);
-            } else {
-                /* the literal reference chain (tile.py:17,21), row before column */
-                st = hm_row_exact(pa, a.Z, &r);
-                if (st == HM_OK) st = hm_col_exact(po, a.Z, &c);
-                nslow++;
+            int st = HM_OK;
+            if (rd) {
+                const double pa = (k & 1) ? la[k >> 1].y : la[k >> 1].x;
+                const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
+                if (FROM_TILES) {
+                    r = __double_as_longlong(pa);
+                    c = __double_as_longlong(po);
+                } else {
+                    /* the literal reference chain (tile.py:17,21), row before column */
+                    st = hm_row_exact(pa, a.Z, &r);
+                    if (st == HM_OK) st = hm_col_exact(po, a.Z, &c);
+                    nslow++;
+                }
             }
-            (void)slow;
             const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
-            if (st != HM_OK) {
-                atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
-            } else if (kept && ((uint64_t)r >= lim || (uint64_t)c >= lim)) {
-                atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
-            } else if (kept) {
+            if (rd && st != HM_OK) atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+            const bool good = rd & (st == HM_OK) & kept;
+            const bool outside = good & (((uint64_t)r >= lim) | ((uint64_t)c >= lim));
+            hm_exotic_append(a.x, outside, r, c, i);
+            if (good & !outside) {
                 dig[k] = (((uint32_t)r >> hb) << wd) | ((uint32_t)c >> hb);
                 rest[k] = (((uint32_t)r & lowm) << hb) | ((uint32_t)c & lowm);
             }
@@ -259,7 +278,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, HM_MAX_F1, dig[k], dig[k] != 0xFFFFFFFFu);
+    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu);
     __syncthreads();
 
     /* exclusive scan of the digit histogram; one run record per digit */
@@ -269,7 +288,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        cnt[q] = d < F ? cur[d] : 0u;
+        cnt[q] = d < F ? cur[hm_cur_slot(d, wd)] : 0u;
         s += cnt[q];
     }
     uint32_t total;
@@ -291,13 +310,13 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F) cur[d] = offq[q];
+        if (d < F) cur[hm_cur_slot(d, wd)] = offq[q];
     }
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT; k++) {
         const bool v = dig[k] != 0xFFFFFFFFu;
-        const uint32_t pos = hm_lds_claim(cur, HM_MAX_F1, dig[k], v);
+        const uint32_t pos = hm_lds_claim(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), v);
         stage[v ? pos : HM_T1 + hm_lane()] = (OutT)rest[k];
     }
     __syncthreads();
@@ -583,7 +602,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t pos)
         {
             const uint32_t x = pack(k);
-            hm_lds_count(cur, dummy, x >> (2 * s), v);
+            hm_lds_count(cur, dummy, hm_cur_slot(x >> (2 * s), w), v);
             stage[v ? pos : HM_TN + hm_lane()] = x;
         }
         __device__ __forceinline__ void vec(const uint4& k, bool v, uint32_t pos)
@@ -597,10 +616,10 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
             const uint4 x = make_uint4(pack(k.x), pack(k.y), pack(k.z), pack(k.w));
 #endif
 #ifndef HM_EXP_NOCOUNT
-            hm_lds_count(cur, dummy, x.x >> (2 * s), v);
-            hm_lds_count(cur, dummy, x.y >> (2 * s), v);
-            hm_lds_count(cur, dummy, x.z >> (2 * s), v);
-            hm_lds_count(cur, dummy, x.w >> (2 * s), v);
+            hm_lds_count(cur, dummy, hm_cur_slot(x.x >> (2 * s), w), v);
+            hm_lds_count(cur, dummy, hm_cur_slot(x.y >> (2 * s), w), v);
+            hm_lds_count(cur, dummy, hm_cur_slot(x.z >> (2 * s), w), v);
+            hm_lds_count(cur, dummy, hm_cur_slot(x.w >> (2 * s), w), v);
 #endif
             *(uint4*)&stage[v ? pos : HM_TN] = x;
         }
@@ -615,7 +634,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        cnt[q] = d < F ? cur[d] : 0u;
+        cnt[q] = d < F ? cur[hm_cur_slot(d, ww)] : 0u;
         s += cnt[q];
     }
     uint32_t tot2;
@@ -644,7 +663,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F) cur[d] = offq[q];
+        if (d < F) cur[hm_cur_slot(d, ww)] = offq[q];
     }
     constexpr int KPT = HM_TN / HM_PN_THREADS;
     uint32_t kv[KPT];
@@ -665,7 +684,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             v[k] = k * HM_PN_THREADS + tid < total;
-            const uint32_t d = kv[k] >> a.restbits;
+            const uint32_t d = hm_cur_slot(kv[k] >> a.restbits, ww);
             const uint32_t k0 = __builtin_amdgcn_readfirstlane(d);
             same[k] = v[k] & (d == k0);
             mk[k] = __ballot(same[k]);
@@ -1664,7 +1683,7 @@ void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool ou
 /* exact resolution of the points k_project_partition (mode 0) deferred */
 __global__ __launch_bounds__(256) void k_redo(HmRedoArgs a)
 {
-    const uint64_t n = *a.redo_count;
+    const uint64_t n = min((uint64_t)*a.redo_count, a.cap);   /* the list holds at most cap */
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < n; q += stride) {
         const uint32_t i = a.redo_idx[q];
@@ -1673,11 +1692,11 @@ __global__ __launch_bounds__(256) void k_redo(HmRedoArgs a)
         if (st == HM_OK) st = hm_col_exact(a.lon[i], a.Z, &c);
         const bool kept = !a.keep || a.keep[i];
         const uint64_t lim = 1ull << a.Z;
-        if (st != HM_OK) {
-            atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
-        } else if (kept && ((uint64_t)r >= lim || (uint64_t)c >= lim)) {
-            atomicMin(a.exotic_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_EXOTIC);
-        } else if (kept) {
+        if (st != HM_OK) atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+        const bool good = (st == HM_OK) & kept;
+        const bool outside = good & (((uint64_t)r >= lim) | ((uint64_t)c >= lim));
+        hm_exotic_append(a.x, outside, r, c, (int64_t)i);
+        if (good & !outside) {
             const unsigned long long o = atomicAdd(a.out_count, 1ull);
             a.rows_out[o] = r;
             a.cols_out[o] = c;
@@ -1691,6 +1710,99 @@ void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n)
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_redo, dim3((unsigned)blocks), dim3(256), 0, s, a);
+}
+
+/* the exotic list overflowed its first capacity: rebuild it over every point */
+template <bool FROM_TILES>
+__global__ __launch_bounds__(256) void k_collect_exotic(const double* lat, const double* lon, const int64_t* rows,
+                                                        const int64_t* cols, const uint8_t* keep, int64_t n, int Z,
+                                                        HmExotic x)
+{
+    __shared__ double tab[HM_YTAB_N];
+    if (!FROM_TILES) hm_load_ytab(tab);
+    __syncthreads();
+    const uint64_t lim = 1ull << Z;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t n_up = (n + 63) & ~63ll;   /* whole waves stay in the loop */
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
+        int64_t r = 0, c = 0;
+        int st = HM_E_ARG;
+        if (i < n) {
+            if (FROM_TILES) {
+                r = rows[i];
+                c = cols[i];
+                st = HM_OK;
+            } else {
+                int slow = 0;
+                st = hm_project_point(lat[i], lon[i], Z, &r, &c, &slow, tab);
+            }
+        }
+        const bool kept = i < n && (!keep || keep[i]);
+        hm_exotic_append(x, kept & (st == HM_OK) & (((uint64_t)r >= lim) | ((uint64_t)c >= lim)), r, c, i);
+    }
+}
+
+void hm_launch_collect_exotic(hipStream_t s, const double* lat, const double* lon, const int64_t* rows,
+                              const int64_t* cols, const uint8_t* keep, int64_t n, int Z, HmExotic x)
+{
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    if (rows)
+        hipLaunchKernelGGL(k_collect_exotic<true>, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, rows, cols, keep,
+                           n, Z, x);
+    else
+        hipLaunchKernelGGL(k_collect_exotic<false>, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, rows, cols, keep,
+                           n, Z, x);
+}
+
+/* grouped counts: exact tile of every point (errors in input order), and a
+ * list of the kept ones with their group and input index */
+__global__ __launch_bounds__(256) void k_project_list(const double* lat, const double* lon, const uint8_t* keep,
+                                                      const uint32_t* group, int64_t n, int Z, int64_t* row,
+                                                      int64_t* col, uint32_t* grp, int64_t* idx,
+                                                      unsigned long long* count, unsigned long long* err_word)
+{
+    __shared__ double tab[HM_YTAB_N];
+    hm_load_ytab(tab);
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t n_up = (n + 63) & ~63ll;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
+        int64_t r = 0, c = 0;
+        int st = HM_E_ARG;
+        if (i < n) {
+            int slow = 0;
+            st = hm_project_point(lat[i], lon[i], Z, &r, &c, &slow, tab);
+            if (st != HM_OK) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+        }
+        const bool p = i < n && st == HM_OK && (!keep || keep[i]);
+        const uint64_t m = __ballot(p);
+        if (m) {
+            const int lead = __ffsll((unsigned long long)m) - 1;
+            unsigned long long b = 0;
+            if (hm_lane() == lead) b = atomicAdd(count, (unsigned long long)__popcll(m));
+            b = __shfl(b, lead, 64);
+            if (p) {
+                const uint64_t q = b + hm_mbcnt(m);
+                row[q] = r;
+                col[q] = c;
+                grp[q] = group ? group[i] : 0u;
+                idx[q] = i;
+            }
+        }
+    }
+}
+
+void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
+                            const uint32_t* group, int64_t n, int Z, int64_t* row, int64_t* col, uint32_t* grp,
+                            int64_t* idx, unsigned long long* count, unsigned long long* err_word)
+{
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_project_list, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, row, col,
+                       grp, idx, count, err_word);
 }
 
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16)
@@ -1717,6 +1829,7 @@ void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a)
 void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a)
 {
     const uint64_t pairs = a.nchildren << a.shard_bits;
+    if (pairs == 0) return;   /* a level with no parent buckets (nothing kept) */
     if (a.nchildren <= 8192 && pairs <= (1u << 20))
         hipLaunchKernelGGL(k_rs_copy_pairs, dim3((unsigned)pairs), dim3(256), 0, s, a);
     else

@@ -112,6 +112,17 @@ struct HmOut {
     int zmin, zmax;
 };
 
+/* kept points whose zoom-Z tile lies outside [0, 2^Z)^2, appended (exact
+ * tile, input index) for the general path (hm_general.hip); count may pass
+ * cap, then the list is rebuilt by k_collect_exotic at the right size */
+struct HmExotic {
+    int64_t* row;
+    int64_t* col;
+    int64_t* idx;
+    uint64_t cap;
+    unsigned long long* count;
+};
+
 struct HmPart1Args {
     const double* lat;
     const double* lon;
@@ -130,7 +141,7 @@ struct HmPart1Args {
     uint32_t* nruns;            /* [F << shard_bits] */
     uint2* runs;
     unsigned long long* err_word;
-    unsigned long long* exotic_word;
+    HmExotic x;
     unsigned long long* slow_count;
 };
 
@@ -237,13 +248,22 @@ struct HmRedoArgs {
     int Z;
     const uint32_t* redo_idx;
     const unsigned long long* redo_count;
+    uint64_t cap;
     int64_t* rows_out;
     int64_t* cols_out;
     unsigned long long* out_count;
     unsigned long long* err_word;
-    unsigned long long* exotic_word;
+    HmExotic x;
 };
 void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n);
+/* every point again (exact projection), appending the kept out-of-square
+ * ones: the exotic list outgrew its first capacity.  rows/cols: tile input */
+void hm_launch_collect_exotic(hipStream_t s, const double* lat, const double* lon, const int64_t* rows,
+                              const int64_t* cols, const uint8_t* keep, int64_t n, int Z, HmExotic x);
+/* grouped counts: project every point exactly (errors), list the kept ones */
+void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
+                            const uint32_t* group, int64_t n, int Z, int64_t* row, int64_t* col, uint32_t* grp,
+                            int64_t* idx, unsigned long long* count, unsigned long long* err_word);
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16);
 /* run scan steps: per-child shard offsets + run totals; flat copy; per-child keys */
 void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a);
@@ -283,3 +303,32 @@ void hm_launch_stream_hour_mask(hipStream_t s, const uint32_t* hour, const uint8
 void hm_launch_stream_extract(hipStream_t s, const HmsTable& t, uint64_t sel, uint64_t* keys_out,
                               uint64_t* counts_out, uint32_t* hours_out, uint32_t base, uint64_t cap,
                               unsigned long long* cursor);
+
+/* general count path (hm_general.hip): sort of 128-bit cell keys + zoom cascade */
+struct HmGenArgs {
+    const int64_t* row;
+    const int64_t* col;
+    const uint32_t* group;      /* or null */
+    const int64_t* index;       /* input index per entry (error reports), or null */
+    uint64_t n;
+    int Z;
+    ulonglong2* keys;
+    unsigned long long* orand;  /* [or_lo, or_hi, and_lo, and_hi] */
+    unsigned long long* err_word;
+};
+/* records of `width` int64: [group,] zoom, row, col, count */
+struct HmGenEmit {
+    int64_t* cells;
+    uint64_t capacity;
+    int width;
+};
+void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a);
+uint64_t hm_rx_tiles(uint64_t n);
+void hm_launch_rx_pass(hipStream_t s, const ulonglong2* in, ulonglong2* out, uint64_t n, int sh, uint64_t* hist,
+                       uint64_t* off, uint64_t* partial, uint64_t* total);
+void hm_launch_rle_prep(hipStream_t s, const ulonglong2* keys, const uint64_t* cnt, uint64_t n, int sh, uint64_t* flag,
+                        uint64_t* c);
+void hm_launch_rle_scatter(hipStream_t s, const ulonglong2* keys, uint64_t n, int sh, const uint64_t* flag,
+                           const uint64_t* idx, const uint64_t* S, const uint64_t* c, ulonglong2* okey, uint64_t* oend);
+void hm_launch_rle_emit(hipStream_t s, const HmGenEmit& e, const ulonglong2* okey, const uint64_t* oend, uint64_t u,
+                        int z, uint64_t* ocnt, uint64_t base, int emit);

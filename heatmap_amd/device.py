@@ -154,18 +154,24 @@ def decode_keys(keys: np.ndarray):
 
 
 class CountBuffers:
-    """Reusable device output buffers for count() (bench / streaming)."""
+    """Reusable device output buffers for count() (bench / streaming): cells
+    inside [0, 2^z)^2 as (HM_KEY, count), cells outside it as 4 int64 records
+    (zoom, row, col, count)."""
 
-    def __init__(self, capacity: int, device: int = 0):
+    def __init__(self, capacity: int, device: int = 0, xcapacity: int = 1024):
         torch = _torch()
         self.capacity = int(capacity)
+        self.xcapacity = int(xcapacity)
         self.keys = torch.empty(max(self.capacity, 1), dtype=torch.int64, device="cuda:%d" % device)
         self.counts = torch.empty(max(self.capacity, 1), dtype=torch.int64, device="cuda:%d" % device)
+        self.xcells = torch.empty(4 * max(self.xcapacity, 1), dtype=torch.int64, device="cuda:%d" % device)
+        self.nx = 0
 
 
 def count_device(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, buffers=None,
                  tiles: bool = False):
-    """Run the count pyramid; returns (n_cells, buffers) with results left in HBM."""
+    """Run the count pyramid; returns (n_cells, buffers) with results left in
+    HBM (buffers.nx: cells outside the square, in buffers.xcells)."""
     torch = _torch()
     ctx = context(device)
     if tiles:
@@ -187,26 +193,86 @@ def count_device(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int
     fn = ctx.L.hm_count_tiles if tiles else ctx.L.hm_count
     while True:
         nout = ctypes.c_int64(0)
+        nx = ctypes.c_int64(0)
         rc = fn(ctx.ptr, _ptr(a), _ptr(b), _ptr(kp), n, int(zmin), int(zmax), _ptr(buffers.keys),
-                _ptr(buffers.counts), buffers.capacity, ctypes.byref(nout))
+                _ptr(buffers.counts), buffers.capacity, ctypes.byref(nout), _ptr(buffers.xcells), buffers.xcapacity,
+                ctypes.byref(nx))
         if rc == _lib.HM_E_CAPACITY:
-            buffers = CountBuffers(int(nout.value * 1.25) + 64, device)
+            cap = buffers.capacity if nout.value <= buffers.capacity else int(nout.value * 1.25) + 64
+            xcap = buffers.xcapacity if nx.value <= buffers.xcapacity else int(nx.value * 1.25) + 64
+            buffers = CountBuffers(cap, device, xcap)
             continue
         if rc != _lib.HM_OK:
             idx, kind = ctx.last_error()
             _lib.raise_for(rc, idx)
+        buffers.nx = nx.value
         return nout.value, buffers
 
 
 def count(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, tiles: bool = False) -> Counts:
-    """Per-(zoom, row, col) counts for zooms zmin..zmax (host arrays)."""
+    """Per-(zoom, row, col) counts for zooms zmin..zmax (host arrays), cells
+    inside and outside [0, 2^z)^2 together."""
     m, buf = count_device(lat, lon, keep, zmin, zmax, device, tiles=tiles)
     ctx = context(device)
     slow, us = ctx.last_stats()
     keys = buf.keys[:m].cpu().numpy().view(np.uint64)
     cnt = buf.counts[:m].cpu().numpy()
     z, r, c = decode_keys(keys)
+    if buf.nx:
+        x = buf.xcells[:4 * buf.nx].cpu().numpy().reshape(-1, 4)
+        z = np.concatenate([z, x[:, 0].astype(np.int32)])
+        r = np.concatenate([r, x[:, 1]])
+        c = np.concatenate([c, x[:, 2]])
+        cnt = np.concatenate([cnt, x[:, 3]])
     return Counts(z, r, c, cnt, slow, us)
+
+
+@dataclass
+class GroupedCounts:
+    group: np.ndarray
+    zoom: np.ndarray
+    row: np.ndarray
+    col: np.ndarray
+    count: np.ndarray
+
+    def sorted(self) -> "GroupedCounts":
+        o = np.lexsort((self.col, self.row, self.zoom, self.group))
+        return GroupedCounts(self.group[o], self.zoom[o], self.row[o], self.col[o], self.count[o])
+
+
+def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0) -> GroupedCounts:
+    """Per-(group, zoom, row, col) counts in one device pass (hm_count_grouped).
+    group: uint32 per point; keep: points to count (all are projected)."""
+    torch = _torch()
+    ctx = context(device)
+    a = _dev(lat, torch.float64, device)
+    b = _dev(lon, torch.float64, device)
+    n = a.numel()
+    g = _dev(np.asarray(group, dtype=np.uint32).view(np.int32) if not isinstance(group, torch.Tensor) else group,
+             torch.int32, device)
+    if b.numel() != n or g.numel() != n:
+        raise ValueError("lat, lon and group must have the same length")
+    kp = None
+    if keep is not None:
+        kp = _dev(keep, torch.uint8, device)
+        if kp.numel() != n:
+            raise ValueError("keep must have one entry per point")
+    cap = max(1024, 2 * n + 64)
+    while True:
+        cells = torch.empty(5 * cap, dtype=torch.int64, device=a.device)
+        nout = ctypes.c_int64(0)
+        rc = ctx.L.hm_count_grouped(ctx.ptr, _ptr(a), _ptr(b), _ptr(kp), _ptr(g), n, int(zmin), int(zmax),
+                                    _ptr(cells), cap, ctypes.byref(nout))
+        if rc == _lib.HM_E_CAPACITY:
+            cap = int(nout.value * 1.25) + 64
+            continue
+        if rc != _lib.HM_OK:
+            idx, kind = ctx.last_error()
+            _lib.raise_for(rc, idx)
+        break
+    x = cells[:5 * nout.value].cpu().numpy().reshape(-1, 5)
+    return GroupedCounts(x[:, 0].astype(np.uint32), x[:, 1].astype(np.int32), x[:, 2].copy(), x[:, 3].copy(),
+                         x[:, 4].copy())
 
 
 _SYNTH_KIND = {"uniform": 0, "hotspots": 1, "skew": 2}

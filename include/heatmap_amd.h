@@ -20,6 +20,10 @@
  *   hm_count_tiles  <- the same pyramid starting from already projected tile
  *                      ids (build_heatmaps on locations whose "tileId" is a
  *                      zoom-zmax id, heatmap.py:60-61).
+ *   hm_count_grouped <- the same counts per user group in one pass: the
+ *                      user|alltime|tile keys of tile_id_timespans_mapper
+ *                      (heatmap.py:64-75) with the group as a u32 column
+ *                      (build_heatmaps_columnar's group:i32[N]).
  *   hm_last_error   <- the exception a Spark task would raise: first failing
  *                      point in input order and its kind.
  *
@@ -46,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 1
+#define HM_ABI_VERSION 2
 
 /* status / per-point error kinds */
 #define HM_OK 0
@@ -55,10 +59,13 @@ extern "C" {
 #define HM_E_INF 3       /* OverflowError("cannot convert float infinity to integer") tile.py:21 */
 #define HM_E_RANGE 8     /* representable by the reference but not by this path:
                             |col| >= 2^63, or |lat*pi/180| beyond glibc's
-                            non-Payne-Hanek range (|lat| >~ 6.0e9 degrees) */
-#define HM_E_EXOTIC 9    /* hm_count*: a valid point whose zoom-zmax tile lies
-                            outside [0, 2^zmax)^2 (|lat| > 85.0511..., or
-                            lon outside [-180, 180)); not binned on device yet */
+                            non-Payne-Hanek range (|lat| >~ 6.0e9 degrees), or
+                            (cells outside the square) a zoom-0 tile row
+                            outside [-16, 16) / column outside [-2^47, 2^47) */
+#define HM_E_EXOTIC 9    /* hm_stream_add only: a kept point whose zoom-zmax tile
+                            lies outside [0, 2^zmax)^2 (|lat| > 85.0511..., or
+                            lon outside [-180, 180)); the resident table's keys
+                            hold in-square tiles.  hm_count* bin such points. */
 #define HM_E_ARG 16      /* bad argument (zoom range, null pointer, n < 0) */
 #define HM_E_CAPACITY 17 /* output arrays too small; *n_out holds the size needed */
 #define HM_E_HIP 18      /* HIP runtime error (no device, launch failure) */
@@ -92,17 +99,34 @@ int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int64_t n, int
 /* Count points per (zoom, row, col) for every zoom in [zmin, zmax].
  * keep: uint8[n] or NULL (NULL = keep all); every point is projected (and
  * can fail) whether kept or not, as dataframe_loader does (heatmap.py:27-29).
- * keys_out/counts_out: capacity entries each (device); *n_out (host) receives
- * the number of non-empty cells written.  Cell order is unspecified.
+ * Cells inside [0, 2^z)^2 go to keys_out/counts_out (HM_KEY layout, capacity
+ * entries each, device); *n_out (host) receives how many there are.  The
+ * reference also bins kept points outside that square (tile.py:17,21 do not
+ * clamp: |lat| > 85.0511... gives negative rows, lon >= 180 columns >= 2^z);
+ * their cells go to xcells_out as 4 int64 per cell (zoom, row, col, count),
+ * xcapacity cells (device, may be NULL with xcapacity 0); *nx_out receives
+ * how many.  Either count above its capacity -> HM_E_CAPACITY with both
+ * sizes set.  Cell order is unspecified.
  * Replaces dataframe_loader + build_heatmaps' reduceByKey (heatmap.py:25-111). */
 int hm_count(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
              int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
-             int64_t* n_out);
+             int64_t* n_out, int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out);
 
 /* Same pyramid from zoom-zmax tile coordinates (int64 row/col). */
 int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep,
                    int64_t n, int zmin, int zmax, uint64_t* keys_out, uint64_t* counts_out,
-                   int64_t capacity, int64_t* n_out);
+                   int64_t capacity, int64_t* n_out, int64_t* xcells_out, int64_t xcapacity,
+                   int64_t* nx_out);
+
+/* Counts per (group, zoom, row, col), zooms [zmin, zmax], of the kept points
+ * (keep as hm_count; group: uint32[n], device, or NULL = one group 0), in one
+ * pass over the points.  cells_out: 5 int64 per cell (group, zoom, row, col,
+ * count), capacity cells (device); *n_out = cells.  Rows/columns outside
+ * [0, 2^z) are counted like the others.  Replaces the per-user keys of
+ * tile_id_timespans_mapper (heatmap.py:64-75) + reduceByKey (:111). */
+int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
+                     const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
+                     int64_t capacity, int64_t* n_out);
 
 /* First failing point of the last call: index in input order (-1 if none)
  * and its HM_E_* kind. */

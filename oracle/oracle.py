@@ -114,17 +114,22 @@ def count(lat, lon, keep=None, zmin=0, zmax=18, threads=0):
 def count_tiles(rows, cols, zmin, zmax):
     """Per-zoom cell counts of zoom-zmax tiles (the hm_count_tiles contract),
     sorted by (zoom, row, col): the per-zoom reduceByKey of heatmap.py:109-111,
-    with every coarser tile the right shift of the zoom-zmax one (SURVEY a-4)."""
+    with every coarser tile the arithmetic right shift of the zoom-zmax one
+    (SURVEY a-4; any int64 tile, negative or past 2^zmax)."""
     rows = np.asarray(rows, dtype=np.int64)
     cols = np.asarray(cols, dtype=np.int64)
     out = {k: [] for k in ("zoom", "row", "col", "count")}
     for z in range(zmin, zmax + 1):
-        key = ((rows >> (zmax - z)) << 32) | (cols >> (zmax - z))
-        u, n = np.unique(key, return_counts=True)
-        out["zoom"].append(np.full(u.size, z, np.int32))
-        out["row"].append(u >> 32)
-        out["col"].append(u & 0xFFFFFFFF)
+        if rows.size == 0:
+            break
+        u, n = np.unique(np.stack([rows >> (zmax - z), cols >> (zmax - z)], 1), axis=0, return_counts=True)
+        out["zoom"].append(np.full(len(u), z, np.int32))
+        out["row"].append(u[:, 0])
+        out["col"].append(u[:, 1])
         out["count"].append(n.astype(np.int64))
+    if not out["zoom"]:
+        return {"zoom": np.zeros(0, np.int32), "row": np.zeros(0, np.int64), "col": np.zeros(0, np.int64),
+                "count": np.zeros(0, np.int64)}
     return {k: np.concatenate(v) for k, v in out.items()}
 
 

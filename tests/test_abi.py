@@ -21,7 +21,7 @@ def declared():
 
 def test_header_declares_the_boundary():
     names = declared()
-    for n in ("hm_project", "hm_count", "hm_count_tiles", "hm_last_error", "hm_ctx_create"):
+    for n in ("hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_last_error", "hm_ctx_create"):
         assert n in names
 
 
@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if n not in exported]
     assert not missing, missing
     assert set(_lib.EXPORTS) == set(declared())
-    assert L.hm_abi_version() == 1
+    assert L.hm_abi_version() == _lib.HM_ABI_VERSION == 2
     assert _lib.status_string(_lib.HM_E_DOMAIN) == "math domain error"
     assert _lib.status_string(_lib.HM_E_NAN) == "cannot convert float NaN to integer"
 

@@ -1,0 +1,88 @@
+"""GPU: the general count path (hm_general.hip) against the oracle.
+
+Kept points outside [0, 2^z)^2 -- polar latitudes (negative rows, rows past
+2^z), longitudes at or beyond +-180 (columns >= 2^z or < 0) -- are binned by the
+reference like any other (tile.py:17,21 never clamp; heatmap.py:27-36 keeps
+them).  Grouped counts (hm_count_grouped) are the per-user keys of
+heatmap.py:64-75 in one pass."""
+import numpy as np
+import pytest
+
+from oracle import oracle
+from heatmap_amd import device, synth
+
+pytestmark = pytest.mark.gpu
+
+
+def _exotic_cloud(n, seed, frac=0.05):
+    rng = np.random.default_rng(seed)
+    lat, lon = synth.generate("hotspots", n, seed=seed)
+    lat, lon = lat.copy(), lon.copy()
+    m = rng.random(n) < frac
+    k = int(m.sum())
+    lat[m] = rng.choice([-1.0, 1.0], k) * rng.uniform(85.06, 89.9, k)
+    lon[m] = rng.choice([180.0, 200.0, -200.0, 540.0, -180.0, 179.99999999999997], k)
+    return lat, lon
+
+
+def _same(got, ref):
+    assert ref["status"] == 0
+    for k in ("zoom", "row", "col", "count"):
+        assert np.array_equal(getattr(got, k), ref[k]), k
+
+
+@pytest.mark.parametrize("zmax", [14, 18, 21])
+def test_exotic_vs_oracle(gpu, zmax):
+    lat, lon = _exotic_cloud(200_000, seed=zmax)
+    keep = (np.arange(lat.size) % 9 != 4).astype(np.uint8)
+    got = device.count(lat, lon, keep, 0, zmax).sorted()
+    _same(got, oracle.count(lat, lon, keep, 0, zmax))
+    assert (got.row < 0).any() and (got.col >= (1 << got.zoom)).any()
+
+
+def test_exotic_only_and_single(gpu):
+    for lat, lon in ((np.array([89.0]), np.array([200.0])),
+                     (np.array([-86.5, 86.5, 89.99999998]), np.array([-540.0, 1e6, 180.0]))):
+        for zmin, zmax in ((0, 21), (6, 14), (0, 0)):
+            _same(device.count(lat, lon, None, zmin, zmax).sorted(), oracle.count(lat, lon, None, zmin, zmax))
+
+
+def test_exotic_tiles(gpu):
+    """hm_count_tiles with tiles outside the square (negative, >= 2^z, huge)."""
+    rng = np.random.default_rng(5)
+    n = 100_000
+    z = 16
+    rows = rng.integers(-(8 << z), 8 << z, n)
+    cols = rng.integers(-(1 << 40), 1 << 40, n)
+    cols[::3] = rng.integers(0, 1 << z, (n + 2) // 3)
+    got = device.count(rows, cols, None, 0, z, tiles=True).sorted()
+    ref = oracle.count_tiles(rows, cols, 0, z)
+    o = np.lexsort((ref["col"], ref["row"], ref["zoom"]))
+    for k in ("zoom", "row", "col", "count"):
+        assert np.array_equal(getattr(got, k), ref[k][o]), k
+
+
+@pytest.mark.parametrize("zmin,zmax,groups", [(0, 14, 7), (6, 21, 1000), (3, 18, 1)])
+def test_grouped_vs_oracle(gpu, zmin, zmax, groups):
+    lat, lon = _exotic_cloud(120_000, seed=groups, frac=0.02)
+    rng = np.random.default_rng(groups)
+    g = rng.integers(0, groups, lat.size).astype(np.uint32) * 7919   # sparse ids
+    keep = (rng.random(lat.size) < 0.8).astype(np.uint8)
+    got = device.count_grouped(lat, lon, g, keep, zmin, zmax).sorted()
+    exp = {k: [] for k in ("group", "zoom", "row", "col", "count")}
+    for gid in np.unique(g[keep.astype(bool)]):
+        ref = oracle.count(lat, lon, keep & (g == gid), zmin, zmax)
+        assert ref["status"] == 0
+        exp["group"].append(np.full(ref["zoom"].size, gid, np.uint32))
+        for k in ("zoom", "row", "col", "count"):
+            exp[k].append(ref[k])
+    for k in exp:
+        assert np.array_equal(getattr(got, k), np.concatenate(exp[k])), k
+
+
+def test_grouped_errors(gpu):
+    lat, lon = synth.uniform(10000, seed=2)
+    lat = lat.copy()
+    lat[777] = np.inf
+    with pytest.raises(ValueError, match="domain"):
+        device.count_grouped(lat, lon, np.zeros(lat.size, np.uint32), None, 0, 10)

@@ -71,18 +71,20 @@ def test_count_guard_band_points(gpu):
         assert np.array_equal(got.col, ref["col"]) and np.array_equal(got.zoom, ref["zoom"])
 
 
-def test_count_redo_overflow_fallback(gpu):
-    """More deferred points than the redo list holds -> fused exact fallback."""
+@pytest.mark.parametrize("keep_polar", [False, True])
+def test_count_redo_overflow_fallback(gpu, keep_polar):
+    """More deferred points than the redo list holds -> fused exact fallback;
+    kept, they also overflow the exotic list (rebuilt by k_collect_exotic)."""
     n = 3_000_000
     lat, lon = synth.uniform(n, seed=9)
     polar = (np.arange(n) % 5) < 2
     lat = np.where(polar, 86.0 + (lat % 3.0), lat)       # 40% beyond the fast window
-    keep = (~polar).astype(np.uint8)                      # polar rows would be exotic: drop them
+    keep = np.ones(n, np.uint8) if keep_polar else (~polar).astype(np.uint8)
     got = device.count(lat, lon, keep, 0, 16).sorted()
     ref = oracle.count(lat, lon, keep, 0, 16)
     assert got.slow_points > (1 << 20)
     assert np.array_equal(got.count, ref["count"]) and np.array_equal(got.row, ref["row"])
-    assert np.array_equal(got.col, ref["col"])
+    assert np.array_equal(got.col, ref["col"]) and np.array_equal(got.zoom, ref["zoom"])
 
 
 def test_count_errors_and_exotic(gpu):
@@ -95,12 +97,10 @@ def test_count_errors_and_exotic(gpu):
     lat[31337] = 10.0
     with pytest.raises(ValueError, match="domain"):
         device.count(lat, lon, None, 0, 14)
-    lat[40000] = 89.0          # valid, but outside the tile domain -> exotic
-    from heatmap_amd._lib import DevicePathUnsupported
-    with pytest.raises(DevicePathUnsupported):
-        device.count(lat, lon, None, 0, 14)
-    keep = np.ones(50000, np.uint8)
-    keep[40000] = 0            # background rows are projected, not binned
-    got = device.count(lat, lon, keep, 0, 14).sorted()
-    ref = oracle.count(lat, lon, keep, 0, 14)
-    assert np.array_equal(got.count, ref["count"])
+    lat[40000] = 89.0          # valid: the reference bins it at a negative row
+    for keep in (None, (np.arange(50000) != 40000).astype(np.uint8)):
+        got = device.count(lat, lon, keep, 0, 14).sorted()
+        ref = oracle.count(lat, lon, keep, 0, 14)
+        assert np.array_equal(got.count, ref["count"]) and np.array_equal(got.row, ref["row"])
+        assert np.array_equal(got.col, ref["col"]) and np.array_equal(got.zoom, ref["zoom"])
+    assert (device.count(lat, lon, None, 0, 14).row < 0).sum() == 15   # one negative row per zoom 0..14

@@ -19,6 +19,9 @@ VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
 
 VARIANTS = {
     "base": [],
+    "noskew": ["HM_SKEW_CUR=0"],
+    "p1_1024x16": ["HM_P1_THREADS=1024", "HM_P1_PPT=16"],
+    "p1_512x16": ["HM_P1_PPT=16"],
     "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py
     # timing-only experiments (results wrong, every access stays in bounds)
     "noload": ["HM_EXP_NOLOAD=1"],
