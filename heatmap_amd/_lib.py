@@ -27,7 +27,7 @@ HM_COUNT_MAX_ZOOM = 21
 HM_ABI_VERSION = 2
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
-           "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_last_error", "hm_last_stats", "hm_synth",
+           "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_extract", "hm_stream_destroy"]
 
 _LIB = None
@@ -78,6 +78,7 @@ def load() -> ctypes.CDLL:
                                      vp, c.c_int64, P(c.c_int64)]
         L.hm_count_grouped.argtypes = [vp, vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, c.c_int64,
                                        P(c.c_int64)]
+        L.hm_count_grouped_tiles.argtypes = L.hm_count_grouped.argtypes
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
         L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]

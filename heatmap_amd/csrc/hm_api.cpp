@@ -60,6 +60,7 @@ enum {
     ST_NSLOTS = 4,
     ST_REDO = 5,
     ST_REDO_OUT = 6,
+    ST_XCURSOR = 7,
     ST_COUNT = 8
 };
 
@@ -251,7 +252,9 @@ static int take_error(hm_ctx* ctx)
 extern "C" int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
                           int64_t* col, uint8_t* status)
 {
-    if (!ctx || n < 0 || zoom < 0 || zoom > 30 || (n > 0 && (!lat || !lon || !row || !col || !status)))
+    /* zoom may be negative: Tile.parent_id of a zoom-0 tile projects at zoom
+     * -1, i.e. times 2**-1 = 0.5 (tile.py:60-61) */
+    if (!ctx || n < 0 || zoom < -30 || zoom > 30 || (n > 0 && (!lat || !lon || !row || !col || !status)))
         return HM_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     int st = reset_state(ctx);
@@ -271,7 +274,7 @@ extern "C" int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int
 /* capacity).  Errors (tiles beyond the key's range) go to the error word.      */
 /* ------------------------------------------------------------------------ */
 static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint32_t* group, const int64_t* index,
-                     uint64_t n, int Z, int zmin, int64_t* cells, int width, int64_t capacity, uint64_t* total)
+                     uint64_t n, int Z, int zmin, const HmGenEmit& e, uint64_t* total)
 {
     *total = 0;
     if (n == 0) return HM_OK;
@@ -330,10 +333,6 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     ENSURE(B_GEN_END, n * 8, end);
     ENSURE(B_GEN_CNT0, n * 8, cnt0);
     ENSURE(B_GEN_CNT1, n * 8, cnt1);
-    HmGenEmit e;
-    e.cells = cells;
-    e.capacity = (uint64_t)capacity;
-    e.width = width;
     const uint64_t* cin = nullptr;
     uint64_t m = n, emitted = 0;
     for (int z = Z; z >= zmin; z--) {
@@ -356,6 +355,53 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     }
     *total = emitted;
     return HM_OK;
+}
+
+#define HM_FALLBACK (-1)   /* count_impl: the pipeline's dense child space is too large */
+
+/* hm_count for data too sparse for the pipeline's dense per-level child
+ * arrays (e.g. uniform clouds at zoom 21): every kept point through the
+ * general path, cells inside the square emitted as HM_KEYs */
+static int count_fallback(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows,
+                          const int64_t* cols, const uint8_t* keep, int64_t n, int zmin, int zmax, uint64_t* keys_out,
+                          uint64_t* counts_out, int64_t capacity, int64_t* n_out, int64_t* xcells_out,
+                          int64_t xcapacity, int64_t* nx_out)
+{
+    int st = reset_state(ctx);
+    if (st) return st;
+    int64_t *row, *col, *idx;
+    ENSURE(B_X_ROW, (uint64_t)n * 8 + 8, row);
+    ENSURE(B_X_COL, (uint64_t)n * 8 + 8, col);
+    ENSURE(B_X_IDX, (uint64_t)n * 8 + 8, idx);
+    uint32_t* grp;
+    ENSURE(B_GL_GRP, (uint64_t)n * 4 + 4, grp);
+    if (rows)
+        hm_launch_tiles_list(ctx->stream, rows, cols, keep, nullptr, n, row, col, grp, idx, ctx->state + ST_XCOUNT);
+    else
+        hm_launch_project_list(ctx->stream, lat, lon, keep, nullptr, n, zmax, row, col, grp, idx,
+                               ctx->state + ST_XCOUNT, ctx->state + ST_ERR);
+    HIPCHK(hipGetLastError());
+    if ((st = read_state(ctx))) return st;
+    if ((st = take_error(ctx))) return st;
+    HmGenEmit e;
+    memset(&e, 0, sizeof(e));
+    e.cells = xcells_out;
+    e.capacity = (uint64_t)xcapacity;
+    e.width = 4;
+    e.split = 1;
+    e.keys = keys_out;
+    e.counts = counts_out;
+    e.kcapacity = (uint64_t)capacity;
+    e.kcursor = ctx->state + ST_CURSOR;
+    e.xcursor = ctx->state + ST_XCURSOR;
+    uint64_t total = 0;
+    if ((st = gen_count(ctx, row, col, nullptr, idx, ctx->host_state[ST_XCOUNT], zmax, zmin, e, &total))) return st;
+    if ((st = read_state(ctx))) return st;
+    *n_out = (int64_t)ctx->host_state[ST_CURSOR];
+    *nx_out = (int64_t)ctx->host_state[ST_XCURSOR];
+    ctx->last_slow = 0;
+    for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
+    return (*n_out > capacity || *nx_out > xcapacity) ? HM_E_CAPACITY : HM_OK;
 }
 
 static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows, const int64_t* cols,
@@ -443,7 +489,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         V.out16 = (l == L - 1);
         const int restbits = 2 * (Z - zs[l]);
         const uint64_t ntiles = (l == 0) ? tiles1 : lv[l - 1].items;
-        if (V.nchildren > (uint64_t)HM_SCAN_LIMIT) return HM_E_NOMEM;
+        if (V.nchildren > (uint64_t)HM_SCAN_LIMIT) return HM_FALLBACK;
         /* run-counter shards: 32 unless the dense child space is large (then
          * per-child contention is low anyway); keeps counters <= 2^25 */
         int sb = 5;
@@ -775,8 +821,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     /* cells outside the square: the general path over the exotic list */
     uint64_t xt = 0;
     if (nx) {
-        if ((st = gen_count(ctx, xl.row, xl.col, nullptr, xl.idx, nx, Z, zmin, xcells_out, 4, xcapacity, &xt)))
-            return st;
+        HmGenEmit e;
+        memset(&e, 0, sizeof(e));
+        e.cells = xcells_out;
+        e.capacity = (uint64_t)xcapacity;
+        e.width = 4;
+        if ((st = gen_count(ctx, xl.row, xl.col, nullptr, xl.idx, nx, Z, zmin, e, &xt))) return st;
         if ((st = read_state(ctx))) return st;
     }
     *nx_out = (int64_t)xt;
@@ -789,8 +839,12 @@ extern "C" int hm_count(hm_ctx* ctx, const double* lat, const double* lon, const
                         int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
     if (n > 0 && (!lat || !lon)) return HM_E_ARG;
-    return count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
-                      xcells_out, xcapacity, nx_out);
+    int st = count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
+                        xcells_out, xcapacity, nx_out);
+    if (st == HM_FALLBACK)
+        st = count_fallback(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity,
+                            n_out, xcells_out, xcapacity, nx_out);
+    return st;
 }
 
 extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep, int64_t n,
@@ -798,16 +852,20 @@ extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* co
                               int64_t* n_out, int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
     if (n > 0 && (!row || !col)) return HM_E_ARG;
-    return count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
-                      xcells_out, xcapacity, nx_out);
+    int st = count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
+                        xcells_out, xcapacity, nx_out);
+    if (st == HM_FALLBACK)
+        st = count_fallback(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity,
+                            n_out, xcells_out, xcapacity, nx_out);
+    return st;
 }
 
-extern "C" int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
-                                const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
-                                int64_t capacity, int64_t* n_out)
+static int grouped_impl(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows, const int64_t* cols,
+                        const uint8_t* keep, const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
+                        int64_t capacity, int64_t* n_out)
 {
     if (!ctx || !n_out || n < 0 || n >= (int64_t)0xFFFFFFF0ll || zmin < 0 || zmax < zmin ||
-        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && !cells_out) || (n > 0 && (!lat || !lon)))
+        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && !cells_out))
         return HM_E_ARG;
     *n_out = 0;
     HIPCHK(hipSetDevice(ctx->device));
@@ -820,17 +878,41 @@ extern "C" int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lo
     ENSURE(B_X_COL, (uint64_t)n * 8, col);
     ENSURE(B_X_IDX, (uint64_t)n * 8, idx);
     ENSURE(B_GL_GRP, (uint64_t)n * 4, grp);
-    hm_launch_project_list(ctx->stream, lat, lon, keep, group, n, zmax, row, col, grp, idx, ctx->state + ST_XCOUNT,
-                           ctx->state + ST_ERR);
+    if (rows)
+        hm_launch_tiles_list(ctx->stream, rows, cols, keep, group, n, row, col, grp, idx, ctx->state + ST_XCOUNT);
+    else
+        hm_launch_project_list(ctx->stream, lat, lon, keep, group, n, zmax, row, col, grp, idx,
+                               ctx->state + ST_XCOUNT, ctx->state + ST_ERR);
     HIPCHK(hipGetLastError());
     if ((st = read_state(ctx))) return st;
     if ((st = take_error(ctx))) return st;
     const uint64_t m = ctx->host_state[ST_XCOUNT];
     uint64_t total = 0;
-    if ((st = gen_count(ctx, row, col, grp, idx, m, zmax, zmin, cells_out, 5, capacity, &total))) return st;
+    HmGenEmit e;
+    memset(&e, 0, sizeof(e));
+    e.cells = cells_out;
+    e.capacity = (uint64_t)capacity;
+    e.width = 5;
+    if ((st = gen_count(ctx, row, col, grp, idx, m, zmax, zmin, e, &total))) return st;
     if ((st = read_state(ctx))) return st;
     *n_out = (int64_t)total;
     return total > (uint64_t)capacity ? HM_E_CAPACITY : HM_OK;
+}
+
+extern "C" int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
+                                const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
+                                int64_t capacity, int64_t* n_out)
+{
+    if (n > 0 && (!lat || !lon)) return HM_E_ARG;
+    return grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+}
+
+extern "C" int hm_count_grouped_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep,
+                                      const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
+                                      int64_t capacity, int64_t* n_out)
+{
+    if (n > 0 && (!row || !col)) return HM_E_ARG;
+    return grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
 }
 
 extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,

@@ -224,26 +224,83 @@ __global__ __launch_bounds__(256) void k_rle_emit(HmGenEmit e, const ulonglong2*
 {
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     const hm_u128 mm = ((hm_u128)1 << (2 * z)) - 1;
-    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < u; j += stride) {
-        const uint64_t cnt = oend[j] - (j ? oend[j - 1] : 0ull);
-        ocnt[j] = cnt;
-        const uint64_t q = base + j;
-        if (!emit || q >= e.capacity) continue;
-        const hm_u128 k = hm_ld128(okey, j);
-        const hm_u128 root = k >> (2 * z);
-        const uint64_t m = (uint64_t)(k & mm);
-        const int64_t sr = (int64_t)(uint64_t)((root >> 48) & 31) - HM_GEN_SR_BIAS;
-        const int64_t sc = (int64_t)(uint64_t)(root & ((((hm_u128)1) << HM_GEN_SC_BITS) - 1)) - HM_GEN_SC_BIAS;
-        /* sr * 2^z, sc * 2^z as unsigned shifts (two's complement) */
-        const int64_t row = (int64_t)(((uint64_t)sr << z) + hm_compact21(m >> 1));
-        const int64_t col = (int64_t)(((uint64_t)sc << z) + hm_compact21(m));
-        int64_t* rec = e.cells + q * e.width;
+    const uint64_t u_up = (u + 63) & ~63ull;   /* split mode appends per wave */
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < u_up; j += stride) {
+        const bool in = j < u;
+        uint64_t cnt = 0;
+        int64_t row = 0, col = 0;
+        hm_u128 root = 0;
+        if (in) {
+            cnt = oend[j] - (j ? oend[j - 1] : 0ull);
+            ocnt[j] = cnt;
+            const hm_u128 k = hm_ld128(okey, j);
+            root = k >> (2 * z);
+            const uint64_t m = (uint64_t)(k & mm);
+            const int64_t sr = (int64_t)(uint64_t)((root >> 48) & 31) - HM_GEN_SR_BIAS;
+            const int64_t sc = (int64_t)(uint64_t)(root & ((((hm_u128)1) << HM_GEN_SC_BITS) - 1)) - HM_GEN_SC_BIAS;
+            /* sr * 2^z, sc * 2^z as unsigned shifts (two's complement) */
+            row = (int64_t)(((uint64_t)sr << z) + hm_compact21(m >> 1));
+            col = (int64_t)(((uint64_t)sc << z) + hm_compact21(m));
+        }
+        if (!emit) continue;
+        uint64_t q = base + j;
+        bool rec = in;
+        if (e.split) {
+            /* hm_count fallback: cells inside [0, 2^z)^2 as (HM_KEY, count),
+             * the others as records; one append per wave and kind */
+            const bool sq = in && (uint64_t)row < (1ull << z) && (uint64_t)col < (1ull << z);
+            rec = in && !sq;
+            const uint64_t ms = __ballot(sq), mx = __ballot(rec);
+            const int ls = ms ? __ffsll((unsigned long long)ms) - 1 : 0;
+            const int lx = mx ? __ffsll((unsigned long long)mx) - 1 : 0;
+            unsigned long long bs = 0, bx = 0;
+            if (ms && hm_lane() == ls) bs = atomicAdd(e.kcursor, (unsigned long long)__popcll(ms));
+            if (mx && hm_lane() == lx) bx = atomicAdd(e.xcursor, (unsigned long long)__popcll(mx));
+            bs = __shfl(bs, ls, 64);
+            bx = __shfl(bx, lx, 64);
+            if (sq) {
+                const uint64_t p = bs + hm_mbcnt(ms);
+                if (p < e.kcapacity) {
+                    e.keys[p] = ((uint64_t)z << 58) | ((uint64_t)row << 29) | (uint64_t)col;
+                    e.counts[p] = cnt;
+                }
+            }
+            q = bx + hm_mbcnt(mx);
+        }
+        if (!rec || q >= e.capacity) continue;
+        int64_t* r = e.cells + q * e.width;
         int f = 0;
-        if (e.width == 5) rec[f++] = (int64_t)(uint64_t)(root >> 53);
-        rec[f++] = z;
-        rec[f++] = row;
-        rec[f++] = col;
-        rec[f] = (int64_t)cnt;
+        if (e.width == 5) r[f++] = (int64_t)(uint64_t)(root >> 53);
+        r[f++] = z;
+        r[f++] = row;
+        r[f++] = col;
+        r[f] = (int64_t)cnt;
+    }
+}
+
+/* grouped counts from tiles (hm_count_grouped_tiles): list the kept ones */
+__global__ __launch_bounds__(256) void k_tiles_list(const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
+                                                    const uint8_t* __restrict__ keep, const uint32_t* __restrict__ group,
+                                                    int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
+                                                    unsigned long long* count)
+{
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    const int64_t n_up = (n + 63) & ~63ll;   /* whole waves stay in the loop */
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
+        const bool p = i < n && (!keep || keep[i]);
+        const uint64_t m = __ballot(p);
+        if (!m) continue;
+        const int lead = __ffsll((unsigned long long)m) - 1;
+        unsigned long long b = 0;
+        if (hm_lane() == lead) b = atomicAdd(count, (unsigned long long)__popcll(m));
+        b = __shfl(b, lead, 64);
+        if (p) {
+            const uint64_t q = b + hm_mbcnt(m);
+            row[q] = rows[i];
+            col[q] = cols[i];
+            grp[q] = group ? group[i] : 0u;
+            idx[q] = i;
+        }
     }
 }
 
@@ -293,4 +350,12 @@ void hm_launch_rle_emit(hipStream_t s, const HmGenEmit& e, const ulonglong2* oke
 {
     hipLaunchKernelGGL(k_rle_emit, dim3(hm_ggrid(u, 256, 16384)), dim3(256), 0, s, e, okey, oend, u, z, ocnt, base,
                        emit);
+}
+
+void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
+                          const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
+                          unsigned long long* count)
+{
+    hipLaunchKernelGGL(k_tiles_list, dim3(hm_ggrid((uint64_t)n, 256, 8192)), dim3(256), 0, s, rows, cols, keep, group,
+                       n, row, col, grp, idx, count);
 }

@@ -316,13 +316,24 @@ struct HmGenArgs {
     unsigned long long* orand;  /* [or_lo, or_hi, and_lo, and_hi] */
     unsigned long long* err_word;
 };
-/* records of `width` int64: [group,] zoom, row, col, count */
+/* records of `width` int64: [group,] zoom, row, col, count; with keys set
+ * (hm_count's fallback) cells inside [0, 2^z)^2 go to keys/counts instead,
+ * both kinds appended at the cursors */
 struct HmGenEmit {
     int64_t* cells;
     uint64_t capacity;
     int width;
+    int split;
+    uint64_t* keys;
+    uint64_t* counts;
+    uint64_t kcapacity;
+    unsigned long long* kcursor;
+    unsigned long long* xcursor;
 };
 void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a);
+void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
+                          const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
+                          unsigned long long* count);
 uint64_t hm_rx_tiles(uint64_t n);
 void hm_launch_rx_pass(hipStream_t s, const ulonglong2* in, ulonglong2* out, uint64_t n, int sh, uint64_t* hist,
                        uint64_t* off, uint64_t* partial, uint64_t* total);

@@ -240,13 +240,16 @@ class GroupedCounts:
         return GroupedCounts(self.group[o], self.zoom[o], self.row[o], self.col[o], self.count[o])
 
 
-def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0) -> GroupedCounts:
-    """Per-(group, zoom, row, col) counts in one device pass (hm_count_grouped).
+def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,
+                  tiles: bool = False) -> GroupedCounts:
+    """Per-(group, zoom, row, col) counts in one device pass (hm_count_grouped;
+    tiles=True: lat/lon are int64 zoom-zmax rows/cols, hm_count_grouped_tiles).
     group: uint32 per point; keep: points to count (all are projected)."""
     torch = _torch()
     ctx = context(device)
-    a = _dev(lat, torch.float64, device)
-    b = _dev(lon, torch.float64, device)
+    dt = torch.int64 if tiles else torch.float64
+    a = _dev(lat, dt, device)
+    b = _dev(lon, dt, device)
     n = a.numel()
     g = _dev(np.asarray(group, dtype=np.uint32).view(np.int32) if not isinstance(group, torch.Tensor) else group,
              torch.int32, device)
@@ -261,8 +264,9 @@ def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, dev
     while True:
         cells = torch.empty(5 * cap, dtype=torch.int64, device=a.device)
         nout = ctypes.c_int64(0)
-        rc = ctx.L.hm_count_grouped(ctx.ptr, _ptr(a), _ptr(b), _ptr(kp), _ptr(g), n, int(zmin), int(zmax),
-                                    _ptr(cells), cap, ctypes.byref(nout))
+        fn = ctx.L.hm_count_grouped_tiles if tiles else ctx.L.hm_count_grouped
+        rc = fn(ctx.ptr, _ptr(a), _ptr(b), _ptr(kp), _ptr(g), n, int(zmin), int(zmax), _ptr(cells), cap,
+                ctypes.byref(nout))
         if rc == _lib.HM_E_CAPACITY:
             cap = int(nout.value * 1.25) + 64
             continue

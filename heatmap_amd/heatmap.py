@@ -9,28 +9,40 @@ heatmap.py:16-129:
            with 'x', 'rt-*' folded into 'route'          (heatmap.py:64-70)
   zooms    detail zooms MAX_ZOOM_LEVEL+DELTA down to DELTA+1 (heatmap.py:109)
 
-Counting runs on the device (hm_count: projection + count pyramid, one launch
-per user group).  The reference re-emits every level's 'all' bins under user
-id 'all', which doubles 'all' once per level; with n = kept points, a = kept
-points whose user id is literally 'all', U = kept points of every other user
-group, the 'all' count of a cell k levels below the detail zoom is
+Counting runs on the device in two passes over the points, whatever the
+number of users:
+  hm_count          every kept point, per (zoom, row, col)  -> n
+  hm_count_grouped  kept points with a group, per (group, zoom, row, col)
+User ids are dictionary-encoded on the host (vectorised) into u32 group ids;
+group 0 is the literal user id 'all'.  The reference re-emits every level's
+'all' bins under user id 'all', which doubles 'all' once per level; with
+a = kept points whose user id is literally 'all' and U = kept points of every
+other group, the 'all' count of a cell k levels below the detail zoom is
     2^k (n + a) + (2^k - 1) U
-(closed form verified against the reference); the
-adapter below applies it to the device counts.  Counts are integers on the
-device and exact as floats while below 2^53.
+(closed form verified against the reference).
+Counts are integers on the device and exact as floats while below 2^53.
+
+Every coarser tile is the arithmetic shift of the detail-zoom tile.  The
+reference re-projects tile centres instead (heatmap.py:60-61,89); the two
+agree on the windows heatmap_amd/chain_window.py lists (generated and checked
+tile by tile by tools/chain_window.c; they contain [0, 2^z)^2 at every zoom).
+Points whose tiles leave those windows (within ~1e-6 deg of a pole, or
+|lon| > 11520) raise DevicePathUnsupported instead of returning rows that
+could differ from the reference's.
 
 build_heatmaps(locations) keeps the reference's RDD-shaped interface for
 locations produced by dataframe_loader (all with count 1.0 and tileId at the
-detail zoom); build_heatmaps_columnar is the fast entry point.
+detail zoom); build_heatmaps_columnar returns the same {row_id: heatmap} dict
+from columns, and heatmap_table the (id, heatmap-JSON) rows as a pyarrow
+Table built without per-cell Python objects.
 """
 from __future__ import annotations
 
 import json
-from collections import defaultdict
 
 import numpy as np
 
-from . import device
+from . import _lib, chain_window, device
 from .tile import Tile
 
 DETAIL_ZOOM_DELTA = 5
@@ -53,7 +65,8 @@ def dataframe_loader(row):
 
 
 def build_timespan_label(timespanType, localDate):
-    """heatmap.py:38-52 (not used by the pipeline: timespan is 'alltime')."""
+    """heatmap.py:38-52 (the batch pipeline's only label is 'alltime',
+    heatmap.py:62-63; the streaming heatmap serves the others)."""
     month = "%02d" % localDate.month
     day = "%02d" % localDate.day
     if timespanType == "alltime":
@@ -101,81 +114,248 @@ def heatmap_to_locations(bucket):
 
 
 # --------------------------------------------------------------------------
-# columnar fast path
+# group coding (host, vectorised over distinct user ids)
 # --------------------------------------------------------------------------
 
-def _group_plan(user_ids, keep):
-    """Per-point group masks: dict label -> uint8 keep mask, plus n/a/U masks."""
-    n = len(user_ids)
+class GroupPlan:
+    """labels[g] is the row-key group of group id g (labels[0] = 'all', the
+    literal user id, merged into the 'all' rows); gid: u32 group of every
+    point; grouped: points counted per group (kept, user id not 'x*')."""
+
+    def __init__(self, labels, gid, grouped):
+        self.labels = labels
+        self.gid = gid
+        self.grouped = grouped
+
+
+def _factorize(user_id):
+    try:
+        import pandas as pd
+
+        codes, uniques = pd.factorize(np.asarray(user_id, dtype=object), use_na_sentinel=True)
+        return codes.astype(np.int64), list(uniques)
+    except ImportError:  # pragma: no cover - pandas is part of the image
+        uniq, inv = np.unique(np.array([str(u) if u is not None else "\0none" for u in user_id]), return_inverse=True)
+        u = [None if x == "\0none" else x for x in uniq.tolist()]
+        codes = inv.astype(np.int64)
+        if None in u:
+            codes[codes == u.index(None)] = -1
+        return codes, u
+
+
+def group_plan(user_id, keep=None) -> GroupPlan:
+    """Dictionary-encode the user ids of the kept points into groups
+    (heatmap.py:64-70).  Background rows are dropped before their user id is
+    read (heatmap.py:28-35), so only kept rows raise: a None id as the
+    reference's None[:1] would (TypeError), an id containing the key separator
+    as ValueError (heatmap.py:80-84 would mis-split its keys)."""
+    n = len(user_id)
     keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool)
-    labels = np.empty(n, dtype=object)
-    for i, u in enumerate(user_ids):
-        if u is None:
-            raise TypeError("'NoneType' object is not subscriptable")   # None[:1], heatmap.py:64
+    codes, uniques = _factorize(user_id)
+    kept_codes = np.unique(codes[keep])
+    if kept_codes.size and kept_codes[0] < 0:
+        raise TypeError("'NoneType' object is not subscriptable")
+    labels = ["all"]
+    index = {"all": 0}
+    lut = np.full(len(uniques) + 1, -1, dtype=np.int64)      # code -> group id; -1: no group
+    for c in kept_codes.tolist():
+        u = uniques[c]
+        if not isinstance(u, str):
+            raise TypeError("user id %r is not a string" % (u,))
         if KEY_SEPERATOR in u:
             raise ValueError("user id %r contains the key separator %r (heatmap.py:80-84 would mis-split it)"
                              % (u, KEY_SEPERATOR))
-        labels[i] = None if u[:1] == "x" else ("route" if u[:3] == "rt-" else u)
-    masks = {}
-    for g in sorted({l for l in labels if l is not None}):
-        masks[g] = keep & (labels == g)
-    lit_all = masks.pop("all", np.zeros(n, dtype=bool))
-    others = np.zeros(n, dtype=bool)
-    for m in masks.values():
-        others |= m
-    return keep, lit_all, others, masks
+        if u[:1] == "x":
+            continue
+        label = "route" if u[:3] == "rt-" else u
+        if label not in index:
+            index[label] = len(labels)
+            labels.append(label)
+        lut[c] = index[label]
+    g = lut[codes]
+    grouped = keep & (g >= 0)
+    return GroupPlan(labels, np.where(grouped, g, 0).astype(np.uint32), grouped)
 
 
-def _device_counter(lat, lon, zmin, zmax, tiles):
-    """counter(mask) -> {zoom: {(row, col): count}} on the device (hm_count)."""
+# --------------------------------------------------------------------------
+# cells: the heatmap bins as arrays
+# --------------------------------------------------------------------------
 
-    def counter(mask):
-        c = device.count(lat, lon, None if mask is None else mask.astype(np.uint8), zmin, zmax, tiles=tiles)
-        out = defaultdict(dict)
-        for z, r, cc, k in zip(c.zoom.tolist(), c.row.tolist(), c.col.tolist(), c.count.tolist()):
-            out[z][(r, cc)] = k
-        return out
+class Cells:
+    """Every bin of every output row: labels[label[i]] | alltime | zoom[i]-delta
+    tile of (row[i], col[i]) -> {zoom[i]_row[i]_col[i]: value[i]}."""
 
-    return counter
+    def __init__(self, labels, label, zoom, row, col, value, delta):
+        self.labels, self.label, self.zoom, self.row, self.col, self.value = labels, label, zoom, row, col, value
+        self.delta = delta
+
+    def __len__(self):
+        return int(self.zoom.size)
 
 
-def assemble_rows(counter, user_id, keep=None, max_zoom_level=None, delta=None):
-    """Heatmap rows of build_heatmaps from per-group cell counts.
+def _sum_by_cell(parts):
+    """parts: [(zoom, row, col, values[k x m])] -> unique (zoom, row, col) and
+    the summed value columns."""
+    z = np.concatenate([p[0] for p in parts]).astype(np.int64)
+    r = np.concatenate([p[1] for p in parts]).astype(np.int64)
+    c = np.concatenate([p[2] for p in parts]).astype(np.int64)
+    v = np.concatenate([p[3] for p in parts], axis=0)
+    if z.size == 0:
+        return z, r, c, v
+    o = np.lexsort((c, r, z))
+    z, r, c, v = z[o], r[o], c[o], v[o]
+    head = np.ones(z.size, dtype=bool)
+    head[1:] = (z[1:] != z[:-1]) | (r[1:] != r[:-1]) | (c[1:] != c[:-1])
+    starts = np.flatnonzero(head)
+    return z[starts], r[starts], c[starts], np.add.reduceat(v, starts, axis=0)
 
-    counter(mask) returns {zoom: {(row, col): count}} of the points selected by
-    `mask` (None = all points) for zooms delta+1 .. max_zoom_level+delta; it is
-    the only place points are touched (the device in the product, the oracle
-    in the CPU tests).  Row layout: heatmap.py:55,85-90,120-126; 'all'
-    weighting: heatmap.py:64-70 applied level by level (module docstring)."""
+
+def _check_chain_window(zoom, row, col, zmax, d):
+    """Raise DevicePathUnsupported when a detail-zoom tile leaves the windows
+    on which the reference's centre re-projection equals the shift."""
+    m = zoom == zmax
+    if not m.any():
+        return
+    rlo, rhi, clo, chi = int(row[m].min()), int(row[m].max()), int(col[m].min()), int(col[m].max())
+
+    def inside(win, lo, hi):
+        return win[0] <= lo and hi < win[1]
+
+    for z in range(zmax, d, -1):
+        # row tile at z - d (heatmap.py:89); level z re-projected from z+1,
+        # the first level at its own zoom (heatmap.py:60-61)
+        checks = [(z, d), (z, 0) if z == zmax else (z + 1, 1)]
+        for zz, j in checks:
+            kk = zmax - zz
+            if not (inside(chain_window.ROWS[zz][j], rlo >> kk, rhi >> kk) and
+                    inside(chain_window.COLS[zz][j], clo >> kk, chi >> kk)):
+                raise _lib.DevicePathUnsupported(
+                    "tiles at zoom %d span rows [%d, %d], cols [%d, %d]: outside the window where the "
+                    "reference's tile-centre re-projection (heatmap.py:60-61,89) equals the shift"
+                    % (zz, rlo >> kk, rhi >> kk, clo >> kk, chi >> kk))
+
+
+def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None) -> Cells:
+    """The bins of build_heatmaps' rows from per-cell counts.
+
+    count_all(keep) -> (zoom, row, col, count) arrays of the kept points;
+    count_grouped(keep, gid) -> (group, zoom, row, col, count) per group id.
+    Both cover zooms delta+1 .. max_zoom_level+delta and are the only places
+    points are touched (the device in the product, the oracle in the CPU
+    tests).  Row layout: heatmap.py:55,85-90,120-126; 'all' weighting:
+    heatmap.py:64-70 applied level by level (module docstring)."""
     mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
     d = DETAIL_ZOOM_DELTA if delta is None else delta
     zmax = mz + d
-    keep, lit_all, others, groups = _group_plan(user_id, keep)
+    n = len(user_id)
+    keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool)
+    plan = group_plan(user_id, keep)
     # every point is projected (and may raise) even when not kept, as
-    # dataframe_loader does (heatmap.py:27-29): the counter checks all points
-    n_cells = counter(keep)
-    a_cells = counter(lit_all) if lit_all.any() else {}
-    u_cells = counter(others) if others.any() else {}
+    # dataframe_loader does (heatmap.py:27-29): count_all sees all points
+    nz, nr, nc, nn = count_all(keep)
+    nz, nr, nc = np.asarray(nz, np.int64), np.asarray(nr, np.int64), np.asarray(nc, np.int64)
+    _check_chain_window(nz, nr, nc, zmax, d)
+    if plan.grouped.any():
+        gg, gz, gr, gc, gn = count_grouped(plan.grouped, plan.gid)
+        gg = np.asarray(gg, np.int64)
+        gz, gr, gc, gn = (np.asarray(x, np.int64) for x in (gz, gr, gc, gn))
+    else:
+        gg = gz = gr = gc = gn = np.zeros(0, np.int64)
+    # 'all' rows: per cell n, a (literal 'all'), U (other groups)
+    nv = np.stack([np.asarray(nn, np.int64), np.zeros(nz.size, np.int64), np.zeros(nz.size, np.int64)], 1)
+    lit = gg == 0
+    gv = np.stack([np.zeros(gz.size, np.int64), np.where(lit, gn, 0), np.where(lit, 0, gn)], 1)
+    az, ar, ac, av = _sum_by_cell([(nz, nr, nc, nv), (gz, gr, gc, gv)])
+    sel = az > d
+    az, ar, ac, av = az[sel], ar[sel], ac[sel], av[sel]
+    k = zmax - az
+    w = np.left_shift(np.int64(1), k)
+    value_all = ((av[:, 0] + av[:, 1]) * w + (w - 1) * av[:, 2]).astype(np.float64)
+    # user-group rows (the literal 'all' group is not a row of its own)
+    us = (~lit) & (gz > d)
+    label = np.concatenate([np.zeros(az.size, np.int64), gg[us]])
+    return Cells(plan.labels, label, np.concatenate([az, gz[us]]), np.concatenate([ar, gr[us]]),
+                 np.concatenate([ac, gc[us]]), np.concatenate([value_all, gn[us].astype(np.float64)]), d)
+
+
+def cells_to_rows(cells: Cells) -> dict:
+    """{row_id: {bin_id: float}} (heatmap.py:85-90,120-126)."""
     rows = {}
-
-    def put(group, z, r, c, v):
-        # row tile = re-projected centre at z - d == arithmetic shift (SURVEY a-4)
-        rid = "%s|alltime|%d_%d_%d" % (group, z - d, r >> d, c >> d)
-        rows.setdefault(rid, {})["%d_%d_%d" % (z, r, c)] = float(v)
-
-    for z in range(zmax, d, -1):
-        k = zmax - z
-        nz = n_cells.get(z, {})
-        az = a_cells.get(z, {})
-        uz = u_cells.get(z, {})
-        for (r, c), cnt in nz.items():
-            put("all", z, r, c, (cnt + az.get((r, c), 0)) * (1 << k) + ((1 << k) - 1) * uz.get((r, c), 0))
-    for g, m in groups.items():
-        gc = counter(m)
-        for z in range(zmax, d, -1):
-            for (r, c), cnt in gc.get(z, {}).items():
-                put(g, z, r, c, cnt)
+    d = cells.delta
+    labels = cells.labels
+    for g, z, r, c, v in zip(cells.label.tolist(), cells.zoom.tolist(), cells.row.tolist(), cells.col.tolist(),
+                             cells.value.tolist()):
+        rid = "%s|alltime|%d_%d_%d" % (labels[g], z - d, r >> d, c >> d)
+        rows.setdefault(rid, {})["%d_%d_%d" % (z, r, c)] = v
     return rows
+
+
+def cells_to_table(cells: Cells):
+    """pyarrow Table(id: string, heatmap: string) of the rows, the heatmap
+    JSON-encoded as heatmap_to_json would (json.dumps of the bin dict, floats
+    as repr: 163838.0), built with vectorised string kernels."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+
+    d = cells.delta
+    if len(cells) == 0:
+        return pa.table({"id": pa.array([], pa.string()), "heatmap": pa.array([], pa.string())})
+    tz, tr, tc = cells.zoom - d, cells.row >> d, cells.col >> d
+    o = np.lexsort((cells.col, cells.row, cells.zoom, tc, tr, tz, cells.label))
+    lab, z, r, c, v = cells.label[o], cells.zoom[o], cells.row[o], cells.col[o], cells.value[o]
+    tz, tr, tc = tz[o], tr[o], tc[o]
+    head = np.ones(lab.size, dtype=bool)
+    head[1:] = (lab[1:] != lab[:-1]) | (tz[1:] != tz[:-1]) | (tr[1:] != tr[:-1]) | (tc[1:] != tc[:-1])
+    starts = np.flatnonzero(head)
+    s = lambda a: pc.cast(pa.array(a), pa.string())  # noqa: E731
+    # float repr of integer-valued counts below 1e16 is "<int>.0"; others via repr
+    vi = v.astype(np.int64)
+    small = (v == vi) & (np.abs(v) < 1e16)
+    vs = pc.binary_join_element_wise(s(vi), pa.scalar(".0"), "")
+    if not small.all():
+        vs = vs.to_pylist()
+        for i in np.flatnonzero(~small).tolist():
+            vs[i] = repr(float(v[i]))
+        vs = pa.array(vs, pa.string())
+    bins = pc.binary_join_element_wise(s(z), s(r), s(c), "_")
+    pieces = pc.binary_join_element_wise(pa.scalar('"'), bins, pa.scalar('": '), vs, "")
+    offsets = np.append(starts, lab.size).astype(np.int32)
+    joined = pc.binary_join(pa.ListArray.from_arrays(pa.array(offsets), pieces), ", ")
+    heat = pc.binary_join_element_wise(pa.scalar("{"), joined, pa.scalar("}"), "")
+    names = pa.array(cells.labels, pa.string()).take(pa.array(lab[starts]))
+    ids = pc.binary_join_element_wise(names, pa.scalar("alltime"),
+                                      pc.binary_join_element_wise(s(tz[starts]), s(tr[starts]), s(tc[starts]), "_"),
+                                      KEY_SEPERATOR)
+    return pa.table({"id": ids, "heatmap": heat})
+
+
+def assemble_rows(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None) -> dict:
+    """assemble_cells -> {row_id: heatmap dict}."""
+    return cells_to_rows(assemble_cells(count_all, count_grouped, user_id, keep, max_zoom_level, delta))
+
+
+# --------------------------------------------------------------------------
+# device entry points
+# --------------------------------------------------------------------------
+
+def _device_counters(lat, lon, zmin, zmax, tiles):
+    def count_all(keep):
+        c = device.count(lat, lon, keep.astype(np.uint8), zmin, zmax, tiles=tiles)
+        return c.zoom, c.row, c.col, c.count
+
+    def count_grouped(keep, gid):
+        g = device.count_grouped(lat, lon, gid, keep.astype(np.uint8), zmin, zmax, tiles=tiles)
+        return g.group, g.zoom, g.row, g.col, g.count
+
+    return count_all, count_grouped
+
+
+def heatmap_cells(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None, tiles=False) -> Cells:
+    """Bins of every build_heatmaps row for columnar input (two device passes)."""
+    mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
+    d = DETAIL_ZOOM_DELTA if delta is None else delta
+    ca, cg = _device_counters(lat, lon, d + 1, mz + d, tiles)
+    return assemble_cells(ca, cg, user_id, keep, mz, d)
 
 
 def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None, tiles=False):
@@ -183,10 +363,13 @@ def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, d
 
     lat/lon: float64 arrays (or, with tiles=True, int64 row/col at the detail
     zoom); user_id: sequence of str; keep: mask of non-background rows."""
-    mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
-    d = DETAIL_ZOOM_DELTA if delta is None else delta
-    counter = _device_counter(lat, lon, d + 1, mz + d, tiles)
-    return assemble_rows(counter, user_id, keep, mz, d)
+    return cells_to_rows(heatmap_cells(lat, lon, user_id, keep, max_zoom_level, delta, tiles))
+
+
+def heatmap_table(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None, tiles=False):
+    """The same rows as a pyarrow Table(id, heatmap JSON): batchMain's
+    DataFrame (heatmap.py:156-157) without per-cell Python objects."""
+    return cells_to_table(heatmap_cells(lat, lon, user_id, keep, max_zoom_level, delta, tiles))
 
 
 def build_heatmaps(locations):

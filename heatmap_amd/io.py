@@ -10,14 +10,16 @@ The reference reads `locations` from Cassandra/CosmosDB into a Spark DataFrame
                   DataFrame, a dict of arrays or a list of Row-like dicts ->
                   fp64 lat/lon, the non-background keep mask
                   (heatmap.py:27-29) and the user ids (mapped to groups by
-                  heatmap._group_plan: 'x*' none, 'rt-*' route, heatmap.py:64-70)
+                  heatmap.group_plan: 'x*' none, 'rt-*' route, heatmap.py:64-70)
   rows_to_table   {row_id: heatmap} -> pyarrow Table ['id', 'heatmap'] with
                   the heatmap JSON-encoded (heatmap_to_json, heatmap.py:128-129,
                   156-157), the DataFrame batchMain writes
   batch_main      load -> device count pyramid -> rows -> table, optionally
                   written as Parquet in place of the Cassandra sink
 
-Only the I/O lives on the host; counting is hm_count on the GPU.
+Only the I/O and the string formatting live on the host (vectorised:
+numpy group coding, pyarrow string kernels); counting is hm_count +
+hm_count_grouped on the GPU.
 """
 from __future__ import annotations
 
@@ -35,10 +37,9 @@ def _columns(source):
     if isinstance(source, str):
         source = pq.read_table(source, columns=[c for c in COLUMNS])
     if isinstance(source, pa.Table):
-        return {c: source.column(c).to_pylist() if c in ("source", "user_id") else
-                source.column(c).to_numpy(zero_copy_only=False) for c in COLUMNS}
+        return {c: source.column(c).to_numpy(zero_copy_only=False) for c in COLUMNS}
     if hasattr(source, "to_dict") and hasattr(source, "columns"):  # pandas DataFrame
-        return {c: source[c].to_numpy() if c in ("latitude", "longitude") else list(source[c]) for c in COLUMNS}
+        return {c: source[c].to_numpy() for c in COLUMNS}
     if isinstance(source, dict):
         return {c: source[c] for c in COLUMNS}
     rows = list(source)  # Row-like dicts, as Spark hands them to dataframe_loader
@@ -46,12 +47,12 @@ def _columns(source):
 
 
 def load_locations(source):
-    """-> (lat f64[n], lon f64[n], keep u8[n], user_ids list[str])."""
+    """-> (lat f64[n], lon f64[n], keep u8[n], user_ids object[n])."""
     cols = _columns(source)
     lat = np.ascontiguousarray(np.asarray(cols["latitude"], dtype=np.float64))
     lon = np.ascontiguousarray(np.asarray(cols["longitude"], dtype=np.float64))
-    keep = np.array([s != "background" for s in cols["source"]], dtype=np.uint8)
-    users = list(cols["user_id"])
+    keep = (np.asarray(cols["source"], dtype=object) != "background").astype(np.uint8)
+    users = np.asarray(cols["user_id"], dtype=object)
     if not (lat.size == lon.size == keep.size == len(users)):
         raise ValueError("location columns differ in length")
     return lat, lon, keep, users
@@ -70,8 +71,7 @@ def batch_main(source, sink: str = None, max_zoom_level: int = None, delta: int 
     """batchMain (heatmap.py:152-158) with columnar I/O: returns the rows table
     and writes it to `sink` (Parquet) when given."""
     lat, lon, keep, users = load_locations(source)
-    rows = heatmap.build_heatmaps_columnar(lat, lon, users, keep, max_zoom_level, delta)
-    table = rows_to_table(rows)
+    table = heatmap.heatmap_table(lat, lon, users, keep, max_zoom_level, delta)
     if sink:
         import pyarrow.parquet as pq
 

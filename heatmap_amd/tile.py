@@ -129,9 +129,8 @@ class Tile:
 
     # --- hierarchy (forward projections on the device) -------------------------
     def parent_id(self):
-        """tile.py:60-61: the tile holding this tile's centre one zoom up."""
-        if self.zoom < 1:
-            raise _lib.DevicePathUnsupported("parent of a zoom-0 tile (zoom -1) is not projected on the device")
+        """tile.py:60-61: the tile holding this tile's centre one zoom up; a
+        zoom-0 tile projects at zoom -1 (2 ** -1 = 0.5), as the reference does."""
         return Tile.tile_id_from_lat_long(self.center_latitude, self.center_longitude, self.zoom - 1)
 
     def parent(self):

@@ -89,7 +89,8 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream);
 int hm_ctx_set_stream(hm_ctx* ctx, void* stream);
 int hm_ctx_destroy(hm_ctx* ctx);
 
-/* Project n points at one zoom (0..30).  row/col: int64[n]; status: uint8[n]
+/* Project n points at one zoom (-30..30; negative zooms scale by 2^zoom, as
+ * Python's 2 ** zoom does for Tile.parent_id at zoom 0, tile.py:60-61).  row/col: int64[n]; status: uint8[n]
  * (HM_OK or the point's error kind; row/col are 0 for failed points).
  * Returns HM_OK if every point projected, else the first failing point's kind.
  * Replaces Tile.row_from_latitude / column_from_longitude (tile.py:15-21). */
@@ -127,6 +128,11 @@ int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const ui
 int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
                      const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
                      int64_t capacity, int64_t* n_out);
+
+/* Same from zoom-zmax tile coordinates (int64 row/col). */
+int hm_count_grouped_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep,
+                           const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
+                           int64_t capacity, int64_t* n_out);
 
 /* First failing point of the last call: index in input order (-1 if none)
  * and its HM_E_* kind. */

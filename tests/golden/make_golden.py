@@ -352,7 +352,7 @@ def tile_utils_golden(Tile, rng):
                            "center_latitude", "center_longitude")},
                "children": t.children(),
                "all_zooms": Tile.tile_ids_for_all_zoom_levels(tid)}
-        rec["parent_id"] = t.parent_id() if t.zoom > 0 else None
+        rec["parent_id"] = t.parent_id()   # zoom 0: projected at zoom -1 (2 ** -1)
         cases.append(rec)
     lat_rows = []
     for _ in range(200):

@@ -102,16 +102,24 @@ def test_config1_zoom_digests():
     _check_zoom_digests(lat, lon, g["zoom_counts"])
 
 
-def _oracle_counter(lat, lon, zmin, zmax):
-    def counter(mask):
-        r = oracle.count(lat, lon, None if mask is None else mask.astype(np.uint8), zmin, zmax)
-        assert r["status"] == 0
-        out = collections.defaultdict(dict)
-        for z, a, b, n in zip(r["zoom"].tolist(), r["row"].tolist(), r["col"].tolist(), r["count"].tolist()):
-            out[z][(a, b)] = n
-        return out
+def _oracle_counters(lat, lon, zmin, zmax):
+    """The oracle's stand-ins for hm_count / hm_count_grouped
+    (heatmap.assemble_cells' counting hooks)."""
 
-    return counter
+    def count_all(keep):
+        r = oracle.count(lat, lon, keep.astype(np.uint8), zmin, zmax)
+        assert r["status"] == 0
+        return r["zoom"], r["row"], r["col"], r["count"]
+
+    def count_grouped(keep, gid):
+        parts = []
+        for g in np.unique(gid[keep]).tolist():
+            r = oracle.count(lat, lon, (keep & (gid == g)).astype(np.uint8), zmin, zmax)
+            assert r["status"] == 0
+            parts.append((np.full(r["zoom"].size, g), r["zoom"], r["row"], r["col"], r["count"]))
+        return tuple(np.concatenate([p[i] for p in parts]) for i in range(5))
+
+    return count_all, count_grouped
 
 
 def _load_rows(name):
@@ -129,8 +137,12 @@ def test_assemble_rows_vs_reference(name):
     keep = np.array([r["source"] != "background" for r in rows])
     users = [r["user_id"] for r in rows]
     mz, d = g["max_zoom_level"], g["detail_zoom_delta"]
-    got = heatmap.assemble_rows(_oracle_counter(lat, lon, d + 1, mz + d), users, keep, mz, d)
-    assert got == g["rows"]
+    cells = heatmap.assemble_cells(*_oracle_counters(lat, lon, d + 1, mz + d), users, keep, mz, d)
+    assert heatmap.cells_to_rows(cells) == g["rows"]
+    # the vectorised (id, JSON) table holds the same rows
+    t = heatmap.cells_to_table(cells).to_pydict()
+    assert {i: json.loads(h) for i, h in zip(t["id"], t["heatmap"])} == g["rows"]
+    assert len(t["id"]) == len(g["rows"])
 
 
 @pytest.mark.parametrize("name", ROW_GOLDENS[:3])
@@ -151,7 +163,7 @@ def test_config1_heatmap_digest():
     h = g["heatmap"]
     lat, lon = synth.uniform(g["n"], seed=0)
     users = ["x"] * g["n"]
-    got = heatmap.assemble_rows(_oracle_counter(lat, lon, h["delta"] + 1, h["max_zoom_level"] + h["delta"]),
+    got = heatmap.assemble_rows(*_oracle_counters(lat, lon, h["delta"] + 1, h["max_zoom_level"] + h["delta"]),
                                 users, None, h["max_zoom_level"], h["delta"])
     assert len(got) == h["rows"]
     items = sorted((k, t, repr(c)) for k, dd in got.items() for t, c in dd.items())
