@@ -13,6 +13,8 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <math.h>
+
 #include <algorithm>
 #include <string>
 #include <vector>
@@ -45,6 +47,7 @@ struct hm_ctx {
     std::vector<Buf> bufs;
     unsigned long long* state = nullptr;      /* device: err, exotic count, slow, cursor, nslots, ... */
     unsigned long long* host_state = nullptr; /* pinned mirror */
+    uint32_t* host_aux = nullptr;             /* pinned: level-1 histogram / region sizes */
     int64_t last_err_index = -1;
     int last_err_kind = 0;
     int64_t last_slow = 0;
@@ -61,7 +64,8 @@ enum {
     ST_REDO = 5,
     ST_REDO_OUT = 6,
     ST_XCURSOR = 7,
-    ST_COUNT = 8
+    ST_OVERFLOW = 8,
+    ST_COUNT = 16
 };
 
 static int hip_fail(hipError_t e, const char* what)
@@ -90,6 +94,7 @@ enum {
     /* exotic list and the general path (hm_general.hip) */
     B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
+    B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_COUNT
 };
 
@@ -165,6 +170,9 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     } else if (hipHostMalloc(&c->host_state, 4 * ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->host_state = nullptr;
         st = HM_E_NOMEM;
+    } else if (hipHostMalloc(&c->host_aux, (2 + 2 * HM_L1_SHARDS) * HM_MAX_F1 * sizeof(uint32_t)) != hipSuccess) {
+        c->host_aux = nullptr;
+        st = HM_E_NOMEM;
     }
     for (int i = 0; i < 10 && st == HM_OK; i++)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) {
@@ -195,6 +203,7 @@ int hm_ctx_destroy(hm_ctx* c)
         if (b.p) (void)hipFree(b.p);
     if (c->state) (void)hipFree(c->state);
     if (c->host_state) (void)hipHostFree(c->host_state);
+    if (c->host_aux) (void)hipHostFree(c->host_aux);
     for (int i = 0; i < 10; i++)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     delete c;
@@ -438,13 +447,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     int nev = 0;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
 
-    /* level-1 tiles: the input tiles, then (lat/lon input only) tiles of the
-     * points the fast path deferred to k_redo, at most redo_cap of them */
+    /* level 1 reads the input in HM_T1-point tiles; points the fast path
+     * defers (lat/lon input only) go to k_redo, at most redo_cap of them */
     const uint32_t tiles_in = (uint32_t)((n + HM_T1 - 1) / HM_T1);
     const bool from_tiles = rows != nullptr;
     uint64_t redo_cap = from_tiles ? 0 : std::max<uint64_t>(1u << 20, (uint64_t)n / 256);
     if (redo_cap > (uint64_t)n) redo_cap = (uint64_t)n;
-    uint32_t tiles1 = tiles_in + (uint32_t)((redo_cap + HM_T1 - 1) / HM_T1);
     /* exotic list: first capacity like the redo list's; rebuilt if it overflows */
     HmExotic xl;
     xl.cap = std::min<uint64_t>((uint64_t)n, std::max<uint64_t>(1u << 20, (uint64_t)n / 256));
@@ -452,20 +460,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     ENSURE(B_X_COL, xl.cap * 8 + 8, xl.col);
     ENSURE(B_X_IDX, xl.cap * 8 + 8, xl.idx);
     xl.count = ctx->state + ST_XCOUNT;
-    uint32_t* root = nullptr;
-    ENSURE(B_ROOT, 4 * sizeof(uint32_t) + 2 * sizeof(uint64_t), root);
-    {
-        /* staged through the pinned scratch: [0, tiles1, 0, 0 | coord 0, 0] */
-        unsigned long long* up = ctx->host_state + ST_COUNT;
-        HIPCHK(hipStreamSynchronize(s));
-        up[0] = (unsigned long long)tiles1 << 32;
-        up[1] = 0;
-        up[2] = 0;
-        up[3] = 0;
-        HIPCHK(hipMemcpyAsync(root, up, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
-    }
-    const uint32_t* parent_item_begin = root;
-    const uint64_t* parent_coord = (const uint64_t*)(root + 4);
+    const uint32_t* parent_item_begin = nullptr;
+    const uint64_t* parent_coord = nullptr;
     uint32_t nparents = 1;
 
     Level lv[HM_MAX_LEVELS];
@@ -488,27 +484,18 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         V.nchildren = (uint64_t)nparents << V.dbits;
         V.out16 = (l == L - 1);
         const int restbits = 2 * (Z - zs[l]);
-        const uint64_t ntiles = (l == 0) ? tiles1 : lv[l - 1].items;
         if (V.nchildren > (uint64_t)HM_SCAN_LIMIT) return HM_FALLBACK;
-        /* run-counter shards: 32 unless the dense child space is large (then
-         * per-child contention is low anyway); keeps counters <= 2^25 */
-        int sb = 5;
-        while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
-        const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
-        if (run_cap >= (1ull << 32)) return HM_E_NOMEM;
-
-        /* outputs of the level's partition kernel: keys (level 1: per tile;
-         * levels >= 2: at the item's global positions) and sharded runs */
-        void* kout;
-        uint2* runs_sh;
-        uint32_t* nruns;
-        const uint64_t nkeys_out = (l == 0) ? ntiles * (uint64_t)HM_T1 : level_keys;
-        ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
-        ENSURE(B_RUNS_SH, run_cap * sizeof(uint2), runs_sh);
-        ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
-        HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
-
         if (l == 0) {
+            /* ---- level 1: projection + partition into per-digit regions ---- */
+            const int F = 1 << V.dbits;
+            const int FS = F * HM_L1_SHARDS;
+            uint32_t *fill, *rbase, *rcap, *hist;
+            uint8_t* smask;
+            ENSURE(B_L1_FILL, FS * 4, fill);
+            ENSURE(B_L1_RBASE, FS * 4, rbase);
+            ENSURE(B_L1_RCAP, FS * 4, rcap);
+            ENSURE(B_L1_HIST, F * 4, hist);
+            ENSURE(B_L1_SMASK, F, smask);
             uint32_t* redo_idx = nullptr;
             int64_t *redo_rows = nullptr, *redo_cols = nullptr;
             if (!from_tiles) {
@@ -527,59 +514,92 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.Z = Z;
             a.dbits = V.dbits;
             a.restbits = restbits;
-            a.tiles = tiles1;
-            a.tile0 = 0;
-            a.shard_bits = sb;
-            a.keys_out = kout;
-            a.nruns = nruns;
-            a.runs = runs_sh;
+            a.fill = fill;
+            a.rbase = rbase;
+            a.rcap = rcap;
+            a.smask = smask;
+            a.overflow = ctx->state + ST_OVERFLOW;
             a.err_word = ctx->state + ST_ERR;
             a.x = xl;
             a.slow_count = ctx->state + ST_SLOW;
             a.redo_idx = redo_idx;
             a.redo_count = ctx->state + ST_REDO;
             a.redo_cap = redo_cap;
-            HIPCHK(hipEventRecord(ev[nev++], s));
-            hm_launch_part1(s, a, tiles_in, V.out16, from_tiles ? 1 : 0);
+            /* region sizes: a sampled digit histogram with a generous margin */
+            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> 22);
+            HIPCHK(hipMemsetAsync(hist, 0, F * 4, s));
+            if (n > 0) hm_launch_sample_digits(s, a, stride, hist);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev[nev++], s));
-            if (!from_tiles) {
-                HmRedoArgs ra;
-                ra.lat = lat;
-                ra.lon = lon;
-                ra.keep = keep;
-                ra.Z = Z;
-                ra.redo_idx = redo_idx;
-                ra.redo_count = ctx->state + ST_REDO;
-                ra.rows_out = redo_rows;
-                ra.cols_out = redo_cols;
-                ra.out_count = ctx->state + ST_REDO_OUT;
-                ra.err_word = ctx->state + ST_ERR;
-                ra.x = xl;
-                ra.cap = redo_cap;
-                hm_launch_redo(s, ra, redo_cap);
-                HIPCHK(hipGetLastError());
+            /* pinned host scratch: hist [F] | caps [FS] | bases [FS] | smask [F] */
+            uint32_t* hh = ctx->host_aux;
+            uint32_t* hc = hh + HM_MAX_F1;
+            uint32_t* hb = hc + HM_MAX_F1 * HM_L1_SHARDS;
+            uint8_t* hm = (uint8_t*)(hb + HM_MAX_F1 * HM_L1_SHARDS);
+            HIPCHK(hipMemcpyAsync(hh, hist, F * 4, hipMemcpyDeviceToHost, s));
+            HIPCHK(hipStreamSynchronize(s));
+            for (int d = 0; d < F; d++) {
+                const double est = (double)hh[d] * (double)stride;
+                const int ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
+                hm[d] = (uint8_t)(ns - 1);
+                const double e = est / ns;
+                const uint32_t c = (uint32_t)std::min(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) + 2.0 * HM_T1);
+                for (int sh = 0; sh < HM_L1_SHARDS; sh++) hc[d * HM_L1_SHARDS + sh] = sh < ns ? c : 0u;
             }
-            if ((st = read_state(ctx))) return st;
-            if ((st = take_error(ctx))) return st;
-            const uint64_t nredo = ctx->host_state[ST_REDO];
-            if (!from_tiles && nredo > redo_cap) {
-                /* adversarial input (mostly polar / guard band): redo the
-                 * level with the exact chain fused into the kernel */
-                HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
-                HIPCHK(hipMemsetAsync(xl.count, 0, sizeof(unsigned long long), s));
-                a.tiles = tiles1 = tiles_in;
-                hm_launch_part1(s, a, tiles_in, V.out16, 2);
+            HIPCHK(hipMemcpyAsync(smask, hm, F, hipMemcpyHostToDevice, s));
+            void* kout = nullptr;
+            uint64_t total_cap = 0;
+            for (int attempt = 0;; attempt++) {
+                total_cap = 0;
+                for (int i = 0; i < FS; i++) {
+                    hb[i] = (uint32_t)total_cap;
+                    total_cap += hc[i];
+                }
+                if (total_cap >= 0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
+                ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (total_cap + 8) * (V.out16 ? 2 : 4), kout);
+                a.keys_out = kout;
+                HIPCHK(hipMemcpyAsync(rcap, hc, FS * 4, hipMemcpyHostToDevice, s));
+                HIPCHK(hipMemcpyAsync(rbase, hb, FS * 4, hipMemcpyHostToDevice, s));
+                HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
+                HIPCHK(hipMemsetAsync(ctx->state + ST_OVERFLOW, 0, 8, s));
+                HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, 16, s));   /* ST_REDO, ST_REDO_OUT */
+                HIPCHK(hipMemsetAsync(ctx->state + ST_SLOW, 0, 8, s));
+                HIPCHK(hipMemsetAsync(xl.count, 0, 8, s));
+                HIPCHK(hipEventRecord(ev[0], s));
+                hm_launch_part1(s, a, tiles_in, V.out16, from_tiles ? 1 : 0);
                 HIPCHK(hipGetLastError());
+                HIPCHK(hipEventRecord(ev[1], s));
+                nev = 2;
+                if (!from_tiles) {
+                    HmRedoArgs ra;
+                    ra.lat = lat;
+                    ra.lon = lon;
+                    ra.keep = keep;
+                    ra.Z = Z;
+                    ra.redo_idx = redo_idx;
+                    ra.redo_count = ctx->state + ST_REDO;
+                    ra.rows_out = redo_rows;
+                    ra.cols_out = redo_cols;
+                    ra.out_count = ctx->state + ST_REDO_OUT;
+                    ra.err_word = ctx->state + ST_ERR;
+                    ra.x = xl;
+                    ra.cap = redo_cap;
+                    hm_launch_redo(s, ra, redo_cap);
+                    HIPCHK(hipGetLastError());
+                }
                 if ((st = read_state(ctx))) return st;
                 if ((st = take_error(ctx))) return st;
-                unsigned long long* up = ctx->host_state + ST_COUNT;
-                up[0] = (unsigned long long)tiles1 << 32;
-                up[1] = up[2] = up[3] = 0;
-                HIPCHK(hipMemcpyAsync(root, up, 4 * sizeof(unsigned long long), hipMemcpyHostToDevice, s));
-            } else if (!from_tiles) {
-                const uint64_t nres = ctx->host_state[ST_REDO_OUT];
-                if (nres) {
+                const uint64_t nredo = ctx->host_state[ST_REDO];
+                if (!from_tiles && nredo > redo_cap) {
+                    /* adversarial input (mostly polar / guard band): redo the
+                     * level with the exact chain fused into the kernel */
+                    HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
+                    HIPCHK(hipMemsetAsync(ctx->state + ST_OVERFLOW, 0, 8, s));
+                    HIPCHK(hipMemsetAsync(xl.count, 0, 8, s));
+                    hm_launch_part1(s, a, tiles_in, V.out16, 2);
+                    HIPCHK(hipGetLastError());
+                } else if (!from_tiles && ctx->host_state[ST_REDO_OUT]) {
+                    /* the deferred points, resolved exactly, as tile input */
+                    const uint64_t nres = ctx->host_state[ST_REDO_OUT];
                     HmPart1Args b = a;
                     b.lat = nullptr;
                     b.lon = nullptr;
@@ -587,13 +607,20 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     b.cols_in = redo_cols;
                     b.keep = nullptr;
                     b.n = (int64_t)nres;
-                    b.tile0 = tiles_in;
                     hm_launch_part1(s, b, (uint32_t)((nres + HM_T1 - 1) / HM_T1), V.out16, 1);
                     HIPCHK(hipGetLastError());
                 }
+                ctx->last_slow = (int64_t)nredo;
+                if ((st = read_state(ctx))) return st;
+                if ((st = take_error(ctx))) return st;
+                if (!ctx->host_state[ST_OVERFLOW]) break;
+                /* a region overflowed: fill[] now holds the exact sizes (the
+                 * shard of every tile is fixed by its block id) */
+                if (attempt > 0) return HM_E_HIP;   /* cannot happen: the same points */
+                HIPCHK(hipMemcpyAsync(hc, fill, FS * 4, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                for (int i = 0; i < FS; i++) hc[i] += 64;
             }
-            ctx->last_slow = (int64_t)nredo;
-            if ((st = read_state(ctx))) return st;
             nx = ctx->host_state[ST_XCOUNT];
             if (nx > xl.cap) {
                 /* more kept out-of-square points than the list held: rebuild it */
@@ -608,7 +635,93 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 nx = ctx->host_state[ST_XCOUNT];
                 if (nx > xl.cap) return HM_E_HIP;   /* cannot happen: the same points */
             }
-        } else {
+            /* the non-empty digits are the level's buckets, one run each */
+            HmL1Args ba;
+            memset(&ba, 0, sizeof(ba));
+            const uint64_t cap = (uint64_t)F + 1;
+            ENSURE(B_BK0 + 0, cap * 4, ba.out.nkeys);
+            ENSURE(B_BK0 + 1, cap * 4, ba.out.nruns);
+            ENSURE(B_BK0 + 2, cap * 4, ba.out.rbase);
+            ENSURE(B_BK0 + 3, cap * 4, ba.out.item_begin);
+            ENSURE(B_BK0 + 4, cap * 4, ba.out.digit);
+            ENSURE(B_BK0 + 5, cap * 8, ba.out.coord);
+            ENSURE(B_BK0 + 6, cap * 4, ba.out.keybase);
+            ENSURE(B_FLAT_A, (uint64_t)FS * sizeof(uint2) + 8, ba.runs);
+            ENSURE(B_EXCL_A, (uint64_t)FS * sizeof(uint64_t) + 8, ba.excl);
+            ENSURE(B_CHILD0, 2 * 4, ba.child_begin);
+            uint64_t* tot;
+            ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+            ba.F = F;
+            ba.dbits = V.dbits;
+            ba.fill = fill;
+            ba.rbase = rbase;
+            ba.smask = smask;
+            ba.item_keys = (L == 1) ? HM_TA : HM_TN;
+            ba.sparse_max = (L == 1) ? HM_SP_MAX : 0u;
+            ba.total = tot;
+            if (L == 1) {
+                ENSURE(B_SLOTS, cap * 4, slots);
+                ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
+                ba.slots = slots;
+                ba.nslots = (uint32_t*)(ctx->state + ST_NSLOTS);
+                ba.slot_bucket = slot_bucket;
+            }
+            hm_launch_level1_buckets(s, ba);
+            HIPCHK(hipGetLastError());
+            unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+            HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            if ((st = read_state(ctx))) return st;
+            V.count = (uint32_t)(down[0] >> 32);
+            V.items = (uint32_t)(down[0] & 0xFFFFFFFFull);
+            if (L == 1) nslots = (uint32_t)(ctx->host_state[ST_NSLOTS] & 0xFFFFFFFFull);
+            level_keys = total_cap;
+            HmBuckets& b = B[0];
+            b.count = V.count;
+            b.nkeys = ba.out.nkeys;
+            b.nruns = ba.out.nruns;
+            b.rbase = ba.out.rbase;
+            b.keybase = ba.out.keybase;
+            b.item_begin = ba.out.item_begin;
+            b.digit = ba.out.digit;
+            b.coord = ba.out.coord;
+            b.slots = (L == 1) ? slots : nullptr;
+            runs_cur.run = ba.runs;
+            runs_cur.excl = ba.excl;
+            {
+                uint4* desc;
+                ENSURE(B_DESC0 + 0, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
+                b.desc = desc;
+                hm_launch_items(s, b, runs_cur, V.items, (L == 1) ? HM_TA : HM_TN, desc);
+                HIPCHK(hipGetLastError());
+            }
+            keys_cur = kout;
+            parent_item_begin = ba.out.item_begin;
+            parent_coord = ba.out.coord;
+            nparents = V.count;
+            slot_k ^= 1;
+            continue;
+        }
+        /* ---- levels >= 2 ---- */
+        const uint64_t ntiles = lv[l - 1].items;
+        /* run-counter shards: 32 unless the dense child space is large (then
+         * per-child contention is low anyway); keeps counters <= 2^25 */
+        int sb = 5;
+        while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
+        const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
+        if (run_cap >= (1ull << 32)) return HM_E_NOMEM;
+
+        /* outputs of the level's partition kernel: keys at the item's global
+         * positions, and sharded runs */
+        void* kout;
+        uint2* runs_sh;
+        uint32_t* nruns;
+        const uint64_t nkeys_out = level_keys;
+        ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
+        ENSURE(B_RUNS_SH, run_cap * sizeof(uint2), runs_sh);
+        ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
+        HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
+
+        {
             HmPartNArgs a;
             memset(&a, 0, sizeof(a));
             a.parent = B[l - 1];

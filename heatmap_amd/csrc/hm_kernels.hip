@@ -103,6 +103,14 @@ __device__ __forceinline__ void hm_exotic_append(const HmExotic& x, bool p, int6
     }
 }
 
+/* region slot of digit d for this block: hot digits are split into
+ * HM_L1_SHARDS sub-regions (block id & smask[d]) so their fill counters see
+ * 1/8 of the tiles' atomics each */
+__device__ __forceinline__ uint32_t hm_l1_slot(const HmPart1Args& a, int d)
+{
+    return (uint32_t)d * HM_L1_SHARDS + (blockIdx.x & (uint32_t)a.smask[d]);
+}
+
 /* ------------------------------------------------------------------------ */
 /* level 1: projection fused with the first partition                        */
 /* ------------------------------------------------------------------------ */
@@ -112,12 +120,13 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 {
     __shared__ uint32_t cur[HM_MAX_F1 + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ OutT stage[HM_T1 + 64];
+    /* copy pieces: <= HM_P1_PIECE staged keys of one digit each */
+    __shared__ uint32_t psrc[HM_T1 / HM_P1_PIECE + HM_MAX_F1], pdst[HM_T1 / HM_P1_PIECE + HM_MAX_F1];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
     __shared__ double tab[HM_YTAB_N];
     constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
-    const uint32_t tile = a.tile0 + blockIdx.x;          /* tile slot in the run layout */
     const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
     const uint32_t lim = 1u << a.Z;
     const double scale = hm_exp2i(a.Z);
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu);
     __syncthreads();
 
-    /* exclusive scan of the digit histogram; one run record per digit */
+    /* exclusive scan of the digit histogram */
     constexpr int PER = HM_MAX_F1 / HM_P1_THREADS;
     uint32_t cnt[PER];
     uint32_t s = 0;
@@ -293,18 +302,18 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     }
     uint32_t total;
     uint32_t off = hm_block_excl_scan<HM_P1_THREADS>(s, scr, &total);
-    /* run records: issue every slot atomic before consuming any result, so a
-     * tile pays one atomic latency, not PER of them */
-    const uint32_t sh = tile & ((1u << a.shard_bits) - 1u);
-    const uint64_t cap = ((uint64_t)a.tiles + (1u << a.shard_bits) - 1) >> a.shard_bits;
-    uint32_t idx[PER];
+    /* reserve each digit's keys in its region (one returning atomic per
+     * non-empty digit); every atomic is issued before any result is used, and
+     * the results are consumed only after the claim below, so the tile pays
+     * about one atomic latency and hides it behind LDS work */
+    uint32_t gpos[PER];
     uint32_t offq[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
         offq[q] = off;
-        idx[q] = 0;
-        if (d < F && cnt[q]) idx[q] = atomicAdd(&a.nruns[((uint64_t)d << a.shard_bits) + sh], 1u);
+        gpos[q] = 0;
+        if (d < F && cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1_slot(a, d)], cnt[q]);
         off += cnt[q];
     }
 #pragma unroll
@@ -319,17 +328,163 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         const uint32_t pos = hm_lds_claim(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), v);
         stage[v ? pos : HM_T1 + hm_lane()] = (OutT)rest[k];
     }
-    __syncthreads();
-    OutT* out = (OutT*)a.keys_out + (uint64_t)tile * HM_T1;
-    for (uint32_t i = tid; i < total; i += HM_P1_THREADS) out[i] = stage[i];
-    /* run records last: the slot atomics' latency hid behind the scatter */
+    /* copy pieces: digit d's staged keys [offq, offq + cnt) go to region
+     * position rbase[d] + gpos, cut into pieces of <= HM_P1_PIECE keys that the
+     * waves take in turn (contiguous reads and writes per wave).  A
+     * reservation past the region's capacity is dropped and flagged (the host
+     * re-runs the level with exact sizes). */
+    bool over = false;
+    uint32_t np = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F && cnt[q])
-            a.runs[hm_run_base(0, a.tiles, 0, d, a.dbits, a.shard_bits) + sh * cap + idx[q]] =
-                make_uint2(tile * HM_T1 + offq[q], cnt[q]);
+        const bool fits = d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)a.rcap[hm_l1_slot(a, d)];
+        over |= d < F && cnt[q] && !fits;
+        np += fits ? (cnt[q] + HM_P1_PIECE - 1) / HM_P1_PIECE : 0u;
     }
+    if (over) atomicOr(a.overflow, 1ull);
+    uint32_t npieces;
+    uint32_t pq = hm_block_excl_scan<HM_P1_THREADS>(np, scr, &npieces);
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)a.rcap[hm_l1_slot(a, d)]) {
+            const uint32_t g = a.rbase[hm_l1_slot(a, d)] + gpos[q];
+            for (uint32_t o = 0; o < cnt[q]; o += HM_P1_PIECE) {
+                psrc[pq] = (offq[q] + o) | ((min(cnt[q] - o, (uint32_t)HM_P1_PIECE) - 1) << 16);
+                pdst[pq] = g + o;
+                pq++;
+            }
+        }
+    }
+    __syncthreads();
+    OutT* out = (OutT*)a.keys_out;
+    const int lane = hm_lane();
+    for (uint32_t j = tid >> 6; j < npieces; j += HM_P1_THREADS / 64) {
+        const uint32_t ps = psrc[j], pd = pdst[j];
+        const uint32_t src = ps & 0xFFFFu, len = (ps >> 16) + 1;
+        for (uint32_t e = lane; e < len; e += 64) out[pd + e] = stage[src + e];
+    }
+}
+
+/* Sampled digit histogram of level 1 (every stride-th point, fast projection
+ * only): sizes the per-digit key regions k_project_partition fills. */
+template <bool FROM_TILES>
+__global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t stride_pts, uint32_t* hist)
+{
+    __shared__ uint32_t h[HM_MAX_F1 + 64];
+    __shared__ double tab[HM_YTAB_N];
+    const int F = 1 << a.dbits;
+    for (int i = threadIdx.x; i < F; i += 256) h[i] = 0;
+    if (!FROM_TILES) hm_load_ytab(tab);
+    __syncthreads();
+    const double scale = hm_exp2i(a.Z);
+    const double kz = HM_INV360 * scale;
+    const uint32_t lim = 1u << a.Z;
+    const int hb = a.restbits >> 1, wd = a.dbits >> 1;
+    const uint64_t m = (uint64_t)(a.n + stride_pts - 1) / stride_pts;
+    const uint64_t step = (uint64_t)gridDim.x * 256;
+    const uint64_t m_up = (m + 63) & ~63ull;
+    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m_up; j += step) {
+        const uint64_t i = j * stride_pts;
+        bool v = j < m && (!a.keep || a.keep[i]);
+        int64_t r = 0, c = 0;
+        if (v) {
+            if (FROM_TILES) {
+                r = a.rows_in[i];
+                c = a.cols_in[i];
+            } else {
+                int32_t r32, c32;
+                v = hm_project_fast(a.lat[i], a.lon[i], scale, kz, &r32, &c32, tab);
+                r = r32;
+                c = c32;
+            }
+            v = v && (uint64_t)r < lim && (uint64_t)c < lim;
+        }
+        const uint32_t d = ((((uint32_t)r) >> hb) << wd) | (((uint32_t)c) >> hb);
+        hm_lds_count(h, HM_MAX_F1, d, v);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < F; i += 256)
+        if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist)
+{
+    const uint64_t m = ((uint64_t)a.n + stride_pts - 1) / stride_pts;
+    uint64_t blocks = (m + 1023) / 1024;
+    if (blocks > 2048) blocks = 2048;
+    if (blocks < 1) blocks = 1;
+    if (a.rows_in)
+        hipLaunchKernelGGL(k_sample_digits<true>, dim3((unsigned)blocks), dim3(256), 0, s, a, stride_pts, hist);
+    else
+        hipLaunchKernelGGL(k_sample_digits<false>, dim3((unsigned)blocks), dim3(256), 0, s, a, stride_pts, hist);
+}
+
+/* Level-1 buckets from the filled regions: one flat run per non-empty digit
+ * (its whole region), the bucket list, work-item prefix and, when level 1 is
+ * the last level, the merge slots of multi-item buckets.  One block. */
+__global__ __launch_bounds__(1024) void k_level1_buckets(HmL1Args a)
+{
+    __shared__ uint32_t scr[1024 / 64 + 1];
+    const int d = threadIdx.x;
+    uint32_t f[HM_L1_SHARDS];
+    uint32_t nk = 0, nr = 0;
+    const int ns = d < a.F ? a.smask[d] + 1 : 0;
+#pragma unroll
+    for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
+        f[sh] = sh < ns ? a.fill[d * HM_L1_SHARDS + sh] : 0u;
+        nk += f[sh];
+        nr += f[sh] != 0;
+    }
+    const uint32_t ne = nk > 0;
+    const uint32_t nit = ne ? (nk <= a.sparse_max ? 0u : (nk + a.item_keys - 1) / a.item_keys) : 0u;
+    uint32_t count, items, runs;
+    const uint32_t idx = hm_block_excl_scan<1024>(ne, scr, &count);
+    const uint32_t ib = hm_block_excl_scan<1024>(nit, scr, &items);
+    const uint32_t r0 = hm_block_excl_scan<1024>(nr, scr, &runs);
+    if (ne) {
+        /* logical key positions of the bucket: [region base, + nk), its
+         * non-empty shards' keys one after the other */
+        const uint32_t kb = a.rbase[d * HM_L1_SHARDS];
+        a.out.nkeys[idx] = nk;
+        a.out.nruns[idx] = nr;
+        a.out.rbase[idx] = r0;
+        a.out.keybase[idx] = kb;
+        a.out.item_begin[idx] = ib;
+        a.out.digit[idx] = (uint32_t)d;
+        const int wd = a.dbits >> 1;
+        a.out.coord[idx] = ((uint64_t)(d >> wd) << 32) | (uint64_t)(d & ((1 << wd) - 1));
+        uint32_t j = r0, at = kb;
+#pragma unroll
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
+            if (f[sh]) {
+                a.runs[j] = make_uint2(a.rbase[d * HM_L1_SHARDS + sh], f[sh]);
+                a.excl[j] = at;
+                at += f[sh];
+                j++;
+            }
+        }
+        if (a.slots) {
+            int32_t sl = -1;
+            if (nit > 1) {
+                sl = (int32_t)atomicAdd(a.nslots, 1u);
+                a.slot_bucket[sl] = idx;
+            }
+            a.slots[idx] = sl;
+        }
+    }
+    if (d == 0) {
+        a.out.item_begin[count] = items;
+        a.child_begin[0] = 0;
+        a.child_begin[1] = count;
+        *a.total = ((uint64_t)count << 32) | items;
+    }
+}
+
+void hm_launch_level1_buckets(hipStream_t s, const HmL1Args& a)
+{
+    hipLaunchKernelGGL(k_level1_buckets, dim3(1), dim3(1024), 0, s, a);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -456,6 +611,43 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
     const int lane = tid & 63;
     const int w = tid >> 6;
     const uint4* kv = (const uint4*)keys;
+    if (it.r1 - it.r0 <= HM_L1_SHARDS) {
+        /* a few long runs (level-1 regions): each a contiguous key range,
+         * streamed directly -- head keys, 16-B body vectors HM_SU per lane in
+         * flight, tail keys; positions in that order, run after run */
+        uint32_t pos0 = 0;
+        for (uint32_t r = it.r0; r < it.r1; r++) {
+        const uint2 run = in.run[r];
+        const uint64_t s0 = in.excl[r];
+        const uint64_t s2 = max(s0, (uint64_t)it.a), e2 = min(s0 + run.y, (uint64_t)it.b);
+        const uint32_t cnt = e2 > s2 ? (uint32_t)(e2 - s2) : 0u;
+        const uint32_t src = run.x + (uint32_t)(s2 - s0);
+        const uint32_t head = min(cnt, (V - (src & (V - 1))) & (V - 1));
+        const uint32_t nv = (cnt - head) / V;
+        const uint32_t tail = cnt - head - nv * V;
+        const uint32_t vb = (src + head) / V;
+        for (uint32_t v0 = 0; v0 < nv; v0 += THREADS * HM_SU) {
+            uint4 x[HM_SU];
+            bool ok[HM_SU];
+#pragma unroll
+            for (int u = 0; u < HM_SU; u++) {
+                const uint32_t v = v0 + u * THREADS + tid;
+                ok[u] = v < nv;
+                x[u] = ok[u] ? kv[vb + v] : make_uint4(0, 0, 0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < HM_SU; u++) f.vec(x[u], ok[u], pos0 + head + V * (v0 + u * THREADS + tid));
+        }
+        const uint32_t t = (uint32_t)tid;
+        const uint32_t kh = t < head ? (uint32_t)keys[src + t] : 0u;
+        const uint32_t kt = t < tail ? (uint32_t)keys[src + head + nv * V + t] : 0u;
+        f.key(kh, t < head, pos0 + t);
+        f.key(kt, t < tail, pos0 + head + nv * V + t);
+        pos0 += cnt;
+        }
+        __syncthreads();
+        return;
+    }
     uint32_t carry = 0;                        /* keys staged by earlier chunks */
     for (uint32_t rc = it.r0; rc < it.r1; rc += RCH) {
         const uint32_t m = min((uint32_t)RCH, it.r1 - rc);

@@ -8,9 +8,11 @@
 #define HM_P1_THREADS 512
 #endif
 #ifndef HM_P1_PPT
-#define HM_P1_PPT 8
+#define HM_P1_PPT 16
 #endif
-#define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 4096 points per tile */
+#define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 8192 points per tile */
+#define HM_P1_PIECE 256                     /* keys per copy piece (one wave, 4 steps) */
+#define HM_L1_SHARDS 8                      /* sub-regions of a hot level-1 digit */
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
 /* levels >= 2 */
@@ -123,6 +125,22 @@ struct HmExotic {
     unsigned long long* count;
 };
 
+struct HmCompactOut {
+    uint32_t* nkeys;
+    uint32_t* nruns;
+    uint32_t* rbase;
+    uint32_t* keybase;
+    uint32_t* item_begin;
+    uint32_t* digit;
+    uint64_t* coord;
+};
+
+/* level 1 (k_project_partition): every kept in-square point's key goes to
+ * the contiguous region of its zoom-z1 digit d -- keys [rbase[d], rbase[d] +
+ * rcap[d]) of keys_out, filled through the counter fill[d] (one returning
+ * atomic per tile and non-empty digit).  Regions are sized from a sampled
+ * histogram (k_sample_digits); a tile whose reservation passes rcap[d] drops
+ * it and raises *overflow, and the host re-runs the level with exact sizes. */
 struct HmPart1Args {
     const double* lat;
     const double* lon;
@@ -131,18 +149,35 @@ struct HmPart1Args {
     const uint8_t* keep;
     int64_t n;
     int Z, dbits, restbits;
-    uint32_t tiles;           /* level-1 tile slots of the run layout (incl. redo tiles) */
-    uint32_t tile0;           /* index of this launch's first tile */
-    int shard_bits;
     uint32_t* redo_idx;       /* fast mode: points the fast path could not settle */
     unsigned long long* redo_count;
     uint64_t redo_cap;
     void* keys_out;
-    uint32_t* nruns;            /* [F << shard_bits] */
-    uint2* runs;
+    uint32_t* fill;           /* [F * HM_L1_SHARDS] per (digit, shard) */
+    const uint32_t* rbase;    /* [F * HM_L1_SHARDS] */
+    const uint32_t* rcap;     /* [F * HM_L1_SHARDS] */
+    const uint8_t* smask;     /* [F]: shards of digit d - 1 (0 or HM_L1_SHARDS - 1) */
+    unsigned long long* overflow;
     unsigned long long* err_word;
     HmExotic x;
     unsigned long long* slow_count;
+};
+
+/* level-1 buckets (k_level1_buckets) from the filled regions */
+struct HmL1Args {
+    int F, dbits;
+    const uint32_t* fill;
+    const uint32_t* rbase;
+    const uint8_t* smask;
+    uint32_t item_keys, sparse_max;
+    HmCompactOut out;
+    uint2* runs;
+    uint64_t* excl;
+    uint32_t* child_begin;
+    uint64_t* total;           /* count << 32 | items */
+    int32_t* slots;            /* last level only */
+    uint32_t* nslots;
+    uint32_t* slot_bucket;
 };
 
 struct HmPartNArgs {
@@ -178,15 +213,6 @@ struct HmRsArgs {
     uint64_t* vals;             /* [nchildren] (1 << 32 | items) for non-empty children */
 };
 
-struct HmCompactOut {
-    uint32_t* nkeys;
-    uint32_t* nruns;
-    uint32_t* rbase;
-    uint32_t* keybase;
-    uint32_t* item_begin;
-    uint32_t* digit;
-    uint64_t* coord;
-};
 
 struct HmCompactArgs {
     uint64_t nchildren;
@@ -241,6 +267,8 @@ void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int6
                        int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow);
 /* mode: 0 fast path + redo list, 1 tile input (exact row/col given), 2 fused exact (fallback) */
 void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool out16, int mode);
+void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist);
+void hm_launch_level1_buckets(hipStream_t s, const HmL1Args& a);
 struct HmRedoArgs {
     const double* lat;
     const double* lon;

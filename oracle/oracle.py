@@ -50,6 +50,10 @@ def lib():
                                 P(P(ctypes.c_int32)), P(P(ctypes.c_int64)), P(P(ctypes.c_int64)),
                                 P(P(ctypes.c_int64)), P(ctypes.c_int)]
         L.hmo_count.restype = ctypes.c_int
+        L.hmo_count_tiles.argtypes = [P(ctypes.c_int64), P(ctypes.c_int64), P(ctypes.c_uint8), ctypes.c_int64,
+                                      ctypes.c_int, ctypes.c_int, P(ctypes.c_int64), P(P(ctypes.c_int32)),
+                                      P(P(ctypes.c_int64)), P(P(ctypes.c_int64)), P(P(ctypes.c_int64))]
+        L.hmo_count_tiles.restype = ctypes.c_int
         L.hmo_free.argtypes = [ctypes.c_void_p]
         L.hmo_row.argtypes = [ctypes.c_double, ctypes.c_int, P(ctypes.c_int64)]
         L.hmo_col.argtypes = [ctypes.c_double, ctypes.c_int, P(ctypes.c_int64)]
@@ -97,40 +101,57 @@ def count(lat, lon, keep=None, zmin=0, zmax=18, threads=0):
                          ctypes.byref(err), ctypes.byref(nout), ctypes.byref(zo), ctypes.byref(ro),
                          ctypes.byref(co), ctypes.byref(no), ctypes.byref(used))
     out = {"status": st, "err_index": err.value, "threads": used.value}
-    m = nout.value
     if st == OK:
-        out["zoom"] = np.ctypeslib.as_array(zo, (max(m, 1),))[:m].copy()
-        out["row"] = np.ctypeslib.as_array(ro, (max(m, 1),))[:m].copy()
-        out["col"] = np.ctypeslib.as_array(co, (max(m, 1),))[:m].copy()
-        out["count"] = np.ctypeslib.as_array(no, (max(m, 1),))[:m].copy()
-        for p in (zo, ro, co, no):
-            lib().hmo_free(ctypes.cast(p, ctypes.c_void_p))
-        order = np.lexsort((out["col"], out["row"], out["zoom"]))
-        for k in ("zoom", "row", "col", "count"):
-            out[k] = out[k][order]
+        out.update(_collect(nout.value, zo, ro, co, no))
     return out
 
 
-def count_tiles(rows, cols, zmin, zmax):
+def _collect(m, zo, ro, co, no):
+    out = {}
+    out["zoom"] = np.ctypeslib.as_array(zo, (max(m, 1),))[:m].copy()
+    out["row"] = np.ctypeslib.as_array(ro, (max(m, 1),))[:m].copy()
+    out["col"] = np.ctypeslib.as_array(co, (max(m, 1),))[:m].copy()
+    out["count"] = np.ctypeslib.as_array(no, (max(m, 1),))[:m].copy()
+    for p in (zo, ro, co, no):
+        lib().hmo_free(ctypes.cast(p, ctypes.c_void_p))
+    z = out["zoom"]
+    if m == 0:
+        return out
+    # zooms come from zmax down, each (row, col)-sorted by the C code: put
+    # the zoom blocks in ascending order; re-sort only if a block is not sorted
+    cuts = np.flatnonzero(z[1:] != z[:-1]) + 1
+    blocks = np.split(np.arange(m), cuts)[::-1]
+    order = np.concatenate(blocks)
+    res = {k: v[order] for k, v in out.items()}
+    r, c, zz = res["row"], res["col"], res["zoom"]
+    same = zz[1:] == zz[:-1]
+    if np.any(same & ((r[1:] < r[:-1]) | ((r[1:] == r[:-1]) & (c[1:] <= c[:-1])))):
+        o = np.lexsort((c, r, zz))
+        res = {k: v[o] for k, v in res.items()}
+    return res
+
+
+def count_tiles(rows, cols, zmin, zmax, keep=None):
     """Per-zoom cell counts of zoom-zmax tiles (the hm_count_tiles contract),
     sorted by (zoom, row, col): the per-zoom reduceByKey of heatmap.py:109-111,
     with every coarser tile the arithmetic right shift of the zoom-zmax one
     (SURVEY a-4; any int64 tile, negative or past 2^zmax)."""
-    rows = np.asarray(rows, dtype=np.int64)
-    cols = np.asarray(cols, dtype=np.int64)
-    out = {k: [] for k in ("zoom", "row", "col", "count")}
-    for z in range(zmin, zmax + 1):
-        if rows.size == 0:
-            break
-        u, n = np.unique(np.stack([rows >> (zmax - z), cols >> (zmax - z)], 1), axis=0, return_counts=True)
-        out["zoom"].append(np.full(len(u), z, np.int32))
-        out["row"].append(u[:, 0])
-        out["col"].append(u[:, 1])
-        out["count"].append(n.astype(np.int64))
-    if not out["zoom"]:
-        return {"zoom": np.zeros(0, np.int32), "row": np.zeros(0, np.int64), "col": np.zeros(0, np.int64),
-                "count": np.zeros(0, np.int64)}
-    return {k: np.concatenate(v) for k, v in out.items()}
+    rows = np.ascontiguousarray(rows, dtype=np.int64)
+    cols = np.ascontiguousarray(cols, dtype=np.int64)
+    kp = None
+    if keep is not None:
+        keep = np.ascontiguousarray(keep, dtype=np.uint8)
+        kp = _p(keep, ctypes.c_uint8)
+    nout = ctypes.c_int64(0)
+    zo = ctypes.POINTER(ctypes.c_int32)()
+    ro = ctypes.POINTER(ctypes.c_int64)()
+    co = ctypes.POINTER(ctypes.c_int64)()
+    no = ctypes.POINTER(ctypes.c_int64)()
+    st = lib().hmo_count_tiles(_p(rows, ctypes.c_int64), _p(cols, ctypes.c_int64), kp, rows.size, zmin, zmax,
+                               ctypes.byref(nout), ctypes.byref(zo), ctypes.byref(ro), ctypes.byref(co),
+                               ctypes.byref(no))
+    assert st == OK
+    return _collect(nout.value, zo, ro, co, no)
 
 
 # --------------------------------------------------------------------------

@@ -53,3 +53,20 @@ def gpu():
 
     _lib.load()
     return torch
+
+
+def cells_digest(zoom, row, col, count):
+    """Order-free digest of a cell multiset: (cells, total count, sum and xor of
+    a 64-bit mix of each (zoom, row, col, count)).  Large comparisons use it
+    instead of sorting hundreds of millions of cells."""
+    import numpy as np
+
+    with np.errstate(over="ignore"):
+        x = (np.asarray(zoom, np.uint64) * np.uint64(0x9E3779B97F4A7C15)) ^ np.asarray(row).astype(np.uint64)
+        x = (x * np.uint64(0xBF58476D1CE4E5B9)) ^ np.asarray(col).astype(np.uint64)
+        x = (x * np.uint64(0x94D049BB133111EB)) ^ np.asarray(count).astype(np.uint64)
+        x ^= x >> np.uint64(31)
+        x *= np.uint64(0xD6E8FEB86659FD93)
+        x ^= x >> np.uint64(32)
+        return (int(x.size), int(np.asarray(count).sum()), int(x.sum(dtype=np.uint64)),
+                int(np.bitwise_xor.reduce(x)) if x.size else 0)

@@ -11,6 +11,7 @@ windows that drop some of the pyramid levels.  Expected counts: oracle.count_til
 import numpy as np
 import pytest
 
+from conftest import cells_digest
 from oracle import oracle
 from heatmap_amd import device
 
@@ -56,9 +57,14 @@ def _bucket_tiles(rng, Z, sizes, patterns):
 
 
 def _check(rows, cols, zmin, zmax):
-    got = device.count(rows, cols, None, zmin, zmax, tiles=True).sorted()
+    got = device.count(rows, cols, None, zmin, zmax, tiles=True)
     ref = oracle.count_tiles(rows, cols, zmin, zmax)
     assert got.zoom.size == ref["zoom"].size
+    if got.zoom.size > 4_000_000:   # order-free comparison of large outputs
+        assert cells_digest(got.zoom, got.row, got.col, got.count) == \
+            cells_digest(ref["zoom"], ref["row"], ref["col"], ref["count"])
+        return
+    got = got.sorted()
     for k in ("zoom", "row", "col", "count"):
         assert np.array_equal(getattr(got, k), ref[k]), k
 
@@ -82,7 +88,7 @@ def test_many_small_buckets(gpu):
     rng = np.random.default_rng(5)
     Z = 18
     side = 1 << (Z - 7)
-    nb = 100_000
+    nb = 50_000
     ids = rng.choice(side * side, size=nb, replace=False)
     sz = rng.integers(1, 600, nb)
     br = np.repeat(ids // side, sz)

@@ -88,15 +88,16 @@ def test_grouped_errors(gpu):
         device.count_grouped(lat, lon, np.zeros(lat.size, np.uint32), None, 0, 10)
 
 
-@pytest.mark.parametrize("n,zmin,zmax", [(1_000_000, 0, 21), (300_000, 12, 20)])
-def test_sparse_fallback_vs_oracle(gpu, n, zmin, zmax):
-    """Uniform clouds at zoom 20-21: the pipeline's dense per-level child space
+@pytest.mark.parametrize("n,zmin,zmax,fallback", [(1_000_000, 0, 21, True), (300_000, 12, 20, False)])
+def test_sparse_fallback_vs_oracle(gpu, n, zmin, zmax, fallback):
+    """Uniform 1M points at zoom 21: the pipeline's dense per-level child space
     would pass its limit, so hm_count takes the general path (in-square cells
-    still come back as HM_KEYs, exotic ones as records)."""
+    still come back as HM_KEYs, exotic ones as records); 300k at zoom 20 stays
+    on the pipeline."""
     lat, lon = synth.uniform(n, seed=11)
     lat, lon = lat.copy(), lon.copy()
     lat[::1000] = 88.5
     lon[1::1000] = 200.0
     got = device.count(lat, lon, None, zmin, zmax)
-    assert got.stage_us[0] == 0.0          # no pipeline stage ran
+    assert (got.stage_us[0] == 0.0) == fallback      # stage 0: the level-1 kernel
     _same(got.sorted(), oracle.count(lat, lon, None, zmin, zmax))
