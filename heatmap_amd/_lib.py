@@ -28,7 +28,8 @@ HM_ABI_VERSION = 2
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
            "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
-           "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_extract", "hm_stream_destroy"]
+           "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_extract", "hm_stream_destroy",
+           "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_dense_cells"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -87,6 +88,11 @@ def load() -> ctypes.CDLL:
         L.hm_stream_cells.argtypes = [vp, P(c.c_int64), P(c.c_int64)]
         L.hm_stream_extract.argtypes = [vp, c.c_int64, vp, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_stream_destroy.argtypes = [vp]
+        L.hm_dense_grid_size.argtypes = [c.c_int]
+        L.hm_dense_grid_size.restype = c.c_int64
+        L.hm_cells_route.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, vp, vp, vp, P(c.c_int64)]
+        L.hm_cells_merge.argtypes = [vp, vp, vp, c.c_int64, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_dense_cells.argtypes = [vp, vp, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
         for name in EXPORTS:
             getattr(L, name).restype = getattr(L, name).restype or c.c_int
         L.hm_status_string.restype = c.c_char_p

@@ -18,8 +18,8 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libheatmap_amd.so")
-SOURCES = ["hm_kernels.hip", "hm_general.hip", "hm_stream.hip", "hm_api.cpp"]
-HEADERS = ["hm_common.h", "hm_device.h", "hm_glibc_emul.h", "hm_project.h", "hm_pipeline.h", "hm_ytab.h"]
+SOURCES = ["hm_kernels.hip", "hm_general.hip", "hm_stream.hip", "hm_merge.hip", "hm_api.cpp"]
+HEADERS = ["hm_common.h", "hm_device.h", "hm_glibc_emul.h", "hm_project.h", "hm_pipeline.h", "hm_ytab.h", "hm_table.h"]
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=" + ARCH,
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unknown-pragmas",
@@ -35,9 +35,11 @@ def _stale() -> bool:
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force: bool = False, verbose: bool = True, out: str = None, defines=()) -> str:
-    """Compile the library (out/defines: tools/variants.py builds tuning variants)."""
+def build(force: bool = False, verbose: bool = True, out: str = None, defines=(), csrc: str = None) -> str:
+    """Compile the library (out/defines/csrc: tools/variants.py builds tuning
+    variants, from a patched copy of the sources for timing experiments)."""
     lib = out or LIB
+    src_dir = csrc or CSRC
     if not force and out is None and not _stale():
         return LIB
     os.makedirs(os.path.dirname(lib), exist_ok=True)
@@ -45,7 +47,7 @@ def build(force: bool = False, verbose: bool = True, out: str = None, defines=()
     objs = []
     for src in SOURCES:
         obj = os.path.join(os.path.dirname(lib), os.path.basename(lib) + "." + src.rsplit(".", 1)[0] + ".o")
-        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(CSRC, src), "-o", obj]
+        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(src_dir, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         subprocess.check_call(cmd)

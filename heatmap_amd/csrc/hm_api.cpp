@@ -95,6 +95,7 @@ enum {
     B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
+    B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE,
     B_COUNT
 };
 
@@ -1026,6 +1027,110 @@ extern "C" int hm_count_grouped_tiles(hm_ctx* ctx, const int64_t* row, const int
 {
     if (n > 0 && (!row || !col)) return HM_E_ARG;
     return grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+}
+
+/* ------------------------------------------------------------------------ */
+/* multi-GPU cell exchange (kernels in hm_merge.hip)                          */
+/* ------------------------------------------------------------------------ */
+
+extern "C" int64_t hm_dense_grid_size(int dense_zmax)
+{
+    if (dense_zmax < 0) return 0;
+    if (dense_zmax > 14) return -1;
+    return (int64_t)(((1ull << (2 * (dense_zmax + 1))) - 1) / 3);
+}
+
+extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks,
+                              int delta, int dense_zmax, uint64_t* grid, uint64_t* keys_out, uint64_t* counts_out,
+                              int64_t* send_counts)
+{
+    if (!ctx || n < 0 || nranks < 1 || nranks > 64 || delta < 0 || delta > 28 || dense_zmax > 14 ||
+        (dense_zmax >= 0 && !grid) || !send_counts || (n > 0 && (!keys || !counts || !keys_out || !counts_out)))
+        return HM_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t gsz = hm_dense_grid_size(dense_zmax);
+    if (gsz > 0) HIPCHK(hipMemsetAsync(grid, 0, (size_t)gsz * 8, s));
+    for (int r = 0; r < nranks; r++) send_counts[r] = 0;
+    if (n == 0) return HM_OK;
+    const unsigned blocks = hm_route_blocks((uint64_t)n);
+    const uint64_t m = (uint64_t)blocks * nranks;
+    HmRouteArgs a;
+    memset(&a, 0, sizeof(a));
+    ENSURE(B_RT_CNT, m * 8, a.block_cnt);
+    uint64_t* off;
+    ENSURE(B_RT_OFF, (m + 1) * 8, off);
+    uint64_t *partial, *tot;
+    ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+    ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+    a.keys = keys;
+    a.counts = counts;
+    a.n = (uint64_t)n;
+    a.nranks = nranks;
+    a.delta = delta;
+    a.dense_zmax = dense_zmax;
+    a.grid = grid;
+    a.block_off = off;
+    a.keys_out = keys_out;
+    a.counts_out = counts_out;
+    hm_launch_cells_route(s, a, false);
+    hm_launch_scan(s, a.block_cnt, m, partial, off, off + m);
+    hm_launch_cells_route(s, a, true);
+    HIPCHK(hipGetLastError());
+    std::vector<uint64_t> h(m + 1);
+    HIPCHK(hipMemcpyAsync(h.data(), off, (m + 1) * 8, hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int r = 0; r < nranks; r++)
+        send_counts[r] = (int64_t)(h[(uint64_t)(r + 1) * blocks] - h[(uint64_t)r * blocks]);
+    return HM_OK;
+}
+
+extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
+                              uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+{
+    if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && (!keys || !counts)) ||
+        (capacity > 0 && (!keys_out || !counts_out)))
+        return HM_E_ARG;
+    *n_out = 0;
+    if (n == 0) return HM_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    uint64_t cap = 1024;
+    while (cap < 2 * (uint64_t)n) cap <<= 1;
+    HmsTable t;
+    ENSURE(B_MG_TABLE, cap * 16, t.slots);
+    ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), t.state);
+    t.mask = cap - 1;
+    HIPCHK(hipMemsetAsync(t.state, 0, 8 * sizeof(unsigned long long), s));
+    hm_launch_stream_init(s, t);
+    hm_launch_cells_merge(s, keys, counts, (uint64_t)n, t);
+    hm_launch_table_extract(s, t, keys_out, counts_out, (uint64_t)capacity, t.state + HMS_ST_CURSOR);
+    HIPCHK(hipGetLastError());
+    unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+    HIPCHK(hipMemcpyAsync(down, t.state, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;   /* cannot happen: load factor <= 1/2 */
+    *n_out = (int64_t)down[HMS_ST_CURSOR];
+    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+}
+
+extern "C" int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out,
+                              uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+{
+    if (!ctx || !n_out || !grid || dense_zmax < 0 || dense_zmax > 14 || capacity < 0 ||
+        (capacity > 0 && (!keys_out || !counts_out)))
+        return HM_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    unsigned long long* cur = ctx->state + ST_CURSOR;
+    HIPCHK(hipMemsetAsync(cur, 0, 8, s));
+    hm_launch_dense_extract(s, grid, (uint64_t)hm_dense_grid_size(dense_zmax), dense_zmax, keys_out, counts_out,
+                            (uint64_t)capacity, cur);
+    HIPCHK(hipGetLastError());
+    int st = read_state(ctx);
+    if (st) return st;
+    *n_out = (int64_t)ctx->host_state[ST_CURSOR];
+    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
 }
 
 extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,

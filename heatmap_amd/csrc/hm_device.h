@@ -112,37 +112,6 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
  * spare words at the end of the same array (an index select, not a pointer
  * select, and non-short-circuit logic: either of those makes the compiler
  * emit exec-mask branches). */
-#ifdef HM_OLD_LDS
-__device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t, uint32_t key, bool valid)
-{
-    const uint64_t vm = __ballot(valid);
-    if (vm == 0) return;
-    const int leader = __ffsll((unsigned long long)vm) - 1;
-    const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
-    if (__ballot(valid && key == kl) == vm) {
-        if (hm_lane() == leader) atomicAdd(&hist[kl], (uint32_t)__popcll(vm));
-    } else if (valid) {
-        atomicAdd(&hist[key], 1u);
-    }
-}
-
-__device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t, uint32_t key, bool valid)
-{
-    const uint64_t vm = __ballot(valid);
-    if (vm == 0) return 0;
-    const int leader = __ffsll((unsigned long long)vm) - 1;
-    const uint32_t kl = __builtin_amdgcn_readlane(key, leader);
-    uint32_t pos = 0;
-    if (__ballot(valid && key == kl) == vm) {
-        uint32_t base = 0;
-        if (hm_lane() == leader) base = atomicAdd(&cur[kl], (uint32_t)__popcll(vm));
-        pos = __builtin_amdgcn_readlane(base, leader) + hm_mbcnt(vm);
-    } else if (valid) {
-        pos = atomicAdd(&cur[key], 1u);
-    }
-    return pos;
-}
-#else
 __device__ __forceinline__ void hm_lds_count(uint32_t* hist, uint32_t dummy, uint32_t key, bool valid)
 {
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
@@ -170,7 +139,74 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t dummy, 
     const uint32_t base = __builtin_amdgcn_readlane(old, m ? __ffsll((unsigned long long)m) - 1 : 0);
     return same ? base + r : old;
 }
+
+/* Multi-round wave aggregation for LDS histograms and slot claims.  Round r
+ * takes the first lane not yet grouped, and every lane holding its key joins
+ * that group; after HM_MERGE_ROUNDS rounds the remaining lanes go alone.  The
+ * grouping needs only the keys (ballots, readlane), so a claim still costs ONE
+ * atomic instruction per key for the whole wave: a group's first lane adds the
+ * group size, a lone lane adds 1, every other lane hits its private dummy word.
+ * Skewed keys (a few hot digits per wave: hotspot clouds) then cost no
+ * same-address serialisation, which single-round merging (lanes equal to the
+ * first lane only) left to the 2nd, 3rd ... hottest digit. */
+#ifndef HM_MERGE_ROUNDS
+#define HM_MERGE_ROUNDS 1
 #endif
+struct HmMerge {
+    uint64_t m[HM_MERGE_ROUNDS];
+    int l[HM_MERGE_ROUNDS];
+    uint32_t idx, inc;
+};
+
+__device__ __forceinline__ HmMerge hm_merge_prep(uint32_t key, bool valid, uint32_t dummy)
+{
+    HmMerge g;
+    uint64_t un = __ballot(valid);
+    const int lane = hm_lane();
+    uint32_t inc = 0;
+    bool lead = false;
+#pragma unroll
+    for (int r = 0; r < HM_MERGE_ROUNDS; r++) {
+        const int l = un ? __ffsll((unsigned long long)un) - 1 : 0;
+        const uint32_t kr = __builtin_amdgcn_readlane(key, l);
+        const uint64_t m = un & __ballot(key == kr);
+        g.m[r] = m;
+        g.l[r] = l;
+        const bool me = (lane == l) & (m != 0);
+        lead |= me;
+        inc = me ? (uint32_t)__popcll(m) : inc;
+        un &= ~m;
+    }
+    const bool own = valid & (((un >> lane) & 1ull) != 0);
+    g.idx = (lead | own) ? key : dummy + (uint32_t)lane;
+    g.inc = own ? 1u : inc;
+    return g;
+}
+
+/* position claimed by this lane, from the atomic's old value */
+__device__ __forceinline__ uint32_t hm_merge_pos(const HmMerge& g, uint32_t old)
+{
+    const int lane = hm_lane();
+    uint32_t pos = old;
+#pragma unroll
+    for (int r = 0; r < HM_MERGE_ROUNDS; r++) {
+        const uint32_t b = __builtin_amdgcn_readlane(old, g.l[r]);
+        pos = ((g.m[r] >> lane) & 1ull) ? b + hm_mbcnt(g.m[r]) : pos;
+    }
+    return pos;
+}
+
+__device__ __forceinline__ void hm_lds_count_m(uint32_t* hist, uint32_t dummy, uint32_t key, bool valid)
+{
+    const HmMerge g = hm_merge_prep(key, valid, dummy);
+    atomicAdd(&hist[g.idx], g.inc);
+}
+
+__device__ __forceinline__ uint32_t hm_lds_claim_m(uint32_t* cur, uint32_t dummy, uint32_t key, bool valid)
+{
+    const HmMerge g = hm_merge_prep(key, valid, dummy);
+    return hm_merge_pos(g, atomicAdd(&cur[g.idx], g.inc));
+}
 
 /* LDS slot of cell (r, c) = (r << w) | c of a row-major 2^w x 2^w histogram:
  * the column is rotated by 8 r, so a 2-D cluster of cells spreads over more

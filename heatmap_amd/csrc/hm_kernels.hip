@@ -190,6 +190,17 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             lo[k] = make_double2(0.0, 0.0);
         }
     }
+    /* this thread's digits' region slots, capacities and bases (small, L2-hot
+     * tables), fetched while the point loads are in flight */
+    constexpr int PERD = HM_MAX_F1 / HM_P1_THREADS;
+    uint32_t slot[PERD], rcap[PERD], rbase[PERD];
+#pragma unroll
+    for (int q = 0; q < PERD; q++) {
+        const int d = tid * PERD + q;
+        slot[q] = d < F ? hm_l1_slot(a, d) : 0u;
+        rcap[q] = d < F ? a.rcap[slot[q]] : 0u;
+        rbase[q] = d < F ? a.rbase[slot[q]] : 0u;
+    }
     /* LDS set-up after the loads are issued: the table's latency overlaps theirs */
     for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
     if (!FROM_TILES) hm_load_ytab(tab);
@@ -287,33 +298,32 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu);
+    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count_m(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu);
     __syncthreads();
 
-    /* exclusive scan of the digit histogram */
+    /* reserve each digit's keys in its region (one returning atomic per
+     * non-empty digit), issued as soon as the histogram is known; the results
+     * are consumed only after the scan and the claim below, so the atomic
+     * latency hides behind LDS work */
     constexpr int PER = HM_MAX_F1 / HM_P1_THREADS;
     uint32_t cnt[PER];
+    uint32_t gpos[PER];
     uint32_t s = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
         cnt[q] = d < F ? cur[hm_cur_slot(d, wd)] : 0u;
+        gpos[q] = 0;
+        if (d < F && cnt[q]) gpos[q] = atomicAdd(&a.fill[slot[q]], cnt[q]);
         s += cnt[q];
     }
+    /* exclusive scan of the digit histogram */
     uint32_t total;
     uint32_t off = hm_block_excl_scan<HM_P1_THREADS>(s, scr, &total);
-    /* reserve each digit's keys in its region (one returning atomic per
-     * non-empty digit); every atomic is issued before any result is used, and
-     * the results are consumed only after the claim below, so the tile pays
-     * about one atomic latency and hides it behind LDS work */
-    uint32_t gpos[PER];
     uint32_t offq[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
         offq[q] = off;
-        gpos[q] = 0;
-        if (d < F && cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1_slot(a, d)], cnt[q]);
         off += cnt[q];
     }
 #pragma unroll
@@ -322,11 +332,20 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (d < F) cur[hm_cur_slot(d, wd)] = offq[q];
     }
     __syncthreads();
+    {
+        /* every slot atomic issued before any result is consumed */
+        uint32_t old[HM_P1_PPT];
+        HmMerge g[HM_P1_PPT];
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT; k++) {
-        const bool v = dig[k] != 0xFFFFFFFFu;
-        const uint32_t pos = hm_lds_claim(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), v);
-        stage[v ? pos : HM_T1 + hm_lane()] = (OutT)rest[k];
+        for (int k = 0; k < HM_P1_PPT; k++) {
+            g[k] = hm_merge_prep(hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu, HM_MAX_F1);
+            old[k] = atomicAdd(&cur[g[k].idx], g[k].inc);
+        }
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT; k++) {
+            const bool v = dig[k] != 0xFFFFFFFFu;
+            stage[v ? hm_merge_pos(g[k], old[k]) : HM_T1 + hm_lane()] = (OutT)rest[k];
+        }
     }
     /* copy pieces: digit d's staged keys [offq, offq + cnt) go to region
      * position rbase[d] + gpos, cut into pieces of <= HM_P1_PIECE keys that the
@@ -338,7 +357,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        const bool fits = d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)a.rcap[hm_l1_slot(a, d)];
+        const bool fits = d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q];
         over |= d < F && cnt[q] && !fits;
         np += fits ? (cnt[q] + HM_P1_PIECE - 1) / HM_P1_PIECE : 0u;
     }
@@ -348,8 +367,8 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)a.rcap[hm_l1_slot(a, d)]) {
-            const uint32_t g = a.rbase[hm_l1_slot(a, d)] + gpos[q];
+        if (d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q]) {
+            const uint32_t g = rbase[q] + gpos[q];
             for (uint32_t o = 0; o < cnt[q]; o += HM_P1_PIECE) {
                 psrc[pq] = (offq[q] + o) | ((min(cnt[q] - o, (uint32_t)HM_P1_PIECE) - 1) << 16);
                 pdst[pq] = g + o;
@@ -690,11 +709,7 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
                     x[u] = make_uint4(0, 0, 0, 0);
                     if (ok[u]) {
                         while (L.pre[r + 1] <= v) r++;
-#ifdef HM_EXP_NOLOAD
-                        x[u] = make_uint4(v, v * 3u, v * 5u, v * 7u);   /* timing experiment only */
-#else
                         x[u] = kv[L.bv[r] + (v - L.pre[r])];
-#endif
                     }
                 }
 #pragma unroll
@@ -794,25 +809,16 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t pos)
         {
             const uint32_t x = pack(k);
-            hm_lds_count(cur, dummy, hm_cur_slot(x >> (2 * s), w), v);
+            hm_lds_count_m(cur, dummy, hm_cur_slot(x >> (2 * s), w), v);
             stage[v ? pos : HM_TN + hm_lane()] = x;
         }
         __device__ __forceinline__ void vec(const uint4& k, bool v, uint32_t pos)
         {
-#ifdef HM_EXP_NOCONFLICT
-            /* timing experiment only: digit's low 6 bits replaced by the lane id */
-            const uint32_t sm = 2 * s, lm = ((uint32_t)hm_lane()) << sm, hm = ~(63u << sm);
-            const uint4 x = make_uint4((pack(k.x) & hm) | lm, (pack(k.y) & hm) | lm, (pack(k.z) & hm) | lm,
-                                       (pack(k.w) & hm) | lm);
-#else
             const uint4 x = make_uint4(pack(k.x), pack(k.y), pack(k.z), pack(k.w));
-#endif
-#ifndef HM_EXP_NOCOUNT
-            hm_lds_count(cur, dummy, hm_cur_slot(x.x >> (2 * s), w), v);
-            hm_lds_count(cur, dummy, hm_cur_slot(x.y >> (2 * s), w), v);
-            hm_lds_count(cur, dummy, hm_cur_slot(x.z >> (2 * s), w), v);
-            hm_lds_count(cur, dummy, hm_cur_slot(x.w >> (2 * s), w), v);
-#endif
+            hm_lds_count_m(cur, dummy, hm_cur_slot(x.x >> (2 * s), w), v);
+            hm_lds_count_m(cur, dummy, hm_cur_slot(x.y >> (2 * s), w), v);
+            hm_lds_count_m(cur, dummy, hm_cur_slot(x.z >> (2 * s), w), v);
+            hm_lds_count_m(cur, dummy, hm_cur_slot(x.w >> (2 * s), w), v);
             *(uint4*)&stage[v ? pos : HM_TN] = x;
         }
     } f{cur, HM_MAX_FN, stage, sw, ww, sp};
@@ -844,12 +850,8 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         const int d = tid * PER + q;
         offq[q] = off;
         idx[q] = 0;
-#ifdef HM_EXP_NOATOM
-        idx[q] = it.j >> a.shard_bits;   /* timing experiment only: counters stay 0 */
-#else
         if (d < F && cnt[q])
             idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
-#endif
         off += cnt[q];
     }
 #pragma unroll
@@ -870,29 +872,18 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     /* claim: every slot atomic issued before any result is consumed (the
      * helper's logic of hm_lds_claim, unrolled over the KPT keys) */
     {
-        uint32_t old[KPT], rk[KPT];
-        uint64_t mk[KPT];
-        bool same[KPT], v[KPT];
+        uint32_t old[KPT];
+        HmMerge g[KPT];
+        bool v[KPT];
 #pragma unroll
         for (int k = 0; k < KPT; k++) {
             v[k] = k * HM_PN_THREADS + tid < total;
-            const uint32_t d = hm_cur_slot(kv[k] >> a.restbits, ww);
-            const uint32_t k0 = __builtin_amdgcn_readfirstlane(d);
-            same[k] = v[k] & (d == k0);
-            mk[k] = __ballot(same[k]);
-            rk[k] = hm_mbcnt(mk[k]);
-            const bool lead = same[k] & (rk[k] == 0);
-            const bool own = v[k] & !same[k];
-            const uint32_t ci = lead ? k0 : (own ? d : HM_MAX_FN + (uint32_t)hm_lane());
-            old[k] = atomicAdd(&cur[ci], lead ? (uint32_t)__popcll(mk[k]) : (uint32_t)own);
+            g[k] = hm_merge_prep(hm_cur_slot(kv[k] >> a.restbits, ww), v[k], HM_MAX_FN);
+            old[k] = atomicAdd(&cur[g[k].idx], g[k].inc);
         }
 #pragma unroll
-        for (int k = 0; k < KPT; k++) {
-            const uint32_t base =
-                __builtin_amdgcn_readlane(old[k], mk[k] ? __ffsll((unsigned long long)mk[k]) - 1 : 0);
-            const uint32_t pos = same[k] ? base + rk[k] : old[k];
-            so[v[k] ? pos : HM_TN + tid % 64] = (OutT)(kv[k] & restmask);
-        }
+        for (int k = 0; k < KPT; k++)
+            so[v[k] ? hm_merge_pos(g[k], old[k]) : HM_TN + tid % 64] = (OutT)(kv[k] & restmask);
     }
     __syncthreads();
     HM_STAMP(10);
@@ -1485,17 +1476,10 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
         uint32_t cnt = 0;
 #pragma unroll
         for (int m = 0; m < KPT; m++) cnt += __popc(own[m] & zmask);
-#ifdef HM_EXP_SPNOEMIT
-        cnt = 0;   /* timing experiment only */
-#endif
         uint32_t tot;
         uint32_t pos = hm_block_excl_scan<HM_SP_THREADS>(cnt, scr, &tot);
         if (tot) {
-#ifdef HM_EXP_SPNOATOM
-            if (tid == 0) sbase = ((uint64_t)b * 1024u) % (a.out.capacity > 16384 ? a.out.capacity - 16384 : 1);
-#else
             if (tid == 0) sbase = atomicAdd(a.out.cursor, (unsigned long long)tot);
-#endif
             __syncthreads();
             const uint64_t base = sbase;
             const uint64_t coord = a.B.coord[b];

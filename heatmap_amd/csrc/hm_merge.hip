@@ -1,0 +1,209 @@
+/* gfx950 kernels of the multi-GPU cell exchange (heatmap_amd/multigpu.py).
+ *
+ * The reference's only data exchange is Spark's two shuffles per level:
+ * reduceByKey (heatmap.py:111) sums the counts of a cell key, groupByKey
+ * (heatmap.py:112) collects a heatmap row's bins on one executor.  Across GPUs
+ * every rank counts its shard with hm_count, then:
+ *   k_cells_route     per cell: zooms <= dense_zmax are added into a dense
+ *                     Morton-ordered u64 grid (zoom z at offset (4^z - 1)/3;
+ *                     summed across ranks by one RCCL reduce); sparser zooms
+ *                     are routed to the rank that owns their heatmap row
+ *                     (zoom, row >> delta, col >> delta): the groupByKey key,
+ *                     so a row's bins meet on one rank.  Block-local owner
+ *                     histograms reserve each block's output with one atomic
+ *                     per owner; the cells then land grouped by owner, ready
+ *                     for one RCCL all-to-all.
+ *   k_cells_merge     received cells -> device hash table (hm_table.h):
+ *                     equal keys from several ranks sum their counts;
+ *   k_table_extract   the table's occupied slots -> (key, count) lists;
+ *   k_dense_extract   the reduced dense grid -> non-empty cells (root rank).
+ */
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "hm_device.h"
+#include "hm_pipeline.h"
+#include "hm_table.h"
+
+#define HM_ROUTE_THREADS 256
+#define HM_MAX_RANKS 64
+
+/* owner rank of a cell: multiplicative hash of its heatmap-row key */
+__device__ __forceinline__ uint32_t hm_owner(uint64_t key, int delta, int nranks)
+{
+    const int64_t z = (int64_t)(key >> 58);
+    const int64_t r = (int64_t)((key >> 29) & 0x1FFFFFFFull), c = (int64_t)(key & 0x1FFFFFFFull);
+    const int64_t rk = (z << 48) ^ ((r >> delta) << 24) ^ (c >> delta);
+    const int64_t h = (int64_t)((uint64_t)rk * 0x9E3779B97F4A7C15ull) >> 33;   /* wrapping multiply */
+    const int64_t m = h % nranks;
+    return (uint32_t)(m < 0 ? m + nranks : m);
+}
+
+__device__ __forceinline__ uint64_t hm_spread29(uint64_t v)
+{
+    v &= 0xFFFFFFFFull;
+    v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+    v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v << 2)) & 0x3333333333333333ull;
+    return (v | (v << 1)) & 0x5555555555555555ull;
+}
+
+__device__ __forceinline__ uint64_t hm_compact29(uint64_t v)
+{
+    v &= 0x5555555555555555ull;
+    v = (v | (v >> 1)) & 0x3333333333333333ull;
+    v = (v | (v >> 2)) & 0x0F0F0F0F0F0F0F0Full;
+    v = (v | (v >> 4)) & 0x00FF00FF00FF00FFull;
+    v = (v | (v >> 8)) & 0x0000FFFF0000FFFFull;
+    return (v | (v >> 16)) & 0x00000000FFFFFFFFull;
+}
+
+/* pass 1 (count) / pass 2 (scatter) over the same block-contiguous cells:
+ * both passes see identical per-block owner counts, so pass 1's block totals,
+ * scanned owner-major, are pass 2's reservations (slots inside a block's
+ * reservation are claimed with LDS atomics, any order) */
+template <bool SCATTER>
+__global__ __launch_bounds__(HM_ROUTE_THREADS) void k_cells_route(HmRouteArgs a)
+{
+    __shared__ uint32_t hist[HM_MAX_RANKS + 64];   /* + 64 dummy words (hm_lds_claim) */
+    __shared__ uint64_t base[HM_MAX_RANKS];
+    const int tid = threadIdx.x;
+    if (tid < a.nranks) hist[tid] = 0;
+    if (SCATTER && tid < a.nranks) base[tid] = a.block_off[(uint64_t)tid * gridDim.x + blockIdx.x];
+    __syncthreads();
+    const uint64_t per = (a.n + gridDim.x - 1) / gridDim.x;
+    const uint64_t b0 = (uint64_t)blockIdx.x * per, b1 = min(b0 + per, (uint64_t)a.n);
+    for (uint64_t i0 = b0; i0 < b1; i0 += HM_ROUTE_THREADS) {
+        const uint64_t i = i0 + tid;
+        const bool in = i < b1;
+        const uint64_t k = in ? a.keys[i] : 0ull;
+        const int z = (int)(k >> 58);
+        const bool dense = in && z <= a.dense_zmax;
+        if (!SCATTER && dense) {
+            const uint64_t r = (k >> 29) & 0x1FFFFFFFull, c = k & 0x1FFFFFFFull;
+            const uint64_t off = ((1ull << (2 * z)) - 1) / 3;
+            atomicAdd((unsigned long long*)&a.grid[off + ((hm_spread29(r) << 1) | hm_spread29(c))],
+                      (unsigned long long)a.counts[i]);
+        }
+        const bool sp = in && !dense;
+        const uint32_t o = sp ? hm_owner(k, a.delta, a.nranks) : 0u;
+        if (SCATTER) {
+            const uint32_t pos = hm_lds_claim(hist, HM_MAX_RANKS, o, sp);
+            if (sp) {
+                const uint64_t q = base[o] + pos;
+                a.keys_out[q] = k;
+                a.counts_out[q] = a.counts[i];
+            }
+        } else {
+            hm_lds_count(hist, HM_MAX_RANKS, o, sp);
+        }
+    }
+    __syncthreads();
+    if (!SCATTER && tid < a.nranks) a.block_cnt[(uint64_t)tid * gridDim.x + blockIdx.x] = hist[tid];
+}
+
+__global__ __launch_bounds__(256) void k_cells_merge(const uint64_t* __restrict__ keys,
+                                                     const uint64_t* __restrict__ counts, uint64_t n, HmsTable t)
+{
+    uint32_t overflow = 0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        hms_insert(t, keys[i], counts[i], &overflow);
+    const uint64_t of = hms_wave_sum(overflow);
+    if ((threadIdx.x & 63) == 0 && of) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)of);
+}
+
+/* occupied slots -> (key, count), one output reservation per wave and 64 slots */
+__global__ __launch_bounds__(256) void k_table_extract(HmsTable t, uint64_t* __restrict__ keys_out,
+                                                       uint64_t* __restrict__ counts_out, uint64_t cap,
+                                                       unsigned long long* cursor)
+{
+    const uint64_t n = t.mask + 1;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const ulonglong2* slots = (const ulonglong2*)t.slots;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; i0 < n; i0 += stride) {
+        const uint64_t i = i0 + lane;
+        const ulonglong2 sl = i < n ? slots[i] : make_ulonglong2(HMS_EMPTY, 0ull);
+        const bool m = sl.x != HMS_EMPTY;
+        const uint64_t bal = __ballot(m);
+        if (!bal) continue;
+        unsigned long long first = 0;
+        if (lane == 0) first = atomicAdd(cursor, (unsigned long long)__popcll(bal));
+        first = __shfl(first, 0, 64);
+        if (m) {
+            const uint64_t pos = first + hm_mbcnt(bal);
+            if (pos < cap) {
+                keys_out[pos] = sl.x;
+                counts_out[pos] = sl.y;
+            }
+        }
+    }
+}
+
+/* non-empty cells of the dense grid (zooms 0..dense_zmax) */
+__global__ __launch_bounds__(256) void k_dense_extract(const uint64_t* __restrict__ grid, uint64_t total,
+                                                       int dense_zmax, uint64_t* __restrict__ keys_out,
+                                                       uint64_t* __restrict__ counts_out, uint64_t cap,
+                                                       unsigned long long* cursor)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; i0 < total; i0 += stride) {
+        const uint64_t i = i0 + lane;
+        const uint64_t v = i < total ? grid[i] : 0ull;
+        const uint64_t bal = __ballot(v != 0);
+        if (!bal) continue;
+        unsigned long long first = 0;
+        if (lane == 0) first = atomicAdd(cursor, (unsigned long long)__popcll(bal));
+        first = __shfl(first, 0, 64);
+        if (v) {
+            int z = 0;
+            while (z < dense_zmax && i >= (((1ull << (2 * (z + 1))) - 1) / 3)) z++;
+            const uint64_t m = i - ((1ull << (2 * z)) - 1) / 3;
+            const uint64_t pos = first + hm_mbcnt(bal);
+            if (pos < cap) {
+                keys_out[pos] = ((uint64_t)z << 58) | (hm_compact29(m >> 1) << 29) | hm_compact29(m);
+                counts_out[pos] = v;
+            }
+        }
+    }
+}
+
+static unsigned hm_mgrid(uint64_t n, unsigned cap)
+{
+    uint64_t b = (n + 255) / 256;
+    if (b > cap) b = cap;
+    return (unsigned)(b ? b : 1);
+}
+
+unsigned hm_route_blocks(uint64_t n) { return hm_mgrid(n, 1024); }
+
+void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter)
+{
+    const unsigned g = hm_route_blocks(a.n);
+    if (scatter)
+        hipLaunchKernelGGL(k_cells_route<true>, dim3(g), dim3(HM_ROUTE_THREADS), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_cells_route<false>, dim3(g), dim3(HM_ROUTE_THREADS), 0, s, a);
+}
+
+void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t)
+{
+    if (n) hipLaunchKernelGGL(k_cells_merge, dim3(hm_mgrid(n, 8192)), dim3(256), 0, s, keys, counts, n, t);
+}
+
+void hm_launch_table_extract(hipStream_t s, const HmsTable& t, uint64_t* keys_out, uint64_t* counts_out, uint64_t cap,
+                             unsigned long long* cursor)
+{
+    hipLaunchKernelGGL(k_table_extract, dim3(hm_mgrid(t.mask + 1, 4096)), dim3(256), 0, s, t, keys_out, counts_out,
+                       cap, cursor);
+}
+
+void hm_launch_dense_extract(hipStream_t s, const uint64_t* grid, uint64_t total, int dense_zmax, uint64_t* keys_out,
+                             uint64_t* counts_out, uint64_t cap, unsigned long long* cursor)
+{
+    hipLaunchKernelGGL(k_dense_extract, dim3(hm_mgrid(total, 4096)), dim3(256), 0, s, grid, total, dense_zmax,
+                       keys_out, counts_out, cap, cursor);
+}

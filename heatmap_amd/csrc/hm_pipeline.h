@@ -371,3 +371,23 @@ void hm_launch_rle_scatter(hipStream_t s, const ulonglong2* keys, uint64_t n, in
                            const uint64_t* idx, const uint64_t* S, const uint64_t* c, ulonglong2* okey, uint64_t* oend);
 void hm_launch_rle_emit(hipStream_t s, const HmGenEmit& e, const ulonglong2* okey, const uint64_t* oend, uint64_t u,
                         int z, uint64_t* ocnt, uint64_t base, int emit);
+
+/* multi-GPU cell exchange (hm_merge.hip) */
+struct HmRouteArgs {
+    const uint64_t* keys;
+    const uint64_t* counts;
+    uint64_t n;
+    int nranks, delta, dense_zmax;
+    uint64_t* grid;            /* dense zooms 0..dense_zmax, Morton order per zoom */
+    uint64_t* block_cnt;       /* [nranks * blocks] pass 1 */
+    const uint64_t* block_off; /* [nranks * blocks] exclusive scan of block_cnt */
+    uint64_t* keys_out;
+    uint64_t* counts_out;
+};
+unsigned hm_route_blocks(uint64_t n);
+void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter);
+void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t);
+void hm_launch_table_extract(hipStream_t s, const HmsTable& t, uint64_t* keys_out, uint64_t* counts_out, uint64_t cap,
+                             unsigned long long* cursor);
+void hm_launch_dense_extract(hipStream_t s, const uint64_t* grid, uint64_t total, int dense_zmax, uint64_t* keys_out,
+                             uint64_t* counts_out, uint64_t cap, unsigned long long* cursor);

@@ -18,19 +18,7 @@
 #include <stdint.h>
 
 #include "hm_pipeline.h"
-
-#define HMS_EMPTY 0xFFFFFFFFFFFFFFFFull
-
-__device__ __forceinline__ uint64_t hms_hash(uint64_t k)
-{
-    /* 64-bit finaliser (MurmurHash3 fmix64) */
-    k ^= k >> 33;
-    k *= 0xFF51AFD7ED558CCDull;
-    k ^= k >> 33;
-    k *= 0xC4CEB9FE1A85EC53ull;
-    k ^= k >> 33;
-    return k;
-}
+#include "hm_table.h"
 
 /* hm_count key (zoom<<58 | row<<29 | col) -> 42-bit cell field of a table key */
 __device__ __forceinline__ uint64_t hms_pack(uint64_t k)
@@ -43,35 +31,6 @@ __device__ __forceinline__ uint64_t hms_unpack(uint64_t p)
 {
     const uint64_t z = (p >> 42) & 31ull, r = (p >> 21) & 0x1FFFFFull, c = p & 0x1FFFFFull;
     return (z << 58) | (r << 29) | c;
-}
-
-__device__ __forceinline__ uint64_t hms_wave_sum(uint64_t v)
-{
-    for (int o = 32; o > 0; o >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, o, 64);
-    return v;
-}
-
-/* Insert-or-add; returns 1 if this call claimed a new slot. */
-__device__ __forceinline__ uint32_t hms_insert(const HmsTable& t, uint64_t k, uint64_t c, uint32_t* overflow)
-{
-    uint64_t h = hms_hash(k) & t.mask;
-    for (uint64_t probe = 0; probe <= t.mask; probe++) {
-        uint64_t cur = __atomic_load_n(&t.slots[2 * h], __ATOMIC_RELAXED);
-        uint32_t claimed = 0;
-        if (cur == HMS_EMPTY) {
-            const unsigned long long prev =
-                atomicCAS((unsigned long long*)&t.slots[2 * h], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
-            claimed = prev == HMS_EMPTY;
-            cur = claimed ? k : prev;
-        }
-        if (cur == k) {
-            atomicAdd((unsigned long long*)&t.slots[2 * h + 1], (unsigned long long)c);
-            return claimed;
-        }
-        h = (h + 1) & t.mask;
-    }
-    *overflow = 1;
-    return 0;
 }
 
 /* Fold n cells (hm_count layout) into the table under tag_a and, if

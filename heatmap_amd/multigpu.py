@@ -5,116 +5,160 @@ Points shard by contiguous ranges; each rank bins its shard with hm_count
 the sum of per-cell counts -- what Spark's two shuffles compute in the
 reference (reduceByKey at heatmap.py:111, groupByKey at :112):
 
-  dense zooms 0..dense_zmax   every rank scatters its cells into one dense
-                              Morton-ordered u64 grid (sum 4^z cells, 11 MB at
-                              dense_zmax = 10) and the grids are summed with
-                              one all_reduce;
-  sparse zooms above it       cells are hash-partitioned by their heatmap row
-                              (zoom, row >> 5, col >> 5) -- the groupByKey key
-                              -- and exchanged with one all_to_all (counts
-                              first, then keys and counts); owners merge what
-                              they receive by sort + segmented sum.
+  dense zooms 0..dense_zmax   hm_cells_route adds every rank's cells into one
+                              dense Morton-ordered u64 grid (sum 4^z cells,
+                              11 MB at dense_zmax = 10) and ONE RCCL reduce
+                              sums the grids on rank 0, which owns those cells
+                              (u64: at config 3's 1e10 points the zoom-0..9
+                              cells pass 2^32);
+  sparse zooms above it       hm_cells_route groups the cells by the rank that
+                              owns their heatmap row (zoom, row >> 5, col >> 5)
+                              -- the groupByKey key -- one RCCL all-to-all of
+                              the group sizes, one of the keys and counts, and
+                              hm_cells_merge sums equal keys on the owner;
+  cells outside [0, 2^z)^2    (hm_count's records; rare) the same routing by
+                              heatmap row, done with torch ops.
 
-Every output cell, and every heatmap row, ends with exactly one owner rank:
-dense cells are kept by the rank the same row hash names.  torch.distributed
-is the plumbing ("nccl" = RCCL on ROCm; "gloo" in the CPU tests).
+Every output cell, and every heatmap row, ends with exactly one owner rank.
+torch.distributed is the plumbing ("nccl" = RCCL on ROCm; "gloo" in the CPU
+tests, which pass torch stand-ins for the three device operations).
 """
 from __future__ import annotations
+
+import ctypes
 
 import torch
 import torch.distributed as dist
 
 DELTA = 5
-_MASK29 = 0x1FFFFFFF
 
 
-def _split(keys: torch.Tensor):
-    return keys >> 58, (keys >> 29) & _MASK29, keys & _MASK29
+class DeviceOps:
+    """hm_cells_route / hm_cells_merge / hm_dense_cells on the device."""
+
+    def __init__(self, device: int = 0):
+        from . import device as _device
+
+        self.ctx = _device.context(device)
+        self.L = self.ctx.L
+
+    @staticmethod
+    def _p(t):
+        return ctypes.c_void_p(t.data_ptr()) if t is not None and t.numel() else ctypes.c_void_p(0)
+
+    def _check(self, rc):
+        from . import _lib
+
+        if rc != _lib.HM_OK:
+            _lib.raise_for(rc)
+
+    def route(self, keys, counts, ws, dense_zmax):
+        n = keys.numel()
+        gsz = int(self.L.hm_dense_grid_size(dense_zmax))
+        grid = torch.empty(max(gsz, 1), dtype=torch.int64, device=keys.device)
+        ko = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
+        co = torch.empty_like(ko)
+        send = (ctypes.c_int64 * ws)()
+        self._check(self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax,
+                                          self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko),
+                                          self._p(co), send))
+        sent = list(send)
+        m = sum(sent)
+        return grid[:gsz], ko[:m], co[:m], sent
+
+    def merge(self, keys, counts):
+        from . import _lib
+
+        n = keys.numel()
+        cap = max(n, 1)
+        ko = torch.empty(cap, dtype=torch.int64, device=keys.device)
+        co = torch.empty_like(ko)
+        nout = ctypes.c_int64(0)
+        rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), n, self._p(ko), self._p(co), cap,
+                                   ctypes.byref(nout))
+        if rc != _lib.HM_OK:
+            _lib.raise_for(rc)
+        return ko[:nout.value], co[:nout.value]
+
+    def dense_cells(self, grid, dense_zmax):
+        from . import _lib
+
+        cap = max(int((grid != 0).sum().item()), 1)
+        ko = torch.empty(cap, dtype=torch.int64, device=grid.device)
+        co = torch.empty_like(ko)
+        nout = ctypes.c_int64(0)
+        rc = self.L.hm_dense_cells(self.ctx.ptr, self._p(grid), dense_zmax, self._p(ko), self._p(co), cap,
+                                   ctypes.byref(nout))
+        if rc != _lib.HM_OK:
+            _lib.raise_for(rc)
+        return ko[:nout.value], co[:nout.value]
 
 
-def owner(keys: torch.Tensor, ws: int) -> torch.Tensor:
-    """Rank that owns each cell: multiplicative hash of its heatmap-row key."""
-    z, r, c = _split(keys)
+def record_owner(cells: torch.Tensor, ws: int) -> torch.Tensor:
+    """Owner rank of cells given as int64 records (zoom, row, col, count):
+    the same heatmap-row hash as hm_cells_route, on arithmetic shifts."""
+    z, r, c = cells[:, 0], cells[:, 1], cells[:, 2]
     rk = (z << 48) ^ ((r >> DELTA) << 24) ^ (c >> DELTA)
-    h = (rk * -7046029254386353131) >> 33          # wrapping int64 multiply
+    h = (rk * -7046029254386353131) >> 33          # wrapping int64 multiply (0x9E3779B97F4A7C15)
     return torch.remainder(h, ws)
 
 
-def _spread(v: torch.Tensor) -> torch.Tensor:
-    v = v & 0xFFFFFFFF
-    v = (v | (v << 16)) & 0x0000FFFF0000FFFF
-    v = (v | (v << 8)) & 0x00FF00FF00FF00FF
-    v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0F
-    v = (v | (v << 2)) & 0x3333333333333333
-    v = (v | (v << 1)) & 0x5555555555555555
-    return v
-
-
-def _compact(v: torch.Tensor) -> torch.Tensor:
-    v = v & 0x5555555555555555
-    v = (v | (v >> 1)) & 0x3333333333333333
-    v = (v | (v >> 2)) & 0x0F0F0F0F0F0F0F0F
-    v = (v | (v >> 4)) & 0x00FF00FF00FF00FF
-    v = (v | (v >> 8)) & 0x0000FFFF0000FFFF
-    v = (v | (v >> 16)) & 0x00000000FFFFFFFF
-    return v
-
-
-def _zoom_offsets(dz: int):
-    off, o = [], 0
-    for z in range(dz + 1):
-        off.append(o)
-        o += 1 << (2 * z)
-    return off, o
-
-
-def _dense_merge(keys, counts, dz, ws, rank):
-    off, total = _zoom_offsets(dz)
-    offt = torch.tensor(off, dtype=torch.int64, device=keys.device)
-    z, r, c = _split(keys)
-    idx = offt[z] + ((_spread(r) << 1) | _spread(c))
-    grid = torch.zeros(total, dtype=torch.int64, device=keys.device)
-    grid.index_add_(0, idx, counts)
-    dist.all_reduce(grid)
-    nz = torch.nonzero(grid).flatten()
-    zc = torch.bucketize(nz, offt, right=True) - 1
-    m = nz - offt[zc]
-    k = (zc << 58) | (_compact(m >> 1) << 29) | _compact(m)
-    mine = owner(k, ws) == rank
-    return k[mine], grid[nz][mine]
-
-
-def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10) -> int:
-    """Exchange and merge the first m cells of `buffers` (int64 keys/counts,
-    HM_KEY layout) in place; returns the number of cells this rank owns.
-    dense_zmax < 0 sends every zoom through the all-to-all."""
-    keys = buffers.keys[:m]
-    counts = buffers.counts[:m]
-    parts_k, parts_c = [], []
-    if dense_zmax >= 0:
-        zk = keys >> 58
-        dm = zk <= dense_zmax
-        dk, dc = _dense_merge(keys[dm], counts[dm], dense_zmax, ws, rank)
-        parts_k.append(dk)
-        parts_c.append(dc)
-        keys, counts = keys[~dm], counts[~dm]
-    own = owner(keys, ws)
-    order = torch.argsort(own)
-    keys = keys[order]
-    counts = counts[order]
-    send = torch.bincount(own, minlength=ws)
+def _exchange(rows: torch.Tensor, owner: torch.Tensor, ws: int) -> torch.Tensor:
+    """All-to-all of fixed-width int64 rows, grouped by owner rank."""
+    order = torch.argsort(owner, stable=True)
+    rows = rows[order]
+    send = torch.bincount(owner, minlength=ws)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)
     sl, rl = send.tolist(), recv.tolist()
+    w = rows.shape[1]
+    out = torch.empty(sum(rl) * w, dtype=rows.dtype, device=rows.device)
+    dist.all_to_all_single(out, rows.reshape(-1).contiguous(), [x * w for x in rl], [x * w for x in sl])
+    return out.reshape(-1, w)
+
+
+def merge_exotic(cells: torch.Tensor, ws: int, rank: int) -> torch.Tensor:
+    """Cells outside [0, 2^z)^2 as (zoom, row, col, count) records: routed to
+    their heatmap row's owner and summed there."""
+    got = _exchange(cells.reshape(-1, 4), record_owner(cells.reshape(-1, 4), ws), ws)
+    if got.shape[0] == 0:
+        return got
+    u, inv = torch.unique(got[:, :3], dim=0, return_inverse=True)
+    tot = torch.zeros(u.shape[0], dtype=torch.int64, device=got.device)
+    tot.index_add_(0, inv, got[:, 3])
+    return torch.cat([u, tot[:, None]], 1)
+
+
+def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=None) -> int:
+    """Exchange and merge the first m cells of `buffers` (int64 keys/counts,
+    HM_KEY layout; records of cells outside the square in buffers.xcells,
+    buffers.nx of them) in place; returns the number of in-square cells this
+    rank owns (buffers.nx becomes the owned exotic count).  dense_zmax < 0
+    sends every zoom through the all-to-all.  `ops`: the device operations
+    (DeviceOps), or stand-ins with the same contract (CPU tests)."""
+    if ops is None:
+        ops = DeviceOps(buffers.keys.device.index or 0)
+    keys = buffers.keys[:m]
+    counts = buffers.counts[:m]
+    grid, sk, sc, sent = ops.route(keys, counts, ws, dense_zmax)
+    if dense_zmax >= 0:
+        dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
+    send = torch.tensor(sent, dtype=torch.int64, device=keys.device)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    rl = recv.tolist()
     nk = torch.empty(sum(rl), dtype=torch.int64, device=keys.device)
     nc = torch.empty_like(nk)
-    dist.all_to_all_single(nk, keys, rl, sl)
-    dist.all_to_all_single(nc, counts, rl, sl)
-    uk, inv = torch.unique(nk, sorted=True, return_inverse=True)
-    tot = torch.zeros(uk.numel(), dtype=torch.int64, device=keys.device)
-    tot.index_add_(0, inv, nc)
+    dist.all_to_all_single(nk, sk, rl, sent)
+    dist.all_to_all_single(nc, sc, rl, sent)
+    parts_k, parts_c = [], []
+    uk, uc = ops.merge(nk, nc)
     parts_k.append(uk)
-    parts_c.append(tot)
+    parts_c.append(uc)
+    if dense_zmax >= 0 and rank == 0:
+        dk, dc = ops.dense_cells(grid, dense_zmax)
+        parts_k.append(dk)
+        parts_c.append(dc)
     k = torch.cat(parts_k)
     c = torch.cat(parts_c)
     n = k.numel()
@@ -122,4 +166,13 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10) -> in
         raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (n, buffers.keys.numel()))
     buffers.keys[:n] = k
     buffers.counts[:n] = c
+    nx = int(getattr(buffers, "nx", 0))
+    nx_all = torch.tensor([nx], dtype=torch.int64, device=keys.device)
+    dist.all_reduce(nx_all)
+    if int(nx_all.item()):
+        x = merge_exotic(buffers.xcells[:4 * nx], ws, rank)
+        if x.numel() > buffers.xcells.numel():
+            buffers.xcells = torch.empty(x.numel(), dtype=torch.int64, device=keys.device)
+        buffers.xcells[:x.numel()] = x.reshape(-1)
+        buffers.nx = x.shape[0]
     return n

@@ -2,7 +2,7 @@
 
 Every generator here uses only IEEE add/multiply on doubles derived from a
 splitmix64 counter stream, so numpy, the C oracle and the HIP generator
-kernel (csrc/hm_synth.hip) produce bit-identical coordinates for the same
+kernel (k_synth in csrc/hm_kernels.hip) produce bit-identical coordinates for the same
 (seed, index).  That lets a GPU box regenerate a 1e9-point cloud in HBM and
 still check it against host-side fixtures.
 

@@ -177,6 +177,28 @@ int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out, uint64_t* 
                       int64_t capacity, int64_t* n_out);
 int hm_stream_destroy(hm_stream* s);
 
+/* Multi-GPU exchange of hm_count cells (one process per GPU; the collectives
+ * are RCCL calls made by the caller, heatmap_amd/multigpu.py).  They replace
+ * the reference's two shuffles, reduceByKey (heatmap.py:111) and groupByKey
+ * (heatmap.py:112):
+ *   hm_cells_route   cells of zoom <= dense_zmax are summed into grid (device
+ *                    u64[hm_dense_grid_size(dense_zmax)], Morton order per zoom,
+ *                    zeroed here; -1 = none) for an RCCL reduce; the others go
+ *                    to keys_out/counts_out (n entries) grouped by owner rank
+ *                    (a hash of the heatmap row key (zoom, row >> delta,
+ *                    col >> delta), so each output row has one owner);
+ *                    send_counts (host int64[nranks]) receives the group sizes
+ *                    for an RCCL all-to-all.  nranks <= 64.
+ *   hm_cells_merge   sum the counts of equal keys over n received cells.
+ *   hm_dense_cells   the non-empty cells of a (reduced) dense grid. */
+int64_t hm_dense_grid_size(int dense_zmax);
+int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks, int delta,
+                   int dense_zmax, uint64_t* grid, uint64_t* keys_out, uint64_t* counts_out, int64_t* send_counts);
+int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, uint64_t* keys_out,
+                   uint64_t* counts_out, int64_t capacity, int64_t* n_out);
+int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out, uint64_t* counts_out,
+                   int64_t capacity, int64_t* n_out);
+
 /* Benchmark/test utility, not part of the reference boundary: fill lat/lon
  * (device) with points start..start+n-1 of a synthetic cloud, bit-identical
  * to heatmap_amd/synth.py.  kind: 0 uniform, 1 hotspots (table = device

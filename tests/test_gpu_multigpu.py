@@ -1,0 +1,88 @@
+"""GPU: the multi-GPU exchange on the device (hm_merge.hip) and the RCCL path.
+
+- hm_cells_route / hm_cells_merge / hm_dense_cells against the CPU stand-ins of
+  tests/test_multigpu_gloo.py (the same contract: dense zooms summed into the
+  Morton grid, sparse cells grouped by heatmap-row owner, equal keys summed);
+- merge_cells over a real RCCL ("nccl") process group of world size 1: the
+  reduce and the all-to-alls run on the GPU, and the merged cells equal one
+  hm_count over the same points.  (8-GPU runs are the driver's; ranks cannot
+  share one GPU under RCCL.)"""
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+
+from heatmap_amd import device, multigpu, synth
+from test_multigpu_gloo import TorchOps
+
+pytestmark = pytest.mark.gpu
+
+
+def _cells(n, seed):
+    lat, lon = synth.generate("hotspots", n, seed=seed)
+    c = device.count(lat, lon, None, 0, 18)
+    keys = (c.zoom.astype(np.int64) << 58) | (c.row << 29) | c.col
+    return torch.from_numpy(keys), torch.from_numpy(c.count)
+
+
+@pytest.mark.parametrize("ws,dz", [(1, 10), (5, 8), (8, -1), (64, 4)])
+def test_route_kernel_contract(gpu, ws, dz):
+    keys, counts = _cells(300_000, ws)
+    ops = multigpu.DeviceOps(0)
+    g, sk, sc, sent = ops.route(keys.cuda(), counts.cuda(), ws, dz)
+    rg, rk, rc, rsent = TorchOps.route(keys, counts, ws, dz)
+    assert sent == rsent
+    assert torch.equal(g.cpu(), rg)
+    sk, sc = sk.cpu(), sc.cpu()
+    at = 0
+    for n in sent:                         # same cells per owner (order inside a group is free)
+        a = torch.argsort(sk[at:at + n])
+        b = torch.argsort(rk[at:at + n])
+        assert torch.equal(sk[at:at + n][a], rk[at:at + n][b])
+        assert torch.equal(sc[at:at + n][a], rc[at:at + n][b])
+        at += n
+    if dz >= 0:
+        dk, dc = ops.dense_cells(g, dz)
+        ek, ec = TorchOps.dense_cells(rg, dz)
+        o, eo = torch.argsort(dk.cpu()), torch.argsort(ek)
+        assert torch.equal(dk.cpu()[o], ek[eo]) and torch.equal(dc.cpu()[o], ec[eo])
+
+
+def test_merge_kernel_sums_duplicates(gpu):
+    keys, counts = _cells(200_000, 3)
+    k = torch.cat([keys, keys[::3], keys[::7]])
+    c = torch.cat([counts, counts[::3] * 2, counts[::7] + 5])
+    p = torch.randperm(k.numel(), generator=torch.Generator().manual_seed(1))
+    uk, uc = multigpu.DeviceOps(0).merge(k[p].cuda(), c[p].cuda())
+    ek, ec = TorchOps.merge(k, c)
+    o = torch.argsort(uk.cpu())
+    assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
+
+
+@pytest.fixture(scope="module")
+def nccl_world():
+    store = dist.HashStore()
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1)
+    yield
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("dz", [-1, 8, 10])
+def test_merge_cells_over_rccl(gpu, nccl_world, dz):
+    n = 2_000_000
+    lat, lon = synth.generate("hotspots", n, seed=dz + 2)
+    lat, lon = lat.copy(), lon.copy()
+    lat[::9973] = 88.5                      # cells outside the square travel as records
+    ref = device.count(lat, lon, None, 0, 18).sorted()
+    m, bufs = device.count_device(torch.from_numpy(lat).cuda(), torch.from_numpy(lon).cuda(), None, 0, 18)
+    m = multigpu.merge_cells(bufs, m, 1, 0, dense_zmax=dz)
+    k = bufs.keys[:m].cpu().numpy().view(np.uint64)
+    z = (k >> np.uint64(58)).astype(np.int32)
+    r = ((k >> np.uint64(29)) & np.uint64(0x1FFFFFFF)).astype(np.int64)
+    c = (k & np.uint64(0x1FFFFFFF)).astype(np.int64)
+    x = bufs.xcells[:4 * bufs.nx].cpu().numpy().reshape(-1, 4)
+    got = device.Counts(np.concatenate([z, x[:, 0].astype(np.int32)]), np.concatenate([r, x[:, 1]]),
+                        np.concatenate([c, x[:, 2]]), np.concatenate([bufs.counts[:m].cpu().numpy(), x[:, 3]]),
+                        0, []).sorted()
+    for f in ("zoom", "row", "col", "count"):
+        assert np.array_equal(getattr(got, f), getattr(ref, f)), f

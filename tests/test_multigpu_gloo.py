@@ -4,6 +4,10 @@ Each rank bins its contiguous shard of the points (here with the oracle, the
 device's stand-in off-GPU), exchanges cells with merge_cells, and the union of
 what the ranks own must equal the single-process count of all points -- the
 sum Spark's reduceByKey / groupByKey shuffles compute (heatmap.py:111-112).
+The three device operations (hm_cells_route / hm_cells_merge /
+hm_dense_cells) are replaced by the torch stand-ins below, which follow the
+same contract; the collectives and the exchange logic are the product's.
+The device kernels themselves run in tests/test_gpu_multigpu.py.
 """
 import os
 import socket
@@ -17,6 +21,8 @@ import torch.multiprocessing as mp
 from oracle import oracle
 from heatmap_amd import multigpu, synth
 
+M29 = 0x1FFFFFFF
+
 
 def _port():
     s = socket.socket()
@@ -26,16 +32,82 @@ def _port():
     return p
 
 
+def _spread(v):
+    v = v & 0xFFFFFFFF
+    for sh, m in ((16, 0x0000FFFF0000FFFF), (8, 0x00FF00FF00FF00FF), (4, 0x0F0F0F0F0F0F0F0F),
+                  (2, 0x3333333333333333), (1, 0x5555555555555555)):
+        v = (v | (v << sh)) & m
+    return v
+
+
+def _compact(v):
+    v = v & 0x5555555555555555
+    for sh, m in ((1, 0x3333333333333333), (2, 0x0F0F0F0F0F0F0F0F), (4, 0x00FF00FF00FF00FF),
+                  (8, 0x0000FFFF0000FFFF), (16, 0x00000000FFFFFFFF)):
+        v = (v | (v >> sh)) & m
+    return v
+
+
+class TorchOps:
+    """CPU stand-ins with the contract of hm_cells_route / hm_cells_merge /
+    hm_dense_cells (include/heatmap_amd.h)."""
+
+    @staticmethod
+    def route(keys, counts, ws, dz):
+        z, r, c = keys >> 58, (keys >> 29) & M29, keys & M29
+        gsz = ((1 << (2 * (dz + 1))) - 1) // 3 if dz >= 0 else 0
+        grid = torch.zeros(gsz, dtype=torch.int64)
+        dense = z <= dz
+        if dz >= 0 and dense.any():
+            zz = z[dense]
+            idx = ((1 << (2 * zz)) - 1) // 3 + ((_spread(r[dense]) << 1) | _spread(c[dense]))
+            grid.index_add_(0, idx, counts[dense])
+        sk, sc = keys[~dense], counts[~dense]
+        rec = torch.stack([sk >> 58, (sk >> 29) & M29, sk & M29], 1)
+        own = multigpu.record_owner(rec, ws)
+        o = torch.argsort(own, stable=True)
+        return grid, sk[o], sc[o], torch.bincount(own, minlength=ws).tolist()
+
+    @staticmethod
+    def merge(keys, counts):
+        u, inv = torch.unique(keys, return_inverse=True)
+        t = torch.zeros(u.numel(), dtype=torch.int64)
+        t.index_add_(0, inv, counts)
+        return u, t
+
+    @staticmethod
+    def dense_cells(grid, dz):
+        nz = torch.nonzero(grid).flatten()
+        off = torch.tensor([((1 << (2 * z)) - 1) // 3 for z in range(dz + 1)], dtype=torch.int64)
+        zc = torch.bucketize(nz, off, right=True) - 1
+        m = nz - off[zc]
+        return (zc << 58) | (_compact(m >> 1) << 29) | _compact(m), grid[nz]
+
+
 class _Bufs:
-    def __init__(self, keys, counts, cap):
+    def __init__(self, keys, counts, xcells, cap):
         self.keys = torch.zeros(cap, dtype=torch.int64)
         self.counts = torch.zeros(cap, dtype=torch.int64)
         self.keys[: len(keys)] = torch.from_numpy(keys)
         self.counts[: len(counts)] = torch.from_numpy(counts)
+        self.xcells = torch.from_numpy(xcells.reshape(-1).copy())
+        self.nx = xcells.shape[0]
 
 
-def _keys(z, r, c):
-    return (z.astype(np.int64) << 58) | (r.astype(np.int64) << 29) | c.astype(np.int64)
+def _split(ref):
+    z, r, c, n = ref["zoom"].astype(np.int64), ref["row"], ref["col"], ref["count"]
+    sq = (r >= 0) & (r < (1 << z)) & (c >= 0) & (c < (1 << z))
+    keys = (z[sq] << 58) | (r[sq] << 29) | c[sq]
+    x = np.stack([z[~sq], r[~sq], c[~sq], n[~sq]], 1)
+    return keys, n[sq], x
+
+
+def _cloud(kind, n, start):
+    lat, lon = synth.generate(kind, n, seed=2, start=start)
+    lat, lon = lat.copy(), lon.copy()
+    lat[::997] = 88.0 + (np.arange(lat[::997].size) % 7) * 0.2     # kept points outside the square
+    lon[5::1009] = 200.0
+    return lat, lon
 
 
 def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out):
@@ -43,12 +115,11 @@ def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     per = n // ws
-    lat, lon = synth.generate(kind, per, seed=2, start=rank * per)
-    ref = oracle.count(lat, lon, None, zmin, zmax)
-    k = _keys(ref["zoom"], ref["row"], ref["col"])
-    b = _Bufs(k, ref["count"], 4 * len(k) + 64)
-    m = multigpu.merge_cells(b, len(k), ws, rank, dense_zmax=dense_zmax)
-    out[rank] = (b.keys[:m].numpy().copy(), b.counts[:m].numpy().copy())
+    lat, lon = _cloud(kind, per, rank * per)
+    k, c, x = _split(oracle.count(lat, lon, None, zmin, zmax))
+    b = _Bufs(k, c, x, 4 * len(k) + 64)
+    m = multigpu.merge_cells(b, len(k), ws, rank, dense_zmax=dense_zmax, ops=TorchOps())
+    out[rank] = (b.keys[:m].numpy().copy(), b.counts[:m].numpy().copy(), b.xcells[:4 * b.nx].numpy().copy())
     dist.destroy_process_group()
 
 
@@ -61,11 +132,15 @@ def test_merge_two_ranks(kind, zmax, dense_zmax):
                        join=True, start_method="spawn")
     keys = np.concatenate([out[r][0] for r in range(ws)])
     counts = np.concatenate([out[r][1] for r in range(ws)])
+    xs = np.concatenate([out[r][2].reshape(-1, 4) for r in range(ws)])
     assert len(np.unique(keys)) == len(keys)            # every cell has exactly one owner
-    o = np.argsort(keys)
-    lat, lon = synth.generate(kind, n, seed=2)
-    ref = oracle.count(lat, lon, None, zmin, zmax)
-    rk = _keys(ref["zoom"], ref["row"], ref["col"])
-    ro = np.argsort(rk)
+    lat = np.concatenate([_cloud(kind, n // ws, r * (n // ws))[0] for r in range(ws)])
+    lon = np.concatenate([_cloud(kind, n // ws, r * (n // ws))[1] for r in range(ws)])
+    rk, rc, rx = _split(oracle.count(lat, lon, None, zmin, zmax))
+    o, ro = np.argsort(keys), np.argsort(rk)
     assert np.array_equal(keys[o], rk[ro])
-    assert np.array_equal(counts[o], ref["count"][ro])
+    assert np.array_equal(counts[o], rc[ro])
+    assert len(rx) > 0
+    xo = np.lexsort((xs[:, 2], xs[:, 1], xs[:, 0]))
+    rxo = np.lexsort((rx[:, 2], rx[:, 1], rx[:, 0]))
+    assert np.array_equal(xs[xo], rx[rxo])

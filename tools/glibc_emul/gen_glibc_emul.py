@@ -25,7 +25,7 @@ those inputs set ``*unsupported = 1`` and the caller reports HM_E_RANGE.
 
 The output header is committed; re-run this script only if libm changes:
     python tools/glibc_emul/gen_glibc_emul.py > heatmap_amd/csrc/hm_glibc_emul.h
-``tests/test_glibc_emul.py`` checks the generated code against the live libm
+``tests/test_math_host.py::test_glibc_restatement_bit_exact`` checks the generated code against the live libm
 on millions of inputs on every CPU test run.
 """
 import re
@@ -534,7 +534,7 @@ def main():
     o.append(" * constants and tables are the library's .rodata words.  glibc is LGPL-2.1;")
     o.append(" * this file restates its arithmetic so tile rows match CPython's math module")
     o.append(" * (reference tile.py:17) bit for bit.  Checked against the live libm by")
-    o.append(" * tests/test_glibc_emul.py. */")
+    o.append(" * tests/test_math_host.py::test_glibc_restatement_bit_exact. */")
     o.append("#pragma once")
     o.append('#include "hm_common.h"')
     o.append("")

@@ -13,7 +13,9 @@ PASSES=(
  "WRITE_SIZE"
  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_WAVE_CYCLES SQ_BUSY_CYCLES"
  "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_ADDR_CONFLICT"
- "SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS_ATOMIC SQ_INSTS_VALU_INT SQ_INSTS_VALU_FMA_F SQ_INSTS_VALU_ADD_F SQ_INSTS_VALU_MUL_F SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT"
+ "SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS_ATOMIC SQ_LDS_ATOMIC_RETURN SQ_INSTS_SMEM SQ_ACTIVE_INST_SCA GRBM_GUI_ACTIVE GRBM_COUNT"
+ "TCC_EA0_ATOMIC TCC_EA0_ATOMIC_LEVEL TCC_ATOMIC TCP_ATOMIC_TAGCONFLICT_STALL_CYCLES TCP_WRITE_TAGCONFLICT_STALL_CYCLES TA_ATOMIC_REQ"
+ "TCC_EA0_WRREQ TCC_EA0_WRREQ_64B TCC_EA0_WRREQ_STALL TCC_EA0_WRREQ_LEVEL"
 )
 i=0
 for p in "${PASSES[@]}"; do
