@@ -13,10 +13,14 @@ written to HBM as (key, count).
         # each rank bins its shard, then the sparse cells are hash-partitioned
         # by heatmap row over RCCL all-to-all and merged
 
-Rank 0 prints one JSON line.  `roofline` is for the dominant kernel
-(k_project_partition), timed with HIP events on the library's stream inside
-the timed region; `traffic` is the per-launch HBM byte count from the
-committed rocprofv3 PMC summary for the same workload (profiles/), or null.
+Rank 0 prints one JSON line.  `roofline` is for the whole step, the unit the
+metric is quoted on: achieved = algorithmic bytes of one step (16 B per point
+read + 16 B per non-empty output cell) / the step's average
+duration from HIP events recorded on the library's stream around the timed
+steps, against the 8 TB/s HBM3E peak; `traffic` is the HBM bytes of one step
+from the committed rocprofv3 PMC summary (profiles/pmc_summary.json, FETCH_SIZE
+doubled per the gfx950 correction + WRITE_SIZE), or null.  `kernels` breaks the
+step down by stage from the library's own HIP events (hm_last_stats).
 `cpu_baseline` times the C oracle (oracle/hm_oracle.c, OpenMP) on a bounded
 sample of the same generator on this host's cores.
 """
@@ -79,7 +83,7 @@ def barrier(ws):
 
 
 def profile_traffic(workload_tag):
-    """Per-launch HBM bytes of k_project_partition from the committed PMC summary."""
+    """HBM bytes of one hm_count step from the committed PMC summary."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
         return None, None
@@ -89,7 +93,7 @@ def profile_traffic(workload_tag):
         e = d.get(workload_tag)
         if not e:
             return None, None
-        return e.get("hbm_bytes_per_launch"), os.path.relpath(path, REPO)
+        return e.get("hbm_bytes_per_step"), os.path.relpath(path, REPO)
     except Exception:
         return None, None
 
@@ -146,16 +150,19 @@ def main():
         m, bufs = step()
     torch.cuda.synchronize()
     barrier(ws)
-    k1, stages = [], []
+    stages = []
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record()
     for _ in range(args.steps):
         m, bufs = step()
         _, us = ctx.last_stats()
-        k1.append(us[0])
-        stages.append(us[:4])
+        stages.append(us[:5])
+    ev1.record()
     torch.cuda.synchronize()
     barrier(ws)
     dt = time.perf_counter() - t0
+    step_ms_ev = ev0.elapsed_time(ev1) / args.steps
     if args.dist:
         import torch.distributed as dist
 
@@ -177,10 +184,19 @@ def main():
         check = "ok" if tot == per * ws * (args.zmax - args.zmin + 1) else "FAIL sum %d" % tot
     ms = dt / args.steps * 1e3
     total_points = per * ws
-    k1_us = float(np.mean(k1))
-    achieved = ALG_BYTES_PER_POINT * per / (k1_us * 1e-6) / 1e9
+    st = np.mean(np.array(stages), axis=0)
     tag = "%s_%d_z%d-%d" % (args.kind, per, args.zmin, args.zmax)
     traffic, traffic_src = profile_traffic(tag)
+    alg_step = ALG_BYTES_PER_POINT * per + ALG_BYTES_PER_CELL * (cells // ws)      # one rank's step
+    achieved = alg_step / (step_ms_ev * 1e-3) / 1e9
+    kernels = {
+        "k_project_partition": {"us": float(st[0]), "alg_bytes": ALG_BYTES_PER_POINT * per,
+                                "GBps": ALG_BYTES_PER_POINT * per / (st[0] * 1e-6) / 1e9 if st[0] else None},
+        "k_partition (levels >= 2)": {"us": float(st[4])},
+        "level buckets, run scans, compaction, host syncs": {"us": float(st[1] - st[4])},
+        "final aggregation (k_aggregate + sparse/small/merged)": {"us": float(st[2])},
+        "k_pool": {"us": float(st[3])},
+    }
     out = {
         "metric": "points binned/sec (whole node, zooms 0-18) + % HBM roofline at 1/2/4/8 GPU",
         "value": total_points / (dt / args.steps),
@@ -198,17 +214,12 @@ def main():
                                                                                     args.zmax, ws),
                    "points_per_gpu": per, "zmin": args.zmin, "zmax": args.zmax,
                    "parallelism": "points sharded, dp%d" % ws},
-        "roofline": {"bound": "hbm", "kernel": "k_project_partition", "achieved": achieved, "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "traffic_source": traffic_src, "avg_launch_us": k1_us,
-                     "alg_bytes_per_launch": ALG_BYTES_PER_POINT * per},
-        "pipeline": {"cells": cells, "alg_bytes": ALG_BYTES_PER_POINT * total_points + ALG_BYTES_PER_CELL * cells,
-                     "alg_GBps": (ALG_BYTES_PER_POINT * total_points + ALG_BYTES_PER_CELL * cells) / (dt / args.steps) / 1e9,
-                     "frac_of_8TBps": (ALG_BYTES_PER_POINT * total_points + ALG_BYTES_PER_CELL * cells)
-                     / (dt / args.steps) / 1e9 / HBM_PEAK_GBS,
-                     "stage_us_mean": [float(x) for x in np.mean(np.array(stages), axis=0)],
-                     "stages": ["project+partition", "partition levels+scans", "aggregate", "pool"],
-                     "slow_path_points": ctx.last_stats()[0], "check": check},
+        "roofline": {"bound": "hbm", "kernel": "hm_count step (all pipeline kernels, one rank)",
+                     "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": traffic, "traffic_source": traffic_src, "avg_launch_us": step_ms_ev * 1e3,
+                     "alg_bytes_per_launch": alg_step, "cells_per_step": cells // ws},
+        "kernels": kernels,
+        "pipeline": {"slow_path_points": ctx.last_stats()[0], "check": check},
     }
     if rank == 0:
         out["cpu_baseline"] = cpu_baseline(args, lat, lon)

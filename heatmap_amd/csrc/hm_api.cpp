@@ -41,6 +41,10 @@ struct Level {
 
 }  // namespace
 
+/* per-call stage events: [0..4] stage boundaries, [5..] pairs around the
+ * level >= 2 partition launches */
+#define HM_NEV 12
+
 struct hm_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -52,7 +56,7 @@ struct hm_ctx {
     int last_err_kind = 0;
     int64_t last_slow = 0;
     double stage_us[8] = {0};
-    hipEvent_t ev[10];
+    hipEvent_t ev[HM_NEV];
 };
 
 enum {
@@ -163,7 +167,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     c->device = device;
     c->stream = (hipStream_t)stream;
     c->bufs.resize(B_COUNT);
-    for (int i = 0; i < 10; i++) c->ev[i] = nullptr;
+    for (int i = 0; i < HM_NEV; i++) c->ev[i] = nullptr;
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -175,7 +179,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
         c->host_aux = nullptr;
         st = HM_E_NOMEM;
     }
-    for (int i = 0; i < 10 && st == HM_OK; i++)
+    for (int i = 0; i < HM_NEV && st == HM_OK; i++)
         if (hipEventCreate(&c->ev[i]) != hipSuccess) {
             c->ev[i] = nullptr;
             st = HM_E_HIP;
@@ -205,7 +209,7 @@ int hm_ctx_destroy(hm_ctx* c)
     if (c->state) (void)hipFree(c->state);
     if (c->host_state) (void)hipHostFree(c->host_state);
     if (c->host_aux) (void)hipHostFree(c->host_aux);
-    for (int i = 0; i < 10; i++)
+    for (int i = 0; i < HM_NEV; i++)
         if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
     delete c;
     return HM_OK;
@@ -476,6 +480,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     uint32_t* slot_bucket = nullptr;
     uint64_t level_keys = 0;    /* keys entering level l >= 2 (global positions) */
     uint64_t nx = 0;            /* kept points outside [0, 2^Z)^2 */
+    int npart = 0;              /* level >= 2 partition launches timed (ev[5..]) */
 
     for (int l = 0; l < L; l++) {
         Level& V = lv[l];
@@ -527,7 +532,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.redo_count = ctx->state + ST_REDO;
             a.redo_cap = redo_cap;
             /* region sizes: a sampled digit histogram with a generous margin */
-            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> 22);
+            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> 20);
             HIPCHK(hipMemsetAsync(hist, 0, F * 4, s));
             if (n > 0) hm_launch_sample_digits(s, a, stride, hist);
             HIPCHK(hipGetLastError());
@@ -704,9 +709,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         }
         /* ---- levels >= 2 ---- */
         const uint64_t ntiles = lv[l - 1].items;
-        /* run-counter shards: 32 unless the dense child space is large (then
-         * per-child contention is low anyway); keeps counters <= 2^25 */
-        int sb = 5;
+        /* run-counter shards: up to 32 (a hot child takes one returning atomic
+         * per parent work item; one counter per child made k_partition 16%
+         * slower), fewer when the dense child space is large; <= 2^25 */
+        int sb = HM_RUN_SHARD_BITS;
         while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
         const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
         if (run_cap >= (1ull << 32)) return HM_E_NOMEM;
@@ -735,8 +741,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.nruns_out = nruns;
             a.runs_out = runs_sh;
             a.items = lv[l - 1].items;
+            HIPCHK(hipEventRecord(ev[5 + 2 * (l - 1)], s));
             hm_launch_partN(s, a, lv[l - 1].items, V.out16);
             HIPCHK(hipGetLastError());
+            HIPCHK(hipEventRecord(ev[6 + 2 * (l - 1)], s));
+            npart = l;
         }
 
         /* run scan: sharded counters -> flat child-ordered runs + key prefix */
@@ -929,6 +938,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         float ms = 0;
         (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
         ctx->stage_us[i] = ms * 1000.0;
+    }
+    for (int l = 1; l <= npart; l++) {
+        float ms = 0;
+        (void)hipEventElapsedTime(&ms, ev[5 + 2 * (l - 1)], ev[6 + 2 * (l - 1)]);
+        ctx->stage_us[4] += ms * 1000.0;
     }
     const unsigned long long nc = ctx->host_state[ST_CURSOR];
     *n_out = (int64_t)nc;

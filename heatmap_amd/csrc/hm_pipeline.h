@@ -25,6 +25,9 @@
 #define HM_LEVEL_ZOOMS 6                    /* <= 6 zooms per level */
 #define HM_MAX_FN 4096
 #define HM_MAX_SHARDS 32                    /* run-counter shards per child */
+#ifndef HM_RUN_SHARD_BITS
+#define HM_RUN_SHARD_BITS 4
+#endif
 /* final aggregation: zoom-zb bucket = 128 x 128 zoom-Z bins */
 #define HM_AG_THREADS 1024
 #define HM_AG_CELLS 16384

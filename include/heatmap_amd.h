@@ -141,9 +141,11 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
 /* Diagnostics of the last hm_project/hm_count call: points resolved by the
  * bit-exact glibc-restating slow path (guard band / out-of-window), and the
  * per-stage device time in microseconds of the last hm_count:
- *   [0] k_project_partition (projection + level-1 partition, the dominant kernel)
- *   [1] remaining partition levels, run scans and compactions (incl. host reads)
- *   [2] k_aggregate (+ merged buckets)   [3] k_pool levels */
+ *   [0] k_project_partition (projection + level-1 partition)
+ *   [1] level-1 buckets, remaining partition levels, run scans and
+ *       compactions (incl. host reads; contains [4])
+ *   [2] final aggregation (k_aggregate, sparse/small/merged buckets)
+ *   [3] k_pool levels   [4] the level >= 2 k_partition launches alone */
 int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_stages);
 
 /* Streaming: micro-batches folded into a heatmap resident in HBM (BASELINE

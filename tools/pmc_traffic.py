@@ -1,13 +1,16 @@
 #!/usr/bin/env python3
-"""Per-launch HBM bytes per kernel from the FETCH_SIZE / WRITE_SIZE passes of
-tools/gpu/profile_round.sh, written into profiles/pmc_summary.json for bench.py.
+"""Per-launch and per-step HBM bytes from rocprofv3 FETCH_SIZE / WRITE_SIZE
+passes, written into profiles/pmc_summary.json for bench.py.
 
-    python tools/pmc_traffic.py gpurun_out/TAG WORKLOAD_TAG [--out profiles/pmc_summary.json]
+    python tools/pmc_traffic.py FETCH_DIR WRITE_DIR WORKLOAD_TAG [--out profiles/pmc_summary.json]
 
+(tools/gpu/pmc.sh: FETCH_DIR = gpurun_out/TAG/p1, WRITE_DIR = gpurun_out/TAG/p2.)
 FETCH_SIZE and WRITE_SIZE are in KiB.  Per MI355X_MICROARCH.md (HBM section),
 FETCH_SIZE counts exactly half the bytes of a 16-B/lane coalesced streaming read
-on gfx950, so it is doubled (k_project_partition reads lat/lon that way);
-WRITE_SIZE is taken as is.
+on gfx950, so it is doubled; WRITE_SIZE is taken as is.  One step = one
+hm_count (one level-1 k_project_partition<.., 0> dispatch); the step's bytes
+are every pipeline kernel's bytes of the run divided by the steps (the
+synthetic-cloud generator and the bench's own check reduction excluded).
 """
 import csv
 import glob
@@ -16,40 +19,50 @@ import os
 import sys
 from collections import defaultdict
 
+EXCLUDE = ("k_synth", "at::native")
+
 
 def per_kernel(d, counter):
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
-    vals = defaultdict(list)
+    vals = defaultdict(float)
     for row in csv.DictReader(open(f[0])):
         if row["Counter_Name"] != counter:
             continue
         k = row["Kernel_Name"].split("(")[0]
-        vals[(k, row.get("Dispatch_Id", row.get("Correlation_Id")))].append(float(row["Counter_Value"]))
-    out = defaultdict(list)
+        vals[(k, row.get("Dispatch_Id", row.get("Correlation_Id")))] += float(row["Counter_Value"])
+    tot, calls = defaultdict(float), defaultdict(int)
     for (k, _), v in vals.items():
-        out[k].append(sum(v))
-    return {k: sum(v) / len(v) for k, v in out.items()}
+        tot[k] += v
+        calls[k] += 1
+    return tot, calls
 
 
 def main():
-    src, tag = sys.argv[1], sys.argv[2]
-    dst = sys.argv[4] if len(sys.argv) > 4 and sys.argv[3] == "--out" else "profiles/pmc_summary.json"
-    fetch = per_kernel(os.path.join(src, "pmc_FETCH_SIZE"), "FETCH_SIZE")
-    write = per_kernel(os.path.join(src, "pmc_WRITE_SIZE"), "WRITE_SIZE")
+    fd, wd, tag = sys.argv[1], sys.argv[2], sys.argv[3]
+    dst = sys.argv[5] if len(sys.argv) > 5 and sys.argv[4] == "--out" else "profiles/pmc_summary.json"
+    fetch, fcalls = per_kernel(fd, "FETCH_SIZE")
+    write, wcalls = per_kernel(wd, "WRITE_SIZE")
+    steps = sum(v for k, v in fcalls.items() if k.startswith("void k_project_partition<") and k.endswith(", 0>"))
     kernels = {}
+    step_bytes = 0.0
     for k in sorted(set(fetch) | set(write)):
+        n = max(fcalls.get(k, 0), wcalls.get(k, 0), 1)
         fb = fetch.get(k, 0.0) * 1024 * 2
         wb = write.get(k, 0.0) * 1024
-        kernels[k] = {"fetch_bytes_corrected": fb, "write_bytes": wb, "hbm_bytes_per_launch": fb + wb}
-    main_k = [k for k in kernels if k.startswith("void k_project_partition<unsigned int, 0>")]
-    entry = {"source": src, "kernels": kernels,
-             "hbm_bytes_per_launch": kernels[main_k[0]]["hbm_bytes_per_launch"] if main_k else None,
-             "note": "FETCH_SIZE x2 (gfx950 16-B streaming-read correction) + WRITE_SIZE, KiB -> B"}
+        kernels[k] = {"fetch_bytes_corrected": fb / n, "write_bytes": wb / n, "hbm_bytes_per_launch": (fb + wb) / n,
+                      "launches": n}
+        if not any(k.startswith(e) or e in k for e in EXCLUDE):
+            step_bytes += fb / max(fcalls.get(k, 1), 1) * fcalls.get(k, 0) / max(steps, 1) + \
+                wb / max(wcalls.get(k, 1), 1) * wcalls.get(k, 0) / max(steps, 1)
+    entry = {"source": [fd, wd], "kernels": kernels, "steps_profiled": steps, "hbm_bytes_per_step": step_bytes,
+             "note": "FETCH_SIZE x2 (gfx950 16-B streaming-read correction) + WRITE_SIZE, KiB -> B; "
+                     "per step = all pipeline kernels of one hm_count"}
     d = json.load(open(dst)) if os.path.exists(dst) else {}
     d[tag] = entry
     json.dump(d, open(dst, "w"), indent=1)
+    print("steps %d, HBM bytes per step %.3f GB" % (steps, step_bytes / 1e9))
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:8]:
-        print("%-60s %10.3f GB" % (k[:60], v["hbm_bytes_per_launch"] / 1e9))
+        print("%-60s %10.3f GB x %d" % (k[:60], v["hbm_bytes_per_launch"] / 1e9, v["launches"]))
 
 
 if __name__ == "__main__":

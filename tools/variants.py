@@ -23,6 +23,8 @@ VARIANTS = {
     # tuning knobs (compile-time macros of the shipped sources)
     "noskew": ["HM_SKEW_CUR=0"],
     "p1_512x8": ["HM_P1_PPT=8"],
+    "rs3": ["HM_RUN_SHARD_BITS=3"],
+    "rs4": ["HM_RUN_SHARD_BITS=4"],
     "p1_256x16": ["HM_P1_THREADS=256"],
     "t512_8k": ["HM_PN_THREADS=512"],
     "su2": ["HM_SU=2"],
