@@ -24,11 +24,13 @@ HM_E_CAPACITY = 17
 HM_E_HIP = 18
 HM_E_NOMEM = 19
 HM_COUNT_MAX_ZOOM = 21
-HM_ABI_VERSION = 2
+HM_ABI_VERSION = 3
+HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
            "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
-           "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_extract", "hm_stream_destroy",
+           "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
+           "hm_stream_destroy",
            "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_dense_cells"]
 
 _LIB = None
@@ -59,6 +61,13 @@ def load() -> ctypes.CDLL:
                 _build.build(verbose=False)
             except Exception as e:  # pragma: no cover - surfaced to the caller
                 raise DeviceUnavailable("heatmap_amd: cannot build %s: %s" % (path, e)) from e
+        # torch first: the library then binds the HIP runtime torch loaded
+        # (one runtime per process; loading ours first left torch's without
+        # devices on the GPU box)
+        try:
+            import torch  # noqa: F401
+        except ImportError:  # pragma: no cover - torch is part of the image
+            pass
         L = ctypes.CDLL(path)
         if L.hm_abi_version() != HM_ABI_VERSION:
             raise DeviceUnavailable("heatmap_amd: %s has ABI %d, this binding needs %d"
@@ -83,9 +92,10 @@ def load() -> ctypes.CDLL:
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
         L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]
-        L.hm_stream_create.argtypes = [vp, c.c_int, c.c_int, c.c_uint32, c.c_int64, P(vp)]
-        L.hm_stream_add.argtypes = [vp, vp, vp, vp, vp, c.c_int64]
-        L.hm_stream_cells.argtypes = [vp, P(c.c_int64), P(c.c_int64)]
+        L.hm_stream_create.argtypes = [vp, c.c_int, c.c_int, c.c_uint32, c.c_int64, c.c_int64, P(vp)]
+        L.hm_stream_add.argtypes = [vp, vp, vp, vp, vp, vp, c.c_int64]
+        L.hm_stream_cells.argtypes = [vp, P(c.c_int64), P(c.c_int64), P(c.c_int64)]
+        L.hm_stream_rollup.argtypes = [vp, c.c_int, c.c_int, c.c_int64, vp, vp, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_stream_extract.argtypes = [vp, c.c_int64, vp, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_stream_destroy.argtypes = [vp]
         L.hm_dense_grid_size.argtypes = [c.c_int]

@@ -1165,20 +1165,24 @@ extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int
 struct hm_stream {
     hm_ctx* ctx = nullptr;
     int zmin = 0, zmax = 0;
+    int cb = 0;                           /* cell bits of a table key */
     uint32_t base = 0;
-    HmsTable t{};
-    uint64_t occupied = 0;
-    unsigned long long* hstate = nullptr; /* pinned mirror of t.state (8 words) */
-    Buf bkeys, bcounts, mask, present;    /* per-batch scratch */
-    int64_t bcap = 0;                     /* cells bkeys/bcounts hold */
+    HmsTable t{};                         /* cells */
+    HmsBuckets bk{};                      /* (group, period) buckets */
+    uint64_t occupied = 0, nbuckets = 0;
+    unsigned long long* hstate = nullptr; /* pinned mirror of t.state */
+    Buf bids, rec, bkeys, bcounts;        /* per-batch scratch */
+    int64_t bcap = 0, rcap = 0;           /* cells bkeys/bcounts, records rec hold */
+    Buf rslots;                           /* rollup table */
 };
 
 static int stream_sync_state(hm_stream* s)
 {
-    HIPCHK(hipMemcpyAsync(s->hstate, s->t.state, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    HIPCHK(hipMemcpyAsync(s->hstate, s->t.state, HMS_ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                           s->ctx->stream));
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
     s->occupied = s->hstate[HMS_ST_OCCUPIED];
+    s->nbuckets = s->hstate[HMS_ST_BUCKETS];
     return s->hstate[HMS_ST_OVERFLOW] ? HM_E_CAPACITY : HM_OK;
 }
 
@@ -1217,6 +1221,7 @@ static int stream_reserve(hm_stream* s, uint64_t incoming)
 
 static int stream_buf(hm_stream* s, Buf& b, size_t bytes)
 {
+    (void)s;
     if (b.cap >= bytes) return HM_OK;
     if (b.p) HIPCHK(hipFree(b.p));
     b.p = nullptr;
@@ -1229,18 +1234,23 @@ static int stream_buf(hm_stream* s, Buf& b, size_t bytes)
     return HM_OK;
 }
 
-/* one count pyramid over the batch (mask = kept points of one hour), folded in */
-static int stream_fold(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
-                       uint64_t tag_a, uint64_t tag_b)
+static int stream_cells_buf(hm_stream* s, int64_t want)
+{
+    if (s->bcap >= want) return HM_OK;
+    int st;
+    if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))
+        return st;
+    s->bcap = want;
+    return HM_OK;
+}
+
+/* a batch of one bucket: hm_count's pyramid, folded in under that bucket */
+static int stream_fold_one(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
+                           uint32_t bucket)
 {
     int64_t m = 0;
     int st;
-    if (s->bcap < 2 * n + 1024) { /* typical batches: fewer cells than 2 per point */
-        const int64_t want = 2 * n + 1024;
-        if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))
-            return st;
-        s->bcap = want;
-    }
+    if ((st = stream_cells_buf(s, 2 * n + 1024))) return st; /* typical batches: fewer cells than 2 per point */
     for (;;) {
         int64_t nx = 0;
         st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, (uint64_t*)s->bkeys.p, (uint64_t*)s->bcounts.p,
@@ -1248,23 +1258,54 @@ static int stream_fold(hm_stream* s, const double* lat, const double* lon, const
         /* the resident table's keys hold tiles inside [0, 2^z)^2 only */
         if (nx > 0) return HM_E_EXOTIC;
         if (st != HM_E_CAPACITY) break;
-        const int64_t want = m + m / 4 + 1024;
-        if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))
-            return st;
-        s->bcap = want;
+        if ((st = stream_cells_buf(s, m + m / 4 + 1024))) return st;
     }
     if (st) return st;
-    if ((st = stream_reserve(s, (uint64_t)m * (tag_b ? 2 : 1)))) return st;
+    if ((st = stream_reserve(s, (uint64_t)m))) return st;
     hm_launch_stream_insert(s->ctx->stream, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m,
-                            tag_a, tag_b, s->t);
+                            true, (uint64_t)bucket << s->cb, s->t);
+    HIPCHK(hipGetLastError());
+    return stream_sync_state(s);
+}
+
+/* a batch of several buckets: one grouped pass with the bucket as group */
+static int stream_fold_grouped(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n)
+{
+    int64_t m = 0;
+    int st;
+    if (s->rcap < 2 * n + 1024) {
+        const int64_t want = 2 * n + 1024;
+        if ((st = stream_buf(s, s->rec, (size_t)want * 40))) return st;
+        s->rcap = want;
+    }
+    for (;;) {
+        st = grouped_impl(s->ctx, lat, lon, nullptr, nullptr, keep, (const uint32_t*)s->bids.p, n, s->zmin, s->zmax,
+                          (int64_t*)s->rec.p, s->rcap, &m);
+        if (st != HM_E_CAPACITY) break;
+        const int64_t want = m + m / 4 + 1024;
+        if ((st = stream_buf(s, s->rec, (size_t)want * 40))) return st;
+        s->rcap = want;
+    }
+    if (st) return st;
+    if ((st = stream_cells_buf(s, m + 1))) return st;
+    hipStream_t q = s->ctx->stream;
+    HIPCHK(hipMemsetAsync(s->t.state + HMS_ST_EXOTIC, 0, 8, q));
+    hm_launch_stream_convert(q, (const int64_t*)s->rec.p, (uint64_t)m, s->cb, (uint64_t*)s->bkeys.p,
+                             (uint64_t*)s->bcounts.p, s->t.state);
+    HIPCHK(hipGetLastError());
+    if ((st = stream_sync_state(s))) return st;
+    if (s->hstate[HMS_ST_EXOTIC]) return HM_E_EXOTIC;   /* checked before anything is inserted */
+    if ((st = stream_reserve(s, (uint64_t)m))) return st;
+    hm_launch_stream_insert(q, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m, false, 0, s->t);
     HIPCHK(hipGetLastError());
     return stream_sync_state(s);
 }
 
 extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_t initial_cells,
-                                hm_stream** out)
+                                int64_t max_buckets, hm_stream** out)
 {
-    if (!ctx || !out || zmin < 0 || zmax < zmin || zmax > HM_MAX_ZOOM || initial_cells < 0) return HM_E_ARG;
+    if (!ctx || !out || zmin < 0 || zmax < zmin || zmax > HM_MAX_ZOOM || initial_cells < 0 || max_buckets < 0)
+        return HM_E_ARG;
     *out = nullptr;
     HIPCHK(hipSetDevice(ctx->device));
     hm_stream* s = new hm_stream();
@@ -1272,17 +1313,29 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
     s->zmin = zmin;
     s->zmax = zmax;
     s->base = base_hour;
+    /* cell bits: the pyramid index of zooms 0..zmax, (4^(zmax+1) - 1)/3 values */
+    const uint64_t ncell = ((1ull << (2 * (zmax + 1))) - 1) / 3;
+    while ((1ull << s->cb) < ncell) s->cb++;
+    const int bb = 64 - s->cb;   /* bucket bits: 21 at zmax 21 */
+    uint64_t nb = 1024;
+    const uint64_t want = max_buckets ? (uint64_t)max_buckets : (1ull << 20);
+    while (nb < want + want / 4 && nb < (1ull << bb)) nb <<= 1;
+    s->bk.mask = nb - 1;
     uint64_t cap = 1024;
     while (cap * 5 < (uint64_t)initial_cells * 8) cap <<= 1;
-    if (hipMalloc((void**)&s->t.state, 8 * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc((void**)&s->hstate, 8 * sizeof(unsigned long long)) != hipSuccess) {
+    if (hipMalloc((void**)&s->t.state, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc((void**)&s->hstate, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&s->bk.keys, nb * 8) != hipSuccess) {
         (void)hipGetLastError();
         hm_stream_destroy(s);
         return HM_E_NOMEM;
     }
     int st = stream_alloc_table(s, cap, &s->t);
+    if (st == HM_OK)
+        st = hip_fail(hipMemsetAsync(s->t.state, 0, HMS_ST_COUNT * sizeof(unsigned long long), ctx->stream), "memset");
     if (st == HM_OK) {
-        st = hip_fail(hipMemsetAsync(s->t.state, 0, 8 * sizeof(unsigned long long), ctx->stream), "memset");
+        hm_launch_stream_fill(ctx->stream, s->bk.keys, nb, HMS_EMPTY);
+        st = hip_fail(hipGetLastError(), "fill");
     }
     if (st == HM_OK) st = stream_sync_state(s);
     if (st) {
@@ -1294,80 +1347,118 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
 }
 
 extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep,
-                             const uint32_t* hour, int64_t n)
+                             const uint32_t* hour, const uint32_t* group, int64_t n)
 {
-    if (!s || n < 0 || (n > 0 && (!lat || !lon))) return HM_E_ARG;
-    HIPCHK(hipSetDevice(s->ctx->device));
-    hipStream_t q = s->ctx->stream;
-    int st;
-    if (!hour || n == 0) return stream_fold(s, lat, lon, keep, n, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT, 0);
-    /* hour range of the kept points */
-    unsigned int* mm = (unsigned int*)(s->t.state + HMS_ST_HOURS);
-    const unsigned int init[2] = {0xFFFFFFFFu, 0u};
-    HIPCHK(hipMemcpyAsync(mm, init, sizeof(init), hipMemcpyHostToDevice, q));
-    hm_launch_stream_hour_range(q, hour, keep, (uint64_t)n, mm);
+    if (!s || n < 0 || (n > 0 && (!lat || !lon)) || n >= (int64_t)0xFFFFFFF0ll) return HM_E_ARG;
+    if (n == 0) return HM_OK;
+    hm_ctx* ctx = s->ctx;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t q = ctx->stream;
+    int st = reset_state(ctx);
+    if (st) return st;
+    /* buckets of the kept points (interned; a failing batch may leave unused
+     * buckets behind, never counts) */
+    const unsigned int mm0[2] = {0xFFFFFFFFu, 0u};
+    HIPCHK(hipMemcpyAsync(s->t.state + HMS_ST_BMM, mm0, sizeof(mm0), hipMemcpyHostToDevice, q));
+    if ((st = stream_buf(s, s->bids, (size_t)(group || hour ? n : 1) * 4))) return st;
+    HmsBucketArgs a;
+    a.group = group;
+    a.hour = hour;
+    a.keep = (group || hour) ? keep : nullptr;
+    a.n = (group || hour) ? (uint64_t)n : 1;   /* neither: the one (no group, undated) bucket */
+    a.base = s->base;
+    a.buckets = s->bk;
+    a.out = (uint32_t*)s->bids.p;
+    a.state = s->t.state;
+    a.err_word = ctx->state + ST_ERR;
+    hm_launch_stream_buckets(q, a);
     HIPCHK(hipGetLastError());
     if ((st = stream_sync_state(s))) return st;
-    const unsigned int lo = ((unsigned int*)(s->hstate + HMS_ST_HOURS))[0];
-    const unsigned int hi = ((unsigned int*)(s->hstate + HMS_ST_HOURS))[1];
-    if (lo > hi) /* nothing kept: still project every point (errors), fold nothing */
-        return stream_fold(s, lat, lon, keep, n, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT, 0);
-    if (lo < s->base || (uint64_t)hi - s->base >= HM_STREAM_MAX_HOURS) return HM_E_RANGE;
-    if ((uint64_t)hi - lo >= HM_STREAM_MAX_SPAN) return HM_E_ARG;
-    if (lo == hi) /* one hour (the usual time-ordered batch): the kept points are that hour's */
-        return stream_fold(s, lat, lon, keep, n, (uint64_t)(lo - s->base) << HMS_TAG_SHIFT,
-                           HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT);
-    const uint32_t span = hi - lo + 1;
-    if ((st = stream_buf(s, s->present, span)) || (st = stream_buf(s, s->mask, (size_t)n))) return st;
-    HIPCHK(hipMemsetAsync(s->present.p, 0, span, q));
-    hm_launch_stream_hour_presence(q, hour, keep, (uint64_t)n, lo, (uint8_t*)s->present.p);
-    HIPCHK(hipGetLastError());
-    std::vector<uint8_t> present(span);
-    HIPCHK(hipMemcpyAsync(present.data(), s->present.p, span, hipMemcpyDeviceToHost, q));
-    HIPCHK(hipStreamSynchronize(q));
-    for (uint32_t d = 0; d < span; d++) {
-        if (!present[d]) continue;
-        hm_launch_stream_hour_mask(q, hour, keep, (uint64_t)n, lo + d, (uint8_t*)s->mask.p);
-        HIPCHK(hipGetLastError());
-        const uint64_t tag = (uint64_t)(lo + d - s->base) << HMS_TAG_SHIFT;
-        if ((st = stream_fold(s, lat, lon, (const uint8_t*)s->mask.p, n, tag, HM_STREAM_ALLTIME_TAG << HMS_TAG_SHIFT)))
-            return st;
-    }
-    return HM_OK;
+    if ((st = read_state(ctx))) return st;
+    if ((st = take_error(ctx))) return st;
+    if (s->hstate[HMS_ST_BFULL]) return HM_E_CAPACITY;   /* max_buckets (group, hour) pairs */
+    const unsigned int* mm = (const unsigned int*)(s->hstate + HMS_ST_BMM);
+    if (mm[0] >= mm[1]) /* one bucket (the usual time-ordered batch), or nothing kept */
+        return stream_fold_one(s, lat, lon, keep, n, mm[0] <= mm[1] ? mm[0] : 0u);
+    return stream_fold_grouped(s, lat, lon, keep, n);
 }
 
-extern "C" int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity)
+extern "C" int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity, int64_t* buckets)
 {
     if (!s) return HM_E_ARG;
     if (cells) *cells = (int64_t)s->occupied;
     if (capacity) *capacity = (int64_t)(s->t.mask + 1);
+    if (buckets) *buckets = (int64_t)s->nbuckets;
     return HM_OK;
+}
+
+extern "C" int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_t select, uint64_t* keys_out,
+                                uint64_t* counts_out, uint32_t* groups_out, uint32_t* periods_out, int64_t capacity,
+                                int64_t* n_out)
+{
+    if (!s || !n_out || span < HM_SPAN_HOUR || span > HM_SPAN_ALLTIME || select < -1 || capacity < 0 ||
+        (capacity > 0 && (!keys_out || !counts_out)))
+        return HM_E_ARG;
+    *n_out = 0;
+    HIPCHK(hipSetDevice(s->ctx->device));
+    hipStream_t q = s->ctx->stream;
+    int st;
+    if (s->occupied == 0) return HM_OK;
+    /* scratch table: at most every cell slot, load <= 1/2; its own state words */
+    uint64_t cap = 1024;
+    while (cap < 2 * s->occupied) cap <<= 1;
+    if ((st = stream_buf(s, s->rslots, cap * 16 + 64))) return st;
+    HmsTable r;
+    r.slots = (uint64_t*)s->rslots.p;
+    r.mask = cap - 1;
+    r.state = (unsigned long long*)((char*)s->rslots.p + cap * 16);
+    HIPCHK(hipMemsetAsync(r.state, 0, 64, q));
+    hm_launch_stream_init(q, r);
+    HmsRollupArgs a;
+    a.from = s->t;
+    a.to = r;
+    a.buckets = s->bk;
+    a.cb = s->cb;
+    a.span = span;
+    a.merge = merge_groups ? 1 : 0;
+    a.base = s->base;
+    a.select = select;
+    a.state = s->t.state;
+    hm_launch_stream_rollup(q, a);
+    HmsEmitArgs e;
+    e.t = r;
+    e.buckets = s->bk;
+    e.cb = s->cb;
+    e.zmin = s->zmin;
+    e.zmax = s->zmax;
+    e.base = s->base;
+    e.keys_out = keys_out;
+    e.counts_out = counts_out;
+    e.groups_out = groups_out;
+    e.periods_out = periods_out;
+    e.cap = (uint64_t)capacity;
+    e.cursor = r.state + HMS_ST_CURSOR;
+    hm_launch_stream_emit(q, e);
+    HIPCHK(hipGetLastError());
+    unsigned long long* down = s->ctx->host_state + 2 * ST_COUNT;
+    HIPCHK(hipMemcpyAsync(down, r.state, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, q));
+    if ((st = stream_sync_state(s))) return st;
+    if (s->hstate[HMS_ST_BFULL]) return HM_E_CAPACITY;   /* no bucket left for a rollup label */
+    if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;         /* cannot happen: load <= 1/2 */
+    *n_out = (int64_t)down[HMS_ST_CURSOR];
+    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
 }
 
 extern "C" int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out, uint64_t* counts_out,
                                  uint32_t* hours_out, int64_t capacity, int64_t* n_out)
 {
-    if (!s || !n_out || capacity < 0 || (capacity > 0 && (!keys_out || !counts_out))) return HM_E_ARG;
-    uint64_t sel;
+    if (!s) return HM_E_ARG;
     if (hour == HM_STREAM_ALLTIME)
-        sel = HM_STREAM_ALLTIME_TAG;
-    else if (hour == HM_STREAM_EACH_HOUR)
-        sel = HMS_SEL_EVERY_HOUR;
-    else if (hour >= (int64_t)s->base && hour - (int64_t)s->base < HM_STREAM_MAX_HOURS)
-        sel = (uint64_t)(hour - s->base);
-    else
-        return HM_E_ARG;
-    *n_out = 0;
-    HIPCHK(hipSetDevice(s->ctx->device));
-    hipStream_t q = s->ctx->stream;
-    unsigned long long* cursor = s->t.state + HMS_ST_CURSOR;
-    HIPCHK(hipMemsetAsync(cursor, 0, sizeof(unsigned long long), q));
-    hm_launch_stream_extract(q, s->t, sel, keys_out, counts_out, hours_out, s->base, (uint64_t)capacity, cursor);
-    HIPCHK(hipGetLastError());
-    int st = stream_sync_state(s);
-    if (st) return st;
-    *n_out = (int64_t)s->hstate[HMS_ST_CURSOR];
-    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+        return hm_stream_rollup(s, HM_SPAN_ALLTIME, 1, -1, keys_out, counts_out, nullptr, nullptr, capacity, n_out);
+    if (hour == HM_STREAM_EACH_HOUR)
+        return hm_stream_rollup(s, HM_SPAN_HOUR, 1, -1, keys_out, counts_out, nullptr, hours_out, capacity, n_out);
+    if (hour < (int64_t)s->base || hour - (int64_t)s->base >= HM_STREAM_MAX_HOURS) return HM_E_ARG;
+    return hm_stream_rollup(s, HM_SPAN_HOUR, 1, hour, keys_out, counts_out, nullptr, hours_out, capacity, n_out);
 }
 
 extern "C" int hm_stream_destroy(hm_stream* s)
@@ -1375,8 +1466,8 @@ extern "C" int hm_stream_destroy(hm_stream* s)
     if (!s) return HM_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
-    for (void* p : {(void*)s->t.slots, (void*)s->t.state, s->bkeys.p, s->bcounts.p, s->mask.p,
-                    s->present.p})
+    for (void* p : {(void*)s->t.slots, (void*)s->t.state, (void*)s->bk.keys, s->bids.p, s->rec.p, s->bkeys.p,
+                    s->bcounts.p, s->rslots.p})
         if (p) (void)hipFree(p);
     if (s->hstate) (void)hipHostFree(s->hstate);
     delete s;

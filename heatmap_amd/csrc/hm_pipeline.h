@@ -312,28 +312,71 @@ void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int6
                      const double* tab, int k);
 
 /* resident streaming heatmap (hm_stream.hip) */
-#define HMS_TAG_SHIFT 47                    /* table key = tag<<47 | zoom<<42 | row<<21 | col */
-#define HM_STREAM_ALLTIME_TAG 0x1FFFFull    /* hour bucket of the alltime heatmap */
-#define HMS_SEL_EVERY_HOUR (1ull << 20)     /* extract selector: every hour bucket */
-enum { HMS_ST_OCCUPIED = 0, HMS_ST_OVERFLOW = 1, HMS_ST_CURSOR = 2, HMS_ST_HOURS = 4 /* min, max as u32 */ };
+#define HMS_EMPTY 0xFFFFFFFFFFFFFFFFull   /* empty hash-table key (hm_table.h) */
+enum {
+    HMS_ST_OCCUPIED = 0, HMS_ST_OVERFLOW = 1, HMS_ST_CURSOR = 2, HMS_ST_BUCKETS = 3, HMS_ST_BFULL = 4,
+    HMS_ST_EXOTIC = 5, HMS_ST_BMM = 6 /* min, max bucket of the batch as u32 */, HMS_ST_COUNT = 8
+};
+#define HMS_NOGROUP 0xFFFFFFFEu          /* kept points without a user group */
+#define HMS_ALLGROUPS 0xFFFFFFFFu        /* rollup over every group */
+#define HMS_UNDATED 0x50000000u          /* period word of points added without an hour */
+#define HMS_MAX_HOUR_OFFSET (1u << 28)   /* hours base .. base + 2^28 - 1 */
+#define HMS_TYPE_DAY 1u
+#define HMS_TYPE_MONTH 2u
+#define HMS_TYPE_YEAR 3u
+#define HMS_TYPE_ALLTIME 4u
+#define HMS_SKIP 0xFFFFFFFFu
+#define HMS_NO_BUCKET 0xFFFFFFFFu
 struct HmsTable {
     uint64_t* slots; /* capacity x {key, count} */
     uint64_t mask;   /* capacity - 1 (power of two) */
     unsigned long long* state;
 };
-void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, uint64_t tag_a,
-                             uint64_t tag_b, const HmsTable& t);
+struct HmsBuckets {
+    uint64_t* keys;  /* capacity x {group << 32 | period word}; the slot index is the bucket id */
+    uint64_t mask;
+};
+struct HmsBucketArgs {
+    const uint32_t* group;   /* NULL: HMS_NOGROUP */
+    const uint32_t* hour;    /* NULL: HMS_UNDATED */
+    const uint8_t* keep;
+    uint64_t n;
+    uint32_t base;
+    HmsBuckets buckets;
+    uint32_t* out;
+    unsigned long long* state;
+    unsigned long long* err_word;
+};
+struct HmsRollupArgs {
+    HmsTable from, to;
+    HmsBuckets buckets;
+    int cb, span, merge;
+    uint32_t base;
+    int64_t select;          /* -1, or the one period value kept */
+    unsigned long long* state;
+};
+struct HmsEmitArgs {
+    HmsTable t;
+    HmsBuckets buckets;
+    int cb, zmin, zmax;
+    uint32_t base;
+    uint64_t* keys_out;
+    uint64_t* counts_out;
+    uint32_t* groups_out;
+    uint32_t* periods_out;
+    uint64_t cap;
+    unsigned long long* cursor;
+};
+void hm_launch_stream_buckets(hipStream_t s, const HmsBucketArgs& a);
+void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int cb, uint64_t* keys, uint64_t* counts,
+                              unsigned long long* state);
+void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, bool from_count,
+                             uint64_t prefix, const HmsTable& t);
 void hm_launch_stream_init(hipStream_t s, const HmsTable& t);
+void hm_launch_stream_fill(hipStream_t s, uint64_t* p, uint64_t n, uint64_t v);
 void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to);
-void hm_launch_stream_hour_range(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
-                                 unsigned int* mm);
-void hm_launch_stream_hour_presence(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n,
-                                    uint32_t lo, uint8_t* present);
-void hm_launch_stream_hour_mask(hipStream_t s, const uint32_t* hour, const uint8_t* keep, uint64_t n, uint32_t h,
-                                uint8_t* mask);
-void hm_launch_stream_extract(hipStream_t s, const HmsTable& t, uint64_t sel, uint64_t* keys_out,
-                              uint64_t* counts_out, uint32_t* hours_out, uint32_t base, uint64_t cap,
-                              unsigned long long* cursor);
+void hm_launch_stream_rollup(hipStream_t s, const HmsRollupArgs& a);
+void hm_launch_stream_emit(hipStream_t s, const HmsEmitArgs& a);
 
 /* general count path (hm_general.hip): sort of 128-bit cell keys + zoom cascade */
 struct HmGenArgs {

@@ -8,7 +8,6 @@
 
 #include "hm_pipeline.h"
 
-#define HMS_EMPTY 0xFFFFFFFFFFFFFFFFull
 
 __device__ __forceinline__ uint64_t hms_hash(uint64_t k)
 {

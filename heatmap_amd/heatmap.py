@@ -182,15 +182,39 @@ def group_plan(user_id, keep=None) -> GroupPlan:
 # --------------------------------------------------------------------------
 
 class Cells:
-    """Every bin of every output row: labels[label[i]] | alltime | zoom[i]-delta
-    tile of (row[i], col[i]) -> {zoom[i]_row[i]_col[i]: value[i]}."""
+    """Every bin of every output row: labels[label[i]] | spans[span[i]] |
+    zoom[i]-delta tile of (row[i], col[i]) -> {zoom[i]_row[i]_col[i]: value[i]}.
+    The batch pipeline's only timespan label is 'alltime' (heatmap.py:62-63);
+    the streaming heatmap's rollups carry year / month / day labels too."""
 
-    def __init__(self, labels, label, zoom, row, col, value, delta):
+    def __init__(self, labels, label, zoom, row, col, value, delta, spans=("alltime",), span=None):
         self.labels, self.label, self.zoom, self.row, self.col, self.value = labels, label, zoom, row, col, value
         self.delta = delta
+        self.spans = list(spans)
+        self.span = np.zeros(np.asarray(zoom).size, np.int64) if span is None else np.asarray(span, np.int64)
 
     def __len__(self):
         return int(self.zoom.size)
+
+
+def concat_cells(parts, labels, delta) -> Cells:
+    """One Cells from per-timespan Cells (same labels and delta), keeping
+    each part's span labels."""
+    spans, span = [], []
+    for c in parts:
+        remap = []
+        for x in c.spans:
+            if x not in spans:
+                spans.append(x)
+            remap.append(spans.index(x))
+        span.append(np.asarray(remap, np.int64)[c.span])
+
+    def cat(name, dtype):
+        return np.concatenate([np.asarray(getattr(c, name), dtype) for c in parts]) if parts else np.zeros(0, dtype)
+
+    return Cells(labels, cat("label", np.int64), cat("zoom", np.int64), cat("row", np.int64), cat("col", np.int64),
+                 cat("value", np.float64), delta, spans or ["alltime"],
+                 np.concatenate(span) if span else np.zeros(0, np.int64))
 
 
 def _sum_by_cell(parts):
@@ -235,34 +259,19 @@ def _check_chain_window(zoom, row, col, zmax, d):
                     % (zz, rlo >> kk, rhi >> kk, clo >> kk, chi >> kk))
 
 
-def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None) -> Cells:
-    """The bins of build_heatmaps' rows from per-cell counts.
+def combine_cells(labels, all_cells, grouped_cells, zmax, d, span_label="alltime") -> Cells:
+    """The bins of one timespan's rows from its per-cell counts.
 
-    count_all(keep) -> (zoom, row, col, count) arrays of the kept points;
-    count_grouped(keep, gid) -> (group, zoom, row, col, count) per group id.
-    Both cover zooms delta+1 .. max_zoom_level+delta and are the only places
-    points are touched (the device in the product, the oracle in the CPU
-    tests).  Row layout: heatmap.py:55,85-90,120-126; 'all' weighting:
-    heatmap.py:64-70 applied level by level (module docstring)."""
-    mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
-    d = DETAIL_ZOOM_DELTA if delta is None else delta
-    zmax = mz + d
-    n = len(user_id)
-    keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool)
-    plan = group_plan(user_id, keep)
-    # every point is projected (and may raise) even when not kept, as
-    # dataframe_loader does (heatmap.py:27-29): count_all sees all points
-    nz, nr, nc, nn = count_all(keep)
-    nz, nr, nc = np.asarray(nz, np.int64), np.asarray(nr, np.int64), np.asarray(nc, np.int64)
+    all_cells = (zoom, row, col, n): every kept point; grouped_cells =
+    (group, zoom, row, col, count) per group id (group 0: the literal user id
+    'all', merged into the 'all' rows).  Row layout: heatmap.py:55,85-90,
+    120-126; 'all' weighting: heatmap.py:64-70 applied level by level (module
+    docstring)."""
+    nz, nr, nc, nn = (np.asarray(x, np.int64) for x in all_cells)
+    gg, gz, gr, gc, gn = (np.asarray(x, np.int64) for x in grouped_cells)
     _check_chain_window(nz, nr, nc, zmax, d)
-    if plan.grouped.any():
-        gg, gz, gr, gc, gn = count_grouped(plan.grouped, plan.gid)
-        gg = np.asarray(gg, np.int64)
-        gz, gr, gc, gn = (np.asarray(x, np.int64) for x in (gz, gr, gc, gn))
-    else:
-        gg = gz = gr = gc = gn = np.zeros(0, np.int64)
     # 'all' rows: per cell n, a (literal 'all'), U (other groups)
-    nv = np.stack([np.asarray(nn, np.int64), np.zeros(nz.size, np.int64), np.zeros(nz.size, np.int64)], 1)
+    nv = np.stack([nn, np.zeros(nz.size, np.int64), np.zeros(nz.size, np.int64)], 1)
     lit = gg == 0
     gv = np.stack([np.zeros(gz.size, np.int64), np.where(lit, gn, 0), np.where(lit, 0, gn)], 1)
     az, ar, ac, av = _sum_by_cell([(nz, nr, nc, nv), (gz, gr, gc, gv)])
@@ -274,18 +283,45 @@ def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=
     # user-group rows (the literal 'all' group is not a row of its own)
     us = (~lit) & (gz > d)
     label = np.concatenate([np.zeros(az.size, np.int64), gg[us]])
-    return Cells(plan.labels, label, np.concatenate([az, gz[us]]), np.concatenate([ar, gr[us]]),
-                 np.concatenate([ac, gc[us]]), np.concatenate([value_all, gn[us].astype(np.float64)]), d)
+    return Cells(labels, label, np.concatenate([az, gz[us]]), np.concatenate([ar, gr[us]]),
+                 np.concatenate([ac, gc[us]]), np.concatenate([value_all, gn[us].astype(np.float64)]), d,
+                 [span_label])
+
+
+def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None) -> Cells:
+    """The bins of build_heatmaps' rows from per-cell counts.
+
+    count_all(keep) -> (zoom, row, col, count) arrays of the kept points;
+    count_grouped(keep, gid) -> (group, zoom, row, col, count) per group id.
+    Both cover zooms delta+1 .. max_zoom_level+delta and are the only places
+    points are touched (the device in the product, the oracle in the CPU
+    tests)."""
+    mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
+    d = DETAIL_ZOOM_DELTA if delta is None else delta
+    zmax = mz + d
+    n = len(user_id)
+    keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool)
+    plan = group_plan(user_id, keep)
+    # every point is projected (and may raise) even when not kept, as
+    # dataframe_loader does (heatmap.py:27-29): count_all sees all points
+    allc = count_all(keep)
+    _check_chain_window(np.asarray(allc[0], np.int64), np.asarray(allc[1], np.int64),
+                        np.asarray(allc[2], np.int64), zmax, d)
+    if plan.grouped.any():
+        grp = count_grouped(plan.grouped, plan.gid)
+    else:
+        grp = tuple(np.zeros(0, np.int64) for _ in range(5))
+    return combine_cells(plan.labels, allc, grp, zmax, d)
 
 
 def cells_to_rows(cells: Cells) -> dict:
     """{row_id: {bin_id: float}} (heatmap.py:85-90,120-126)."""
     rows = {}
     d = cells.delta
-    labels = cells.labels
-    for g, z, r, c, v in zip(cells.label.tolist(), cells.zoom.tolist(), cells.row.tolist(), cells.col.tolist(),
-                             cells.value.tolist()):
-        rid = "%s|alltime|%d_%d_%d" % (labels[g], z - d, r >> d, c >> d)
+    labels, spans = cells.labels, cells.spans
+    for g, t, z, r, c, v in zip(cells.label.tolist(), cells.span.tolist(), cells.zoom.tolist(), cells.row.tolist(),
+                                cells.col.tolist(), cells.value.tolist()):
+        rid = "%s|%s|%d_%d_%d" % (labels[g], spans[t], z - d, r >> d, c >> d)
         rows.setdefault(rid, {})["%d_%d_%d" % (z, r, c)] = v
     return rows
 
@@ -301,11 +337,12 @@ def cells_to_table(cells: Cells):
     if len(cells) == 0:
         return pa.table({"id": pa.array([], pa.string()), "heatmap": pa.array([], pa.string())})
     tz, tr, tc = cells.zoom - d, cells.row >> d, cells.col >> d
-    o = np.lexsort((cells.col, cells.row, cells.zoom, tc, tr, tz, cells.label))
-    lab, z, r, c, v = cells.label[o], cells.zoom[o], cells.row[o], cells.col[o], cells.value[o]
+    o = np.lexsort((cells.col, cells.row, cells.zoom, tc, tr, tz, cells.span, cells.label))
+    lab, sp, z, r, c, v = cells.label[o], cells.span[o], cells.zoom[o], cells.row[o], cells.col[o], cells.value[o]
     tz, tr, tc = tz[o], tr[o], tc[o]
     head = np.ones(lab.size, dtype=bool)
-    head[1:] = (lab[1:] != lab[:-1]) | (tz[1:] != tz[:-1]) | (tr[1:] != tr[:-1]) | (tc[1:] != tc[:-1])
+    head[1:] = ((lab[1:] != lab[:-1]) | (sp[1:] != sp[:-1]) | (tz[1:] != tz[:-1]) | (tr[1:] != tr[:-1]) |
+                (tc[1:] != tc[:-1]))
     starts = np.flatnonzero(head)
     s = lambda a: pc.cast(pa.array(a), pa.string())  # noqa: E731
     # float repr of integer-valued counts below 1e16 is "<int>.0"; others via repr
@@ -323,7 +360,8 @@ def cells_to_table(cells: Cells):
     joined = pc.binary_join(pa.ListArray.from_arrays(pa.array(offsets), pieces), ", ")
     heat = pc.binary_join_element_wise(pa.scalar("{"), joined, pa.scalar("}"), "")
     names = pa.array(cells.labels, pa.string()).take(pa.array(lab[starts]))
-    ids = pc.binary_join_element_wise(names, pa.scalar("alltime"),
+    spans = pa.array(cells.spans, pa.string()).take(pa.array(sp[starts]))
+    ids = pc.binary_join_element_wise(names, spans,
                                       pc.binary_join_element_wise(s(tz[starts]), s(tr[starts]), s(tc[starts]), "_"),
                                       KEY_SEPERATOR)
     return pa.table({"id": ids, "heatmap": heat})

@@ -1,42 +1,111 @@
 """Streaming micro-batches merged into a heatmap resident in HBM (BASELINE
 config 5) -- host side of hm_stream_* (include/heatmap_amd.h).
 
-The reference recomputes its pyramid per Spark job (heatmap.py:152-158) under
-the one live timespan label 'alltime' (heatmap.py:62-63).  StreamingHeatmap
-keeps that alltime heatmap plus one bucket per epoch hour in a device hash
-table; each add() runs the count pyramid on the batch and folds its cells in,
-so a caller sees the same counts as one hm_count over every point so far.
+The reference recomputes its pyramid per Spark job (heatmap.py:152-158) and
+keys every bin by user group and timespan label (heatmap.py:54-55,62-75; only
+'alltime' is live there, the year/month/day labels of build_timespan_label,
+heatmap.py:38-52, are commented out).  StreamingHeatmap keeps one device
+bucket per (user group, epoch hour); each add() runs ONE count pass over the
+batch (however many hours and groups it holds) and folds its cells in.  Every
+label is a device rollup of the hour buckets:
+
+  counts(ALLTIME) / hourly()   per-cell counts of every kept point so far
+  rows(timespan)               build_heatmaps' rows, {id: {bin: count}}, for
+                               'alltime', 'year', 'month' or 'day' (UTC dates
+                               of the epoch hours), with the reference's user
+                               groups and level-by-level 'all' weighting
+                               (heatmap.heatmap.combine_cells)
+
+so a caller sees the same rows as heatmap.assemble_rows over every point so
+far, restricted to the label's period.
 """
 from __future__ import annotations
 
 import ctypes
+import datetime
 
 import numpy as np
 
 from . import _lib, device
+from . import heatmap as _hm
 
 ALLTIME = -1
 EACH_HOUR = -2
-MAX_HOURS = 131071
+MAX_HOURS = 1 << 28
+SPANS = {"hour": _lib.HM_SPAN_HOUR, "day": _lib.HM_SPAN_DAY, "month": _lib.HM_SPAN_MONTH,
+         "year": _lib.HM_SPAN_YEAR, "alltime": _lib.HM_SPAN_ALLTIME}
+NOGROUP = 0xFFFFFFFE      # kept points whose user id makes no group ('x*', or no user ids)
+ALLGROUPS = 0xFFFFFFFF    # merged rollups
+
+
+def span_label(timespan: str, period: int) -> str:
+    """build_timespan_label (heatmap.py:38-52) of a rollup period: days since
+    1970-01-01, year*12 + month - 1, or the year."""
+    if timespan == "alltime":
+        return "alltime"
+    if timespan == "day":
+        d = datetime.date(1970, 1, 1) + datetime.timedelta(days=int(period))
+    elif timespan == "month":
+        d = datetime.date(int(period) // 12, int(period) % 12 + 1, 1)
+    elif timespan == "year":
+        d = datetime.date(int(period), 1, 1)
+    else:
+        raise ValueError("no reference timespan label for %r" % (timespan,))
+    return _hm.build_timespan_label(timespan, d)
 
 
 class StreamingHeatmap:
     def __init__(self, zmin: int = 0, zmax: int = 18, base_hour: int = 0, initial_cells: int = 1 << 20,
-                 device_index: int = 0):
+                 device_index: int = 0, max_buckets: int = 0):
         self._torch = device._torch()
         self.ctx = device.context(device_index)
         self.device_index = device_index
         self.zmin, self.zmax, self.base_hour = int(zmin), int(zmax), int(base_hour)
+        self.labels = ["all"]          # group id -> row-key group (0: the literal user id 'all')
+        self._index = {"all": 0}
         p = ctypes.c_void_p()
         rc = self.ctx.L.hm_stream_create(self.ctx.ptr, self.zmin, self.zmax, self.base_hour, int(initial_cells),
-                                         ctypes.byref(p))
+                                         int(max_buckets), ctypes.byref(p))
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
         self.ptr = p
 
-    def add(self, lat, lon, keep=None, hour=None):
-        """Fold one micro-batch in.  hour: uint32 epoch hours (one per point) or
-        None (alltime only).  Projection errors raise as hm_count's do."""
+    # ------------------------------------------------------------------ input
+
+    def _groups(self, user_id, keep, n):
+        """Persistent group ids of a batch's user ids (heatmap.py:64-70): kept
+        points only are validated, as heatmap.group_plan does."""
+        if len(user_id) != n:
+            raise ValueError("user_id must have one entry per point")
+        if keep is None:
+            kb = np.ones(n, dtype=bool)
+        else:
+            kb = (keep.cpu().numpy() if hasattr(keep, "cpu") else np.asarray(keep)).astype(bool)
+        codes, uniques = _hm._factorize(user_id)
+        kept_codes = np.unique(codes[kb])
+        if kept_codes.size and kept_codes[0] < 0:
+            raise TypeError("'NoneType' object is not subscriptable")
+        lut = np.full(len(uniques) + 1, NOGROUP, dtype=np.uint32)   # code -1 -> last entry
+        for c in kept_codes.tolist():
+            u = uniques[c]
+            if not isinstance(u, str):
+                raise TypeError("user id %r is not a string" % (u,))
+            if _hm.KEY_SEPERATOR in u:
+                raise ValueError("user id %r contains the key separator %r" % (u, _hm.KEY_SEPERATOR))
+            if u[:1] == "x":
+                continue
+            label = "route" if u[:3] == "rt-" else u
+            if label not in self._index:
+                self._index[label] = len(self.labels)
+                self.labels.append(label)
+            lut[c] = self._index[label]
+        return lut[codes]
+
+    def add(self, lat, lon, keep=None, hour=None, user_id=None, group=None):
+        """Fold one micro-batch in.  hour: uint32 epoch hours (one per point)
+        or None (undated: alltime only).  user_id: the reference's user id per
+        point (host strings), or group: explicit uint32 group ids.  Projection
+        errors raise as hm_count's do; a failing batch changes no counts."""
         torch = self._torch
         self.ctx.bind_stream()
         la = device._dev(lat, torch.float64, self.device_index)
@@ -44,67 +113,130 @@ class StreamingHeatmap:
         n = la.numel()
         if lo.numel() != n:
             raise ValueError("lat and lon must have the same length")
+        if user_id is not None and group is not None:
+            raise ValueError("pass user_id or group, not both")
+        if user_id is not None:
+            group = self._groups(user_id, keep, n)
+
+        def u32(x, what):
+            if x is None:
+                return None
+            if not isinstance(x, torch.Tensor):
+                x = torch.from_numpy(np.ascontiguousarray(np.asarray(x, dtype=np.uint32)).view(np.int32))
+            t = device._dev(x, torch.int32, self.device_index)  # uint32 bits
+            if t.numel() != n:
+                raise ValueError("%s must have one entry per point" % what)
+            return t
+
+        hr = u32(hour, "hour")
+        gr = u32(group, "group")
         kp = device._dev(keep, torch.uint8, self.device_index) if keep is not None else None
-        hr = None
-        if hour is not None:
-            h = hour
-            if not isinstance(h, torch.Tensor):
-                h = torch.from_numpy(np.ascontiguousarray(np.asarray(h, dtype=np.uint32)).view(np.int32))
-            hr = device._dev(h, torch.int32, self.device_index)  # uint32 bits
-            if hr.numel() != n:
-                raise ValueError("hour must have one entry per point")
         if kp is not None and kp.numel() != n:
             raise ValueError("keep must have one entry per point")
-        rc = self.ctx.L.hm_stream_add(self.ptr, device._ptr(la), device._ptr(lo), device._ptr(kp), device._ptr(hr), n)
+        rc = self.ctx.L.hm_stream_add(self.ptr, device._ptr(la), device._ptr(lo), device._ptr(kp), device._ptr(hr),
+                                      device._ptr(gr), n)
         if rc != _lib.HM_OK:
             idx, kind = self.ctx.last_error()
             _lib.raise_for(rc, idx)
 
+    # ---------------------------------------------------------------- queries
+
     def cells(self):
-        """(occupied table slots over every bucket, table capacity)"""
-        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
-        self.ctx.L.hm_stream_cells(self.ptr, ctypes.byref(a), ctypes.byref(b))
+        """(occupied cell-table slots, table capacity)"""
+        a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self.ctx.L.hm_stream_cells(self.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
         return a.value, b.value
 
-    def extract_device(self, hour: int = ALLTIME):
-        """(n, keys, counts, hours) as torch CUDA tensors (hm_count key layout)."""
+    def buckets(self) -> int:
+        """(group, period) buckets in use, rollup labels included"""
+        c = ctypes.c_int64(0)
+        self.ctx.L.hm_stream_cells(self.ptr, None, None, ctypes.byref(c))
+        return c.value
+
+    def rollup_device(self, timespan: str = "alltime", merge_groups: bool = True, select: int = -1):
+        """(n, keys, counts, groups, periods) as torch CUDA tensors: the cells
+        of `timespan` summed per (group, period), or over every group."""
         torch = self._torch
         self.ctx.bind_stream()
+        span = SPANS[timespan]
         cap = max(1024, self.cells()[0])
         dev = "cuda:%d" % self.device_index
         while True:
             keys = torch.empty(cap, dtype=torch.int64, device=dev)
             counts = torch.empty(cap, dtype=torch.int64, device=dev)
-            hours = torch.empty(cap, dtype=torch.int32, device=dev) if hour == EACH_HOUR else None
+            groups = torch.empty(cap, dtype=torch.int32, device=dev)
+            periods = torch.empty(cap, dtype=torch.int32, device=dev)
             n = ctypes.c_int64(0)
-            rc = self.ctx.L.hm_stream_extract(self.ptr, int(hour), device._ptr(keys), device._ptr(counts),
-                                              device._ptr(hours), cap, ctypes.byref(n))
-            if rc == _lib.HM_E_CAPACITY:
+            rc = self.ctx.L.hm_stream_rollup(self.ptr, span, int(bool(merge_groups)), int(select), device._ptr(keys),
+                                             device._ptr(counts), device._ptr(groups), device._ptr(periods), cap,
+                                             ctypes.byref(n))
+            if rc == _lib.HM_E_CAPACITY and n.value > cap:
                 cap = n.value + 1024
                 continue
             if rc != _lib.HM_OK:
                 _lib.raise_for(rc)
-            return n.value, keys, counts, hours
+            return n.value, keys, counts, groups, periods
+
+    def rollup(self, timespan: str = "alltime", merge_groups: bool = True, select: int = -1):
+        """Host arrays (group u32, period u32, zoom, row, col, count)."""
+        n, keys, counts, groups, periods = self.rollup_device(timespan, merge_groups, select)
+        z, r, c = device.decode_keys(keys[:n].cpu().numpy().view(np.uint64))
+        return (groups[:n].cpu().numpy().view(np.uint32), periods[:n].cpu().numpy().view(np.uint32), z, r, c,
+                counts[:n].cpu().numpy())
+
+    def extract_device(self, hour: int = ALLTIME):
+        """(n, keys, counts, hours) as torch CUDA tensors (hm_count key
+        layout), summed over groups: hour = ALLTIME, EACH_HOUR or one hour."""
+        if hour == ALLTIME:
+            n, k, c, _, _ = self.rollup_device("alltime")
+            return n, k, c, None
+        n, k, c, _, p = self.rollup_device("hour", True, -1 if hour == EACH_HOUR else int(hour))
+        return n, k, c, (p if hour == EACH_HOUR else None)
 
     def counts(self, hour: int = ALLTIME) -> device.Counts:
-        """Cells of one bucket (ALLTIME or an epoch hour) as host arrays."""
+        """Cells of every kept point (ALLTIME) or of one epoch hour."""
         n, keys, counts, _ = self.extract_device(hour)
-        k = keys[:n].cpu().numpy().view(np.uint64)
-        z, r, c = device.decode_keys(k)
+        z, r, c = device.decode_keys(keys[:n].cpu().numpy().view(np.uint64))
         return device.Counts(z, r, c, counts[:n].cpu().numpy(), 0, [])
 
     def hourly(self):
-        """{epoch hour: Counts} for every non-empty hour bucket."""
-        n, keys, counts, hours = self.extract_device(EACH_HOUR)
-        k = keys[:n].cpu().numpy().view(np.uint64)
-        cnt = counts[:n].cpu().numpy()
-        hr = hours[:n].cpu().numpy().view(np.uint32)
+        """{epoch hour: Counts} for every non-empty hour."""
+        _, hr, z, r, c, cnt = self.rollup("hour")
         out = {}
         for h in np.unique(hr).tolist():
             m = hr == h
-            z, r, c = device.decode_keys(k[m])
-            out[int(h)] = device.Counts(z, r, c, cnt[m], 0, [])
+            out[int(h)] = device.Counts(z[m], r[m], c[m], cnt[m], 0, [])
         return out
+
+    def heatmap_cells(self, timespan: str = "alltime", max_zoom_level=None, delta=None) -> "_hm.Cells":
+        """The bins of build_heatmaps' rows for `timespan` ('alltime', 'year',
+        'month', 'day'): every period of the span, each with its label."""
+        d = _hm.DETAIL_ZOOM_DELTA if delta is None else int(delta)
+        mz = self.zmax - d if max_zoom_level is None else int(max_zoom_level)
+        if mz + d != self.zmax or self.zmin > d + 1:
+            raise ValueError("rows need zooms %d..%d; the stream holds %d..%d" % (d + 1, mz + d, self.zmin, self.zmax))
+        if timespan not in ("alltime", "year", "month", "day"):
+            raise ValueError("timespan must be 'alltime', 'year', 'month' or 'day'")
+        _, ap, az, ar, ac, an = self.rollup(timespan, merge_groups=True)
+        gg, gp, gz, gr, gc, gn = self.rollup(timespan, merge_groups=False)
+        grouped = gg != NOGROUP
+        gg, gp, gz, gr, gc, gn = gg[grouped], gp[grouped], gz[grouped], gr[grouped], gc[grouped], gn[grouped]
+        parts = []
+        for p in np.unique(ap).tolist():
+            m, q = ap == p, gp == p
+            parts.append(_hm.combine_cells(self.labels, (az[m], ar[m], ac[m], an[m]),
+                                           (gg[q].astype(np.int64), gz[q], gr[q], gc[q], gn[q]), mz + d, d,
+                                           span_label(timespan, p)))
+        return _hm.concat_cells(parts, self.labels, d)
+
+    def rows(self, timespan: str = "alltime", max_zoom_level=None, delta=None) -> dict:
+        """{row_id: {bin_id: float}} as build_heatmaps would give over every
+        point so far, row ids '<group>|<timespan label>|<tile>'."""
+        return _hm.cells_to_rows(self.heatmap_cells(timespan, max_zoom_level, delta))
+
+    def table(self, timespan: str = "alltime", max_zoom_level=None, delta=None):
+        """The same rows as a pyarrow Table(id, heatmap JSON)."""
+        return _hm.cells_to_table(self.heatmap_cells(timespan, max_zoom_level, delta))
 
     def close(self):
         if getattr(self, "ptr", None):

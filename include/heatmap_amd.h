@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 2
+#define HM_ABI_VERSION 3
 
 /* status / per-point error kinds */
 #define HM_OK 0
@@ -150,31 +150,47 @@ int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_sta
 
 /* Streaming: micro-batches folded into a heatmap resident in HBM (BASELINE
  * config 5).  The reference recomputes the pyramid per
- * Spark job (heatmap.py:152-158) under the single timespan label 'alltime'
- * (heatmap.py:62-63); a stream keeps that alltime heatmap plus one bucket per
- * epoch hour (uint32 hours since 1970, hour = unix_seconds / 3600).
+ * Spark job (heatmap.py:152-158) and keys each bin by user group and timespan
+ * label (heatmap.py:38-75, only 'alltime' live); a stream keeps per (group,
+ * epoch hour) buckets (hour = unix_seconds / 3600, uint32) and answers every
+ * label -- hour, day, month, year (UTC calendar), alltime -- as a rollup.
  *   hm_stream_create  zooms [zmin, zmax] (zmax <= HM_MAX_ZOOM); hours
- *                     base_hour .. base_hour + HM_STREAM_MAX_HOURS - 1;
- *                     initial_cells sizes the table (it grows as needed).
+ *                     base_hour .. base_hour + 2^28 - 1; initial_cells sizes
+ *                     the cell table (it grows); max_buckets (0: 2^20) bounds
+ *                     the distinct (group, hour) and rollup-label buckets.
  *   hm_stream_add     hm_count semantics per point (projection errors, keep);
- *                     hour: uint32[n] (device) or NULL (alltime only).  The
- *                     kept points of one batch may span at most
- *                     HM_STREAM_MAX_SPAN hours; each distinct hour costs one
- *                     count pyramid over the batch (batches are time-ordered).
+ *                     hour: uint32[n] (device) or NULL (undated: alltime
+ *                     only); group: uint32[n] (device, < 0xFFFFFFFE) or NULL
+ *                     (no group).  One count pass per batch however many hours
+ *                     and groups it holds; a failing batch changes no counts.
+ *   hm_stream_rollup  cells of span HM_SPAN_* summed per (group, period), or
+ *                     over every group (merge_groups: group = 0xFFFFFFFF);
+ *                     select = -1 or the one period wanted.  Periods: epoch
+ *                     hour, days since 1970-01-01, year*12 + month - 1, year,
+ *                     0 (alltime).  groups_out/periods_out may be NULL.  Keys
+ *                     in hm_count's layout, unspecified order; HM_E_CAPACITY
+ *                     with *n_out = cells needed when capacity is too small.
  *   hm_stream_extract hour = HM_STREAM_ALLTIME, HM_STREAM_EACH_HOUR (hours_out
- *                     receives each cell's hour) or one epoch hour; keys in
- *                     hm_count's layout, unspecified order.  HM_E_CAPACITY
- *                     with *n_out = cells needed when capacity is too small. */
+ *                     receives each cell's hour) or one epoch hour, summed
+ *                     over groups (a rollup). */
 #define HM_STREAM_ALLTIME (-1)
 #define HM_STREAM_EACH_HOUR (-2)
-#define HM_STREAM_MAX_HOURS 131071
-#define HM_STREAM_MAX_SPAN 65536
+#define HM_STREAM_MAX_HOURS (1 << 28)
+#define HM_SPAN_HOUR 0
+#define HM_SPAN_DAY 1
+#define HM_SPAN_MONTH 2
+#define HM_SPAN_YEAR 3
+#define HM_SPAN_ALLTIME 4
 typedef struct hm_stream hm_stream;
-int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_t initial_cells, hm_stream** out);
+int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_t initial_cells, int64_t max_buckets,
+                     hm_stream** out);
 int hm_stream_add(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, const uint32_t* hour,
-                  int64_t n);
-/* occupied table slots over all buckets, and the table capacity */
-int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity);
+                  const uint32_t* group, int64_t n);
+/* occupied cell-table slots, the table capacity, and the buckets in use */
+int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity, int64_t* buckets);
+int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_t select, uint64_t* keys_out,
+                     uint64_t* counts_out, uint32_t* groups_out, uint32_t* periods_out, int64_t capacity,
+                     int64_t* n_out);
 int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out, uint64_t* counts_out, uint32_t* hours_out,
                       int64_t capacity, int64_t* n_out);
 int hm_stream_destroy(hm_stream* s);

@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if n not in exported]
     assert not missing, missing
     assert set(_lib.EXPORTS) == set(declared())
-    assert L.hm_abi_version() == _lib.HM_ABI_VERSION == 2
+    assert L.hm_abi_version() == _lib.HM_ABI_VERSION == 3
     assert _lib.status_string(_lib.HM_E_DOMAIN) == "math domain error"
     assert _lib.status_string(_lib.HM_E_NAN) == "cannot convert float NaN to integer"
 
@@ -74,7 +74,7 @@ L = _lib.load()
 p = ctypes.c_void_p()
 st = L.hm_ctx_create(ctypes.byref(p), 0, None)
 print("CTX", st)
-print("STREAM ARG", L.hm_stream_create(None, 0, 18, 0, 0, ctypes.byref(p)))
+print("STREAM ARG", L.hm_stream_create(None, 0, 18, 0, 0, 0, ctypes.byref(p)))
 """
     r = subprocess.run([sys.executable, "-c", code], cwd=REPO, capture_output=True, text=True, timeout=300)
     if "SKIP" in r.stdout:

@@ -1,16 +1,23 @@
 """Streaming micro-batches into a resident heatmap (hm_stream_*, BASELINE config 5)
-vs the oracle: after any sequence of add() calls, the alltime bucket equals one
-oracle count over every kept point so far, and each hour bucket equals the
-oracle count over that hour's kept points.  Parity anchor: the oracle is pinned
-to the reference's goldens (tests/test_oracle.py); the hour buckets have no
-reference counterpart (its timespan labels other than 'alltime' are dead code,
-heatmap.py:62-63), so they are checked for consistency with the same oracle."""
+vs the oracle: after any sequence of add() calls, the alltime rollup equals one
+oracle count over every kept point so far, each hour equals the oracle count
+over that hour's kept points, and rows() equals the oracle's literal
+restatement of build_heatmaps (oracle.build_heatmap_rows, pinned to the
+reference's row goldens by tests/test_oracle.py) over every point so far --
+for 'alltime' and, restricted to each period with the period's
+build_timespan_label (heatmap.py:38-52), for 'year', 'month' and 'day' (those
+labels are dead code in the reference, heatmap.py:62-63: parity for them is
+pinned only through the alltime rows and the label function)."""
+import datetime
+import json
+
 import numpy as np
 import pytest
 
 from oracle import oracle
-from heatmap_amd import _lib, synth
-from heatmap_amd.stream import ALLTIME, StreamingHeatmap
+from heatmap_amd import _lib, heatmap, synth
+from heatmap_amd.device import Counts
+from heatmap_amd.stream import ALLTIME, NOGROUP, StreamingHeatmap
 
 pytestmark = pytest.mark.gpu
 BASE = 480000  # epoch hour (2024-10-04)
@@ -55,7 +62,7 @@ def test_stream_matches_oracle(gpu, kind, zmin, zmax, initial):
     h0 = int(np.unique(hour)[0])
     _same(s.counts(h0), oracle.count(lat, lon, keep & (hour == h0).astype(np.uint8), zmin, zmax))
     cells, cap = s.cells()
-    assert cells == sum(len(c.count) for c in hourly.values()) + len(s.counts(ALLTIME).count)
+    assert cells == sum(len(c.count) for c in hourly.values())   # one bucket per hour; labels are rollups
     assert cells * 8 <= cap * 5
     s.close()
 
@@ -103,4 +110,88 @@ def test_stream_single_hour_batches(gpu):
     _same(s.counts(ALLTIME), oracle.count(lat2, lon2, keep2, 2, 17))
     for h, c in s.hourly().items():
         _same(c, oracle.count(lat2, lon2, keep2 & (hour2 == h).astype(np.uint8), 2, 17))
+    s.close()
+
+
+def _reference_rows(lat, lon, keep, users, mz, d, label="alltime"):
+    src = np.where(keep.astype(bool), "mobile", "background")
+    rows = oracle.build_heatmap_rows(lat, lon, src, users, mz, d)
+    return {k.replace("|alltime|", "|%s|" % label, 1): v for k, v in rows.items()}
+
+
+USERS = ["all", "u1", "u2", "xhidden", "rt-7", "rt-9", "u3"]
+
+
+def test_stream_rows_match_reference(gpu):
+    """rows() over several multi-hour, multi-user batches == build_heatmaps over
+    the concatenated points (alltime), and per period for year/month/day.  The
+    hours cross a day, month and year boundary (2024-12-31 21:00 .. 2025-01-01
+    03:00 UTC); batches repeat hours and users, so buckets are shared."""
+    mz, d = 9, 5
+    h0 = int(datetime.datetime(2024, 12, 31, 21, tzinfo=datetime.timezone.utc).timestamp()) // 3600
+    rng = np.random.default_rng(5)
+    bs = []
+    for b in range(4):
+        n = 1500
+        lat, lon = synth.generate("hotspots", n, seed=21, start=b * n)
+        keep = (rng.random(n) > 0.15).astype(np.uint8)
+        hour = (h0 + rng.integers(0, 7, n)).astype(np.uint32)
+        users = [USERS[i] for i in rng.integers(0, len(USERS), n)]
+        bs.append((lat, lon, keep, hour, users))
+    s = StreamingHeatmap(0, mz + d, base_hour=h0 - 100)
+    for lat, lon, keep, hour, users in bs:
+        s.add(lat, lon, keep, hour, user_id=users)
+    lat = np.concatenate([b[0] for b in bs])
+    lon = np.concatenate([b[1] for b in bs])
+    keep = np.concatenate([b[2] for b in bs])
+    hour = np.concatenate([b[3] for b in bs])
+    users = sum((b[4] for b in bs), [])
+    assert s.rows("alltime") == _reference_rows(lat, lon, keep, users, mz, d)
+    # the device row table (ids + heatmap JSON) carries the same rows
+    t = s.table("alltime")
+    got = {i: json.loads(h) for i, h in zip(t.column("id").to_pylist(), t.column("heatmap").to_pylist())}
+    assert got == _reference_rows(lat, lon, keep, users, mz, d)
+    day = hour // 24
+    dates = [datetime.date(1970, 1, 1) + datetime.timedelta(days=int(x)) for x in day]
+    for span in ("day", "month", "year"):
+        key = np.array([heatmap.build_timespan_label(span, x) for x in dates])
+        want = {}
+        for lab in np.unique(key).tolist():
+            m = key == lab
+            want.update(_reference_rows(lat[m], lon[m], keep[m], [u for u, t in zip(users, m) if t], mz, d, lab))
+        got = s.rows(span)
+        assert got == want, span
+        assert len({k.split("|")[1] for k in got}) == 2   # the hours span two days, months and years
+    # group rollups: every group's alltime cells == the oracle count of its points
+    g, p, z, r, c, cnt = s.rollup("alltime", merge_groups=False)
+    for lab in ("u1", "route"):
+        gid = s.labels.index(lab)
+        pts = np.array([(u == lab or (lab == "route" and u.startswith("rt-"))) for u in users]) & (keep == 1)
+        ref = oracle.count(lat, lon, pts.astype(np.uint8), 0, mz + d)
+        m = g == gid
+        _same(Counts(z[m], r[m], c[m], cnt[m], 0, []), ref)
+    # x* users have no group of their own but are in every 'all' count
+    assert (g == NOGROUP).any()
+    s.close()
+
+
+def test_stream_batch_is_atomic(gpu):
+    """A batch whose SECOND hour holds a kept point outside the square (lon 200)
+    raises and changes no counts (one count pass, checked before insertion)."""
+    lat, lon = synth.generate("hotspots", 4000, seed=3)
+    hour = np.full(4000, BASE, np.uint32)
+    hour[2000:] += 1
+    s = StreamingHeatmap(0, 16, base_hour=BASE)
+    s.add(lat, lon, None, hour, user_id=["u%d" % (i % 5) for i in range(4000)])
+    before = s.counts().sorted()
+    lon2 = lon.copy()
+    lon2[3000] = 200.0
+    with pytest.raises(_lib.DevicePathUnsupported):
+        s.add(lat, lon2, None, hour, user_id=["u%d" % (i % 5) for i in range(4000)])
+    with pytest.raises(_lib.DevicePathUnsupported):   # one hour: the hm_count path
+        s.add(lat, lon2, None, np.full(4000, BASE + 5, np.uint32))
+    after = s.counts().sorted()
+    for k in ("zoom", "row", "col", "count"):
+        assert np.array_equal(getattr(before, k), getattr(after, k))
+    assert sorted(s.hourly()) == [BASE, BASE + 1]
     s.close()
