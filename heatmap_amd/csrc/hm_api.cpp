@@ -536,35 +536,34 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             HIPCHK(hipMemsetAsync(hist, 0, F * 4, s));
             if (n > 0) hm_launch_sample_digits(s, a, stride, hist);
             HIPCHK(hipGetLastError());
-            /* pinned host scratch: hist [F] | caps [FS] | bases [FS] | smask [F] */
-            uint32_t* hh = ctx->host_aux;
-            uint32_t* hc = hh + HM_MAX_F1;
+            /* pinned host scratch (the overflow retry): caps [FS] | bases [FS] */
+            uint32_t* hc = ctx->host_aux + HM_MAX_F1;
             uint32_t* hb = hc + HM_MAX_F1 * HM_L1_SHARDS;
-            uint8_t* hm = (uint8_t*)(hb + HM_MAX_F1 * HM_L1_SHARDS);
-            HIPCHK(hipMemcpyAsync(hh, hist, F * 4, hipMemcpyDeviceToHost, s));
-            HIPCHK(hipStreamSynchronize(s));
-            for (int d = 0; d < F; d++) {
-                const double est = (double)hh[d] * (double)stride;
-                const int ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
-                hm[d] = (uint8_t)(ns - 1);
-                const double e = est / ns;
-                const uint32_t c = (uint32_t)std::min(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) + 2.0 * HM_T1);
-                for (int sh = 0; sh < HM_L1_SHARDS; sh++) hc[d * HM_L1_SHARDS + sh] = sh < ns ? c : 0u;
-            }
-            HIPCHK(hipMemcpyAsync(smask, hm, F, hipMemcpyHostToDevice, s));
+            /* the region sizes are computed on the device (k_l1_sizes); the key
+             * buffer takes the host's bound of their total: est sums to at
+             * most nn, at most M (digit, shard) entries are non-empty, and
+             * sum sqrt(e stride) <= sqrt(M nn stride) (Cauchy-Schwarz) */
+            const double nn = (double)n + (double)F * (double)stride;
+            const double M = F + std::min((double)F, nn / (64.0 * HM_T1)) * (HM_L1_SHARDS - 1);
+            const double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 + 1024.0;
+            if (bound >= (double)0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
+            hm_launch_l1_sizes(s, hist, F, stride, rcap, rbase, smask);
+            HIPCHK(hipGetLastError());
             void* kout = nullptr;
-            uint64_t total_cap = 0;
+            uint64_t total_cap = (uint64_t)bound;
             for (int attempt = 0;; attempt++) {
-                total_cap = 0;
-                for (int i = 0; i < FS; i++) {
-                    hb[i] = (uint32_t)total_cap;
-                    total_cap += hc[i];
+                if (attempt > 0) {
+                    total_cap = 0;
+                    for (int i = 0; i < FS; i++) {
+                        hb[i] = (uint32_t)total_cap;
+                        total_cap += hc[i];
+                    }
+                    if (total_cap >= 0xFFF00000ull) return HM_FALLBACK;
+                    HIPCHK(hipMemcpyAsync(rcap, hc, FS * 4, hipMemcpyHostToDevice, s));
+                    HIPCHK(hipMemcpyAsync(rbase, hb, FS * 4, hipMemcpyHostToDevice, s));
                 }
-                if (total_cap >= 0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
                 ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (total_cap + 8) * (V.out16 ? 2 : 4), kout);
                 a.keys_out = kout;
-                HIPCHK(hipMemcpyAsync(rcap, hc, FS * 4, hipMemcpyHostToDevice, s));
-                HIPCHK(hipMemcpyAsync(rbase, hb, FS * 4, hipMemcpyHostToDevice, s));
                 HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
                 HIPCHK(hipMemsetAsync(ctx->state + ST_OVERFLOW, 0, 8, s));
                 HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, 16, s));   /* ST_REDO, ST_REDO_OUT */
@@ -592,9 +591,25 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     hm_launch_redo(s, ra, redo_cap);
                     HIPCHK(hipGetLastError());
                 }
+                if (!from_tiles) {
+                    /* the deferred points, resolved exactly, as tile input; the
+                     * launch covers the list's capacity and reads its length
+                     * on the device (no host round trip) */
+                    HmPart1Args b = a;
+                    b.lat = nullptr;
+                    b.lon = nullptr;
+                    b.rows_in = redo_rows;
+                    b.cols_in = redo_cols;
+                    b.keep = nullptr;
+                    b.n = (int64_t)redo_cap;
+                    b.n_dev = ctx->state + ST_REDO_OUT;
+                    hm_launch_part1(s, b, (uint32_t)((redo_cap + HM_T1 - 1) / HM_T1), V.out16, 1);
+                    HIPCHK(hipGetLastError());
+                }
                 if ((st = read_state(ctx))) return st;
                 if ((st = take_error(ctx))) return st;
                 const uint64_t nredo = ctx->host_state[ST_REDO];
+                ctx->last_slow = (int64_t)nredo;
                 if (!from_tiles && nredo > redo_cap) {
                     /* adversarial input (mostly polar / guard band): redo the
                      * level with the exact chain fused into the kernel */
@@ -603,22 +618,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     HIPCHK(hipMemsetAsync(xl.count, 0, 8, s));
                     hm_launch_part1(s, a, tiles_in, V.out16, 2);
                     HIPCHK(hipGetLastError());
-                } else if (!from_tiles && ctx->host_state[ST_REDO_OUT]) {
-                    /* the deferred points, resolved exactly, as tile input */
-                    const uint64_t nres = ctx->host_state[ST_REDO_OUT];
-                    HmPart1Args b = a;
-                    b.lat = nullptr;
-                    b.lon = nullptr;
-                    b.rows_in = redo_rows;
-                    b.cols_in = redo_cols;
-                    b.keep = nullptr;
-                    b.n = (int64_t)nres;
-                    hm_launch_part1(s, b, (uint32_t)((nres + HM_T1 - 1) / HM_T1), V.out16, 1);
-                    HIPCHK(hipGetLastError());
+                    if ((st = read_state(ctx))) return st;
+                    if ((st = take_error(ctx))) return st;
                 }
-                ctx->last_slow = (int64_t)nredo;
-                if ((st = read_state(ctx))) return st;
-                if ((st = take_error(ctx))) return st;
                 if (!ctx->host_state[ST_OVERFLOW]) break;
                 /* a region overflowed: fill[] now holds the exact sizes (the
                  * shard of every tile is fixed by its block id) */
@@ -1169,9 +1171,13 @@ struct hm_stream {
     uint32_t base = 0;
     HmsTable t{};                         /* cells */
     HmsBuckets bk{};                      /* (group, period) buckets */
-    uint64_t occupied = 0, nbuckets = 0;
+    uint32_t *bflag = nullptr, *blist = nullptr, *bloc = nullptr; /* per bucket: last batch, list, run */
+    uint32_t epoch = 0;
+    uint64_t occupied = 0, nbuckets = 0;  /* occupied: exact, or an upper bound while stale */
+    bool stale = false;
     unsigned long long* hstate = nullptr; /* pinned mirror of t.state */
     Buf bids, rec, bkeys, bcounts;        /* per-batch scratch */
+    Buf plat, plon, pkeep, pstart, pcnt;  /* partition path: bucket-contiguous batch */
     int64_t bcap = 0, rcap = 0;           /* cells bkeys/bcounts, records rec hold */
     Buf rslots;                           /* rollup table */
 };
@@ -1183,7 +1189,17 @@ static int stream_sync_state(hm_stream* s)
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
     s->occupied = s->hstate[HMS_ST_OCCUPIED];
     s->nbuckets = s->hstate[HMS_ST_BUCKETS];
+    s->stale = false;
     return s->hstate[HMS_ST_OVERFLOW] ? HM_E_CAPACITY : HM_OK;
+}
+
+/* after an insert of m cells: the occupancy grows by at most m; the exact
+ * count is read at the next sync (no host round trip per batch) */
+static int stream_inserted(hm_stream* s, uint64_t m)
+{
+    s->occupied += m;
+    s->stale = true;
+    return HM_OK;
 }
 
 static int stream_alloc_table(hm_stream* s, uint64_t cap, HmsTable* t)
@@ -1204,11 +1220,14 @@ static int stream_alloc_table(hm_stream* s, uint64_t cap, HmsTable* t)
 static int stream_reserve(hm_stream* s, uint64_t incoming)
 {
     uint64_t cap = s->t.mask + 1;
+    if ((s->occupied + incoming) * 8 <= cap * 5) return HM_OK;
+    int st;
+    if (s->stale && (st = stream_sync_state(s))) return st;   /* the exact count */
     const uint64_t need = s->occupied + incoming;
     if (need * 8 <= cap * 5) return HM_OK;
     while (need * 8 > cap * 5) cap <<= 1;
     HmsTable nt;
-    int st = stream_alloc_table(s, cap, &nt);
+    st = stream_alloc_table(s, cap, &nt);
     if (st) return st;
     HIPCHK(hipMemsetAsync(s->t.state, 0, 2 * sizeof(unsigned long long), s->ctx->stream));
     hm_launch_stream_rehash(s->ctx->stream, s->t, nt);
@@ -1265,7 +1284,7 @@ static int stream_fold_one(hm_stream* s, const double* lat, const double* lon, c
     hm_launch_stream_insert(s->ctx->stream, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m,
                             true, (uint64_t)bucket << s->cb, s->t);
     HIPCHK(hipGetLastError());
-    return stream_sync_state(s);
+    return stream_inserted(s, (uint64_t)m);
 }
 
 /* a batch of several buckets: one grouped pass with the bucket as group */
@@ -1298,7 +1317,99 @@ static int stream_fold_grouped(hm_stream* s, const double* lat, const double* lo
     if ((st = stream_reserve(s, (uint64_t)m))) return st;
     hm_launch_stream_insert(q, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m, false, 0, s->t);
     HIPCHK(hipGetLastError());
-    return stream_sync_state(s);
+    return stream_inserted(s, (uint64_t)m);
+}
+
+/* a batch of a few buckets: gathered into one run per bucket (+ one run of
+ * the points not kept), one hm_count per run, all counted before anything is
+ * inserted.  Errors: the batch is re-counted as a whole so the reported point
+ * is the first failing one in input order, as hm_count's. */
+static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
+                             uint32_t nparts)
+{
+    hm_ctx* ctx = s->ctx;
+    hipStream_t q = ctx->stream;
+    int st;
+    std::vector<uint32_t> hb(nparts);
+    std::vector<uint64_t> start(2 * (nparts + 2), 0);   /* starts | run sizes, then cursors */
+    if ((st = stream_buf(s, s->pstart, (size_t)(nparts + 2) * 16))) return st;
+    uint64_t* dstart = (uint64_t*)s->pstart.p;
+    HmsScatterArgs a;
+    a.lat = lat;
+    a.lon = lon;
+    a.keep = keep;
+    a.bids = (const uint32_t*)s->bids.p;
+    a.loc = s->bloc;
+    a.n = (uint64_t)n;
+    a.nparts = nparts;
+    a.start = dstart;
+    a.cursor = (unsigned long long*)(dstart + nparts + 2);
+    hm_launch_stream_batch_list(q, s->blist, nparts, s->bloc);
+    HIPCHK(hipMemsetAsync(a.cursor, 0, (size_t)(nparts + 2) * 8, q));
+    hm_launch_stream_part_count(q, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(hb.data(), s->blist, nparts * 4, hipMemcpyDeviceToHost, q));
+    HIPCHK(hipMemcpyAsync(start.data() + nparts + 2, a.cursor, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, q));
+    HIPCHK(hipStreamSynchronize(q));
+    uint64_t kept = 0;
+    for (uint32_t j = 0; j < nparts; j++) {
+        start[j] = kept;
+        kept += start[nparts + 2 + j];
+    }
+    start[nparts] = kept;
+    start[nparts + 1] = (uint64_t)n;
+    if (kept + start[2 * nparts + 2] != (uint64_t)n) return HM_E_HIP;   /* cannot happen */
+    if ((st = stream_buf(s, s->plat, (size_t)n * 8)) || (st = stream_buf(s, s->plon, (size_t)n * 8))) return st;
+    HIPCHK(hipMemcpyAsync(dstart, start.data(), (size_t)(nparts + 2) * 8, hipMemcpyHostToDevice, q));
+    HIPCHK(hipMemsetAsync(a.cursor, 0, (size_t)(nparts + 2) * 8, q));
+    a.lat_out = (double*)s->plat.p;
+    a.lon_out = (double*)s->plon.p;
+    hm_launch_stream_scatter(q, a);
+    HIPCHK(hipGetLastError());
+    const uint64_t nun = (uint64_t)n - kept;
+    if (nun) {
+        if ((st = stream_buf(s, s->pkeep, (size_t)nun))) return st;
+        HIPCHK(hipMemsetAsync(s->pkeep.p, 0, nun, q));
+    }
+    if ((st = stream_cells_buf(s, 2 * (int64_t)kept + 1024))) return st;
+    for (;;) {
+        uint64_t off = 0;
+        bool grow = false;
+        for (uint32_t j = 0; j <= nparts && !grow; j++) {
+            const uint64_t nj = (j < nparts ? start[j + 1] : (uint64_t)n) - start[j];
+            if (!nj) continue;
+            int64_t m = 0, nx = 0;
+            st = hm_count(ctx, (const double*)s->plat.p + start[j], (const double*)s->plon.p + start[j],
+                          j < nparts ? nullptr : (const uint8_t*)s->pkeep.p, (int64_t)nj, s->zmin, s->zmax,
+                          (uint64_t*)s->bkeys.p + off, (uint64_t*)s->bcounts.p + off, s->bcap - (int64_t)off, &m,
+                          nullptr, 0, &nx);
+            /* the resident table's keys hold tiles inside [0, 2^z)^2 only (and
+             * with no record buffer given, hm_count reports them as capacity) */
+            if (nx > 0) return HM_E_EXOTIC;
+            if (st == HM_E_CAPACITY) {
+                if ((st = stream_cells_buf(s, (int64_t)(off + m) * 5 / 4 + 1024))) return st;
+                grow = true;
+                break;
+            }
+            if (st != HM_OK && st != HM_E_CAPACITY) {
+                /* the first failing point in input order */
+                int64_t m2 = 0, nx2 = 0;
+                const int st2 = hm_count(ctx, lat, lon, keep, n, s->zmin, s->zmax, nullptr, nullptr, 0, &m2, nullptr,
+                                         0, &nx2);
+                return st2 != HM_OK && st2 != HM_E_CAPACITY ? st2 : st;
+            }
+            if (j < nparts) {
+                hm_launch_stream_rekey(q, (uint64_t*)s->bkeys.p + off, (uint64_t)m, (uint64_t)hb[j] << s->cb);
+                HIPCHK(hipGetLastError());
+                off += (uint64_t)m;
+            }
+        }
+        if (grow) continue;
+        if ((st = stream_reserve(s, off))) return st;
+        hm_launch_stream_insert(q, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, off, false, 0, s->t);
+        HIPCHK(hipGetLastError());
+        return stream_inserted(s, off);
+    }
 }
 
 extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_t initial_cells,
@@ -1324,8 +1435,9 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
     uint64_t cap = 1024;
     while (cap * 5 < (uint64_t)initial_cells * 8) cap <<= 1;
     if (hipMalloc((void**)&s->t.state, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
-        hipHostMalloc((void**)&s->hstate, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc((void**)&s->bk.keys, nb * 8) != hipSuccess) {
+        hipHostMalloc((void**)&s->hstate, 2 * HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc((void**)&s->bk.keys, nb * 8) != hipSuccess || hipMalloc((void**)&s->bflag, nb * 4) != hipSuccess ||
+        hipMalloc((void**)&s->blist, nb * 4) != hipSuccess || hipMalloc((void**)&s->bloc, nb * 4) != hipSuccess) {
         (void)hipGetLastError();
         hm_stream_destroy(s);
         return HM_E_NOMEM;
@@ -1336,6 +1448,7 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
     if (st == HM_OK) {
         hm_launch_stream_fill(ctx->stream, s->bk.keys, nb, HMS_EMPTY);
         st = hip_fail(hipGetLastError(), "fill");
+        if (st == HM_OK) st = hip_fail(hipMemsetAsync(s->bflag, 0, nb * 4, ctx->stream), "memset");
     }
     if (st == HM_OK) st = stream_sync_state(s);
     if (st) {
@@ -1354,38 +1467,60 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
     hm_ctx* ctx = s->ctx;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t q = ctx->stream;
-    int st = reset_state(ctx);
-    if (st) return st;
+    int st;
     /* buckets of the kept points (interned; a failing batch may leave unused
      * buckets behind, never counts) */
-    const unsigned int mm0[2] = {0xFFFFFFFFu, 0u};
-    HIPCHK(hipMemcpyAsync(s->t.state + HMS_ST_BMM, mm0, sizeof(mm0), hipMemcpyHostToDevice, q));
-    if ((st = stream_buf(s, s->bids, (size_t)(group || hour ? n : 1) * 4))) return st;
+    /* reset BFULL, EXOTIC, BMM, NLIST, ERR in one copy */
+    unsigned long long* init = s->hstate + HMS_ST_COUNT;
+    init[0] = 0;                                    /* BFULL */
+    init[1] = 0;                                    /* EXOTIC */
+    init[2] = 0;                                    /* BMM */
+    init[3] = 0;                                    /* NLIST */
+    init[4] = ~0ull;                                /* ERR */
+    HIPCHK(hipMemcpyAsync(s->t.state + HMS_ST_BFULL, init, 5 * 8, hipMemcpyHostToDevice, q));
+    const bool per_point = group || hour;
+    if (per_point && (st = stream_buf(s, s->bids, (size_t)n * 4))) return st;
     HmsBucketArgs a;
     a.group = group;
     a.hour = hour;
-    a.keep = (group || hour) ? keep : nullptr;
-    a.n = (group || hour) ? (uint64_t)n : 1;   /* neither: the one (no group, undated) bucket */
+    a.keep = per_point ? keep : nullptr;
+    a.n = per_point ? (uint64_t)n : 1;   /* neither: the one (no group, undated) bucket */
     a.base = s->base;
     a.buckets = s->bk;
-    a.out = (uint32_t*)s->bids.p;
+    a.out = per_point ? (uint32_t*)s->bids.p : nullptr;
+    if (++s->epoch == 0) s->epoch = 1;   /* wrapped: stale flags only cost an exchange */
+    a.bflag = s->bflag;
+    a.epoch = s->epoch;
+    a.list = s->blist;
     a.state = s->t.state;
-    a.err_word = ctx->state + ST_ERR;
+    a.err_word = s->t.state + HMS_ST_ERR;
     hm_launch_stream_buckets(q, a);
+    hm_launch_stream_collect(q, s->bflag, s->bk.mask + 1, s->epoch, s->blist, s->t.state);
     HIPCHK(hipGetLastError());
     if ((st = stream_sync_state(s))) return st;
-    if ((st = read_state(ctx))) return st;
-    if ((st = take_error(ctx))) return st;
+    const uint32_t nparts = (uint32_t)s->hstate[HMS_ST_NLIST];
+    const uint32_t lo = (uint32_t)s->hstate[HMS_ST_BMM];
+    const unsigned long long e = s->hstate[HMS_ST_ERR];
+    if (e != ~0ull) {
+        ctx->last_err_index = (int64_t)(e >> 8);
+        ctx->last_err_kind = (int)(e & 0xFF);
+        return ctx->last_err_kind;
+    }
     if (s->hstate[HMS_ST_BFULL]) return HM_E_CAPACITY;   /* max_buckets (group, hour) pairs */
-    const unsigned int* mm = (const unsigned int*)(s->hstate + HMS_ST_BMM);
-    if (mm[0] >= mm[1]) /* one bucket (the usual time-ordered batch), or nothing kept */
-        return stream_fold_one(s, lat, lon, keep, n, mm[0] <= mm[1] ? mm[0] : 0u);
+    if (nparts <= 1) /* one bucket (the usual time-ordered batch), or nothing kept */
+        return stream_fold_one(s, lat, lon, keep, n, nparts ? lo : 0u);
+    if (nparts <= HMS_MAX_PARTS) return stream_fold_parts(s, lat, lon, keep, n, nparts);
     return stream_fold_grouped(s, lat, lon, keep, n);
 }
 
 extern "C" int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity, int64_t* buckets)
 {
     if (!s) return HM_E_ARG;
+    if (s->stale) {
+        HIPCHK(hipSetDevice(s->ctx->device));
+        const int st = stream_sync_state(s);
+        if (st) return st;
+    }
     if (cells) *cells = (int64_t)s->occupied;
     if (capacity) *capacity = (int64_t)(s->t.mask + 1);
     if (buckets) *buckets = (int64_t)s->nbuckets;
@@ -1466,8 +1601,9 @@ extern "C" int hm_stream_destroy(hm_stream* s)
     if (!s) return HM_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
-    for (void* p : {(void*)s->t.slots, (void*)s->t.state, (void*)s->bk.keys, s->bids.p, s->rec.p, s->bkeys.p,
-                    s->bcounts.p, s->rslots.p})
+    for (void* p : {(void*)s->t.slots, (void*)s->t.state, (void*)s->bk.keys, (void*)s->bflag, (void*)s->blist,
+                    (void*)s->bloc, s->bids.p, s->rec.p, s->bkeys.p, s->bcounts.p, s->rslots.p, s->plat.p, s->plon.p,
+                    s->pkeep.p, s->pstart.p, s->pcnt.p})
         if (p) (void)hipFree(p);
     if (s->hstate) (void)hipHostFree(s->hstate);
     delete s;

@@ -128,6 +128,10 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
+    /* the resolved-redo launch is sized for the list's capacity; its length
+     * is read here (no host round trip) */
+    const int64_t n = (FROM_TILES && a.n_dev) ? min((int64_t)*a.n_dev, a.n) : a.n;
+    if (base >= n) return;
     const uint32_t lim = 1u << a.Z;
     const double scale = hm_exp2i(a.Z);
     const double kz = HM_INV360 * scale;
@@ -142,7 +146,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
      * tail code below writes the same registers in its other branches, which
      * makes the compiler wait for each load pair before the next one: one
      * 32-B pair per lane in flight instead of all of them. */
-    if (!FROM_TILES && base + HM_T1 <= a.n) {
+    if (!FROM_TILES && base + HM_T1 <= n) {
         const double2* lat2 = (const double2*)(a.lat + base);
         const double2* lon2 = (const double2*)(a.lon + base);
 #pragma unroll
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     for (int k = 0; k < HM_P1_PPT / 2; k++) {
         const int64_t i0 = base + 2 * ((int64_t)k * HM_P1_THREADS + tid);
         kp[k] = 0x0101;
-        if (i0 + 1 < a.n) {
+        if (i0 + 1 < n) {
             if (FROM_TILES) {
                 la[k].x = __longlong_as_double(a.rows_in[i0]);
                 la[k].y = __longlong_as_double(a.rows_in[i0 + 1]);
@@ -174,7 +178,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
                 lo[k] = *(const double2*)(a.lon + i0);
             }
             if (a.keep) kp[k] = (uint16_t)a.keep[i0] | ((uint16_t)a.keep[i0 + 1] << 8);
-        } else if (i0 < a.n) {
+        } else if (i0 < n) {
             if (FROM_TILES) {
                 la[k].x = __longlong_as_double(a.rows_in[i0]);
                 lo[k].x = __longlong_as_double(a.cols_in[i0]);
@@ -229,7 +233,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
             r = r32;
             c = c32;
         }
-        const bool inb = i < a.n;
+        const bool inb = i < n;
         const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
         const bool dom = ((uint64_t)r < lim) & ((uint64_t)c < lim);
         redo |= (uint32_t)(inb & !(ok & dom)) << k;
@@ -426,6 +430,53 @@ __global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t s
     __syncthreads();
     for (int i = threadIdx.x; i < F; i += 256)
         if (h[i]) atomicAdd(&hist[i], h[i]);
+}
+
+/* Level-1 region sizes from the sampled histogram, on the device (no host
+ * round trip): per digit est = hist * stride; a digit above 64 tiles gets
+ * HM_L1_SHARDS shards; per shard cap = e + e/16 + 8 sqrt(e * stride) + 2 T1
+ * (e = est / shards); bases = exclusive prefix over (digit, shard).  The same
+ * formula as the host's retry path.  One block of 1024 threads. */
+__global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ hist, int F, uint64_t stride,
+                                                   uint32_t* __restrict__ rcap, uint32_t* __restrict__ rbase,
+                                                   uint8_t* __restrict__ smask)
+{
+    __shared__ unsigned long long wsum[1024 / 64];
+    const int d = threadIdx.x;
+    const int lane = d & 63, w = d >> 6;
+    uint32_t c = 0;
+    int ns = 1;
+    if (d < F) {
+        const double est = (double)hist[d] * (double)stride;
+        ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
+        const double e = est / ns;
+        c = (uint32_t)fmin(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) + 2.0 * HM_T1);
+        smask[d] = (uint8_t)(ns - 1);
+    }
+    const unsigned long long mine = d < F ? (unsigned long long)c * (unsigned long long)ns : 0ull;
+    unsigned long long incl = mine;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(incl, o, 64);
+        if (lane >= o) incl += y;
+    }
+    if (lane == 63) wsum[w] = incl;
+    __syncthreads();
+    unsigned long long before = 0;
+    for (int i = 0; i < w; i++) before += wsum[i];
+    unsigned long long pos = before + incl - mine;
+    if (d < F)
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
+            const uint32_t cs = sh < ns ? c : 0u;
+            rcap[d * HM_L1_SHARDS + sh] = cs;
+            rbase[d * HM_L1_SHARDS + sh] = (uint32_t)pos;   /* total < 2^32: the host's bound */
+            pos += cs;
+        }
+}
+
+void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, uint64_t stride, uint32_t* rcap, uint32_t* rbase,
+                        uint8_t* smask)
+{
+    hipLaunchKernelGGL(k_l1_sizes, dim3(1), dim3(1024), 0, s, hist, F, stride, rcap, rbase, smask);
 }
 
 void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist)

@@ -151,6 +151,7 @@ struct HmPart1Args {
     const int64_t* cols_in;
     const uint8_t* keep;
     int64_t n;
+    const unsigned long long* n_dev;   /* tile input: min(*n_dev, n) points (the resolved redo list) */
     int Z, dbits, restbits;
     uint32_t* redo_idx;       /* fast mode: points the fast path could not settle */
     unsigned long long* redo_count;
@@ -271,6 +272,8 @@ void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int6
 /* mode: 0 fast path + redo list, 1 tile input (exact row/col given), 2 fused exact (fallback) */
 void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool out16, int mode);
 void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist);
+void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, uint64_t stride, uint32_t* rcap, uint32_t* rbase,
+                        uint8_t* smask);
 void hm_launch_level1_buckets(hipStream_t s, const HmL1Args& a);
 struct HmRedoArgs {
     const double* lat;
@@ -315,8 +318,10 @@ void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int6
 #define HMS_EMPTY 0xFFFFFFFFFFFFFFFFull   /* empty hash-table key (hm_table.h) */
 enum {
     HMS_ST_OCCUPIED = 0, HMS_ST_OVERFLOW = 1, HMS_ST_CURSOR = 2, HMS_ST_BUCKETS = 3, HMS_ST_BFULL = 4,
-    HMS_ST_EXOTIC = 5, HMS_ST_BMM = 6 /* min, max bucket of the batch as u32 */, HMS_ST_COUNT = 8
+    HMS_ST_EXOTIC = 5, HMS_ST_BMM = 6 /* a bucket of the batch (the only one if NLIST == 1) */, HMS_ST_NLIST = 7,
+    HMS_ST_ERR = 8 /* first bad hour: index << 8 | HM_E_RANGE */, HMS_ST_COUNT = 16
 };
+#define HMS_MAX_PARTS 64                 /* batches of more buckets take the grouped general path */
 #define HMS_NOGROUP 0xFFFFFFFEu          /* kept points without a user group */
 #define HMS_ALLGROUPS 0xFFFFFFFFu        /* rollup over every group */
 #define HMS_UNDATED 0x50000000u          /* period word of points added without an hour */
@@ -343,9 +348,25 @@ struct HmsBucketArgs {
     uint64_t n;
     uint32_t base;
     HmsBuckets buckets;
-    uint32_t* out;
+    uint32_t* out;           /* bucket per kept point (NULL: not needed) */
+    uint32_t* bflag;         /* per bucket: epoch of the last batch that met it */
+    uint32_t epoch;          /* this batch's (nonzero) */
+    uint32_t* list;          /* the batch's distinct buckets */
     unsigned long long* state;
     unsigned long long* err_word;
+};
+struct HmsScatterArgs {
+    const double* lat;
+    const double* lon;
+    const uint8_t* keep;
+    const uint32_t* bids;
+    const uint32_t* loc;     /* bucket -> run */
+    uint64_t n;
+    uint32_t nparts;         /* kept runs; run nparts = points not kept */
+    const uint64_t* start;   /* nparts + 1 run starts */
+    unsigned long long* cursor;   /* k_stream_part_count: the run sizes */
+    double* lat_out;
+    double* lon_out;
 };
 struct HmsRollupArgs {
     HmsTable from, to;
@@ -368,6 +389,12 @@ struct HmsEmitArgs {
     unsigned long long* cursor;
 };
 void hm_launch_stream_buckets(hipStream_t s, const HmsBucketArgs& a);
+void hm_launch_stream_batch_list(hipStream_t s, const uint32_t* list, uint32_t nlist, uint32_t* loc);
+void hm_launch_stream_collect(hipStream_t s, const uint32_t* bflag, uint64_t nb, uint32_t epoch, uint32_t* list,
+                              unsigned long long* state);
+void hm_launch_stream_part_count(hipStream_t s, const HmsScatterArgs& a);
+void hm_launch_stream_scatter(hipStream_t s, const HmsScatterArgs& a);
+void hm_launch_stream_rekey(hipStream_t s, uint64_t* keys, uint64_t m, uint64_t prefix);
 void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int cb, uint64_t* keys, uint64_t* counts,
                               unsigned long long* state);
 void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, bool from_count,

@@ -56,7 +56,9 @@ __device__ __forceinline__ uint32_t hms_intern(const HmsBuckets& b, uint64_t k, 
 {
     uint64_t h = hms_hash(k) & b.mask;
     for (uint64_t probe = 0; probe <= b.mask; probe++) {
-        uint64_t cur = __atomic_load_n(&b.keys[h], __ATOMIC_RELAXED);
+        /* a plain (L1-cacheable) read: a key word changes once, EMPTY -> key,
+         * so a stale EMPTY only sends us to the CAS, which returns the truth */
+        uint64_t cur = b.keys[h];
         if (cur == HMS_EMPTY) {
             const unsigned long long prev =
                 atomicCAS((unsigned long long*)&b.keys[h], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
@@ -72,64 +74,200 @@ __device__ __forceinline__ uint32_t hms_intern(const HmsBuckets& b, uint64_t k, 
     return HMS_NO_BUCKET;
 }
 
+/* a bucket met by a wave: flagged with the batch epoch (a plain store -- the
+ * waves of a batch start together, so a flag read-then-atomic would put
+ * thousands of same-address atomics on one L2 channel); k_stream_collect
+ * lists the flagged buckets afterwards */
+__device__ __forceinline__ void hms_seen(const HmsBucketArgs& a, uint32_t b)
+{
+    if (b != HMS_NO_BUCKET && a.bflag[b] != a.epoch) a.bflag[b] = a.epoch;
+}
+
 /* Bucket of every kept point: (group or HMS_NOGROUP, hour - base or
- * HMS_UNDATED).  A wave whose kept points share one key interns it once.
- * Hours outside [base, base + 2^28) are input errors (first index wins). */
+ * HMS_UNDATED).  Each wave walks a contiguous range of the batch, HMS_WC
+ * (key, bucket) pairs cached in registers (wave-uniform): a point whose key
+ * is cached costs no probe and no atomic (a time-ordered batch is one key, a
+ * batch of a few hours a few); a miss interns the key once for the wave
+ * (ballot match) and evicts round-robin.  Also the list of the batch's
+ * distinct buckets and their min/max.  Hours outside [base, base + 2^28) are
+ * input errors (first index wins). */
+#define HMS_WC 4
 __global__ __launch_bounds__(256) void k_stream_buckets(HmsBucketArgs a)
 {
+    constexpr int U = 4;   /* points per lane per step, loads issued together */
     const uint32_t lane = threadIdx.x & 63;
-    uint32_t lo = 0xFFFFFFFFu, hi = 0, claimed = 0, full = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    const uint64_t n_up = (a.n + 63) & ~63ull;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
-        bool kept = i < a.n && (!a.keep || a.keep[i]);
-        uint64_t key = 0;
-        if (kept) {
-            uint32_t pw = HMS_UNDATED;
-            if (a.hour) {
-                const uint32_t h = a.hour[i];
-                if (h < a.base || h - a.base >= HMS_MAX_HOUR_OFFSET) {
-                    atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_RANGE);
-                    kept = false;
-                }
-                pw = h - a.base;
-            }
-            key = ((uint64_t)(a.group ? a.group[i] : HMS_NOGROUP) << 32) | pw;
-        }
-        const uint64_t km = __ballot(kept);
-        if (!km) continue;
-        const int leader = __ffsll((unsigned long long)km) - 1;
-        const uint64_t k0 = __shfl((unsigned long long)key, leader, 64);
-        uint32_t b = 0;
-        if (__ballot(kept && key != k0) == 0) {
-            if ((int)lane == leader) b = hms_intern(a.buckets, k0, &claimed);
-            b = __shfl(b, leader, 64);
-        } else if (kept) {
-            b = hms_intern(a.buckets, key, &claimed);
-        }
-        if (kept) {
-            full |= b == HMS_NO_BUCKET;
-            lo = b < lo ? b : lo;
-            hi = b > hi ? b : hi;
-            a.out[i] = b;
-        }
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
+    const uint64_t per = ((a.n + waves - 1) / waves + 64 * U - 1) / (64 * U) * (64 * U);
+    const uint64_t w0 = wave * per, w1 = min(w0 + per, a.n);
+    uint32_t claimed = 0, full = 0;
+    uint64_t ck[HMS_WC];
+    uint32_t cb[HMS_WC];
+#pragma unroll
+    for (int c = 0; c < HMS_WC; c++) {
+        ck[c] = HMS_EMPTY;
+        cb[c] = HMS_NO_BUCKET;
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        const uint32_t x = __shfl_xor(lo, o, 64), y = __shfl_xor(hi, o, 64);
-        lo = x < lo ? x : lo;
-        hi = y > hi ? y : hi;
+    uint32_t victim = 0;
+    for (uint64_t i0 = w0; i0 < w1; i0 += 64 * U) {
+        uint64_t key[U];
+        bool kept[U];
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint64_t i = i0 + (uint64_t)u * 64 + lane;
+            kept[u] = i < w1 && (!a.keep || a.keep[i]);
+            const uint32_t h = (a.hour && i < w1) ? a.hour[i] : a.base;
+            const uint32_t g = (a.group && i < w1) ? a.group[i] : HMS_NOGROUP;
+            if (kept[u] && a.hour && (h < a.base || h - a.base >= HMS_MAX_HOUR_OFFSET)) {
+                atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_RANGE);
+                kept[u] = false;
+            }
+            key[u] = ((uint64_t)g << 32) | (a.hour ? h - a.base : HMS_UNDATED);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t mine = HMS_NO_BUCKET;
+            bool hit = false;
+#pragma unroll
+            for (int c = 0; c < HMS_WC; c++)
+                if (key[u] == ck[c]) {
+                    mine = cb[c];
+                    hit = true;
+                }
+            uint64_t pending = __ballot(kept[u] && !hit);
+            while (pending) {
+                const int leader = __ffsll((unsigned long long)pending) - 1;
+                const uint64_t k0 = __shfl((unsigned long long)key[u], leader, 64);
+                const uint64_t match = __ballot(kept[u] && key[u] == k0) & pending;
+                uint32_t b = 0;
+                if ((int)lane == leader) b = hms_intern(a.buckets, k0, &claimed);
+                b = __shfl(b, leader, 64);
+                if (lane == 0) hms_seen(a, b);
+                full |= b == HMS_NO_BUCKET;
+#pragma unroll
+                for (int c = 0; c < HMS_WC; c++)
+                    if (c == (int)victim) {
+                        ck[c] = k0;
+                        cb[c] = b;
+                    }
+                victim = (victim + 1) % HMS_WC;
+                if ((match >> lane) & 1ull) mine = b;
+                pending &= ~match;
+            }
+            const uint64_t i = i0 + (uint64_t)u * 64 + lane;
+            if (kept[u] && a.out) a.out[i] = mine;
+        }
     }
     const uint64_t cl = hms_wave_sum(claimed);
-    const uint64_t fl = hms_wave_sum(full);
     if (lane == 0) {
-        unsigned int* mm = (unsigned int*)(a.state + HMS_ST_BMM);
-        if (lo <= hi) {
-            atomicMin(&mm[0], lo);
-            atomicMax(&mm[1], hi);
-        }
         if (cl) atomicAdd(&a.state[HMS_ST_BUCKETS], (unsigned long long)cl);
-        if (fl) atomicAdd(&a.state[HMS_ST_BFULL], (unsigned long long)fl);
+        if (full) atomicAdd(&a.state[HMS_ST_BFULL], 1ull);
     }
+}
+
+/* the buckets flagged with this batch's epoch -> the batch's list (one
+ * atomic per wave that finds any); HMS_ST_BMM receives one of them (THE one
+ * when the batch has a single bucket) */
+__global__ __launch_bounds__(256) void k_stream_collect(const uint32_t* __restrict__ bflag, uint64_t nb, uint32_t epoch,
+                                                        uint32_t* __restrict__ list, unsigned long long* state)
+{
+    const uint32_t lane = threadIdx.x & 63;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; i0 < nb; i0 += stride) {
+        const uint64_t i = i0 + lane;
+        const bool m = i < nb && bflag[i] == epoch;
+        const uint64_t bal = __ballot(m);
+        if (!bal) continue;
+        unsigned long long first = 0;
+        if (lane == 0) first = atomicAdd(&state[HMS_ST_NLIST], (unsigned long long)__popcll(bal));
+        first = __shfl(first, 0, 64);
+        if (m) {
+            list[first + hm_mbcnt(bal)] = (uint32_t)i;
+            if (hm_mbcnt(bal) == 0) state[HMS_ST_BMM] = i;
+        }
+    }
+}
+
+/* the batch's distinct buckets -> their run index j (loc[bucket]) */
+__global__ __launch_bounds__(256) void k_stream_batch_list(const uint32_t* __restrict__ list, uint32_t nlist,
+                                                           uint32_t* __restrict__ loc)
+{
+    const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j < nlist) loc[list[j]] = j;
+}
+
+/* points per run: the kept points of each of the batch's buckets, and (run
+ * nparts) the points not kept; a block histogram, one atomic per run */
+__global__ __launch_bounds__(256) void k_stream_part_count(HmsScatterArgs a)
+{
+    __shared__ uint32_t h[HMS_MAX_PARTS + 1 + 64];
+    const int tid = threadIdx.x;
+    const uint32_t np = a.nparts + 1;
+    if (tid < (int)np) h[tid] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const uint64_t n_up = (a.n + 255) & ~255ull;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + tid; i < n_up; i += stride) {
+        const bool in = i < a.n;
+        const bool kept = in && (!a.keep || a.keep[i]);
+        const uint32_t part = in ? (kept ? a.loc[a.bids[i]] : a.nparts) : 0u;
+        hm_lds_count(h, HMS_MAX_PARTS + 1, part, in);
+    }
+    __syncthreads();
+    if (tid < (int)np && h[tid]) atomicAdd(&a.cursor[tid], (unsigned long long)h[tid]);
+}
+
+/* Gather a batch into bucket-contiguous runs (the partition path for batches
+ * of a few buckets): run j = the kept points of the batch's j-th bucket, run
+ * nparts = the points not kept (projected for their errors only).  Per block
+ * chunk: LDS histogram, one global reservation per run, LDS slot claims. */
+__global__ __launch_bounds__(256) void k_stream_scatter(HmsScatterArgs a)
+{
+    __shared__ uint32_t cur[HMS_MAX_PARTS + 1 + 64];   /* + 64 dummy words */
+    __shared__ uint64_t base[HMS_MAX_PARTS + 1];
+    const int tid = threadIdx.x;
+    const uint32_t np = a.nparts + 1;
+    const uint64_t chunk = 256 * 16;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * chunk; c0 < a.n; c0 += (uint64_t)gridDim.x * chunk) {
+        if (tid < (int)np) cur[tid] = 0;
+        __syncthreads();
+        uint32_t part[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint64_t i = c0 + (uint64_t)k * 256 + tid;
+            const bool in = i < a.n;
+            const bool kept = in && (!a.keep || a.keep[i]);
+            part[k] = in ? (kept ? a.loc[a.bids[i]] : a.nparts) : 0xFFFFFFFFu;
+            hm_lds_count(cur, HMS_MAX_PARTS + 1, part[k], in);
+        }
+        __syncthreads();
+        if (tid < (int)np) {
+            const uint32_t c = cur[tid];
+            base[tid] = a.start[tid] + (c ? atomicAdd(&a.cursor[tid], (unsigned long long)c) : 0ull);
+            cur[tid] = 0;
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint64_t i = c0 + (uint64_t)k * 256 + tid;
+            const bool in = i < a.n;
+            const uint32_t pos = hm_lds_claim(cur, HMS_MAX_PARTS + 1, part[k], in);
+            if (in) {
+                const uint64_t q = base[part[k]] + pos;
+                a.lat_out[q] = a.lat[i];
+                a.lon_out[q] = a.lon[i];
+            }
+        }
+        __syncthreads();
+    }
+}
+
+/* hm_count keys of one bucket's cells -> cell-table keys, in place */
+__global__ __launch_bounds__(256) void k_stream_rekey(uint64_t* __restrict__ keys, uint64_t m, uint64_t prefix)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride)
+        keys[i] = prefix | hms_cell(keys[i]);
 }
 
 /* grouped-path records (bucket, zoom, row, col, count) -> cell-table keys;
@@ -251,6 +389,7 @@ __global__ __launch_bounds__(256) void k_stream_rollup(HmsRollupArgs a)
 {
     uint64_t claimed = 0;
     uint32_t overflow = 0, bclaimed = 0, full = 0;
+    const uint32_t lane = threadIdx.x & 63;
     const uint64_t n = a.from.mask + 1;
     const uint64_t cmask = (1ull << a.cb) - 1ull;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -264,7 +403,15 @@ __global__ __launch_bounds__(256) void k_stream_rollup(HmsRollupArgs a)
         if (lp == HMS_SKIP) continue;
         if (a.select >= 0 && (int64_t)hms_period_value(lp, a.base) != a.select) continue;
         const uint32_t g = a.merge ? HMS_ALLGROUPS : (uint32_t)(bk >> 32);
-        const uint32_t b = hms_intern(a.buckets, ((uint64_t)g << 32) | lp, &bclaimed);
+        const uint64_t key = ((uint64_t)g << 32) | lp;
+        /* the lanes sharing the first lane's label bucket intern it once (a
+         * merged rollup is one label for the whole wave); the rest probe alone */
+        const uint64_t k0 = __builtin_amdgcn_readfirstlane(key);
+        const uint64_t same = __ballot(key == k0);
+        uint32_t b = 0;
+        if (lane == (uint32_t)(__ffsll((unsigned long long)same) - 1)) b = hms_intern(a.buckets, k0, &bclaimed);
+        b = __shfl(b, __ffsll((unsigned long long)same) - 1, 64);
+        if (key != k0) b = hms_intern(a.buckets, key, &bclaimed);
         if (b == HMS_NO_BUCKET) {
             full = 1;
             continue;
@@ -283,33 +430,43 @@ __global__ __launch_bounds__(256) void k_stream_rollup(HmsRollupArgs a)
     }
 }
 
-/* occupied slots of a rollup table -> (group, period, hm_count key, count);
- * one output reservation per wave and 64 slots; past `cap`: counted only */
+/* occupied slots of a rollup table -> (group, period, hm_count key, count).
+ * Each wave owns chunks of HMS_XCHUNK slots: it counts the occupied ones,
+ * reserves its output with ONE atomic per chunk, then re-reads the (cache-hot)
+ * chunk and writes in slot order.  Past `cap`: counted, not written. */
+#define HMS_XCHUNK (64 * 64)
 __global__ __launch_bounds__(256) void k_stream_emit(HmsEmitArgs a)
 {
-    const uint64_t n = a.t.mask + 1;
+    const uint64_t n = a.t.mask + 1;   /* power of two >= 1024 */
     const uint32_t lane = threadIdx.x & 63;
     const uint64_t cmask = (1ull << a.cb) - 1ull;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
     const ulonglong2* slots = (const ulonglong2*)a.t.slots;
-    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; i0 < n; i0 += stride) {
-        const uint64_t i = i0 + lane;
-        const ulonglong2 sl = i < n ? slots[i] : make_ulonglong2(HMS_EMPTY, 0ull);
-        const bool m = sl.x != HMS_EMPTY;
-        const uint64_t bal = __ballot(m);
-        if (!bal) continue;
+    for (uint64_t c0 = wave * HMS_XCHUNK; c0 < n; c0 += waves * HMS_XCHUNK) {
+        const uint64_t c1 = c0 + HMS_XCHUNK < n ? c0 + HMS_XCHUNK : n;
+        uint64_t cnt = 0;
+        for (uint64_t i = c0 + lane; i < c1; i += 64) cnt += slots[i].x != HMS_EMPTY;
+        cnt = hms_wave_sum(cnt);
+        if (!cnt) continue;
         unsigned long long first = 0;
-        if (lane == 0) first = atomicAdd(a.cursor, (unsigned long long)__popcll(bal));
+        if (lane == 0) first = atomicAdd(a.cursor, (unsigned long long)cnt);
         first = __shfl(first, 0, 64);
-        if (m) {
-            const uint64_t pos = first + hm_mbcnt(bal);
-            if (pos < a.cap) {
-                const uint64_t bk = a.buckets.keys[sl.x >> a.cb];
-                a.keys_out[pos] = hms_cell_key(sl.x & cmask, a.zmin, a.zmax);
-                a.counts_out[pos] = sl.y;
-                if (a.groups_out) a.groups_out[pos] = (uint32_t)(bk >> 32);
-                if (a.periods_out) a.periods_out[pos] = hms_period_value((uint32_t)bk, a.base);
+        for (uint64_t j0 = c0; j0 < c1; j0 += 64) {
+            const ulonglong2 sl = slots[j0 + lane];
+            const bool m = sl.x != HMS_EMPTY;
+            const uint64_t bal = __ballot(m);
+            if (m) {
+                const uint64_t pos = first + hm_mbcnt(bal);
+                if (pos < a.cap) {
+                    const uint64_t bk = a.buckets.keys[sl.x >> a.cb];
+                    a.keys_out[pos] = hms_cell_key(sl.x & cmask, a.zmin, a.zmax);
+                    a.counts_out[pos] = sl.y;
+                    if (a.groups_out) a.groups_out[pos] = (uint32_t)(bk >> 32);
+                    if (a.periods_out) a.periods_out[pos] = hms_period_value((uint32_t)bk, a.base);
+                }
             }
+            first += __popcll(bal);
         }
     }
 }
@@ -323,7 +480,42 @@ static dim3 hms_grid(uint64_t n)
 
 void hm_launch_stream_buckets(hipStream_t s, const HmsBucketArgs& a)
 {
-    if (a.n) hipLaunchKernelGGL(k_stream_buckets, hms_grid(a.n), dim3(256), 0, s, a);
+    /* ~8+ steps of 256 points per wave: runs of one key stay in registers */
+    uint64_t b = (a.n + 8192 - 1) / 8192;
+    if (b > 2048) b = 2048;
+    if (a.n) hipLaunchKernelGGL(k_stream_buckets, dim3((unsigned)(b ? b : 1)), dim3(256), 0, s, a);
+}
+
+void hm_launch_stream_collect(hipStream_t s, const uint32_t* bflag, uint64_t nb, uint32_t epoch, uint32_t* list,
+                              unsigned long long* state)
+{
+    uint64_t b = (nb + 4095) / 4096;
+    if (b > 1024) b = 1024;
+    hipLaunchKernelGGL(k_stream_collect, dim3((unsigned)(b ? b : 1)), dim3(256), 0, s, bflag, nb, epoch, list, state);
+}
+
+void hm_launch_stream_batch_list(hipStream_t s, const uint32_t* list, uint32_t nlist, uint32_t* loc)
+{
+    if (nlist) hipLaunchKernelGGL(k_stream_batch_list, dim3((nlist + 255) / 256), dim3(256), 0, s, list, nlist, loc);
+}
+
+void hm_launch_stream_part_count(hipStream_t s, const HmsScatterArgs& a)
+{
+    uint64_t b = (a.n + 32767) / 32768;
+    if (b > 512) b = 512;
+    if (a.n) hipLaunchKernelGGL(k_stream_part_count, dim3((unsigned)(b ? b : 1)), dim3(256), 0, s, a);
+}
+
+void hm_launch_stream_scatter(hipStream_t s, const HmsScatterArgs& a)
+{
+    uint64_t b = (a.n + 4095) / 4096;
+    if (b > 2048) b = 2048;
+    if (a.n) hipLaunchKernelGGL(k_stream_scatter, dim3((unsigned)(b ? b : 1)), dim3(256), 0, s, a);
+}
+
+void hm_launch_stream_rekey(hipStream_t s, uint64_t* keys, uint64_t m, uint64_t prefix)
+{
+    if (m) hipLaunchKernelGGL(k_stream_rekey, hms_grid(m), dim3(256), 0, s, keys, m, prefix);
 }
 
 void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int cb, uint64_t* keys, uint64_t* counts,
@@ -364,5 +556,6 @@ void hm_launch_stream_rollup(hipStream_t s, const HmsRollupArgs& a)
 
 void hm_launch_stream_emit(hipStream_t s, const HmsEmitArgs& a)
 {
-    hipLaunchKernelGGL(k_stream_emit, hms_grid(a.t.mask + 1), dim3(256), 0, s, a);
+    const uint64_t chunks = (a.t.mask + HMS_XCHUNK) / HMS_XCHUNK, blocks = (chunks + 3) / 4;
+    hipLaunchKernelGGL(k_stream_emit, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
 }

@@ -31,7 +31,9 @@ __device__ __forceinline__ uint32_t hms_insert(const HmsTable& t, uint64_t k, ui
 {
     uint64_t h = hms_hash(k) & t.mask;
     for (uint64_t probe = 0; probe <= t.mask; probe++) {
-        uint64_t cur = __atomic_load_n(&t.slots[2 * h], __ATOMIC_RELAXED);
+        /* plain read: a key word changes once (EMPTY -> key); a stale EMPTY
+         * only sends us to the CAS, which returns the current key */
+        uint64_t cur = t.slots[2 * h];
         uint32_t claimed = 0;
         if (cur == HMS_EMPTY) {
             const unsigned long long prev =

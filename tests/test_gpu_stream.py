@@ -195,3 +195,35 @@ def test_stream_batch_is_atomic(gpu):
         assert np.array_equal(getattr(before, k), getattr(after, k))
     assert sorted(s.hourly()) == [BASE, BASE + 1]
     s.close()
+
+
+@pytest.mark.parametrize("nusers,nhours", [(1, 2), (3, 5), (150, 1)])
+def test_stream_paths_per_bucket_count(gpu, nusers, nhours):
+    """One bucket (hm_count), a few (gathered runs, one hm_count each) and more
+    than HMS_MAX_PARTS (the grouped general path) give the same counts: every
+    group's alltime cells and every hour's cells == the oracle's."""
+    n = 30000
+    lat, lon = synth.generate("skew", n, seed=nusers + nhours)
+    rng = np.random.default_rng(nusers)
+    keep = (rng.random(n) > 0.05).astype(np.uint8)
+    hour = (BASE + rng.integers(0, nhours, n)).astype(np.uint32)
+    gid = rng.integers(0, nusers, n).astype(np.uint32)
+    s = StreamingHeatmap(0, 17, base_hour=BASE)
+    s.add(lat, lon, keep, hour, group=gid)
+    s.add(lat[:5000], lon[:5000], keep[:5000], hour[:5000], group=gid[:5000])
+    lat2, lon2 = np.concatenate([lat, lat[:5000]]), np.concatenate([lon, lon[:5000]])
+    keep2, hour2, gid2 = (np.concatenate([x, x[:5000]]) for x in (keep, hour, gid))
+    _same(s.counts(), oracle.count(lat2, lon2, keep2, 0, 17))
+    for h, c in s.hourly().items():
+        _same(c, oracle.count(lat2, lon2, keep2 & (hour2 == h).astype(np.uint8), 0, 17))
+    g, p, z, r, c, cnt = s.rollup("alltime", merge_groups=False)
+    for u in sorted(set(range(nusers)) & {0, 1, nusers - 1}):
+        m = g == u
+        _same(Counts(z[m], r[m], c[m], cnt[m], 0, []),
+              oracle.count(lat2, lon2, keep2 & (gid2 == u).astype(np.uint8), 0, 17))
+    bad = lat.copy()
+    bad[n - 7] = np.nan                      # error in the last bucket's run: reported at its input index
+    with pytest.raises(ValueError):
+        s.add(bad, lon, keep, hour, group=gid)
+    _same(s.counts(), oracle.count(lat2, lon2, keep2, 0, 17))
+    s.close()
