@@ -303,7 +303,7 @@ __global__ __launch_bounds__(256) void k_stream_insert(const uint64_t* __restric
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const uint64_t k = FROM_COUNT ? prefix | hms_cell(keys[i]) : keys[i];
-        claimed += hms_insert(t, k, counts[i], &overflow);
+        claimed += hms_insert_unique(t, k, counts[i], &overflow);   /* a batch's cells are distinct */
     }
     claimed = hms_wave_sum(claimed);
     const uint64_t of = hms_wave_sum(overflow);
@@ -322,7 +322,7 @@ __global__ __launch_bounds__(256) void k_stream_rehash(HmsTable from, HmsTable t
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
     for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         const ulonglong2 sl = ((const ulonglong2*)from.slots)[i];
-        if (sl.x != HMS_EMPTY) claimed += hms_insert(to, sl.x, sl.y, &overflow);
+        if (sl.x != HMS_EMPTY) claimed += hms_insert_unique(to, sl.x, sl.y, &overflow);
     }
     claimed = hms_wave_sum(claimed);
     const uint64_t of = hms_wave_sum(overflow);

@@ -51,3 +51,30 @@ __device__ __forceinline__ uint32_t hms_insert(const HmsTable& t, uint64_t k, ui
     return 0;
 }
 
+
+/* Insert-or-add of a key no other thread of the launch inserts (the stream's
+ * batch cells are distinct keys): only the key claim needs an atomic; the
+ * count is a plain store (fresh slot) or a plain read-modify-write. */
+__device__ __forceinline__ uint32_t hms_insert_unique(const HmsTable& t, uint64_t k, uint64_t c, uint32_t* overflow)
+{
+    uint64_t h = hms_hash(k) & t.mask;
+    for (uint64_t probe = 0; probe <= t.mask; probe++) {
+        uint64_t cur = t.slots[2 * h];
+        if (cur == HMS_EMPTY) {
+            const unsigned long long prev =
+                atomicCAS((unsigned long long*)&t.slots[2 * h], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
+            if (prev == HMS_EMPTY) {
+                t.slots[2 * h + 1] = c;
+                return 1;
+            }
+            cur = prev;
+        }
+        if (cur == k) {
+            t.slots[2 * h + 1] += c;
+            return 0;
+        }
+        h = (h + 1) & t.mask;
+    }
+    *overflow = 1;
+    return 0;
+}
