@@ -532,7 +532,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.redo_count = ctx->state + ST_REDO;
             a.redo_cap = redo_cap;
             /* region sizes: a sampled digit histogram with a generous margin */
-            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> 20);
+            /* ~256K samples below 2^28 points (launch-bound batches), ~1M above */
+            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> ((uint64_t)n < (1ull << 28) ? 18 : 20));
             HIPCHK(hipMemsetAsync(hist, 0, F * 4, s));
             if (n > 0) hm_launch_sample_digits(s, a, stride, hist);
             HIPCHK(hipGetLastError());
