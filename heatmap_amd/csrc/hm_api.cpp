@@ -745,7 +745,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.runs_out = runs_sh;
             a.items = lv[l - 1].items;
             HIPCHK(hipEventRecord(ev[5 + 2 * (l - 1)], s));
-            hm_launch_partN(s, a, lv[l - 1].items, V.out16);
+            hm_launch_partN(s, a, lv[l - 1].items, V.out16, l == 1);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[6 + 2 * (l - 1)], s));
             npart = l;

@@ -36,12 +36,13 @@
 
 #ifdef HM_STAMPS
 /* phase timing (profiling builds only, tools/stamps.py): thread 0 of the first
- * HM_STAMP_BLOCKS blocks of k_partition records s_memtime at 12 points */
+ * HM_STAMP_BLOCKS blocks of one kernel records s_memtime at up to 12 points.
+ * HM_STAMPS = 1: k_partition, 2: k_project_partition, 3: k_partition_fr */
 #define HM_STAMP_BLOCKS 65536
 __device__ unsigned long long g_stamps[HM_STAMP_BLOCKS * 12];
-#define HM_STAMP(k)                                                                            \
+#define HM_STAMP_M(m, k)                                                                       \
     do {                                                                                       \
-        if (threadIdx.x == 0 && hm_block_id() < HM_STAMP_BLOCKS)                               \
+        if (HM_STAMPS == (m) && threadIdx.x == 0 && hm_block_id() < HM_STAMP_BLOCKS)           \
             g_stamps[hm_block_id() * 12 + (k)] = __builtin_amdgcn_s_memtime();                 \
     } while (0)
 extern "C" int hm_debug_stamps(void* host, size_t bytes)
@@ -49,8 +50,9 @@ extern "C" int hm_debug_stamps(void* host, size_t bytes)
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 #else
-#define HM_STAMP(k) do { } while (0)
+#define HM_STAMP_M(m, k) do { } while (0)
 #endif
+#define HM_STAMP(k) HM_STAMP_M(1, k)
 
 #define HM_YTAB_N (HM_YTAB_ROWS * HM_YTAB_STRIDE)
 __constant__ double c_ytab[HM_YTAB_N] = HM_YTAB_INIT;
@@ -120,8 +122,9 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
 {
     __shared__ uint32_t cur[HM_MAX_F1 + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ OutT stage[HM_T1 + 64];
-    /* copy pieces: <= HM_P1_PIECE staged keys of one digit each */
-    __shared__ uint32_t psrc[HM_T1 / HM_P1_PIECE + HM_MAX_F1], pdst[HM_T1 / HM_P1_PIECE + HM_MAX_F1];
+    /* digit of each staged key, and per digit (region position - stage offset) */
+    __shared__ uint16_t sdig[HM_T1 + 64];
+    __shared__ uint32_t dbase[HM_MAX_F1];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
     __shared__ double tab[HM_YTAB_N];
     constexpr bool FROM_TILES = MODE == 1;
@@ -132,6 +135,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
      * is read here (no host round trip) */
     const int64_t n = (FROM_TILES && a.n_dev) ? min((int64_t)*a.n_dev, a.n) : a.n;
     if (base >= n) return;
+    if (MODE == 0) HM_STAMP_M(2, 0);
     const uint32_t lim = 1u << a.Z;
     const double scale = hm_exp2i(a.Z);
     const double kz = HM_INV360 * scale;
@@ -209,6 +213,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
     for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
     if (!FROM_TILES) hm_load_ytab(tab);
     __syncthreads();
+    if (MODE == 0) HM_STAMP_M(2, 1);
     /* fast path for every point, branch-free; points the fast path cannot
      * settle (guard band, polar/out-of-range/non-finite input) are marked in
      * `redo` and resolved afterwards in one ballot-guarded pass */
@@ -247,6 +252,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
          * ~200 VGPRs and halve occupancy */
         __builtin_amdgcn_sched_barrier(0);
     }
+    if (MODE == 0) HM_STAMP_M(2, 2);
     if (MODE == 0) {
         /* defer: k_redo resolves these with the exact chain and feeds them
          * back as extra tiles (keeps the exact path out of this kernel's
@@ -301,10 +307,23 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         const uint32_t ws = hm_wave_sum((uint32_t)nslow);
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
+    /* one returning atomic per point: the digit histogram and the point's
+     * rank within its digit (its slot is the digit's offset + rank) */
+    uint32_t rank[HM_P1_PPT];
 #pragma unroll
-    for (int k = 0; k < HM_P1_PPT; k++) hm_lds_count_m(cur, HM_MAX_F1, hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu);
+    for (int k0 = 0; k0 < HM_P1_PPT; k0 += 4) {
+        HmMerge gm[4];
+        uint32_t old[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            gm[u] = hm_merge_prep(hm_cur_slot(dig[k0 + u], wd), dig[k0 + u] != 0xFFFFFFFFu, HM_MAX_F1);
+            old[u] = atomicAdd(&cur[gm[u].idx], gm[u].inc);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) rank[k0 + u] = hm_merge_pos(gm[u], old[u]);
+    }
     __syncthreads();
-
+    if (MODE == 0) HM_STAMP_M(2, 3);
     /* reserve each digit's keys in its region (one returning atomic per
      * non-empty digit), issued as soon as the histogram is known; the results
      * are consumed only after the scan and the claim below, so the atomic
@@ -336,58 +355,41 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         if (d < F) cur[hm_cur_slot(d, wd)] = offq[q];
     }
     __syncthreads();
-    {
-        /* every slot atomic issued before any result is consumed */
-        uint32_t old[HM_P1_PPT];
-        HmMerge g[HM_P1_PPT];
+    if (MODE == 0) HM_STAMP_M(2, 4);
 #pragma unroll
-        for (int k = 0; k < HM_P1_PPT; k++) {
-            g[k] = hm_merge_prep(hm_cur_slot(dig[k], wd), dig[k] != 0xFFFFFFFFu, HM_MAX_F1);
-            old[k] = atomicAdd(&cur[g[k].idx], g[k].inc);
-        }
-#pragma unroll
-        for (int k = 0; k < HM_P1_PPT; k++) {
-            const bool v = dig[k] != 0xFFFFFFFFu;
-            stage[v ? hm_merge_pos(g[k], old[k]) : HM_T1 + hm_lane()] = (OutT)rest[k];
-        }
+    for (int k = 0; k < HM_P1_PPT; k++) {
+        const bool v = dig[k] != 0xFFFFFFFFu;
+        const uint32_t pos = v ? cur[hm_cur_slot(v ? dig[k] : 0u, wd)] + rank[k] : HM_T1 + hm_lane();
+        stage[pos] = (OutT)rest[k];
+        sdig[pos] = (uint16_t)dig[k];
     }
-    /* copy pieces: digit d's staged keys [offq, offq + cnt) go to region
-     * position rbase[d] + gpos, cut into pieces of <= HM_P1_PIECE keys that the
-     * waves take in turn (contiguous reads and writes per wave).  A
+    /* lane-parallel copy-out: staged key i of digit d goes to region
+     * position dbase[d] + i (= rbase + gpos + i - offset of d), so a wave
+     * stores 64 consecutive staged keys (one or a few digits' runs).  A
      * reservation past the region's capacity is dropped and flagged (the host
      * re-runs the level with exact sizes). */
     bool over = false;
-    uint32_t np = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        const bool fits = d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q];
-        over |= d < F && cnt[q] && !fits;
-        np += fits ? (cnt[q] + HM_P1_PIECE - 1) / HM_P1_PIECE : 0u;
-    }
-    if (over) atomicOr(a.overflow, 1ull);
-    uint32_t npieces;
-    uint32_t pq = hm_block_excl_scan<HM_P1_THREADS>(np, scr, &npieces);
-#pragma unroll
-    for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
-        if (d < F && cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q]) {
-            const uint32_t g = rbase[q] + gpos[q];
-            for (uint32_t o = 0; o < cnt[q]; o += HM_P1_PIECE) {
-                psrc[pq] = (offq[q] + o) | ((min(cnt[q] - o, (uint32_t)HM_P1_PIECE) - 1) << 16);
-                pdst[pq] = g + o;
-                pq++;
-            }
+        if (d < F) {
+            const bool fits = cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q];
+            over |= cnt[q] && !fits;
+            dbase[d] = fits ? rbase[q] + gpos[q] - offq[q] : 0xFFFFFFFFu;
         }
     }
+    if (MODE == 0) HM_STAMP_M(2, 5);
+    if (over) atomicOr(a.overflow, 1ull);
     __syncthreads();
-    OutT* out = (OutT*)a.keys_out;
-    const int lane = hm_lane();
-    for (uint32_t j = tid >> 6; j < npieces; j += HM_P1_THREADS / 64) {
-        const uint32_t ps = psrc[j], pd = pdst[j];
-        const uint32_t src = ps & 0xFFFFu, len = (ps >> 16) + 1;
-        for (uint32_t e = lane; e < len; e += 64) out[pd + e] = stage[src + e];
+    if (MODE == 0) HM_STAMP_M(2, 6);
+    {
+        OutT* out = (OutT*)a.keys_out;
+        for (uint32_t i = tid; i < total; i += HM_P1_THREADS) {
+            const uint32_t b = dbase[sdig[i]];
+            if (b != 0xFFFFFFFFu) out[b + i] = stage[i];
+        }
     }
+    if (MODE == 0) HM_STAMP_M(2, 7);
 }
 
 /* Sampled digit histogram of level 1 (every stride-th point, fast projection
@@ -406,8 +408,8 @@ __global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t s
     const uint32_t lim = 1u << a.Z;
     const int hb = a.restbits >> 1, wd = a.dbits >> 1;
     const uint64_t m = (uint64_t)(a.n + stride_pts - 1) / stride_pts;
-    const uint64_t step = (uint64_t)gridDim.x * 256;
     const uint64_t m_up = (m + 63) & ~63ull;
+    const uint64_t step = (uint64_t)gridDim.x * 256;
     for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < m_up; j += step) {
         const uint64_t i = j * stride_pts;
         bool v = j < m && (!a.keep || a.keep[i]);
@@ -949,6 +951,148 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
         }
     }
     HM_STAMP(11);
+}
+
+/* Level 2 from the level-1 regions: every parent item spans at most
+ * HM_L1_SHARDS contiguous runs, so each thread loads its HM_FR_KPT keys
+ * straight into registers (key i of the item at thread i % T) -- no LDS
+ * staging of the streamed keys.  One returning LDS atomic per key gives both
+ * the digit histogram and the key's rank within its digit; after the scan a
+ * key's slot is offset[digit] + rank.  Small blocks (512 threads, ~34 KB of
+ * LDS) so that 4 blocks share a CU and one block's loads overlap the others'
+ * LDS phases.  Output contract identical to k_partition. */
+template <typename OutT>
+__global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a)
+{
+    constexpr int T = HM_FR_THREADS;
+    constexpr int KPT = HM_TN / T;
+    constexpr int PER = HM_MAX_FN / T;
+    __shared__ uint32_t cur[HM_MAX_FN + 64];   /* + 64 dummy words */
+    constexpr uint32_t V = 16 / sizeof(OutT);   /* keys per 16-B vector */
+    /* key e of the item at stage[sh + e], sh = it.a mod V: the copy-out then
+     * moves 16-B vectors aligned on both sides */
+    __shared__ __attribute__((aligned(16))) OutT stage[HM_TN + 64 + V];
+    __shared__ uint32_t scr[T / 64 + 1];
+    const int tid = threadIdx.x;
+    const int F = 1 << a.dbits;
+    const uint32_t g = hm_block_id();
+    if (g >= a.items) return;
+    HM_STAMP_M(3, 0);
+    const HmItem it = hm_item(a.parent, g);
+    /* the item's runs (<= HM_L1_SHARDS, block-uniform): logical start and
+     * source index of each */
+    const uint32_t nr = min(it.r1 - it.r0, (uint32_t)HM_L1_SHARDS);
+    const uint32_t nr1 = nr ? nr - 1 : 0u;
+    uint32_t rpos[HM_L1_SHARDS], rsrc[HM_L1_SHARDS];
+#pragma unroll
+    for (int j = 0; j < HM_L1_SHARDS; j++) {
+        const uint32_t r = it.r0 + min((uint32_t)j, nr1);
+        rpos[j] = (uint32_t)a.in.excl[r];
+        rsrc[j] = a.in.run[r].x;
+    }
+    const uint32_t total = it.b - it.a;
+    uint32_t kv[KPT];
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+        const uint32_t i = (uint32_t)(k * T + tid);
+        const uint32_t p = it.a + i;
+        uint32_t src = rsrc[0] + (p - rpos[0]);
+#pragma unroll
+        for (int j = 1; j < HM_L1_SHARDS; j++)
+            src = ((uint32_t)j < nr && rpos[j] <= p) ? rsrc[j] + (p - rpos[j]) : src;
+        kv[k] = i < total ? a.keys_in[src] : 0u;
+    }
+    for (int i = tid; i < F; i += T) cur[i] = 0;
+    __syncthreads();
+    HM_STAMP_M(3, 1);
+    const int sw = a.restbits >> 1, ww = a.dbits >> 1, sp = sw + ww;
+    const uint32_t m = (1u << sw) - 1u;
+    /* re-encode each key as (digit << 2s) | rest, then count and rank */
+    uint32_t rank[KPT];
+    /* HM_FR_GROUP atomics in flight per thread (more costs registers) */
+#pragma unroll
+    for (int k0 = 0; k0 < KPT; k0 += HM_FR_GROUP) {
+        HmMerge gm[HM_FR_GROUP];
+        uint32_t old[HM_FR_GROUP];
+#pragma unroll
+        for (int u = 0; u < HM_FR_GROUP; u++) {
+            const int k = k0 + u;
+            const uint32_t r = kv[k] >> sp, c = kv[k] & ((1u << sp) - 1u);
+            const uint32_t d = ((r >> sw) << ww) | (c >> sw);
+            kv[k] = (d << (2 * sw)) | ((r & m) << sw) | (c & m);
+            const bool v = (uint32_t)(k * T + tid) < total;
+            gm[u] = hm_merge_prep(hm_cur_slot(d, ww), v, HM_MAX_FN);
+            old[u] = atomicAdd(&cur[gm[u].idx], gm[u].inc);
+        }
+#pragma unroll
+        for (int u = 0; u < HM_FR_GROUP; u++) rank[k0 + u] = hm_merge_pos(gm[u], old[u]);
+    }
+    HM_STAMP_M(3, 2);
+    __syncthreads();
+    HM_STAMP_M(3, 3);
+    uint32_t cnt[PER];
+    uint32_t s = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        cnt[q] = d < F ? cur[hm_cur_slot(d, ww)] : 0u;
+        s += cnt[q];
+    }
+    uint32_t tot2;
+    uint32_t off = hm_block_excl_scan<T>(s, scr, &tot2);
+    const uint32_t tile0 = a.parent.item_begin[it.bucket];
+    const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
+    const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
+    uint32_t idx[PER], offq[PER];
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        offq[q] = off;
+        idx[q] = 0;
+        if (d < F && cnt[q])
+            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
+        off += cnt[q];
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F) cur[hm_cur_slot(d, ww)] = offq[q];
+    }
+    __syncthreads();
+    HM_STAMP_M(3, 4);
+    const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
+    const uint32_t sh0 = it.a & (V - 1);
+#pragma unroll
+    for (int k = 0; k < KPT; k++) {
+        const bool v = (uint32_t)(k * T + tid) < total;
+        const uint32_t d = kv[k] >> a.restbits;
+        const uint32_t pos = v ? sh0 + cur[hm_cur_slot(v ? d : 0u, ww)] + rank[k] : (uint32_t)HM_TN + V + (uint32_t)(tid & 63);
+        stage[pos] = (OutT)(kv[k] & restmask);
+    }
+    __syncthreads();
+    HM_STAMP_M(3, 5);
+    {
+        /* 16-B vectors [V t, V t + V) of stage map to out[it.a - sh0 + V t ..) */
+        OutT* out = (OutT*)a.keys_out + (it.a - sh0);
+        const uint32_t end = sh0 + total, nv = (end + V - 1) / V;
+        for (uint32_t t = tid; t < nv; t += T) {
+            const uint32_t e0 = t * V;
+            if (e0 >= sh0 && e0 + V <= end) {
+                *(uint4*)(out + e0) = *(const uint4*)(stage + e0);
+            } else {
+                for (uint32_t e = max(e0, sh0); e < min(e0 + V, end); e++) out[e] = stage[e];
+            }
+        }
+    }
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        const int d = tid * PER + q;
+        if (d < F && cnt[q]) {
+            const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
+            a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);
+        }
+    }
+    HM_STAMP_M(3, 6);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -2032,9 +2176,16 @@ void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon,
                        grp, idx, count, err_word);
 }
 
-void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16)
+void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16, bool few_runs)
 {
     if (items == 0) return;
+    if (few_runs && HM_K2_FR) {
+        if (out16)
+            hipLaunchKernelGGL(k_partition_fr<uint16_t>, hm_grid2(items), dim3(HM_FR_THREADS), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_partition_fr<uint32_t>, hm_grid2(items), dim3(HM_FR_THREADS), 0, s, a);
+        return;
+    }
     if (out16)
         hipLaunchKernelGGL(k_partition<uint16_t>, hm_grid2(items), dim3(HM_PN_THREADS), 0, s, a);
     else

@@ -11,7 +11,6 @@
 #define HM_P1_PPT 16
 #endif
 #define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 8192 points per tile */
-#define HM_P1_PIECE 256                     /* keys per copy piece (one wave, 4 steps) */
 #define HM_L1_SHARDS 8                      /* sub-regions of a hot level-1 digit */
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
@@ -22,7 +21,17 @@
 #ifndef HM_TN
 #define HM_TN 8192                          /* keys per partition work item */
 #endif
-#define HM_LEVEL_ZOOMS 6                    /* <= 6 zooms per level */
+/* level 2 from the level-1 regions (k_partition_fr): keys in registers */
+#ifndef HM_FR_THREADS
+#define HM_FR_THREADS 1024
+#endif
+#ifndef HM_K2_FR
+#define HM_K2_FR 1                          /* 0: k_partition (run streaming), 1: k_partition_fr */
+#endif
+#ifndef HM_FR_GROUP
+#define HM_FR_GROUP 4
+#endif
+#define HM_LEVEL_ZOOMS 6                   /* <= 6 zooms per level */
 #define HM_MAX_FN 4096
 #define HM_MAX_SHARDS 32                    /* run-counter shards per child */
 #ifndef HM_RUN_SHARD_BITS
@@ -298,7 +307,9 @@ void hm_launch_collect_exotic(hipStream_t s, const double* lat, const double* lo
 void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
                             const uint32_t* group, int64_t n, int Z, int64_t* row, int64_t* col, uint32_t* grp,
                             int64_t* idx, unsigned long long* count, unsigned long long* err_word);
-void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16);
+/* few_runs: every parent item spans <= HM_L1_SHARDS runs (parents are the
+ * level-1 regions): k_partition_fr, else k_partition */
+void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16, bool few_runs);
 /* run scan steps: per-child shard offsets + run totals; flat copy; per-child keys */
 void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a);
 void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a);

@@ -19,7 +19,9 @@ VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
 
 VARIANTS = {
     "base": [],
-    "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py
+    "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py (k_partition)
+    "stamps1": ["HM_STAMPS=2"],              # k_project_partition
+    "stamps2": ["HM_STAMPS=3"],              # k_partition_fr
     # tuning knobs (compile-time macros of the shipped sources)
     "noskew": ["HM_SKEW_CUR=0"],
     "p1_512x8": ["HM_P1_PPT=8"],
@@ -29,6 +31,7 @@ VARIANTS = {
     "t512_8k": ["HM_PN_THREADS=512"],
     "su2": ["HM_SU=2"],
     "su8": ["HM_SU=8"],
+    "k2old": ["HM_K2_FR=0"],                # level 2 through k_partition (run streaming)
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
@@ -42,6 +45,8 @@ PATCHES = {
     "noatom1": [("hm_kernels.hip", "if (d < F && cnt[q]) gpos[q] = atomicAdd(&a.fill[slot[q]], cnt[q]);",
                  "if (d < F && cnt[q]) gpos[q] = 0;")],
 }
+# compile-time macros added to a patched build
+PATCH_DEFINES = {}
 
 
 def build(names):
@@ -62,7 +67,7 @@ def build(names):
                 t = open(p).read()
                 assert old in t, (n, f, old)
                 open(p, "w").write(t.replace(old, new))
-            b.build(force=True, verbose=False, out=out, csrc=src)
+            b.build(force=True, verbose=False, out=out, csrc=src, defines=PATCH_DEFINES.get(n, []))
             shutil.rmtree(tmp)
         else:
             b.build(force=True, verbose=False, out=out, defines=VARIANTS[n])
