@@ -118,7 +118,7 @@ __device__ __forceinline__ uint32_t hm_l1_slot(const HmPart1Args& a, int d)
 /* ------------------------------------------------------------------------ */
 
 template <typename OutT, int MODE>
-__global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args a)
+__global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partition(HmPart1Args a)
 {
     __shared__ uint32_t cur[HM_MAX_F1 + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ OutT stage[HM_T1 + 64];
@@ -250,7 +250,7 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
         asm volatile("" : "+v"(dig[k]), "+v"(rest[k]));
         /* one point at a time: interleaving all eight projections would need
          * ~200 VGPRs and halve occupancy */
-        __builtin_amdgcn_sched_barrier(0);
+        if ((k % HM_P1_ILP) == HM_P1_ILP - 1) __builtin_amdgcn_sched_barrier(0);
     }
     if (MODE == 0) HM_STAMP_M(2, 2);
     if (MODE == 0) {
@@ -311,16 +311,16 @@ __global__ __launch_bounds__(HM_P1_THREADS) void k_project_partition(HmPart1Args
      * rank within its digit (its slot is the digit's offset + rank) */
     uint32_t rank[HM_P1_PPT];
 #pragma unroll
-    for (int k0 = 0; k0 < HM_P1_PPT; k0 += 4) {
-        HmMerge gm[4];
-        uint32_t old[4];
+    for (int k0 = 0; k0 < HM_P1_PPT; k0 += HM_P1_GROUP) {
+        HmMerge gm[HM_P1_GROUP];
+        uint32_t old[HM_P1_GROUP];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < HM_P1_GROUP; u++) {
             gm[u] = hm_merge_prep(hm_cur_slot(dig[k0 + u], wd), dig[k0 + u] != 0xFFFFFFFFu, HM_MAX_F1);
             old[u] = atomicAdd(&cur[gm[u].idx], gm[u].inc);
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) rank[k0 + u] = hm_merge_pos(gm[u], old[u]);
+        for (int u = 0; u < HM_P1_GROUP; u++) rank[k0 + u] = hm_merge_pos(gm[u], old[u]);
     }
     __syncthreads();
     if (MODE == 0) HM_STAMP_M(2, 3);
@@ -1099,58 +1099,84 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
 /* run scan: sharded run counters -> one flat, child-ordered run list        */
 /* ------------------------------------------------------------------------ */
 
-/* per child: exclusive shard offsets within the child, and its run total */
+/* per (child, shard) counter: exclusive offset within the child, and per
+ * child its run total.  Lanes read consecutive counters (coalesced); a
+ * child's S = 2^shard_bits shards are S consecutive lanes, scanned with
+ * shuffles.  Every lane of a wave runs every step. */
 __global__ __launch_bounds__(256) void k_rs_count(HmRsArgs a)
 {
+    const uint32_t S = 1u << a.shard_bits;
+    const uint64_t npairs = a.nchildren << a.shard_bits;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
-    const uint32_t S = 1u << a.shard_bits;
-    for (uint64_t c = (uint64_t)blockIdx.x * 256 + threadIdx.x; c < a.nchildren; c += stride) {
-        uint32_t acc = 0;
-        for (uint32_t s = 0; s < S; s++) {
-            const uint64_t k = (c << a.shard_bits) + s;
-            const uint32_t n = a.nruns[k];
-            a.shoff[k] = acc;
-            acc += n;
+    const uint32_t sl = (uint32_t)hm_lane() & (S - 1);
+    for (uint64_t k = (uint64_t)blockIdx.x * 256 + threadIdx.x; k - (uint64_t)hm_lane() < npairs; k += stride) {
+        const bool in = k < npairs;
+        const uint32_t n = in ? a.nruns[k] : 0u;
+        uint32_t v = n;
+        for (uint32_t o = 1; o < S; o <<= 1) {
+            const uint32_t t = __shfl_up(v, o, 64);
+            if (sl >= o) v += t;
         }
-        a.nr[c] = acc;
+        if (in) {
+            a.shoff[k] = v - n;
+            if (sl == S - 1) a.nr[k >> a.shard_bits] = v;
+        }
     }
 }
 
-/* copy shard (c, s) of the sharded layout to flat[runbase[c] + shoff .. ) */
-__device__ __forceinline__ void hm_rs_copy_shard(const HmRsArgs& a, uint64_t c, uint32_t s, uint32_t t, uint32_t nt)
+/* sharded run list of child c -> flat[runbase[c] .. + nr[c]), one wave per
+ * child: lanes 0..S-1 hold the child's shards (count, flat offset, source),
+ * and the wave copies the child's runs HM_RS_SLICE at a time, 8 loads per lane
+ * in flight, each run's shard found by a shuffle search over the S lanes.
+ * The hottest child (one run per parent work item, tens of thousands) is the
+ * critical path: 8-deep loads cut its chain of dependent memory steps 8x. */
+#define HM_RS_SLICE 512
+__global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
 {
-    const uint64_t k = (c << a.shard_bits) + s;
-    const uint32_t n = a.nruns[k];
-    if (n == 0) return;
-    const uint64_t p = c >> a.dbits;
-    const uint64_t d = c & ((1ull << a.dbits) - 1);
-    const uint32_t t0 = a.parent_item_begin[p];
-    const uint32_t tp = a.parent_item_begin[p + 1] - t0;
-    const uint32_t cap = (tp + (1u << a.shard_bits) - 1) >> a.shard_bits;
-    const uint64_t src = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits) + (uint64_t)s * cap;
-    const uint64_t dst = a.runbase[c] + a.shoff[k];
-    for (uint32_t i = t; i < n; i += nt) {
-        const uint2 r = a.runs[src + i];
-        a.flat[dst + i] = r;
-        a.cnt[dst + i] = r.y;
-    }
-}
-
-/* few children (level 1): one block per (child, shard) */
-__global__ __launch_bounds__(256) void k_rs_copy_pairs(HmRsArgs a)
-{
-    const uint64_t pair = blockIdx.x;
-    hm_rs_copy_shard(a, pair >> a.shard_bits, (uint32_t)(pair & ((1u << a.shard_bits) - 1)), threadIdx.x, 256);
-}
-
-/* many children: one wave per child */
-__global__ __launch_bounds__(256) void k_rs_copy_children(HmRsArgs a)
-{
-    const uint64_t stride = (uint64_t)gridDim.x * 4;
     const uint32_t S = 1u << a.shard_bits;
-    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < a.nchildren; c += stride) {
-        if (a.nr[c] == 0) continue;
-        for (uint32_t s = 0; s < S; s++) hm_rs_copy_shard(a, c, s, threadIdx.x & 63, 64);
+    const uint32_t lane = (uint32_t)hm_lane();
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < a.nchildren; c += nw) {
+        const uint64_t nr = a.nr[c];
+        if (nr == 0) continue;
+        const uint64_t k = (c << a.shard_bits) + lane;
+        uint32_t n = 0;
+        uint64_t src = 0;
+        if (lane < S) {
+            n = a.nruns[k];
+            const uint64_t p = c >> a.dbits;
+            const uint64_t d = c & ((1ull << a.dbits) - 1);
+            const uint32_t t0 = a.parent_item_begin[p];
+            const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+            const uint32_t cap = (tp + S - 1) >> a.shard_bits;
+            src = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits) + (uint64_t)lane * cap;
+        }
+        const uint32_t incl = hm_wave_incl_scan(n);   /* shard offsets within the child */
+        const uint64_t rb = a.runbase[c];
+        for (uint64_t j0 = 0; j0 < nr; j0 += HM_RS_SLICE) {
+            uint2 r[HM_RS_SLICE / 64];
+#pragma unroll
+            for (int u = 0; u < HM_RS_SLICE / 64; u++) {
+                const uint64_t x = j0 + (uint64_t)u * 64 + lane;
+                const uint32_t xc = (uint32_t)min(x, nr - 1);
+                uint32_t l = 0;
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (__shfl(incl, l + st - 1, 64) <= xc) l += st;
+                l = min(l, 63u);
+                const uint32_t off = xc - (__shfl(incl, l, 64) - __shfl(n, l, 64));
+                const uint64_t sj = __shfl(src, l, 64) + off;
+                r[u] = x < nr ? a.runs[sj] : make_uint2(0, 0);
+            }
+#pragma unroll
+            for (int u = 0; u < HM_RS_SLICE / 64; u++) {
+                const uint64_t x = j0 + (uint64_t)u * 64 + lane;
+                if (x < nr) {
+                    a.flat[rb + x] = r[u];
+                    a.cnt[rb + x] = r[u].y;
+                }
+            }
+        }
     }
 }
 
@@ -1644,6 +1670,22 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
             key[m] = i < nk ? (uint32_t)ks[i] : 0u;
             own[m] = 0;
         }
+#if HM_SP_FLAT
+        /* every level at once: each key adds 1 to its cell at every level (no
+         * level-to-level barrier); counts stay <= HM_SP_MAX */
+#pragma unroll
+        for (int m = 0; m < KPT; m++) {
+            const uint32_t i = tid + m * HM_SP_THREADS;
+            if (i < nk) {
+                for (int l = 0; l < lg; l++) {
+                    const uint32_t c = hm_sp_cell(key[m], lg, l, cofs[l]);
+                    const uint32_t old = atomicAdd(&g[c >> 1], 1u << (16 * (c & 1)));
+                    own[m] |= (hm_sp_half(old, c) == 0 ? 1u : 0u) << l;
+                }
+            }
+        }
+        __syncthreads();
+#else
         for (int l = 0; l < lg; l++) {
 #pragma unroll
             for (int m = 0; m < KPT; m++) {
@@ -1662,6 +1704,7 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
             }
             __syncthreads();
         }
+#endif
         /* levels in [zmin, zmax]: one reservation, thread-contiguous slots */
         uint32_t zmask = 0;
         for (int l = 0; l < lg; l++) {
@@ -2201,17 +2244,14 @@ static unsigned hm_grid(uint64_t n, unsigned per, unsigned cap)
 
 void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a)
 {
-    hipLaunchKernelGGL(k_rs_count, dim3(hm_grid(a.nchildren, 256, 16384)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rs_count, dim3(hm_grid(a.nchildren << a.shard_bits, 256, 16384)), dim3(256), 0, s, a);
 }
 
 void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a)
 {
     const uint64_t pairs = a.nchildren << a.shard_bits;
     if (pairs == 0) return;   /* a level with no parent buckets (nothing kept) */
-    if (a.nchildren <= 8192 && pairs <= (1u << 20))
-        hipLaunchKernelGGL(k_rs_copy_pairs, dim3((unsigned)pairs), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_rs_copy_children, dim3(hm_grid(a.nchildren, 4, 16384)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rs_copy, dim3(hm_grid(a.nchildren, 4, 16384)), dim3(256), 0, s, a);
 }
 
 void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a)

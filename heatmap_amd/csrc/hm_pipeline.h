@@ -11,6 +11,15 @@
 #define HM_P1_PPT 16
 #endif
 #define HM_T1 (HM_P1_THREADS * HM_P1_PPT) /* 8192 points per tile */
+#ifndef HM_P1_GROUP
+#define HM_P1_GROUP 4                       /* LDS count+rank atomics in flight per thread */
+#endif
+#ifndef HM_P1_ILP
+#define HM_P1_ILP 1                         /* projections the scheduler may interleave */
+#endif
+#ifndef HM_P1_WAVES
+#define HM_P1_WAVES 1                       /* waves per SIMD the register budget targets */
+#endif
 #define HM_L1_SHARDS 8                      /* sub-regions of a hot level-1 digit */
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
@@ -48,6 +57,9 @@
 #define HM_SP_THREADS 512
 #ifndef HM_SP_MAX
 #define HM_SP_MAX 2048
+#endif
+#ifndef HM_SP_FLAT
+#define HM_SP_FLAT 0                        /* 1: all pyramid levels counted in one pass */
 #endif
 #define HM_SP_WORDS ((HM_AG_CELLS / 3 * 4 + 1) / 2 + 1)   /* 4^7 + ... + 4 cells */
 #define HM_SP_GRID (256 * 3)
