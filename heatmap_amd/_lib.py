@@ -118,7 +118,8 @@ def raise_for(st: int, index: int = -1):
     """Raise the reference's exception for a per-point error kind."""
     if st == HM_OK:
         return
-    where = "" if index < 0 else " (point %d)" % index
+    per_point = st in (HM_E_NAN, HM_E_DOMAIN, HM_E_INF, HM_E_RANGE, HM_E_EXOTIC)
+    where = "" if index < 0 or not per_point else " (point %d)" % index
     if st == HM_E_NAN:
         raise ValueError("cannot convert float NaN to integer")
     if st == HM_E_DOMAIN:

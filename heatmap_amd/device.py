@@ -168,10 +168,20 @@ class CountBuffers:
         self.nx = 0
 
 
+# points per hm_count call: the ABI takes n < 2^32 - 16 (u32 key positions);
+# 2^31 keeps the level-1 regions' sampled margins inside the u32 key space
+MAX_CALL_POINTS = 1 << 31
+
+
 def count_device(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, buffers=None,
-                 tiles: bool = False):
+                 tiles: bool = False, chunk: int = MAX_CALL_POINTS):
     """Run the count pyramid; returns (n_cells, buffers) with results left in
-    HBM (buffers.nx: cells outside the square, in buffers.xcells)."""
+    HBM (buffers.nx: cells outside the square, in buffers.xcells).
+
+    Inputs of more than `chunk` points (one call holds < 2^32) are counted
+    chunk by chunk in input order, so the first failing point is still the one
+    reported, and the chunks' cells are summed on the device (hm_cells_merge;
+    cells outside the square with torch ops)."""
     torch = _torch()
     ctx = context(device)
     if tiles:
@@ -188,8 +198,12 @@ def count_device(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int
         kp = _dev(keep, torch.uint8, device)
         if kp.numel() != n:
             raise ValueError("keep must have one entry per point")
+    if n > chunk:
+        return _count_chunked(a, b, kp, n, zmin, zmax, device, tiles, int(chunk))
     if buffers is None:
-        buffers = CountBuffers(max(1024, 4 * n + 64), device)
+        # cells <= 4 n + ... for small inputs; large ones start at 64M cells and
+        # grow on HM_E_CAPACITY (the call is then repeated)
+        buffers = CountBuffers(max(1024, min(4 * n + 64, 1 << 26)), device)
     fn = ctx.L.hm_count_tiles if tiles else ctx.L.hm_count
     while True:
         nout = ctypes.c_int64(0)
@@ -209,10 +223,48 @@ def count_device(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int
         return nout.value, buffers
 
 
-def count(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, tiles: bool = False) -> Counts:
+def _count_chunked(a, b, kp, n, zmin, zmax, device, tiles, chunk):
+    torch = _torch()
+    ctx = context(device)
+    keys, counts, xcells = [], [], []
+    for s in range(0, n, chunk):
+        e = min(n, s + chunk)
+        try:
+            m, buf = count_device(a[s:e], b[s:e], None if kp is None else kp[s:e], zmin, zmax, device,
+                                  tiles=tiles, chunk=chunk)
+        except _lib.DevicePathUnsupported as ex:
+            idx, _ = ctx.last_error()
+            raise _lib.DevicePathUnsupported(str(ex).split(" (point")[0] +
+                                             ("" if idx < 0 else " (point %d)" % (idx + s))) from None
+        keys.append(buf.keys[:m].clone())
+        counts.append(buf.counts[:m].clone())
+        if buf.nx:
+            xcells.append(buf.xcells[:4 * buf.nx].reshape(-1, 4).clone())
+    k = torch.cat(keys)
+    c = torch.cat(counts)
+    cap = max(int(k.numel()), 1)
+    out = CountBuffers(cap, device, 1024)
+    nout = ctypes.c_int64(0)
+    rc = ctx.L.hm_cells_merge(ctx.ptr, _ptr(k), _ptr(c), int(k.numel()), _ptr(out.keys), _ptr(out.counts), cap,
+                              ctypes.byref(nout))
+    if rc != _lib.HM_OK:
+        _lib.raise_for(rc)
+    if xcells:
+        x = torch.cat(xcells)
+        u, inv = torch.unique(x[:, :3], dim=0, return_inverse=True)
+        tot = torch.zeros(u.shape[0], dtype=torch.int64, device=x.device).index_add_(0, inv, x[:, 3])
+        rec = torch.cat([u, tot[:, None]], dim=1)
+        out.xcapacity = rec.shape[0]
+        out.xcells = rec.reshape(-1).contiguous()
+        out.nx = rec.shape[0]
+    return nout.value, out
+
+
+def count(lat, lon, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0, tiles: bool = False,
+          chunk: int = MAX_CALL_POINTS) -> Counts:
     """Per-(zoom, row, col) counts for zooms zmin..zmax (host arrays), cells
     inside and outside [0, 2^z)^2 together."""
-    m, buf = count_device(lat, lon, keep, zmin, zmax, device, tiles=tiles)
+    m, buf = count_device(lat, lon, keep, zmin, zmax, device, tiles=tiles, chunk=chunk)
     ctx = context(device)
     slow, us = ctx.last_stats()
     keys = buf.keys[:m].cpu().numpy().view(np.uint64)
