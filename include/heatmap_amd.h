@@ -58,10 +58,11 @@ extern "C" {
 #define HM_E_DOMAIN 2    /* ValueError("math domain error")  tan(+-inf) / log(<=0), tile.py:17 */
 #define HM_E_INF 3       /* OverflowError("cannot convert float infinity to integer") tile.py:21 */
 #define HM_E_RANGE 8     /* representable by the reference but not by this path:
-                            |col| >= 2^63, or |lat*pi/180| beyond glibc's
-                            non-Payne-Hanek range (|lat| >~ 6.0e9 degrees), or
-                            (cells outside the square) a zoom-0 tile row
-                            outside [-16, 16) / column outside [-2^47, 2^47) */
+                            |col| >= 2^63, or (cells outside the square) a
+                            zoom-0 tile row outside [-16, 16) / column outside
+                            [-2^47, 2^47).  (Latitudes of any magnitude are
+                            projected: glibc's Payne-Hanek reduction is
+                            restated, csrc/hm_branred.h.) */
 #define HM_E_EXOTIC 9    /* hm_stream_add only: a kept point whose zoom-zmax tile
                             lies outside [0, 2^zmax)^2 (|lat| > 85.0511..., or
                             lon outside [-180, 180)); the resident table's keys

@@ -24,7 +24,7 @@ def host_math():
     out_dir = os.path.join(REPO, "tests", "host_math", "_build")
     out = os.path.join(out_dir, "libhm_host_math.so")
     deps = [src] + [os.path.join(REPO, "heatmap_amd", "csrc", f) for f in
-                    ("hm_project.h", "hm_glibc_emul.h", "hm_common.h", "hm_ytab.h")]
+                    ("hm_project.h", "hm_glibc_emul.h", "hm_branred.h", "hm_common.h", "hm_ytab.h")]
     if not os.path.exists(out) or any(os.path.getmtime(d) > os.path.getmtime(out) for d in deps):
         os.makedirs(out_dir, exist_ok=True)
         subprocess.check_call(["gcc", "-O2", "-mfma", "-ffp-contract=off", "-fPIC", "-shared", "-w",

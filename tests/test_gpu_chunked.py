@@ -25,9 +25,9 @@ def test_chunked_vs_oracle(gpu, zmax, chunk):
 
 def test_chunked_error_index(gpu):
     lat, lon = _exotic_cloud(200_000, seed=3, frac=0.0)
-    lat = lat.copy()
-    lat[150_123] = 1e12          # |lat*pi/180| >= 1.05e8: HM_E_RANGE
-    lat[190_000] = 2e12
+    lon = lon.copy()
+    lon[150_123] = 1e300         # column beyond int64: HM_E_RANGE
+    lon[190_000] = -1e300
     with pytest.raises(_lib.DevicePathUnsupported, match=r"\(point 150123\)"):
         device.count(lat, lon, None, 0, 14, chunk=70_000)
 

@@ -101,3 +101,22 @@ def test_sparse_fallback_vs_oracle(gpu, n, zmin, zmax, fallback):
     got = device.count(lat, lon, None, zmin, zmax)
     assert (got.stage_us[0] == 0.0) == fallback      # stage 0: the level-1 kernel
     _same(got.sorted(), oracle.count(lat, lon, None, zmin, zmax))
+
+
+def test_huge_latitudes(gpu):
+    """|lat pi/180| >= 105414350: glibc reduces with __branred, restated on the
+    device (hm_branred.h); projection statuses/rows and counts equal the
+    oracle's (live libm)."""
+    rng = np.random.default_rng(12)
+    n = 100_000
+    lat = np.exp(rng.uniform(np.log(6.1e9), np.log(1e300), n)) * rng.choice([-1.0, 1.0], n)
+    lon = rng.uniform(-180.0, 180.0, n)
+    for z in (0, 14, 18, 21):
+        p = device.project(lat, lon, z)
+        ro, co, so, _ = oracle.project(lat, lon, z)
+        assert np.array_equal(p.status, so), z
+        ok = so == 0
+        assert np.array_equal(p.row[ok], ro[ok]) and np.array_equal(p.col[ok], co[ok]), z
+    keep = (oracle.project(lat, lon, 18)[2] == 0).astype(np.uint8)
+    lat2, lon2 = np.where(keep == 1, lat, 10.0), lon
+    _same(device.count(lat2, lon2, None, 0, 18).sorted(), oracle.count(lat2, lon2, None, 0, 18))

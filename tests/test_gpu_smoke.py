@@ -21,10 +21,6 @@ def test_project_kat(gpu):
         re_, ce = d["row_err"][m], d["col_err"][m]
         exp = np.where(re_ != 0, re_, np.where(ce == 8, 8, ce))
         ok = (p.status == exp) & ((exp != 0) | ((p.row == d["row"][m]) & (p.col == d["col"][m])))
-        # documented gap: |lat*pi/180| >= 105414350 needs glibc's Payne-Hanek
-        # reduction (__branred), reported as HM_E_RANGE instead of a row
-        big = np.abs(d["lat"][m] * np.pi / 180) >= 105414350.0
-        ok |= big & (p.status == 8)
         bad += int((~ok).sum())
     assert bad == 0
 

@@ -51,11 +51,6 @@ def test_product_math_vs_kat(host_math):
         re_, ce = d["row_err"][m], d["col_err"][m]
         exp = np.where(re_ != 0, re_, ce)
         ok = (st == exp) & ((exp != 0) | ((r == d["row"][m]) & (c == d["col"][m])))
-        # documented gap: |lat*pi/180| >= 105414350 needs glibc's Payne-Hanek
-        # reduction, reported as HM_E_RANGE (DevicePathUnsupported) instead
-        with np.errstate(over="ignore"):
-            big = np.abs(d["lat"][m] * np.pi / 180) >= 105414350.0
-        ok |= big & (st == HM_E_RANGE)
         bad += int((~ok).sum())
         slow_total += int(slow.sum())
     assert bad == 0
@@ -125,3 +120,35 @@ def test_glibc_restatement_bit_exact(host_math, fn, lo, hi):
     bad = host_math.hmh_glibc_check(fn, _dp(x), x.size, ctypes.byref(un))
     assert bad == 0
     assert un.value == 0
+
+
+@pytest.mark.parametrize("fn", [0, 1])
+def test_glibc_branred_bit_exact(host_math, fn):
+    """tan/cos beyond 105414350, where glibc reduces with __branred
+    (hm_branred.h): log-uniform magnitudes up to DBL_MAX, both signs, plus the
+    threshold's neighbourhood and multiples of pi/2 (hard cases)."""
+    rng = np.random.default_rng(77 + fn)
+    x = np.exp(rng.uniform(np.log(1.0e8), np.log(1.79e308), 300_000)) * rng.choice([-1.0, 1.0], 300_000)
+    near = 105414350.0 + rng.uniform(-64.0, 64.0, 20_000)
+    k = rng.integers(1, 1 << 52, 20_000).astype(np.float64) * (np.pi / 2)
+    x = np.concatenate([x, near, -near, k, np.nextafter(k, np.inf), np.nextafter(k, -np.inf)])
+    un = ctypes.c_int64(0)
+    bad = host_math.hmh_glibc_check(fn, _dp(x), x.size, ctypes.byref(un))
+    assert un.value == 0
+    assert bad == 0
+
+
+def test_product_math_huge_latitudes(host_math):
+    """Latitudes beyond ~6e9 degrees reach glibc's __branred (hm_branred.h):
+    rows, statuses and columns equal the oracle's (live libm) at every zoom."""
+    rng = np.random.default_rng(11)
+    n = 200_000
+    lat = np.exp(rng.uniform(np.log(6.1e9), np.log(1e300), n)) * rng.choice([-1.0, 1.0], n)
+    lon = rng.uniform(-180.0, 180.0, n)
+    for z in (0, 7, 18, 21, 30):
+        r, c, st, _ = _host_project(host_math, lat, lon, z)
+        ro, co, so, _ = oracle.project(lat, lon, z)
+        assert np.array_equal(st, so), z
+        ok = so == 0
+        assert ok.sum() > n // 4
+        assert np.array_equal(r[ok], ro[ok]) and np.array_equal(c[ok], co[ok]), z

@@ -20,8 +20,8 @@ emitted code is exact on any IEEE-754 binary64 machine with a correct fma and
 correctly rounded division -- gfx950 included.  Control flow keeps the
 original branch structure as labels/gotos.  Constants and tables are copied
 from libm's ``.rodata`` (they are data, not code).  The calls into
-``__branred`` (Payne-Hanek reduction for |x| >= 2^27-ish) are not restated:
-those inputs set ``*unsupported = 1`` and the caller reports HM_E_RANGE.
+``__branred`` (Payne-Hanek reduction for |x| >= 105414350) go to the
+hand-written restatement in ``heatmap_amd/csrc/hm_branred.h``.
 
 The output header is committed; re-run this script only if libm changes:
     python tools/glibc_emul/gen_glibc_emul.py > heatmap_amd/csrc/hm_glibc_emul.h
@@ -117,6 +117,7 @@ class Tr:
         self.consts = {}
         self.used_tables = set()
         self.ptrbase = {}      # reg -> table base address (symbolic)
+        self.lea_stack = {}    # reg -> stack slot whose address a leaq put there (__branred arguments)
         self.flags = None      # description of last flag-setting insn
         self.targets = set()
         for (a, mn, ops, c) in self.lines:
@@ -364,6 +365,9 @@ class Tr:
                     self.ptrbase[reg] = a
                 else:
                     e("/* %s %s (address of stack slot, only for __branred) */" % (mn, ops_s))
+                    ref, kind = self.mem_ref(src, comment)
+                    assert kind == "stack", (self.name, ops_s)
+                    self.lea_stack[ALIAS[dst[1:]][0]] = ref
                 continue
             if mn == "leal":
                 src, dst = ops
@@ -486,7 +490,11 @@ class Tr:
 
     def extern_str(self, what):
         if what == "branred":
-            return "*unsupported = 1; return 0.0;"
+            # int __branred(double x, double *a, double *aa): x in xmm0, a/aa
+            # the stack slots the preceding leaq's put in rdi/rsi (hm_branred.h)
+            a, aa = self.lea_stack["rdi"], self.lea_stack["rsi"]
+            return ("{ double ba_ = 0.0, baa_ = 0.0; rax = (uint64_t)(uint32_t)hm_branred(x0.d, &ba_, &baa_); "
+                    "%s.d = ba_; %s.d = baa_; }" % (a, aa))
         if what == "math_invalid":
             return "*unsupported = 2; return (x0.d - x0.d) / (x0.d - x0.d);"
         if what == "math_divzero":
@@ -537,6 +545,7 @@ def main():
     o.append(" * tests/test_math_host.py::test_glibc_restatement_bit_exact. */")
     o.append("#pragma once")
     o.append('#include "hm_common.h"')
+    o.append('#include "hm_branred.h"')
     o.append("")
     o.append("HM_EMUL_BEGIN")
     o.append("")

@@ -40,6 +40,9 @@ VARIANTS = {
     "p1ilp2": ["HM_P1_ILP=2"],
     "frg8": ["HM_FR_GROUP=8"],
     "spflat": ["HM_SP_FLAT=1"],
+    "fr512_4k": ["HM_FR_THREADS=512", "HM_TN=4096"],
+    "ta64k": ["HM_TA=65536"],
+    "ta128k": ["HM_TA=131072"],
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
