@@ -18,6 +18,14 @@ label is a device rollup of the hour buckets:
 
 so a caller sees the same rows as heatmap.assemble_rows over every point so
 far, restricted to the label's period.
+
+Kept points whose zoom-zmax tile lies outside [0, 2^zmax)^2 (|lat| > 85.0511,
+lon outside [-180, 180): the reference bins them, tile.py:17,21 never clamp)
+do not fit the resident table's keys.  A batch holding any (hm_stream_add
+answers HM_E_EXOTIC before inserting anything) is split on the device: the
+in-square points go to the table, the out-of-square ones are counted per
+(group, hour) by hm_count_grouped and their (rare, pre-aggregated) cell
+records are kept beside the table and joined into every rollup.
 """
 from __future__ import annotations
 
@@ -36,6 +44,38 @@ SPANS = {"hour": _lib.HM_SPAN_HOUR, "day": _lib.HM_SPAN_DAY, "month": _lib.HM_SP
          "year": _lib.HM_SPAN_YEAR, "alltime": _lib.HM_SPAN_ALLTIME}
 NOGROUP = 0xFFFFFFFE      # kept points whose user id makes no group ('x*', or no user ids)
 ALLGROUPS = 0xFFFFFFFF    # merged rollups
+
+
+UNDATED_HOUR = -1         # hour of points added without one (alltime only)
+
+
+def _sum_records(rec: np.ndarray, w: int) -> np.ndarray:
+    """Sum column w of int64 records over equal leading columns [0, w)."""
+    if not len(rec):
+        return rec
+    u, inv = np.unique(rec[:, :w], axis=0, return_inverse=True)
+    tot = np.zeros(len(u), dtype=np.int64)
+    np.add.at(tot, inv.reshape(-1), rec[:, w])
+    return np.concatenate([u, tot[:, None]], axis=1)
+
+
+def _period(timespan: str, hour: np.ndarray) -> np.ndarray:
+    """hm_stream_rollup's period of each epoch hour: the hour, days since
+    1970-01-01, year * 12 + month - 1, or the year (UTC civil calendar)."""
+    if timespan == "hour":
+        return hour
+    days = hour // 24
+    if timespan == "day":
+        return days
+    z = days + 719468                    # civil_from_days (H. Hinnant), as k_stream_rollup
+    era = np.floor_divide(z, 146097)
+    doe = z - era * 146097
+    yoe = (doe - doe // 1460 + doe // 36524 - doe // 146096) // 365
+    doy = doe - (365 * yoe + yoe // 4 - yoe // 100)
+    mp = (5 * doy + 2) // 153
+    m = np.where(mp < 10, mp + 3, mp - 9)
+    y = yoe + era * 400 + (m <= 2)
+    return y * 12 + m - 1 if timespan == "month" else y
 
 
 def span_label(timespan: str, period: int) -> str:
@@ -63,6 +103,8 @@ class StreamingHeatmap:
         self.zmin, self.zmax, self.base_hour = int(zmin), int(zmax), int(base_hour)
         self.labels = ["all"]          # group id -> row-key group (0: the literal user id 'all')
         self._index = {"all": 0}
+        # cells outside [0, 2^zmax)^2: (group, hour or UNDATED_HOUR, zoom, row, col, count)
+        self._x = np.zeros((0, 6), dtype=np.int64)
         p = ctypes.c_void_p()
         rc = self.ctx.L.hm_stream_create(self.ctx.ptr, self.zmin, self.zmax, self.base_hour, int(initial_cells),
                                          int(max_buckets), ctypes.byref(p))
@@ -135,9 +177,44 @@ class StreamingHeatmap:
             raise ValueError("keep must have one entry per point")
         rc = self.ctx.L.hm_stream_add(self.ptr, device._ptr(la), device._ptr(lo), device._ptr(kp), device._ptr(hr),
                                       device._ptr(gr), n)
+        if rc == _lib.HM_E_EXOTIC:
+            self._add_split(la, lo, kp, hr, gr, n)
+            return
         if rc != _lib.HM_OK:
             idx, kind = self.ctx.last_error()
             _lib.raise_for(rc, idx)
+
+    def _add_split(self, la, lo, kp, hr, gr, n):
+        """The batch holds kept points outside the square: project once on the
+        device (zoom zmax), insert the in-square ones, count the others per
+        (group, hour) with hm_count_grouped.  A projection error raises before
+        anything is inserted (hm_stream_add checks the whole batch)."""
+        torch = self._torch
+        row = torch.empty(n, dtype=torch.int64, device=la.device)
+        col = torch.empty(n, dtype=torch.int64, device=la.device)
+        st = torch.empty(n, dtype=torch.uint8, device=la.device)
+        self.ctx.L.hm_project(self.ctx.ptr, device._ptr(la), device._ptr(lo), n, self.zmax, device._ptr(row),
+                              device._ptr(col), device._ptr(st))
+        lim = 1 << self.zmax
+        out = (st == 0) & ((row < 0) | (row >= lim) | (col < 0) | (col >= lim))
+        if kp is not None:
+            out &= kp != 0
+        keep_in = (~out).to(torch.uint8) if kp is None else (kp * (~out).to(torch.uint8))
+        rc = self.ctx.L.hm_stream_add(self.ptr, device._ptr(la), device._ptr(lo), device._ptr(keep_in),
+                                      device._ptr(hr), device._ptr(gr), n)
+        if rc != _lib.HM_OK:
+            idx, kind = self.ctx.last_error()
+            _lib.raise_for(rc, idx)
+        sel = out.nonzero().flatten()
+        g = (gr[sel].to(torch.int64) & 0xFFFFFFFF) if gr is not None else torch.full_like(sel, NOGROUP)
+        h = (hr[sel].to(torch.int64) & 0xFFFFFFFF) if hr is not None else torch.full_like(sel, UNDATED_HOUR)
+        pair, inv = torch.unique(torch.stack([g, h], 1), dim=0, return_inverse=True)
+        gc = device.count_grouped(la[sel], lo[sel], inv.to(torch.int32), None, self.zmin, self.zmax,
+                                  device=self.device_index)
+        pg = pair.cpu().numpy()[gc.group.astype(np.int64)]
+        rec = np.stack([pg[:, 0], pg[:, 1], gc.zoom.astype(np.int64), gc.row, gc.col, gc.count.astype(np.int64)],
+                       axis=1)
+        self._x = _sum_records(np.concatenate([self._x, rec]), 5)
 
     # ---------------------------------------------------------------- queries
 
@@ -178,11 +255,35 @@ class StreamingHeatmap:
             return n.value, keys, counts, groups, periods
 
     def rollup(self, timespan: str = "alltime", merge_groups: bool = True, select: int = -1):
-        """Host arrays (group u32, period u32, zoom, row, col, count)."""
+        """Host arrays (group u32, period u32, zoom, row, col, count), cells
+        outside the square included."""
         n, keys, counts, groups, periods = self.rollup_device(timespan, merge_groups, select)
         z, r, c = device.decode_keys(keys[:n].cpu().numpy().view(np.uint64))
-        return (groups[:n].cpu().numpy().view(np.uint32), periods[:n].cpu().numpy().view(np.uint32), z, r, c,
-                counts[:n].cpu().numpy())
+        out = (groups[:n].cpu().numpy().view(np.uint32), periods[:n].cpu().numpy().view(np.uint32), z, r, c,
+               counts[:n].cpu().numpy())
+        if not len(self._x):
+            return out
+        x = self._exotic_rollup(timespan, merge_groups, select)
+        return tuple(np.concatenate([a, b.astype(a.dtype)]) for a, b in zip(out, x))
+
+    def _exotic_rollup(self, timespan, merge_groups, select):
+        """The out-of-square records summed per (group, period) of `timespan`
+        (the periods hm_stream_rollup uses)."""
+        g, h, z, r, c, n = self._x.T
+        dated = h != UNDATED_HOUR
+        if timespan == "alltime":
+            period = np.zeros_like(h)
+        else:
+            g, h, z, r, c, n = g[dated], h[dated], z[dated], r[dated], c[dated], n[dated]
+            period = _period(timespan, h)
+        if select >= 0:
+            m = period == select
+            g, period, z, r, c, n = g[m], period[m], z[m], r[m], c[m], n[m]
+        if merge_groups:
+            g = np.full_like(g, ALLGROUPS)
+        rec = _sum_records(np.stack([g, period, z, r, c, n], axis=1), 5) if len(g) else np.zeros((0, 6), np.int64)
+        return (rec[:, 0].astype(np.uint32), rec[:, 1].astype(np.uint32), rec[:, 2].astype(np.int32), rec[:, 3],
+                rec[:, 4], rec[:, 5])
 
     def extract_device(self, hour: int = ALLTIME):
         """(n, keys, counts, hours) as torch CUDA tensors (hm_count key
@@ -194,10 +295,17 @@ class StreamingHeatmap:
         return n, k, c, (p if hour == EACH_HOUR else None)
 
     def counts(self, hour: int = ALLTIME) -> device.Counts:
-        """Cells of every kept point (ALLTIME) or of one epoch hour."""
+        """Cells of every kept point (ALLTIME) or of one epoch hour (cells
+        outside the square included)."""
         n, keys, counts, _ = self.extract_device(hour)
         z, r, c = device.decode_keys(keys[:n].cpu().numpy().view(np.uint64))
-        return device.Counts(z, r, c, counts[:n].cpu().numpy(), 0, [])
+        cnt = counts[:n].cpu().numpy()
+        if len(self._x):
+            _, _, xz, xr, xc, xn = self._exotic_rollup("alltime" if hour == ALLTIME else "hour", True,
+                                                       -1 if hour == ALLTIME else int(hour))
+            z, r, c, cnt = (np.concatenate([z, xz.astype(z.dtype)]), np.concatenate([r, xr]),
+                            np.concatenate([c, xc]), np.concatenate([cnt, xn]))
+        return device.Counts(z, r, c, cnt, 0, [])
 
     def hourly(self):
         """{epoch hour: Counts} for every non-empty hour."""

@@ -176,20 +176,25 @@ def test_stream_rows_match_reference(gpu):
 
 
 def test_stream_batch_is_atomic(gpu):
-    """A batch whose SECOND hour holds a kept point outside the square (lon 200)
-    raises and changes no counts (one count pass, checked before insertion)."""
+    """A batch whose SECOND hour holds a failing point (NaN latitude) raises
+    and changes no counts (one count pass, checked before insertion), also
+    when the batch holds points outside the square (the split path)."""
     lat, lon = synth.generate("hotspots", 4000, seed=3)
     hour = np.full(4000, BASE, np.uint32)
     hour[2000:] += 1
     s = StreamingHeatmap(0, 16, base_hour=BASE)
     s.add(lat, lon, None, hour, user_id=["u%d" % (i % 5) for i in range(4000)])
     before = s.counts().sorted()
+    lat2 = lat.copy()
+    lat2[3000] = np.nan
+    with pytest.raises(ValueError):
+        s.add(lat2, lon, None, hour, user_id=["u%d" % (i % 5) for i in range(4000)])
+    with pytest.raises(ValueError):   # one hour: the hm_count path
+        s.add(lat2, lon, None, np.full(4000, BASE + 5, np.uint32))
     lon2 = lon.copy()
-    lon2[3000] = 200.0
-    with pytest.raises(_lib.DevicePathUnsupported):
-        s.add(lat, lon2, None, hour, user_id=["u%d" % (i % 5) for i in range(4000)])
-    with pytest.raises(_lib.DevicePathUnsupported):   # one hour: the hm_count path
-        s.add(lat, lon2, None, np.full(4000, BASE + 5, np.uint32))
+    lon2[100] = 200.0                 # outside the square, with the NaN: the split path must not insert
+    with pytest.raises(ValueError):
+        s.add(lat2, lon2, None, hour)
     after = s.counts().sorted()
     for k in ("zoom", "row", "col", "count"):
         assert np.array_equal(getattr(before, k), getattr(after, k))
@@ -226,4 +231,42 @@ def test_stream_paths_per_bucket_count(gpu, nusers, nhours):
     with pytest.raises(ValueError):
         s.add(bad, lon, keep, hour, group=gid)
     _same(s.counts(), oracle.count(lat2, lon2, keep2, 0, 17))
+    s.close()
+
+
+def test_stream_exotic_points(gpu):
+    """Kept points outside [0, 2^zmax)^2 (|lat| in (85.06, 89.9), lon at or
+    beyond +-180) are binned like the reference's (tile.py:17,21 never clamp):
+    counts, hours and rows over several batches equal the oracle's over the
+    concatenated points, with users and undated batches mixed in."""
+    mz, d = 9, 5
+    rng = np.random.default_rng(9)
+    bs = []
+    for b in range(4):
+        n = 3000
+        lat, lon = synth.generate("hotspots", n, seed=31, start=b * n)
+        lat, lon = lat.copy(), lon.copy()
+        m = rng.random(n) < 0.03
+        k = int(m.sum())
+        lat[m] = rng.choice([-1.0, 1.0], k) * rng.uniform(85.06, 89.9, k)
+        lon[m] = rng.choice([180.0, 200.0, -200.0, 540.0, -180.0, 179.99999999999997], k)
+        keep = (rng.random(n) > 0.1).astype(np.uint8)
+        hour = (BASE + rng.integers(0, 3, n)).astype(np.uint32)
+        users = [USERS[i] for i in rng.integers(0, len(USERS), n)]
+        bs.append((lat, lon, keep, hour, users))
+    s = StreamingHeatmap(0, mz + d, base_hour=BASE - 10)
+    for b, (lat, lon, keep, hour, users) in enumerate(bs):
+        s.add(lat, lon, keep, hour if b != 2 else None, user_id=users)
+    lat = np.concatenate([b[0] for b in bs])
+    lon = np.concatenate([b[1] for b in bs])
+    keep = np.concatenate([b[2] for b in bs])
+    users = sum((b[4] for b in bs), [])
+    c = s.counts(ALLTIME)
+    assert (c.row < 0).any() and (c.col >= (1 << c.zoom)).any()
+    _same(c, oracle.count(lat, lon, keep, 0, mz + d))
+    for h in range(BASE, BASE + 3):
+        sel = np.concatenate([(b[3] == h) & (b[2] == 1) if i != 2 else np.zeros(len(b[0]), bool)
+                              for i, b in enumerate(bs)])
+        _same(s.counts(h), oracle.count(lat, lon, sel.astype(np.uint8), 0, mz + d))
+    assert s.rows("alltime") == _reference_rows(lat, lon, keep, users, mz, d)
     s.close()
