@@ -66,7 +66,10 @@ extern "C" {
 #define HM_E_EXOTIC 9    /* hm_stream_add only: a kept point whose zoom-zmax tile
                             lies outside [0, 2^zmax)^2 (|lat| > 85.0511..., or
                             lon outside [-180, 180)); the resident table's keys
-                            hold in-square tiles.  hm_count* bin such points. */
+                            hold in-square tiles, nothing was inserted.  The
+                            host side (heatmap_amd/stream.py) then splits the
+                            batch and counts those points with hm_count_grouped;
+                            hm_count* bin such points directly. */
 #define HM_E_ARG 16      /* bad argument (zoom range, null pointer, n < 0) */
 #define HM_E_CAPACITY 17 /* output arrays too small; *n_out holds the size needed */
 #define HM_E_HIP 18      /* HIP runtime error (no device, launch failure) */
