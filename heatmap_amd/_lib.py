@@ -31,7 +31,8 @@ EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_st
            "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
-           "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_dense_cells"]
+           "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_cells_merge_runs",
+           "hm_dense_cells"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -102,6 +103,8 @@ def load() -> ctypes.CDLL:
         L.hm_dense_grid_size.restype = c.c_int64
         L.hm_cells_route.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, vp, vp, vp, P(c.c_int64)]
         L.hm_cells_merge.argtypes = [vp, vp, vp, c.c_int64, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_cells_merge_runs.argtypes = [vp, vp, vp, c.c_int64, P(c.c_int64), c.c_int, vp, vp, c.c_int64,
+                                          P(c.c_int64)]
         L.hm_dense_cells.argtypes = [vp, vp, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
         for name in EXPORTS:
             getattr(L, name).restype = getattr(L, name).restype or c.c_int

@@ -1102,12 +1102,18 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     return HM_OK;
 }
 
-extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
-                              uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, const int64_t* runs,
+                       int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
 {
     if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && (!keys || !counts)) ||
-        (capacity > 0 && (!keys_out || !counts_out)))
+        (capacity > 0 && (!keys_out || !counts_out)) || nruns < 0 || (nruns > 0 && !runs))
         return HM_E_ARG;
+    int64_t sum = 0;
+    for (int i = 0; i < nruns; i++) {
+        if (runs[i] < 0) return HM_E_ARG;
+        sum += runs[i];
+    }
+    if (runs && sum != n) return HM_E_ARG;
     *n_out = 0;
     if (n == 0) return HM_OK;
     HIPCHK(hipSetDevice(ctx->device));
@@ -1120,7 +1126,16 @@ extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     t.mask = cap - 1;
     HIPCHK(hipMemsetAsync(t.state, 0, 8 * sizeof(unsigned long long), s));
     hm_launch_stream_init(s, t);
-    hm_launch_cells_merge(s, keys, counts, (uint64_t)n, t);
+    if (runs) {
+        /* runs of distinct keys: no two threads of a launch insert one key */
+        int64_t off = 0;
+        for (int i = 0; i < nruns; i++) {
+            hm_launch_cells_merge_unique(s, keys + off, counts + off, (uint64_t)runs[i], t);
+            off += runs[i];
+        }
+    } else {
+        hm_launch_cells_merge(s, keys, counts, (uint64_t)n, t);
+    }
     hm_launch_table_extract(s, t, keys_out, counts_out, (uint64_t)capacity, t.state + HMS_ST_CURSOR);
     HIPCHK(hipGetLastError());
     unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
@@ -1129,6 +1144,19 @@ extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;   /* cannot happen: load factor <= 1/2 */
     *n_out = (int64_t)down[HMS_ST_CURSOR];
     return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+}
+
+extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
+                              uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+{
+    return cells_merge(ctx, keys, counts, n, nullptr, 0, keys_out, counts_out, capacity, n_out);
+}
+
+extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
+                                   const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out,
+                                   int64_t capacity, int64_t* n_out)
+{
+    return cells_merge(ctx, keys, counts, n, runs, nruns, keys_out, counts_out, capacity, n_out);
 }
 
 extern "C" int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out,

@@ -114,31 +114,84 @@ __global__ __launch_bounds__(256) void k_cells_merge(const uint64_t* __restrict_
     if ((threadIdx.x & 63) == 0 && of) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)of);
 }
 
-/* occupied slots -> (key, count), one output reservation per wave and 64 slots */
-__global__ __launch_bounds__(256) void k_table_extract(HmsTable t, uint64_t* __restrict__ keys_out,
-                                                       uint64_t* __restrict__ counts_out, uint64_t cap,
-                                                       unsigned long long* cursor)
+/* one run of distinct keys (one rank's cells): only the key claim is atomic,
+ * the count a plain store or read-modify-write (hms_insert_unique) */
+__global__ __launch_bounds__(256) void k_cells_merge_unique(const uint64_t* __restrict__ keys,
+                                                            const uint64_t* __restrict__ counts, uint64_t n,
+                                                            HmsTable t)
 {
-    const uint64_t n = t.mask + 1;
-    const uint32_t lane = threadIdx.x & 63;
+    uint32_t overflow = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+        hms_insert_unique(t, keys[i], counts[i], &overflow);
+    const uint64_t of = hms_wave_sum(overflow);
+    if ((threadIdx.x & 63) == 0 && of) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)of);
+}
+
+/* occupied slots -> (key, count).  Block b owns the contiguous slot range
+ * [b C, b C + C): a first sweep counts its occupied slots and ONE atomic per
+ * block reserves their output range; a second sweep writes them in slot order
+ * (per 1024-slot step: wave ballots + a block scan).  One reservation per
+ * 64-slot wave put a million same-address atomics on the cursor for a 64M-slot
+ * table (~88 per us: 12.6 ms); now it is a few thousand. */
+#define HM_TX_THREADS 256
+#define HM_TX_SPT 4
+__global__ __launch_bounds__(HM_TX_THREADS) void k_table_extract(HmsTable t, uint64_t* __restrict__ keys_out,
+                                                               uint64_t* __restrict__ counts_out, uint64_t cap,
+                                                               unsigned long long* cursor, uint64_t chunk)
+{
+    __shared__ uint32_t wsum[HM_TX_THREADS / 64 + 1];
+    __shared__ unsigned long long sbase;
+    const uint64_t n = t.mask + 1;
+    const uint64_t b0 = (uint64_t)blockIdx.x * chunk, b1 = min(b0 + chunk, n);
+    if (b0 >= n) return;
     const ulonglong2* slots = (const ulonglong2*)t.slots;
-    for (uint64_t i0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) & ~63ull; i0 < n; i0 += stride) {
-        const uint64_t i = i0 + lane;
-        const ulonglong2 sl = i < n ? slots[i] : make_ulonglong2(HMS_EMPTY, 0ull);
-        const bool m = sl.x != HMS_EMPTY;
-        const uint64_t bal = __ballot(m);
-        if (!bal) continue;
-        unsigned long long first = 0;
-        if (lane == 0) first = atomicAdd(cursor, (unsigned long long)__popcll(bal));
-        first = __shfl(first, 0, 64);
-        if (m) {
-            const uint64_t pos = first + hm_mbcnt(bal);
-            if (pos < cap) {
-                keys_out[pos] = sl.x;
-                counts_out[pos] = sl.y;
-            }
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    constexpr uint32_t STEP = HM_TX_THREADS * HM_TX_SPT;
+    uint32_t c = 0;
+    for (uint64_t i = b0 + tid; i < b1; i += HM_TX_THREADS) c += slots[i].x != HMS_EMPTY;
+    c = hm_wave_sum(c);
+    if (lane == 0) wsum[w] = c;
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t tot = 0;
+        for (int k = 0; k < HM_TX_THREADS / 64; k++) tot += wsum[k];
+        sbase = tot ? atomicAdd(cursor, (unsigned long long)tot) : 0ull;
+    }
+    __syncthreads();
+    uint64_t base = sbase;
+    for (uint64_t s0 = b0; s0 < b1; s0 += STEP) {
+        ulonglong2 sl[HM_TX_SPT];
+        uint64_t bal[HM_TX_SPT];
+        uint32_t mine = 0;
+#pragma unroll
+        for (int k = 0; k < HM_TX_SPT; k++) {
+            const uint64_t i = s0 + (uint64_t)(w * HM_TX_SPT + k) * 64 + lane;   /* a wave's 4 x 64 slots */
+            sl[k] = i < b1 ? slots[i] : make_ulonglong2(HMS_EMPTY, 0ull);
+            bal[k] = __ballot(sl[k].x != HMS_EMPTY);
+            mine += (uint32_t)__popcll(bal[k]);
         }
+        __syncthreads();
+        if (lane == 0) wsum[w] = mine;
+        __syncthreads();
+        uint32_t before = 0, tot = 0;
+        for (int k = 0; k < HM_TX_THREADS / 64; k++) {
+            before += k < w ? wsum[k] : 0u;
+            tot += wsum[k];
+        }
+        uint64_t pos = base + before;
+#pragma unroll
+        for (int k = 0; k < HM_TX_SPT; k++) {
+            if (sl[k].x != HMS_EMPTY) {
+                const uint64_t q = pos + hm_mbcnt(bal[k]);
+                if (q < cap) {
+                    keys_out[q] = sl[k].x;
+                    counts_out[q] = sl[k].y;
+                }
+            }
+            pos += (uint32_t)__popcll(bal[k]);
+        }
+        base += tot;
     }
 }
 
@@ -189,6 +242,12 @@ void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter)
         hipLaunchKernelGGL(k_cells_route<false>, dim3(g), dim3(HM_ROUTE_THREADS), 0, s, a);
 }
 
+void hm_launch_cells_merge_unique(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n,
+                                  const HmsTable& t)
+{
+    if (n) hipLaunchKernelGGL(k_cells_merge_unique, dim3(hm_mgrid(n, 8192)), dim3(256), 0, s, keys, counts, n, t);
+}
+
 void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t)
 {
     if (n) hipLaunchKernelGGL(k_cells_merge, dim3(hm_mgrid(n, 8192)), dim3(256), 0, s, keys, counts, n, t);
@@ -197,8 +256,11 @@ void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* 
 void hm_launch_table_extract(hipStream_t s, const HmsTable& t, uint64_t* keys_out, uint64_t* counts_out, uint64_t cap,
                              unsigned long long* cursor)
 {
-    hipLaunchKernelGGL(k_table_extract, dim3(hm_mgrid(t.mask + 1, 4096)), dim3(256), 0, s, t, keys_out, counts_out,
-                       cap, cursor);
+    const uint64_t n = t.mask + 1;
+    uint64_t chunk = 16384;
+    while ((n + chunk - 1) / chunk > 16384) chunk <<= 1;
+    hipLaunchKernelGGL(k_table_extract, dim3((unsigned)((n + chunk - 1) / chunk)), dim3(HM_TX_THREADS), 0, s, t,
+                       keys_out, counts_out, cap, cursor, chunk);
 }
 
 void hm_launch_dense_extract(hipStream_t s, const uint64_t* grid, uint64_t total, int dense_zmax, uint64_t* keys_out,

@@ -483,6 +483,8 @@ struct HmRouteArgs {
 unsigned hm_route_blocks(uint64_t n);
 void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter);
 void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t);
+void hm_launch_cells_merge_unique(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n,
+                                  const HmsTable& t);
 void hm_launch_table_extract(hipStream_t s, const HmsTable& t, uint64_t* keys_out, uint64_t* counts_out, uint64_t cap,
                              unsigned long long* cursor);
 void hm_launch_dense_extract(hipStream_t s, const uint64_t* grid, uint64_t total, int dense_zmax, uint64_t* keys_out,

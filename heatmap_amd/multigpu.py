@@ -66,7 +66,9 @@ class DeviceOps:
         m = sum(sent)
         return grid[:gsz], ko[:m], co[:m], sent
 
-    def merge(self, keys, counts):
+    def merge(self, keys, counts, runs=None):
+        """Sum equal keys; runs (list of sizes): consecutive runs of distinct
+        keys (one sending rank's cells each), merged without count atomics."""
         from . import _lib
 
         n = keys.numel()
@@ -74,8 +76,13 @@ class DeviceOps:
         ko = torch.empty(cap, dtype=torch.int64, device=keys.device)
         co = torch.empty_like(ko)
         nout = ctypes.c_int64(0)
-        rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), n, self._p(ko), self._p(co), cap,
-                                   ctypes.byref(nout))
+        if runs is not None:
+            ra = (ctypes.c_int64 * max(len(runs), 1))(*runs)
+            rc = self.L.hm_cells_merge_runs(self.ctx.ptr, self._p(keys), self._p(counts), n, ra, len(runs),
+                                            self._p(ko), self._p(co), cap, ctypes.byref(nout))
+        else:
+            rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), n, self._p(ko), self._p(co),
+                                       cap, ctypes.byref(nout))
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
         return ko[:nout.value], co[:nout.value]
@@ -152,7 +159,7 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
     dist.all_to_all_single(nk, sk, rl, sent)
     dist.all_to_all_single(nc, sc, rl, sent)
     parts_k, parts_c = [], []
-    uk, uc = ops.merge(nk, nc)
+    uk, uc = ops.merge(nk, nc, rl)     # rank r's cells are distinct keys: one run per sender
     parts_k.append(uk)
     parts_c.append(uc)
     if dense_zmax >= 0 and rank == 0:

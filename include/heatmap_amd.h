@@ -211,13 +211,18 @@ int hm_stream_destroy(hm_stream* s);
  *                    col >> delta), so each output row has one owner);
  *                    send_counts (host int64[nranks]) receives the group sizes
  *                    for an RCCL all-to-all.  nranks <= 64.
- *   hm_cells_merge   sum the counts of equal keys over n received cells.
+ *   hm_cells_merge   sum the counts of equal keys over n received cells;
+ *   hm_cells_merge_runs  the same when the n cells are nruns consecutive runs
+ *                    (host int64 sizes) each of distinct keys -- one rank's
+ *                    cells each -- so only the key claim is atomic.
  *   hm_dense_cells   the non-empty cells of a (reduced) dense grid. */
 int64_t hm_dense_grid_size(int dense_zmax);
 int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks, int delta,
                    int dense_zmax, uint64_t* grid, uint64_t* keys_out, uint64_t* counts_out, int64_t* send_counts);
 int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, uint64_t* keys_out,
                    uint64_t* counts_out, int64_t capacity, int64_t* n_out);
+int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, const int64_t* runs,
+                        int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out);
 int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out, uint64_t* counts_out,
                    int64_t capacity, int64_t* n_out);
 

@@ -59,6 +59,22 @@ def test_merge_kernel_sums_duplicates(gpu):
     assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
 
 
+def test_merge_runs_of_distinct_keys(gpu):
+    """hm_cells_merge_runs: three runs (one per sending rank), each of distinct
+    keys, overlapping across runs; an empty run in between."""
+    keys, counts = _cells(200_000, 4)
+    runs = [keys, keys[::3], keys[1::7]]
+    vals = [counts, counts[::3] * 2, counts[1::7] + 5]
+    perm = [torch.randperm(r.numel(), generator=torch.Generator().manual_seed(i)) for i, r in enumerate(runs)]
+    k = torch.cat([r[q] for r, q in zip(runs, perm)] + [keys[:0]])
+    c = torch.cat([v[q] for v, q in zip(vals, perm)] + [counts[:0]])
+    sizes = [r.numel() for r in runs[:2]] + [0] + [runs[2].numel()]
+    uk, uc = multigpu.DeviceOps(0).merge(k.cuda(), c.cuda(), sizes)
+    ek, ec = TorchOps.merge(k, c)
+    o = torch.argsort(uk.cpu())
+    assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
+
+
 @pytest.fixture(scope="module")
 def nccl_world():
     store = dist.HashStore()

@@ -69,7 +69,7 @@ class TorchOps:
         return grid, sk[o], sc[o], torch.bincount(own, minlength=ws).tolist()
 
     @staticmethod
-    def merge(keys, counts):
+    def merge(keys, counts, runs=None):
         u, inv = torch.unique(keys, return_inverse=True)
         t = torch.zeros(u.numel(), dtype=torch.int64)
         t.index_add_(0, inv, counts)
