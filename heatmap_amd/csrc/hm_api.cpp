@@ -99,7 +99,7 @@ enum {
     B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
-    B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE,
+    B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG,
     B_COUNT
 };
 
@@ -482,6 +482,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     uint64_t nx = 0;            /* kept points outside [0, 2^Z)^2 */
     int npart = 0;              /* level >= 2 partition launches timed (ev[5..]) */
 
+    uint32_t* seg1 = nullptr;   /* level-1 items' run tables (k_partition_fr) */
     for (int l = 0; l < L; l++) {
         Level& V = lv[l];
         V.zc = zs[l];
@@ -700,7 +701,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 uint4* desc;
                 ENSURE(B_DESC0 + 0, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
                 b.desc = desc;
-                hm_launch_items(s, b, runs_cur, V.items, (L == 1) ? HM_TA : HM_TN, desc);
+                if (L > 1) ENSURE(B_SEG, ((uint64_t)V.items + 1) * 16 * sizeof(uint32_t), seg1);
+                hm_launch_items(s, b, runs_cur, V.items, (L == 1) ? HM_TA : HM_TN, desc, L > 1 ? seg1 : nullptr);
                 HIPCHK(hipGetLastError());
             }
             keys_cur = kout;
@@ -744,8 +746,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.nruns_out = nruns;
             a.runs_out = runs_sh;
             a.items = lv[l - 1].items;
+            a.seg = l == 1 ? seg1 : nullptr;
             HIPCHK(hipEventRecord(ev[5 + 2 * (l - 1)], s));
-            hm_launch_partN(s, a, lv[l - 1].items, V.out16, l == 1);
+            hm_launch_partN(s, a, lv[l - 1].items, V.out16, l == 1 && seg1 != nullptr);
             HIPCHK(hipGetLastError());
             HIPCHK(hipEventRecord(ev[6 + 2 * (l - 1)], s));
             npart = l;
@@ -860,7 +863,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             uint4* desc;
             ENSURE(B_DESC0 + l, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
             b.desc = desc;
-            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? HM_TA : HM_TN, desc);
+            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? HM_TA : HM_TN, desc, nullptr);
             HIPCHK(hipGetLastError());
         }
 

@@ -105,19 +105,12 @@ __device__ __forceinline__ void hm_exotic_append(const HmExotic& x, bool p, int6
     }
 }
 
-/* region slot of digit d for this block: hot digits are split into
- * HM_L1_SHARDS sub-regions (block id & smask[d]) so their fill counters see
- * 1/8 of the tiles' atomics each */
-__device__ __forceinline__ uint32_t hm_l1_slot(const HmPart1Args& a, int d)
-{
-    return (uint32_t)d * HM_L1_SHARDS + (blockIdx.x & (uint32_t)a.smask[d]);
-}
 
 /* ------------------------------------------------------------------------ */
 /* level 1: projection fused with the first partition                        */
 /* ------------------------------------------------------------------------ */
 
-template <typename OutT, int MODE>
+template <typename OutT, int MODE, bool FULL>
 __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partition(HmPart1Args a)
 {
     __shared__ uint32_t cur[HM_MAX_F1 + 64];   /* + 64 dummy words (hm_lds_count) */
@@ -130,7 +123,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
-    const int64_t base = (int64_t)blockIdx.x * HM_T1;   /* first input point */
+    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;   /* first input point */
     /* the resolved-redo launch is sized for the list's capacity; its length
      * is read here (no host round trip) */
     const int64_t n = (FROM_TILES && a.n_dev) ? min((int64_t)*a.n_dev, a.n) : a.n;
@@ -142,22 +135,15 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     uint32_t dig[HM_P1_PPT];
     uint32_t rest[HM_P1_PPT];
     int nslow = 0;
-    /* issue every load of the tile before any arithmetic: 16 points x 16 B per
-     * lane in flight (double2 = two consecutive points of one array) */
+    /* the polynomial table's loads go out FIRST: the barrier before the
+     * projection waits for them (vmcnt retires in issue order), and must not
+     * wait for the tile's 128 KB of points -- the projection then starts as
+     * soon as the first points land */
+    constexpr bool FULLT = FULL && !FROM_TILES;   /* a whole tile of lat/lon input */
     double2 la[HM_P1_PPT / 2], lo[HM_P1_PPT / 2];
-    uint16_t kp[HM_P1_PPT / 2];
-    /* Full tiles (block-uniform branch) load unconditionally.  The per-lane
-     * tail code below writes the same registers in its other branches, which
-     * makes the compiler wait for each load pair before the next one: one
-     * 32-B pair per lane in flight instead of all of them. */
-    if (!FROM_TILES && base + HM_T1 <= n) {
-        const double2* lat2 = (const double2*)(a.lat + base);
-        const double2* lon2 = (const double2*)(a.lon + base);
-#pragma unroll
-        for (int k = 0; k < HM_P1_PPT / 2; k++) {
-            la[k] = lat2[k * HM_P1_THREADS + tid];
-            lo[k] = lon2[k * HM_P1_THREADS + tid];
-        }
+    uint32_t kp[HM_P1_PPT / 2];   /* keep bytes of 2 points (u32: no packing, no early wait) */
+    if (FULLT) {
+        /* keep bytes first of all: consumed before the points */
         if (a.keep) {
             const uint16_t* kp2 = (const uint16_t*)(a.keep + base);
 #pragma unroll
@@ -165,6 +151,49 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         } else {
 #pragma unroll
             for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = 0x0101;
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int TPT = (HM_YTAB_N + HM_P1_THREADS - 1) / HM_P1_THREADS;
+    double tv[TPT];
+    if (!FROM_TILES) {
+#pragma unroll
+        for (int q = 0; q < TPT; q++) {
+            const int i = q * HM_P1_THREADS + tid;
+            tv[q] = i < HM_YTAB_N ? c_ytab[i] : 0.0;
+        }
+    }
+    /* this thread's digits' region slots, capacities and bases (small, L2-hot
+     * tables), also before the points, and without a dependent load: a hot
+     * digit's slot is d*8 + (block & 7), a cold one's d*8 (smask 7 or 0), so
+     * both candidates are fetched and the mask picks one later.  (Waiting for
+     * the mask before the dependent loads would wait for every point load
+     * issued before it.) */
+    constexpr int PERD = HM_MAX_F1 / HM_P1_THREADS;
+    uint32_t smk[PERD], rcap2[PERD][2], rbase2[PERD][2];
+#pragma unroll
+    for (int q = 0; q < PERD; q++) {
+        const int d = tid * PERD + q;
+        const uint32_t s0 = (uint32_t)d * HM_L1_SHARDS, s1 = s0 + (blockIdx.x & (HM_L1_SHARDS - 1));
+        smk[q] = d < F ? a.smask[d] : 0u;
+        rcap2[q][0] = d < F ? a.rcap[s0] : 0u;
+        rcap2[q][1] = d < F ? a.rcap[s1] : 0u;
+        rbase2[q][0] = d < F ? a.rbase[s0] : 0u;
+        rbase2[q][1] = d < F ? a.rbase[s1] : 0u;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    /* issue every load of the tile before any arithmetic: 16 points x 16 B per
+     * lane in flight (double2 = two consecutive points of one array).  Full
+     * tiles are a launch of their own (FULL): straight-line loads, so the
+     * table's wait below counts exactly the loads issued after it; the tail
+     * tile's per-lane code would make the compiler drain everything there. */
+    if (FULLT) {
+        const double2* lat2 = (const double2*)(a.lat + base);
+        const double2* lon2 = (const double2*)(a.lon + base);
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT / 2; k++) {
+            la[k] = lat2[k * HM_P1_THREADS + tid];
+            lo[k] = lon2[k * HM_P1_THREADS + tid];
         }
     } else
 #pragma unroll
@@ -198,22 +227,26 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
             lo[k] = make_double2(0.0, 0.0);
         }
     }
-    /* this thread's digits' region slots, capacities and bases (small, L2-hot
-     * tables), fetched while the point loads are in flight */
-    constexpr int PERD = HM_MAX_F1 / HM_P1_THREADS;
+    /* LDS set-up after the loads are issued */
+    for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
+    if (!FROM_TILES) {
+#pragma unroll
+        for (int q = 0; q < TPT; q++) {
+            const int i = q * HM_P1_THREADS + tid;
+            if (i < HM_YTAB_N) tab[i] = tv[q];
+        }
+    }
+    __syncthreads();
+    if (MODE == 0) HM_STAMP_M(2, 1);
     uint32_t slot[PERD], rcap[PERD], rbase[PERD];
 #pragma unroll
     for (int q = 0; q < PERD; q++) {
         const int d = tid * PERD + q;
-        slot[q] = d < F ? hm_l1_slot(a, d) : 0u;
-        rcap[q] = d < F ? a.rcap[slot[q]] : 0u;
-        rbase[q] = d < F ? a.rbase[slot[q]] : 0u;
+        const int hot = smk[q] != 0;
+        slot[q] = (uint32_t)d * HM_L1_SHARDS + (hot ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u);
+        rcap[q] = hot ? rcap2[q][1] : rcap2[q][0];
+        rbase[q] = hot ? rbase2[q][1] : rbase2[q][0];
     }
-    /* LDS set-up after the loads are issued: the table's latency overlaps theirs */
-    for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
-    if (!FROM_TILES) hm_load_ytab(tab);
-    __syncthreads();
-    if (MODE == 0) HM_STAMP_M(2, 1);
     /* fast path for every point, branch-free; points the fast path cannot
      * settle (guard band, polar/out-of-range/non-finite input) are marked in
      * `redo` and resolved afterwards in one ballot-guarded pass */
@@ -609,7 +642,8 @@ __device__ __forceinline__ HmItem hm_item(const HmBuckets& B, uint32_t g)
 /* Descriptor of work item g (T keys per item): its bucket (binary search over
  * item_begin), its logical positions [a, b) and the runs [r0, r1) that
  * overlap them.  One thread per item; the searches of all items overlap. */
-__global__ __launch_bounds__(256) void k_items(HmBuckets B, HmRuns in, uint32_t items, uint32_t T, uint4* desc)
+__global__ __launch_bounds__(256) void k_items(HmBuckets B, HmRuns in, uint32_t items, uint32_t T, uint4* desc,
+                                               uint32_t* seg)
 {
     const uint32_t g = blockIdx.x * 256 + threadIdx.x;
     if (g >= items) return;
@@ -624,11 +658,27 @@ __global__ __launch_bounds__(256) void k_items(HmBuckets B, HmRuns in, uint32_t 
     const uint32_t r1 = rb + hm_lower_bound(in.excl + rb, nr, b);       /* first run starting >= b */
     desc[2 * g] = make_uint4(bk, j, nitems, r0);
     desc[2 * g + 1] = make_uint4(r1, 0u, (uint32_t)a, (uint32_t)b);
+    if (seg) {
+        /* the item's <= HM_L1_SHARDS runs as (logical start, source index)
+         * pairs, unused entries repeating the last run (k_partition_fr) */
+        uint4* sg = (uint4*)(seg + 16 * (size_t)g);
+        uint32_t v[2 * HM_L1_SHARDS];
+        const uint32_t last = r1 > r0 ? r1 - 1 : r0;
+#pragma unroll
+        for (int q = 0; q < HM_L1_SHARDS; q++) {
+            const uint32_t r = min(r0 + q, last);
+            v[2 * q] = (uint32_t)in.excl[r];
+            v[2 * q + 1] = in.run[r].x;
+        }
+#pragma unroll
+        for (int q = 0; q < HM_L1_SHARDS / 2; q++) sg[q] = make_uint4(v[4 * q], v[4 * q + 1], v[4 * q + 2], v[4 * q + 3]);
+    }
 }
 
-void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc)
+void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc,
+                     uint32_t* seg)
 {
-    if (items) hipLaunchKernelGGL(k_items, dim3((items + 255) / 256), dim3(256), 0, s, B, in, items, T, desc);
+    if (items) hipLaunchKernelGGL(k_items, dim3((items + 255) / 256), dim3(256), 0, s, B, in, items, T, desc, seg);
 }
 
 /* Run chunk staged in LDS, dense per run i of the chunk: its 16-B-aligned
@@ -980,16 +1030,13 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     HM_STAMP_M(3, 0);
     const HmItem it = hm_item(a.parent, g);
     /* the item's runs (<= HM_L1_SHARDS, block-uniform): logical start and
-     * source index of each */
+     * source index of each, from k_items' per-item table -- one 64-B load
+     * next to the descriptor's, not a chain of dependent loads */
+    const uint4* sg = (const uint4*)(a.seg + 16 * (size_t)g);
+    const uint4 s0 = sg[0], s1 = sg[1], s2 = sg[2], s3 = sg[3];
+    const uint32_t rpos[HM_L1_SHARDS] = {s0.x, s0.z, s1.x, s1.z, s2.x, s2.z, s3.x, s3.z};
+    const uint32_t rsrc[HM_L1_SHARDS] = {s0.y, s0.w, s1.y, s1.w, s2.y, s2.w, s3.y, s3.w};
     const uint32_t nr = min(it.r1 - it.r0, (uint32_t)HM_L1_SHARDS);
-    const uint32_t nr1 = nr ? nr - 1 : 0u;
-    uint32_t rpos[HM_L1_SHARDS], rsrc[HM_L1_SHARDS];
-#pragma unroll
-    for (int j = 0; j < HM_L1_SHARDS; j++) {
-        const uint32_t r = it.r0 + min((uint32_t)j, nr1);
-        rpos[j] = (uint32_t)a.in.excl[r];
-        rsrc[j] = a.in.run[r].x;
-    }
     const uint32_t total = it.b - it.a;
     uint32_t kv[KPT];
 #pragma unroll
@@ -2077,20 +2124,32 @@ void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int6
                        err_word, slow);
 }
 
-void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool out16, int mode)
+void hm_launch_part1(hipStream_t s, const HmPart1Args& a0, uint32_t grid, bool out16, int mode)
 {
     if (grid == 0) return;
-    dim3 g(grid), b(HM_P1_THREADS);
-#define HM_P1_CASE(T, M) hipLaunchKernelGGL((k_project_partition<T, M>), g, b, 0, s, a)
-    if (out16) {
-        if (mode == 0) HM_P1_CASE(uint16_t, 0);
-        else if (mode == 1) HM_P1_CASE(uint16_t, 1);
-        else HM_P1_CASE(uint16_t, 2);
-    } else {
-        if (mode == 0) HM_P1_CASE(uint32_t, 0);
-        else if (mode == 1) HM_P1_CASE(uint32_t, 1);
-        else HM_P1_CASE(uint32_t, 2);
+    dim3 b(HM_P1_THREADS);
+    /* lat/lon input: the whole tiles in one launch (FULL), the partial last
+     * tile in another; tile input (mode 1) reads its length on the device */
+    const uint32_t full = mode == 1 ? 0u : (uint32_t)std::min<int64_t>(grid, a0.n / HM_T1);
+    HmPart1Args a = a0;
+    a.tile0 = 0;
+#define HM_P1_CASE(T, M, FL, G) hipLaunchKernelGGL((k_project_partition<T, M, FL>), dim3(G), b, 0, s, a)
+#define HM_P1_MODES(T, FL, G)                      \
+    do {                                           \
+        if (mode == 0) HM_P1_CASE(T, 0, FL, G);    \
+        else if (mode == 1) HM_P1_CASE(T, 1, FL, G); \
+        else HM_P1_CASE(T, 2, FL, G);              \
+    } while (0)
+    if (full) {
+        if (out16) HM_P1_MODES(uint16_t, true, full);
+        else HM_P1_MODES(uint32_t, true, full);
     }
+    if (grid > full) {
+        a.tile0 = full;
+        if (out16) HM_P1_MODES(uint16_t, false, grid - full);
+        else HM_P1_MODES(uint32_t, false, grid - full);
+    }
+#undef HM_P1_MODES
 #undef HM_P1_CASE
 }
 

@@ -172,6 +172,7 @@ struct HmPart1Args {
     const int64_t* cols_in;
     const uint8_t* keep;
     int64_t n;
+    int64_t tile0;            /* first tile of the launch (hm_launch_part1 sets it) */
     const unsigned long long* n_dev;   /* tile input: min(*n_dev, n) points (the resolved redo list) */
     int Z, dbits, restbits;
     uint32_t* redo_idx;       /* fast mode: points the fast path could not settle */
@@ -211,6 +212,7 @@ struct HmPartNArgs {
     HmRuns in;
     int dbits, restbits, shard_bits;
     uint32_t items;             /* blocks of the (2-D) grid that have an item */
+    const uint32_t* seg;        /* level-1 parents: per item its runs (k_items), for k_partition_fr */
     void* keys_out;             /* item g writes its keys at its positions [a, b) */
     uint32_t* nruns_out;
     uint2* runs_out;
@@ -329,7 +331,9 @@ void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a);
 /* exclusive scan of v[0..n) into out (any n), total into *total; partial: 4096 u64 */
 void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total);
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
-void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc);
+/* seg (or null): per item 16 u32, its <= HM_L1_SHARDS runs (k_partition_fr) */
+void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc,
+                     uint32_t* seg);
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots);
 /* small buckets: sort pass, scan, one reservation, emit pass (partial: 4096 u64) */
 void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial);

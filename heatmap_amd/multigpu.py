@@ -66,15 +66,21 @@ class DeviceOps:
         m = sum(sent)
         return grid[:gsz], ko[:m], co[:m], sent
 
-    def merge(self, keys, counts, runs=None):
+    def merge(self, keys, counts, runs=None, out=None):
         """Sum equal keys; runs (list of sizes): consecutive runs of distinct
-        keys (one sending rank's cells each), merged without count atomics."""
+        keys (one sending rank's cells each), merged without count atomics.
+        out: (keys, counts) tensors to write into (their length is the
+        capacity; MemoryError if the merged cells do not fit)."""
         from . import _lib
 
         n = keys.numel()
-        cap = max(n, 1)
-        ko = torch.empty(cap, dtype=torch.int64, device=keys.device)
-        co = torch.empty_like(ko)
+        if out is not None:
+            ko, co = out
+            cap = ko.numel()
+        else:
+            cap = max(n, 1)
+            ko = torch.empty(cap, dtype=torch.int64, device=keys.device)
+            co = torch.empty_like(ko)
         nout = ctypes.c_int64(0)
         if runs is not None:
             ra = (ctypes.c_int64 * max(len(runs), 1))(*runs)
@@ -83,19 +89,27 @@ class DeviceOps:
         else:
             rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), n, self._p(ko), self._p(co),
                                        cap, ctypes.byref(nout))
+        if rc == _lib.HM_E_CAPACITY and out is not None:
+            raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (nout.value, cap))
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
         return ko[:nout.value], co[:nout.value]
 
-    def dense_cells(self, grid, dense_zmax):
+    def dense_cells(self, grid, dense_zmax, out=None):
         from . import _lib
 
-        cap = max(int((grid != 0).sum().item()), 1)
-        ko = torch.empty(cap, dtype=torch.int64, device=grid.device)
-        co = torch.empty_like(ko)
+        if out is not None:
+            ko, co = out
+            cap = ko.numel()
+        else:
+            cap = max(int((grid != 0).sum().item()), 1)
+            ko = torch.empty(cap, dtype=torch.int64, device=grid.device)
+            co = torch.empty_like(ko)
         nout = ctypes.c_int64(0)
         rc = self.L.hm_dense_cells(self.ctx.ptr, self._p(grid), dense_zmax, self._p(ko), self._p(co), cap,
                                    ctypes.byref(nout))
+        if rc == _lib.HM_E_CAPACITY and out is not None:
+            raise MemoryError("merge_cells: %d dense cells exceed the buffer capacity %d" % (nout.value, cap))
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
         return ko[:nout.value], co[:nout.value]
@@ -136,6 +150,60 @@ def merge_exotic(cells: torch.Tensor, ws: int, rank: int) -> torch.Tensor:
     return torch.cat([u, tot[:, None]], 1)
 
 
+def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, dense_zmax: int = 10):
+    """Run `steps` count + merge steps with step k's merge overlapping step
+    k+1's count: count(buffers) -> (m, buffers) runs on the calling thread
+    (its hm context, the current stream); merge_cells runs on a helper thread
+    with its own HIP stream and hm context, which alone issues the RCCL
+    collectives (in step order, as on every rank).  bufsets: >= 2 CountBuffers
+    used in turn; a set is counted into again only after its merge finished.
+    Returns (cells owned after the last merge, per-step stage timings of the
+    counts, the last step's buffers)."""
+    import queue
+    import threading
+
+    todo, free = queue.Queue(), queue.Queue()
+    for b in bufsets:
+        free.put(b)
+    owned, err, last = [], [], [None]
+    side = torch.cuda.Stream()
+
+    def merger():
+        try:
+            with torch.cuda.stream(side):
+                while True:
+                    item = todo.get()
+                    if item is None:
+                        return
+                    m, b = item
+                    owned.append(merge_cells(b, m, ws, rank, dense_zmax))
+                    side.synchronize()
+                    last[0] = b
+                    free.put(b)
+        except BaseException as e:   # surfaced on the calling thread
+            err.append(e)
+            free.put(None)
+
+    th = threading.Thread(target=merger, name="hm-merge")
+    th.start()
+    stages = []
+    try:
+        for _ in range(steps):
+            b = free.get()
+            if b is None:
+                break
+            m, b = count(b)
+            if ctx is not None:
+                stages.append(ctx.last_stats()[1][:5])
+            todo.put((m, b))
+    finally:
+        todo.put(None)
+        th.join()
+    if err:
+        raise err[0]
+    return (owned[-1] if owned else 0), stages, last[0]
+
+
 def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=None) -> int:
     """Exchange and merge the first m cells of `buffers` (int64 keys/counts,
     HM_KEY layout; records of cells outside the square in buffers.xcells,
@@ -158,21 +226,29 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
     nc = torch.empty_like(nk)
     dist.all_to_all_single(nk, sk, rl, sent)
     dist.all_to_all_single(nc, sc, rl, sent)
-    parts_k, parts_c = [], []
-    uk, uc = ops.merge(nk, nc, rl)     # rank r's cells are distinct keys: one run per sender
-    parts_k.append(uk)
-    parts_c.append(uc)
-    if dense_zmax >= 0 and rank == 0:
-        dk, dc = ops.dense_cells(grid, dense_zmax)
-        parts_k.append(dk)
-        parts_c.append(dc)
-    k = torch.cat(parts_k)
-    c = torch.cat(parts_c)
-    n = k.numel()
-    if n > buffers.keys.numel():
-        raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (n, buffers.keys.numel()))
-    buffers.keys[:n] = k
-    buffers.counts[:n] = c
+    if isinstance(ops, DeviceOps):
+        # merged cells straight into the buffers (the sent copies are in nk)
+        uk, _ = ops.merge(nk, nc, rl, out=(buffers.keys, buffers.counts))
+        n = uk.numel()
+        if dense_zmax >= 0 and rank == 0:
+            dk, _ = ops.dense_cells(grid, dense_zmax, out=(buffers.keys[n:], buffers.counts[n:]))
+            n += dk.numel()
+    else:
+        parts_k, parts_c = [], []
+        uk, uc = ops.merge(nk, nc, rl)
+        parts_k.append(uk)
+        parts_c.append(uc)
+        if dense_zmax >= 0 and rank == 0:
+            dk, dc = ops.dense_cells(grid, dense_zmax)
+            parts_k.append(dk)
+            parts_c.append(dc)
+        k = torch.cat(parts_k)
+        c = torch.cat(parts_c)
+        n = k.numel()
+        if n > buffers.keys.numel():
+            raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (n, buffers.keys.numel()))
+        buffers.keys[:n] = k
+        buffers.counts[:n] = c
     nx = int(getattr(buffers, "nx", 0))
     nx_all = torch.tensor([nx], dtype=torch.int64, device=keys.device)
     dist.all_reduce(nx_all)

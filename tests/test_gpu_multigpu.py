@@ -102,3 +102,24 @@ def test_merge_cells_over_rccl(gpu, nccl_world, dz):
                         0, []).sorted()
     for f in ("zoom", "row", "col", "count"):
         assert np.array_equal(getattr(got, f), getattr(ref, f)), f
+
+
+def test_pipelined_steps_over_rccl(gpu, nccl_world):
+    """bench.py's N>1 schedule: step k's merge (helper thread, own stream)
+    overlaps step k+1's count; after 5 steps over 2 buffer sets the last
+    merged cells equal one count of the cloud."""
+    n = 3_000_000
+    lat, lon = synth.generate("hotspots", n, seed=17)
+    la, lo = torch.from_numpy(lat).cuda(), torch.from_numpy(lon).cuda()
+    ref = device.count(lat, lon, None, 0, 18).sorted()
+    ctx = device.context(0)
+    bufsets = [device.CountBuffers(1 << 24), device.CountBuffers(1 << 24)]
+    m, stages, bufs = multigpu.pipelined_steps(lambda b: device.count_device(la, lo, None, 0, 18, buffers=b),
+                                               bufsets, 5, 1, 0, ctx)
+    torch.cuda.synchronize()
+    assert len(stages) == 5 and bufs.nx == 0
+    k = bufs.keys[:m].cpu().numpy().view(np.uint64)
+    got = device.Counts((k >> np.uint64(58)).astype(np.int32), ((k >> np.uint64(29)) & np.uint64(0x1FFFFFFF)).astype(np.int64),
+                        (k & np.uint64(0x1FFFFFFF)).astype(np.int64), bufs.counts[:m].cpu().numpy(), 0, []).sorted()
+    for f in ("zoom", "row", "col", "count"):
+        assert np.array_equal(getattr(got, f), getattr(ref, f)), f
