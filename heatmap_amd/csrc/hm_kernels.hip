@@ -1717,22 +1717,6 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
             key[m] = i < nk ? (uint32_t)ks[i] : 0u;
             own[m] = 0;
         }
-#if HM_SP_FLAT
-        /* every level at once: each key adds 1 to its cell at every level (no
-         * level-to-level barrier); counts stay <= HM_SP_MAX */
-#pragma unroll
-        for (int m = 0; m < KPT; m++) {
-            const uint32_t i = tid + m * HM_SP_THREADS;
-            if (i < nk) {
-                for (int l = 0; l < lg; l++) {
-                    const uint32_t c = hm_sp_cell(key[m], lg, l, cofs[l]);
-                    const uint32_t old = atomicAdd(&g[c >> 1], 1u << (16 * (c & 1)));
-                    own[m] |= (hm_sp_half(old, c) == 0 ? 1u : 0u) << l;
-                }
-            }
-        }
-        __syncthreads();
-#else
         for (int l = 0; l < lg; l++) {
 #pragma unroll
             for (int m = 0; m < KPT; m++) {
@@ -1751,7 +1735,6 @@ __global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
             }
             __syncthreads();
         }
-#endif
         /* levels in [zmin, zmax]: one reservation, thread-contiguous slots */
         uint32_t zmask = 0;
         for (int l = 0; l < lg; l++) {

@@ -58,9 +58,6 @@
 #ifndef HM_SP_MAX
 #define HM_SP_MAX 2048
 #endif
-#ifndef HM_SP_FLAT
-#define HM_SP_FLAT 0                        /* 1: all pyramid levels counted in one pass */
-#endif
 #define HM_SP_WORDS ((HM_AG_CELLS / 3 * 4 + 1) / 2 + 1)   /* 4^7 + ... + 4 cells */
 #define HM_SP_GRID (256 * 3)
 /* small final buckets (k_small_sort / k_small_emit): one wavefront per bucket */

@@ -33,13 +33,13 @@ VARIANTS = {
     "su8": ["HM_SU=8"],
     "k2old": ["HM_K2_FR=0"],                # level 2 through k_partition (run streaming)
     "p1_1024x8": ["HM_P1_THREADS=1024", "HM_P1_PPT=8"],
+    "p1_1024x16": ["HM_P1_THREADS=1024"],
     "p1_1024x8w8": ["HM_P1_THREADS=1024", "HM_P1_PPT=8", "HM_P1_WAVES=8"],
     "mr2": ["HM_MERGE_ROUNDS=2"],
     "p1g8": ["HM_P1_GROUP=8"],
     "p1g16": ["HM_P1_GROUP=16"],
     "p1ilp2": ["HM_P1_ILP=2"],
     "frg8": ["HM_FR_GROUP=8"],
-    "spflat": ["HM_SP_FLAT=1"],
     "fr512_4k": ["HM_FR_THREADS=512", "HM_TN=4096"],
     "ta64k": ["HM_TA=65536"],
     "ta128k": ["HM_TA=131072"],
