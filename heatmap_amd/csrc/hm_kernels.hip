@@ -1245,7 +1245,8 @@ __global__ __launch_bounds__(256) void k_rs_keys(HmRsArgs a)
         const uint32_t nk = (uint32_t)(ke - kb);
         a.nkeys[c] = nk;
         a.keybase[c] = (uint32_t)kb;
-        /* last level: sparse buckets have no dense work items (k_aggregate_sparse) */
+        /* last level: buckets of <= HM_SP_MAX keys get no dense work items
+         * (one wavefront each: k_small_sort / k_small_emit) */
         const uint32_t nit = nk <= a.sparse_max ? 0u : (nk + a.item_keys - 1) / a.item_keys;
         a.vals[c] = (1ull << 32) | (uint64_t)nit;
     }
@@ -1628,161 +1629,6 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
 }
 
 /* ------------------------------------------------------------------------ */
-/* final level, sparse buckets (<= HM_SP_MAX keys): key-driven pyramid        */
-/* ------------------------------------------------------------------------ */
-
-/* Cell index of key k (row << lg | col) at pyramid level l (zoom Z - l) in
- * the concatenated level grids: level l starts at cell cofs[l] and is the
- * row-major (2^(lg-l))^2 block of the bucket. */
-__device__ __forceinline__ uint32_t hm_sp_cell(uint32_t k, int lg, int l, uint32_t cofs)
-{
-    const uint32_t r = (k >> lg) >> l, c = (k & ((1u << lg) - 1)) >> l;
-    return cofs + ((r << (lg - l)) | c);
-}
-__device__ __forceinline__ uint32_t hm_sp_half(uint32_t w, uint32_t cell) { return (w >> (16 * (cell & 1))) & 0xFFFFu; }
-
-/* A dense 128x128 grid per bucket costs the same LDS passes (init, pyramid,
- * a 21845-cell emission scan) whether the bucket holds 200 keys or 200
- * million; uniform or skewed clouds at zoom 18 make millions of ~200-key
- * buckets.  Here a bucket costs O(keys): the keys are staged, then level by
- * level every distinct cell of the previous level adds its count to its
- * parent cell; the lane whose atomic saw 0 owns the cell (emits it, later
- * clears it).  Counts fit u16 (<= HM_SP_MAX), so two cells share a word and
- * all levels fit one 43-KB array that stays zero between buckets.  One output
- * reservation per bucket.  Persistent: block b takes buckets b, b + grid, ... */
-__global__ __launch_bounds__(HM_SP_THREADS) void k_aggregate_sparse(HmAggArgs a)
-{
-    constexpr int KPT = HM_SP_MAX / HM_SP_THREADS;
-    __shared__ uint32_t g[HM_SP_WORDS];
-    __shared__ uint16_t ks[HM_SP_MAX];
-    __shared__ uint32_t scr[HM_SP_THREADS / 64 + 1];
-    __shared__ unsigned long long sbase;
-    __shared__ HmRunLds<128> L;
-    const int tid = threadIdx.x;
-    const int lg = a.lg;
-    uint32_t cofs[HM_AG_LG + 1];
-    cofs[0] = 0;
-    for (int l = 0; l < lg; l++) cofs[l + 1] = cofs[l] + (1u << (2 * (lg - l)));
-    for (uint32_t i = tid; i < HM_SP_WORDS; i += HM_SP_THREADS) g[i] = 0;
-    __syncthreads();
-    const uint32_t nblk = gridDim.x * gridDim.y;
-    const uint32_t lane = hm_lane();
-    /* buckets are screened 64 per step (one load per lane; every wave ballots
-     * the same mask, so the loop stays block-uniform) */
-    uint32_t b0 = hm_block_id() * 64, bs = 0, nkl = 0;
-    uint64_t msk = 0;
-    for (;;) {
-        while (msk == 0 && b0 < a.B.count) {
-            const uint32_t bl = b0 + lane;
-            nkl = bl < a.B.count ? a.B.nkeys[bl] : 0u;
-            msk = __ballot((nkl > HM_SPW_MAX) & (nkl <= HM_SP_MAX));
-            bs = b0;
-            b0 += nblk * 64;
-        }
-        if (msk == 0) break;
-        const uint32_t b = bs + (uint32_t)__builtin_ctzll(msk);
-        msk &= msk - 1;
-        const uint32_t nk = __shfl(nkl, (int)(b - bs), 64);
-        HmItem it;
-        it.bucket = b;
-        it.j = 0;
-        it.nitems = 1;
-        it.r0 = a.B.rbase[b];
-        it.r1 = it.r0 + a.B.nruns[b];
-        it.a = a.B.keybase[b];
-        it.b = it.a + nk;
-        struct {
-            uint16_t* ks;
-            __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t pos)
-            {
-                if (v) ks[pos] = (uint16_t)k;
-            }
-            __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t pos)
-            {
-                if (v) {
-                    const uint32_t w[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-                    for (int q = 0; q < 4; q++) {
-                        ks[pos + 2 * q] = (uint16_t)(w[q] & 0xFFFFu);
-                        ks[pos + 2 * q + 1] = (uint16_t)(w[q] >> 16);
-                    }
-                }
-            }
-        } f{ks};
-        hm_stream_runs<uint16_t, HM_SP_THREADS, 128, false>(it, a.keys, a.in, L, scr, f);
-        uint32_t key[KPT], own[KPT];
-#pragma unroll
-        for (int m = 0; m < KPT; m++) {
-            const uint32_t i = tid + m * HM_SP_THREADS;
-            key[m] = i < nk ? (uint32_t)ks[i] : 0u;
-            own[m] = 0;
-        }
-        for (int l = 0; l < lg; l++) {
-#pragma unroll
-            for (int m = 0; m < KPT; m++) {
-                const uint32_t i = tid + m * HM_SP_THREADS;
-                const bool v = (i < nk) & (l == 0 || ((own[m] >> (l - 1)) & 1u));
-                if (v) {
-                    uint32_t inc = 1;
-                    if (l > 0) {
-                        const uint32_t pc = hm_sp_cell(key[m], lg, l - 1, cofs[l - 1]);
-                        inc = hm_sp_half(g[pc >> 1], pc);
-                    }
-                    const uint32_t c = hm_sp_cell(key[m], lg, l, cofs[l]);
-                    const uint32_t old = atomicAdd(&g[c >> 1], inc << (16 * (c & 1)));
-                    own[m] |= (hm_sp_half(old, c) == 0 ? 1u : 0u) << l;
-                }
-            }
-            __syncthreads();
-        }
-        /* levels in [zmin, zmax]: one reservation, thread-contiguous slots */
-        uint32_t zmask = 0;
-        for (int l = 0; l < lg; l++) {
-            const int z = a.Z - l;
-            zmask |= (uint32_t)(z >= a.out.zmin && z <= a.out.zmax) << l;
-        }
-        uint32_t cnt = 0;
-#pragma unroll
-        for (int m = 0; m < KPT; m++) cnt += __popc(own[m] & zmask);
-        uint32_t tot;
-        uint32_t pos = hm_block_excl_scan<HM_SP_THREADS>(cnt, scr, &tot);
-        if (tot) {
-            if (tid == 0) sbase = atomicAdd(a.out.cursor, (unsigned long long)tot);
-            __syncthreads();
-            const uint64_t base = sbase;
-            const uint64_t coord = a.B.coord[b];
-#pragma unroll
-            for (int m = 0; m < KPT; m++) {
-                uint32_t e = own[m] & zmask;
-                while (e) {
-                    const int l = __ffs(e) - 1;
-                    e &= e - 1;
-                    const uint32_t c = hm_sp_cell(key[m], lg, l, cofs[l]);
-                    const uint64_t q = base + pos++;
-                    if (q < a.out.capacity) {
-                        a.out.keys[q] = hm_cell_key(a.Z - l, coord, lg - l, c - cofs[l]);
-                        a.out.counts[q] = hm_sp_half(g[c >> 1], c);
-                    }
-                }
-            }
-        }
-        __syncthreads();
-        /* every non-zero cell has an owner: owners zero their words */
-#pragma unroll
-        for (int m = 0; m < KPT; m++) {
-            uint32_t e = own[m];
-            while (e) {
-                const int l = __ffs(e) - 1;
-                e &= e - 1;
-                g[hm_sp_cell(key[m], lg, l, cofs[l]) >> 1] = 0;
-            }
-        }
-        if (tid == 0) a.totals[b] = nk;
-        __syncthreads();
-    }
-}
-
-/* ------------------------------------------------------------------------ */
 /* final level, small buckets (<= HM_SPW_MAX keys): one wavefront per bucket  */
 /* ------------------------------------------------------------------------ */
 
@@ -1961,7 +1807,7 @@ __device__ __forceinline__ uint32_t hm_small_zmask(const HmAggArgs& a)
 }
 
 /* Persistent: wave w takes the 64-bucket batches w, w + waves, ...; buckets of
- * more than HM_SPW_MAX keys are left to k_aggregate_sparse / k_aggregate
+ * more than HM_SPW_MAX keys are left to k_aggregate
  * (their count stays 0). */
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
 {
@@ -2017,8 +1863,20 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
                 hm_small_sort<2>(a, ks, nk, kb, zmask, b);
             else if (nk <= 256)
                 hm_small_sort<4>(a, ks, nk, kb, zmask, b);
-            else
+            else if (HM_SPW_MAX <= 512 || nk <= 512)
                 hm_small_sort<8>(a, ks, nk, kb, zmask, b);
+#if HM_SPW_MAX > 512
+            else if (HM_SPW_MAX <= 1024 || nk <= 1024)
+                hm_small_sort<16>(a, ks, nk, kb, zmask, b);
+#endif
+#if HM_SPW_MAX > 1024
+            else if (HM_SPW_MAX <= 2048 || nk <= 2048)
+                hm_small_sort<32>(a, ks, nk, kb, zmask, b);
+#endif
+#if HM_SPW_MAX > 2048
+            else
+                hm_small_sort<64>(a, ks, nk, kb, zmask, b);
+#endif
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -2057,8 +1915,20 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
                 hm_small_emit<2>(a, nk, kb, coord, zmask, q);
             else if (nk <= 256)
                 hm_small_emit<4>(a, nk, kb, coord, zmask, q);
-            else
+            else if (HM_SPW_MAX <= 512 || nk <= 512)
                 hm_small_emit<8>(a, nk, kb, coord, zmask, q);
+#if HM_SPW_MAX > 512
+            else if (HM_SPW_MAX <= 1024 || nk <= 1024)
+                hm_small_emit<16>(a, nk, kb, coord, zmask, q);
+#endif
+#if HM_SPW_MAX > 1024
+            else if (HM_SPW_MAX <= 2048 || nk <= 2048)
+                hm_small_emit<32>(a, nk, kb, coord, zmask, q);
+#endif
+#if HM_SPW_MAX > 2048
+            else
+                hm_small_emit<64>(a, nk, kb, coord, zmask, q);
+#endif
         }
     }
 }
@@ -2320,10 +2190,6 @@ void hm_launch_compact(hipStream_t s, const HmCompactArgs& a)
 void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint32_t nslots)
 {
     if (items) hipLaunchKernelGGL(k_aggregate, hm_grid2(items), dim3(HM_AG_THREADS), 0, s, a);
-    if (a.B.count) {
-        const uint32_t blocks = a.B.count < HM_SP_GRID ? a.B.count : HM_SP_GRID;
-        hipLaunchKernelGGL(k_aggregate_sparse, dim3(blocks), dim3(HM_SP_THREADS), 0, s, a);
-    }
     if (nslots) hipLaunchKernelGGL(k_aggregate_merged, hm_grid2(nslots), dim3(HM_AG_THREADS), 0, s, a);
 }
 void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)

@@ -1,10 +1,10 @@
 """Final-level bucket paths at their size boundaries (hm_count_tiles input).
 
 The last pipeline level bins each zoom-(Z-7) bucket (128 x 128 zoom-Z tiles)
-by one of four kernels chosen by its key count: k_small_sort/k_small_emit
-(<= 512 keys, one wavefront; register sorts of 64/128/256/512), k_aggregate_sparse
-(<= 2048), k_aggregate (dense, one 256K-key work item) and k_aggregate_merged
-(several items).  Every boundary is hit with several key patterns, and with zoom
+by one of three kernels chosen by its key count: k_small_sort/k_small_emit
+(<= 2048 keys, one wavefront; register sorts of 64/128/256/512/1024/2048 keys),
+k_aggregate (dense, one 256K-key work item) and k_aggregate_merged (several
+items).  Every boundary is hit with several key patterns, and with zoom
 windows that drop some of the pyramid levels.  Expected counts: oracle.count_tiles
 (the per-zoom reduceByKey of heatmap.py:109-111 over tile ids).
 """
@@ -17,7 +17,7 @@ from heatmap_amd import device
 
 pytestmark = pytest.mark.gpu
 
-SIZES = [1, 2, 3, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 777, 1024, 2047, 2048, 2049,
+SIZES = [1, 2, 3, 63, 64, 65, 127, 128, 129, 255, 256, 257, 511, 512, 513, 777, 1023, 1024, 1025, 2047, 2048, 2049,
          4096, 70000, 300000]
 PATTERNS = ["spread", "same", "row", "pairs", "corner"]
 

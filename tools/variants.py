@@ -125,7 +125,8 @@ def main():
                 print(json.dumps({"variant": n, "error": r.returncode}), flush=True)
                 break
     elif cmd == "one":
-        one(names[0], int(float(os.environ.get("HM_POINTS", "1e9"))), 3, int(os.environ.get("HM_ZMAX", "18")))
+        one(names[0], int(float(os.environ.get("HM_POINTS", "1e9"))), int(os.environ.get("HM_STEPS", "3")),
+            int(os.environ.get("HM_ZMAX", "18")))
 
 
 if __name__ == "__main__":
