@@ -1806,12 +1806,31 @@ __device__ __forceinline__ uint32_t hm_small_zmask(const HmAggArgs& a)
     return zmask;
 }
 
-/* Persistent: wave w takes the 64-bucket batches w, w + waves, ...; buckets of
- * more than HM_SPW_MAX keys are left to k_aggregate
- * (their count stays 0). */
+/* The register sort of bucket size nk runs with K = ceil(nk / 64) rounded up
+ * to a power of two, for K in the instantiation's range only: a kernel's VGPR
+ * budget is its widest K's (K = 32 needs ~200, two waves per SIMD), so buckets
+ * of <= HM_SPW_SPLIT keys get their own narrow, high-occupancy instantiation
+ * and LO < nk <= HI selects a kernel's share. */
+template <uint32_t LO, uint32_t HI, typename F>
+__device__ __forceinline__ void hm_small_dispatch(uint32_t nk, F&& f)
+{
+    if constexpr (LO < 64) if (nk <= 64) { f(std::integral_constant<int, 1>{}); return; }
+    if constexpr (LO < 128 && HI >= 128) if (nk <= 128) { f(std::integral_constant<int, 2>{}); return; }
+    if constexpr (LO < 256 && HI >= 256) if (nk <= 256) { f(std::integral_constant<int, 4>{}); return; }
+    if constexpr (LO < 512 && HI >= 512) if (nk <= 512) { f(std::integral_constant<int, 8>{}); return; }
+    if constexpr (LO < 1024 && HI >= 1024) if (nk <= 1024) { f(std::integral_constant<int, 16>{}); return; }
+    if constexpr (LO < 2048 && HI >= 2048) if (nk <= 2048) { f(std::integral_constant<int, 32>{}); return; }
+    if constexpr (HI >= 4096) f(std::integral_constant<int, 64>{});
+}
+
+/* Persistent: wave w takes the 64-bucket batches w, w + waves, ...; a bucket
+ * is this instantiation's when LO < nkeys <= HI (larger ones are
+ * k_aggregate's). The LO == 0 instantiation runs first and zeroes the cell
+ * count of every bucket that is not its own. */
+template <uint32_t LO, uint32_t HI>
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
 {
-    __shared__ uint16_t kss[HM_SPW_THREADS / 64][HM_SPW_MAX];
+    __shared__ uint16_t kss[HM_SPW_THREADS / 64][HI];
     const uint32_t lane = hm_lane();
     uint16_t* ks = kss[threadIdx.x >> 6];
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
@@ -1821,13 +1840,11 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
         const uint32_t bl = b0 + lane;
         const bool in = (lane < a.spbatch) & (bl < a.B.count);
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
-        const bool small = in & (nkl <= HM_SPW_MAX);
+        const bool small = in & (LO == 0 || nkl > LO) & (nkl <= HI);
         const uint32_t rbl = small ? a.B.rbase[bl] : 0u, nrl = small ? a.B.nruns[bl] : 0u;
         const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
-        if (in) {
-            a.spcnt[bl] = 0;
-            if (small) a.totals[bl] = nkl;
-        }
+        if (LO == 0 && in && !small) a.spcnt[bl] = 0;
+        if (small) a.totals[bl] = nkl;
         uint64_t m = __ballot(small);
         while (m) {
             const int i = __builtin_ctzll(m);
@@ -1857,26 +1874,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
                 fill += tot;
             }
             __builtin_amdgcn_wave_barrier();
-            if (nk <= 64)
-                hm_small_sort<1>(a, ks, nk, kb, zmask, b);
-            else if (nk <= 128)
-                hm_small_sort<2>(a, ks, nk, kb, zmask, b);
-            else if (nk <= 256)
-                hm_small_sort<4>(a, ks, nk, kb, zmask, b);
-            else if (HM_SPW_MAX <= 512 || nk <= 512)
-                hm_small_sort<8>(a, ks, nk, kb, zmask, b);
-#if HM_SPW_MAX > 512
-            else if (HM_SPW_MAX <= 1024 || nk <= 1024)
-                hm_small_sort<16>(a, ks, nk, kb, zmask, b);
-#endif
-#if HM_SPW_MAX > 1024
-            else if (HM_SPW_MAX <= 2048 || nk <= 2048)
-                hm_small_sort<32>(a, ks, nk, kb, zmask, b);
-#endif
-#if HM_SPW_MAX > 2048
-            else
-                hm_small_sort<64>(a, ks, nk, kb, zmask, b);
-#endif
+            hm_small_dispatch<LO, HI>(nk, [&](auto kc) { hm_small_sort<decltype(kc)::value>(a, ks, nk, kb, zmask, b); });
             __builtin_amdgcn_wave_barrier();
         }
     }
@@ -1888,6 +1886,7 @@ __global__ void k_small_reserve(HmAggArgs a)
     if (threadIdx.x == 0) *a.spbase = atomicAdd(a.out.cursor, (unsigned long long)*a.sptotal);
 }
 
+template <uint32_t LO, uint32_t HI>
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
 {
     const uint32_t lane = hm_lane();
@@ -1899,7 +1898,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
         const uint32_t bl = b0 + lane;
         const bool in = (lane < a.spbatch) & (bl < a.B.count);
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
-        const bool small = in & (nkl <= HM_SPW_MAX);
+        const bool small = in & (LO == 0 || nkl > LO) & (nkl <= HI);
         const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
         const uint64_t cl = small ? a.B.coord[bl] : 0ull;
         const uint64_t ol = small ? a.spoff[bl] : 0ull;
@@ -1909,26 +1908,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
             m &= m - 1;
             const uint32_t nk = __shfl(nkl, i, 64), kb = __shfl(kbl, i, 64);
             const uint64_t coord = __shfl(cl, i, 64), q = base + __shfl(ol, i, 64);
-            if (nk <= 64)
-                hm_small_emit<1>(a, nk, kb, coord, zmask, q);
-            else if (nk <= 128)
-                hm_small_emit<2>(a, nk, kb, coord, zmask, q);
-            else if (nk <= 256)
-                hm_small_emit<4>(a, nk, kb, coord, zmask, q);
-            else if (HM_SPW_MAX <= 512 || nk <= 512)
-                hm_small_emit<8>(a, nk, kb, coord, zmask, q);
-#if HM_SPW_MAX > 512
-            else if (HM_SPW_MAX <= 1024 || nk <= 1024)
-                hm_small_emit<16>(a, nk, kb, coord, zmask, q);
-#endif
-#if HM_SPW_MAX > 1024
-            else if (HM_SPW_MAX <= 2048 || nk <= 2048)
-                hm_small_emit<32>(a, nk, kb, coord, zmask, q);
-#endif
-#if HM_SPW_MAX > 2048
-            else
-                hm_small_emit<64>(a, nk, kb, coord, zmask, q);
-#endif
+            hm_small_dispatch<LO, HI>(nk, [&](auto kc) { hm_small_emit<decltype(kc)::value>(a, nk, kb, coord, zmask, q); });
         }
     }
 }
@@ -2205,10 +2185,14 @@ void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
     const uint32_t per_block = b.spbatch * (HM_SPW_THREADS / 64);
     const uint32_t wb = (a.B.count + per_block - 1) / per_block;
     const dim3 g(wb < HM_SPW_GRID ? wb : HM_SPW_GRID);
-    hipLaunchKernelGGL(k_small_sort, g, dim3(HM_SPW_THREADS), 0, s, b);
+    hipLaunchKernelGGL((k_small_sort<0, HM_SPW_SPLIT>), g, dim3(HM_SPW_THREADS), 0, s, b);
+    if (HM_SPW_MAX > HM_SPW_SPLIT)
+        hipLaunchKernelGGL((k_small_sort<HM_SPW_SPLIT, HM_SPW_MAX>), g, dim3(HM_SPW_THREADS), 0, s, b);
     hm_launch_scan(s, b.spcnt, b.B.count, partial, (uint64_t*)b.spoff, b.sptotal);
     hipLaunchKernelGGL(k_small_reserve, dim3(1), dim3(64), 0, s, b);
-    hipLaunchKernelGGL(k_small_emit, g, dim3(HM_SPW_THREADS), 0, s, b);
+    hipLaunchKernelGGL((k_small_emit<0, HM_SPW_SPLIT>), g, dim3(HM_SPW_THREADS), 0, s, b);
+    if (HM_SPW_MAX > HM_SPW_SPLIT)
+        hipLaunchKernelGGL((k_small_emit<HM_SPW_SPLIT, HM_SPW_MAX>), g, dim3(HM_SPW_THREADS), 0, s, b);
 }
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {

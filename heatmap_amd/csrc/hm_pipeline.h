@@ -63,6 +63,10 @@
 #define HM_SPW_MAX HM_SP_MAX                /* <= 2048 keys: 32 per lane (a 512-2048-key
                                                block pyramid was 0.17 ms slower per 10M) */
 #endif
+/* buckets of <= HM_SPW_SPLIT keys: the narrow (high-occupancy) instantiation */
+#ifndef HM_SPW_SPLIT
+#define HM_SPW_SPLIT 512
+#endif
 static_assert(HM_SPW_MAX >= HM_SP_MAX, "every bucket without a dense work item needs the wavefront path");
 #define HM_SPW_THREADS 256
 #define HM_SPW_GRID (256 * 8)
