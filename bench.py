@@ -237,6 +237,7 @@ def main():
         "config": {"workload": "%.3g %s points per GPU, zooms %d-%d, %d x MI355X" % (per, args.kind, args.zmin,
                                                                                     args.zmax, ws),
                    "points_per_gpu": per, "zmin": args.zmin, "zmax": args.zmax,
+                   "partition_levels": int(ctx.last_stats()[1][7]),
                    "parallelism": "points sharded, dp%d" % ws},
         "roofline": {"bound": "hbm", "kernel": "hm_count step (all pipeline kernels, one rank)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,

@@ -51,6 +51,7 @@ struct hm_ctx {
     std::vector<Buf> bufs;
     unsigned long long* state = nullptr;      /* device: err, exotic count, slow, cursor, nslots, ... */
     unsigned long long* host_state = nullptr; /* pinned mirror */
+    int last_levels = 0;                      /* partition levels of the last count (stats [7]) */
     uint32_t* host_aux = nullptr;             /* pinned: level-1 histogram / region sizes */
     int64_t last_err_index = -1;
     int last_err_kind = 0;
@@ -228,6 +229,7 @@ int hm_last_stats(hm_ctx* c, int64_t* slow_points, double* stage_us, int n_stage
     if (!c) return HM_E_ARG;
     if (slow_points) *slow_points = c->last_slow;
     for (int i = 0; i < n_stages && i < 8; i++) stage_us[i] = c->stage_us[i];
+    if (n_stages > 7) stage_us[7] = (double)c->last_levels;
     return HM_OK;
 }
 
@@ -414,8 +416,44 @@ static int count_fallback(hm_ctx* ctx, const double* lat, const double* lon, con
     *n_out = (int64_t)ctx->host_state[ST_CURSOR];
     *nx_out = (int64_t)ctx->host_state[ST_XCURSOR];
     ctx->last_slow = 0;
+    ctx->last_levels = 0;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
     return (*n_out > capacity || *nx_out > xcapacity) ? HM_E_CAPACITY : HM_OK;
+}
+
+/* Level plan for dense, evenly spread clouds (uniform-like). With 6 zooms
+ * per level, each level-2 work item (HM_TN keys) of such a cloud scatters
+ * over ~3400 of its 4^6 digits: runs of one or two keys, each a run-slot
+ * atomic, a run record and a scan entry (1e9 uniform points: 24 ms of
+ * level-2 partitioning). Levels of 3 zooms (64 digits) keep the runs long
+ * at the price of one more pass over the keys (1e9 uniform points: 68 -> 48
+ * ms per count; the same plan costs hotspot clouds 60%, so it is chosen only
+ * when level 1's sampled histogram is flat -- no digit above 4x the mean --
+ * and the mean level-1 bucket holds >= HM_SPREAD_MIN_KEYS keys; the
+ * environment variable of that name overrides the threshold). */
+#define HM_SPREAD_MIN_KEYS (1u << 19)
+#define HM_SPREAD_ZOOMS 3
+static void spread_replan(const uint32_t* h, int F, int64_t n, int zb, int* zs, int* L)
+{
+    uint64_t tot = 0, mx = 0;
+    int ne = 0;
+    for (int i = 0; i < F; i++) {
+        tot += h[i];
+        mx = std::max<uint64_t>(mx, h[i]);
+        ne += h[i] != 0;
+    }
+    double min_keys = HM_SPREAD_MIN_KEYS;
+    if (const char* e = getenv("HM_SPREAD_MIN_KEYS")) min_keys = atof(e);
+    if (ne == 0 || (double)n < min_keys * ne || (double)mx * ne > 4.0 * (double)tot) return;
+    int step = HM_SPREAD_ZOOMS;
+    while (zs[0] + step * (HM_MAX_LEVELS - 1) < zb) step++;
+    if (step >= HM_LEVEL_ZOOMS) return;
+    int l = 1, z = zs[0];
+    while (z < zb) {
+        z = std::min(z + step, zb);
+        zs[l++] = z;
+    }
+    *L = l;
 }
 
 static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows, const int64_t* cols,
@@ -451,6 +489,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     hipEvent_t* ev = ctx->ev;
     int nev = 0;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
+    ctx->last_levels = L;
 
     /* level 1 reads the input in HM_T1-point tiles; points the fast path
      * defers (lat/lon input only) go to k_redo, at most redo_cap of them */
@@ -680,7 +719,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             HIPCHK(hipGetLastError());
             unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
             HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            if (L > 1) HIPCHK(hipMemcpyAsync(ctx->host_aux, hist, F * 4, hipMemcpyDeviceToHost, s));
             if ((st = read_state(ctx))) return st;
+            /* levels 2.. may take the spread plan (the level-1 pass is the
+             * same under both: its output is u32 keys whenever L > 1) */
+            if (L > 1) spread_replan(ctx->host_aux, F, n, zb, zs, &L);
+            ctx->last_levels = L;
             V.count = (uint32_t)(down[0] >> 32);
             V.items = (uint32_t)(down[0] & 0xFFFFFFFFull);
             if (L == 1) nslots = (uint32_t)(ctx->host_state[ST_NSLOTS] & 0xFFFFFFFFull);

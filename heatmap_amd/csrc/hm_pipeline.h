@@ -40,7 +40,9 @@
 #ifndef HM_FR_GROUP
 #define HM_FR_GROUP 4
 #endif
+#ifndef HM_LEVEL_ZOOMS
 #define HM_LEVEL_ZOOMS 6                   /* <= 6 zooms per level */
+#endif
 #define HM_MAX_FN 4096
 #define HM_MAX_SHARDS 32                    /* run-counter shards per child */
 #ifndef HM_RUN_SHARD_BITS

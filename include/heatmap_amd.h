@@ -149,7 +149,9 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
  *   [1] level-1 buckets, remaining partition levels, run scans and
  *       compactions (incl. host reads; contains [4])
  *   [2] final aggregation (k_aggregate, sparse/small/merged buckets)
- *   [3] k_pool levels   [4] the level >= 2 k_partition launches alone */
+ *   [3] k_pool levels   [4] the level >= 2 k_partition launches alone
+ *   [7] partition levels of the pipeline plan (0 if the call took the
+ *       general path); 3 zooms per level for dense, evenly spread clouds */
 int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_stages);
 
 /* Streaming: micro-batches folded into a heatmap resident in HBM (BASELINE

@@ -43,6 +43,7 @@ VARIANTS = {
     "fr512_4k": ["HM_FR_THREADS=512", "HM_TN=4096"],
     "ta64k": ["HM_TA=65536"],
     "ta128k": ["HM_TA=131072"],
+    "lz3": ["HM_LEVEL_ZOOMS=3"],            # levels z5, z8, z11 (zmax 18)
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
