@@ -100,7 +100,7 @@ enum {
     B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
-    B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG,
+    B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
     B_COUNT
 };
 
@@ -832,6 +832,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_CNT, (nflat + 1) * sizeof(uint64_t), ra.cnt);
         ra.flat = flat;
         ra.excl = excl;
+        ENSURE(B_RS_BIG, (HM_RS_BIG_MAX + 1) * sizeof(uint32_t), ra.big);
+        ra.nbig = ra.big + HM_RS_BIG_MAX;
+        ra.big_min = HM_RS_BIG;
+        if (const char* e = getenv("HM_RS_BIG_MIN")) ra.big_min = (uint64_t)atoll(e);
+        HIPCHK(hipMemsetAsync(ra.nbig, 0, sizeof(uint32_t), s));
         hm_launch_rs_copy(s, ra);
         hm_launch_scan(s, ra.cnt, nflat, partial, excl, tot + 1);
         ra.total_keys = tot + 1;

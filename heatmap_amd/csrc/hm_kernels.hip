@@ -1175,54 +1175,154 @@ __global__ __launch_bounds__(256) void k_rs_count(HmRsArgs a)
  * child: lanes 0..S-1 hold the child's shards (count, flat offset, source),
  * and the wave copies the child's runs HM_RS_SLICE at a time, 8 loads per lane
  * in flight, each run's shard found by a shuffle search over the S lanes.
- * The hottest child (one run per parent work item, tens of thousands) is the
- * critical path: 8-deep loads cut its chain of dependent memory steps 8x. */
+ * A child of more than a.big_min runs (HM_RS_BIG by default; one run per
+ * parent work item: the hot tile of a skewed cloud has 10^5) is listed instead, and k_rs_copy_big
+ * spreads its slices over every wave of the grid. */
 #define HM_RS_SLICE 512
-__global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
+
+struct HmRsChild {
+    uint32_t n, incl;
+    uint64_t src;
+};
+
+/* lanes 0..S-1: shard counts and sources of child c (loads only) */
+__device__ __forceinline__ HmRsChild hm_rs_child_load(const HmRsArgs& a, uint64_t c)
 {
     const uint32_t S = 1u << a.shard_bits;
     const uint32_t lane = (uint32_t)hm_lane();
-    const uint64_t nw = (uint64_t)gridDim.x * 4;
-    for (uint64_t c = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6); c < a.nchildren; c += nw) {
-        const uint64_t nr = a.nr[c];
-        if (nr == 0) continue;
-        const uint64_t k = (c << a.shard_bits) + lane;
-        uint32_t n = 0;
-        uint64_t src = 0;
-        if (lane < S) {
-            n = a.nruns[k];
-            const uint64_t p = c >> a.dbits;
-            const uint64_t d = c & ((1ull << a.dbits) - 1);
-            const uint32_t t0 = a.parent_item_begin[p];
-            const uint32_t tp = a.parent_item_begin[p + 1] - t0;
-            const uint32_t cap = (tp + S - 1) >> a.shard_bits;
-            src = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits) + (uint64_t)lane * cap;
+    const uint64_t k = (c << a.shard_bits) + lane;
+    HmRsChild h;
+    h.n = 0;
+    h.src = 0;
+    h.incl = 0;
+    if (lane < S) {
+        h.n = a.nruns[k];
+        const uint64_t p = c >> a.dbits;
+        const uint64_t d = c & ((1ull << a.dbits) - 1);
+        const uint32_t t0 = a.parent_item_begin[p];
+        const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+        const uint32_t cap = (tp + S - 1) >> a.shard_bits;
+        h.src = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits) + (uint64_t)lane * cap;
+    }
+    return h;
+}
+
+__device__ __forceinline__ HmRsChild hm_rs_child(const HmRsArgs& a, uint64_t c)
+{
+    HmRsChild h = hm_rs_child_load(a, c);
+    h.incl = hm_wave_incl_scan(h.n);   /* shard offsets within the child */
+    return h;
+}
+
+/* runs j0 .. j0 + 64 U of the child (each lane's shard: a shuffle search) */
+template <int U = HM_RS_SLICE / 64>
+__device__ __forceinline__ void hm_rs_slice(const HmRsArgs& a, const HmRsChild& h, uint64_t nr, uint64_t rb,
+                                            uint64_t j0)
+{
+    const uint32_t lane = (uint32_t)hm_lane();
+    uint2 r[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t x = j0 + (uint64_t)u * 64 + lane;
+        const uint32_t xc = (uint32_t)min(x, nr - 1);
+        uint32_t l = 0;
+#pragma unroll
+        for (int st = 32; st > 0; st >>= 1)
+            if (__shfl(h.incl, l + st - 1, 64) <= xc) l += st;
+        l = min(l, 63u);
+        const uint32_t off = xc - (__shfl(h.incl, l, 64) - __shfl(h.n, l, 64));
+        const uint64_t sj = __shfl(h.src, l, 64) + off;
+        r[u] = x < nr ? a.runs[sj] : make_uint2(0, 0);
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint64_t x = j0 + (uint64_t)u * 64 + lane;
+        if (x < nr) {
+            a.flat[rb + x] = r[u];
+            a.cnt[rb + x] = r[u].y;
         }
-        const uint32_t incl = hm_wave_incl_scan(n);   /* shard offsets within the child */
-        const uint64_t rb = a.runbase[c];
-        for (uint64_t j0 = 0; j0 < nr; j0 += HM_RS_SLICE) {
-            uint2 r[HM_RS_SLICE / 64];
-#pragma unroll
-            for (int u = 0; u < HM_RS_SLICE / 64; u++) {
-                const uint64_t x = j0 + (uint64_t)u * 64 + lane;
-                const uint32_t xc = (uint32_t)min(x, nr - 1);
-                uint32_t l = 0;
-#pragma unroll
-                for (int st = 32; st > 0; st >>= 1)
-                    if (__shfl(incl, l + st - 1, 64) <= xc) l += st;
-                l = min(l, 63u);
-                const uint32_t off = xc - (__shfl(incl, l, 64) - __shfl(n, l, 64));
-                const uint64_t sj = __shfl(src, l, 64) + off;
-                r[u] = x < nr ? a.runs[sj] : make_uint2(0, 0);
+    }
+}
+
+/* a wave takes 64 consecutive children at a time: their run counts and
+ * bases in one lane-per-child load, then the non-empty ones in turn (most
+ * children of a sparse level are empty or hold a few runs: the per-child
+ * chain of dependent loads is what this kernel waits on) */
+__global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
+{
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint32_t lane = (uint32_t)hm_lane();
+    for (uint64_t c0 = ((uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6)) * 64; c0 < a.nchildren; c0 += nw * 64) {
+        const uint64_t cl = c0 + lane;
+        const uint64_t nrl = cl < a.nchildren ? a.nr[cl] : 0ull;
+        const uint64_t rbl = nrl ? a.runbase[cl] : 0ull;
+        /* the copied children in order; the next one's shard table loads
+         * are issued before the current one's run copy */
+        uint64_t m = __ballot((nrl != 0) & (nrl <= a.big_min));
+        uint64_t mb = __ballot(nrl > a.big_min);
+        while (mb) {
+            const int i = __builtin_ctzll(mb);
+            mb &= mb - 1;
+            uint32_t slot = 0;
+            if (lane == 0) slot = atomicAdd(a.nbig, 1u);
+            slot = __shfl(slot, 0, 64);
+            if (slot < HM_RS_BIG_MAX) {
+                if (lane == 0) a.big[slot] = (uint32_t)(c0 + (uint64_t)i);
+            } else {
+                m |= 1ull << i;   /* list full: copied here */
             }
-#pragma unroll
-            for (int u = 0; u < HM_RS_SLICE / 64; u++) {
-                const uint64_t x = j0 + (uint64_t)u * 64 + lane;
-                if (x < nr) {
-                    a.flat[rb + x] = r[u];
-                    a.cnt[rb + x] = r[u].y;
-                }
+        }
+        if (!m) continue;
+        int i = __builtin_ctzll(m);
+        m &= m - 1;
+        HmRsChild h = hm_rs_child_load(a, c0 + (uint64_t)i);
+        for (;;) {
+            const int inext = m ? __builtin_ctzll(m) : -1;
+            HmRsChild hn;
+            if (inext >= 0) {
+                m &= m - 1;
+                hn = hm_rs_child_load(a, c0 + (uint64_t)inext);
             }
+            h.incl = hm_wave_incl_scan(h.n);
+            const uint64_t nr = __shfl(nrl, i, 64);
+            const uint64_t rb = __shfl(rbl, i, 64);
+            /* a sparse level's children hold a few runs: one 64-run step */
+            if (nr <= 64)
+                hm_rs_slice<1>(a, h, nr, rb, 0);
+            else if (nr <= 256)
+                hm_rs_slice<4>(a, h, nr, rb, 0);
+            else
+                for (uint64_t j0 = 0; j0 < nr; j0 += HM_RS_SLICE) hm_rs_slice(a, h, nr, rb, j0);
+            if (inext < 0) break;
+            i = inext;
+            h = hn;
+        }
+    }
+}
+
+/* the listed children: wave w copies slices w, w + waves, ... of each */
+__global__ __launch_bounds__(256) void k_rs_copy_big(HmRsArgs a)
+{
+    const uint32_t nb = min(*a.nbig, (uint32_t)HM_RS_BIG_MAX);
+    const uint64_t nw = (uint64_t)gridDim.x * 4;
+    const uint64_t w = (uint64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const uint32_t lane = (uint32_t)hm_lane();
+    for (uint32_t e0 = 0; e0 < nb; e0 += 64) {
+        /* 64 listed children per lane-parallel load */
+        const bool in = e0 + lane < nb;
+        const uint32_t cl = in ? a.big[e0 + lane] : 0u;
+        const uint64_t nrl = in ? a.nr[cl] : 0ull;
+        const uint64_t rbl = in ? a.runbase[cl] : 0ull;
+        const uint32_t ne = min(64u, nb - e0);
+        for (uint32_t j = 0; j < ne; j++) {
+            const uint64_t nr = __shfl(nrl, (int)j, 64);
+            /* rotate the starting wave per child so short tails spread out */
+            const uint64_t w0 = (w + (uint64_t)(e0 + j) * 97) % nw;
+            if (w0 * HM_RS_SLICE >= nr) continue;
+            const uint64_t c = __shfl(cl, (int)j, 64);
+            const uint64_t rb = __shfl(rbl, (int)j, 64);
+            const HmRsChild h = hm_rs_child(a, c);
+            for (uint64_t j0 = w0 * HM_RS_SLICE; j0 < nr; j0 += nw * HM_RS_SLICE) hm_rs_slice(a, h, nr, rb, j0);
         }
     }
 }
@@ -2143,7 +2243,8 @@ void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a)
 {
     const uint64_t pairs = a.nchildren << a.shard_bits;
     if (pairs == 0) return;   /* a level with no parent buckets (nothing kept) */
-    hipLaunchKernelGGL(k_rs_copy, dim3(hm_grid(a.nchildren, 4, 16384)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rs_copy, dim3(hm_grid((a.nchildren + 63) / 64, 4, 16384)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_rs_copy_big, dim3(1024), dim3(256), 0, s, a);
 }
 
 void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a)

@@ -241,7 +241,12 @@ struct HmRsArgs {
     uint32_t* nkeys;            /* [nchildren] */
     uint32_t* keybase;          /* [nchildren] */
     uint64_t* vals;             /* [nchildren] (1 << 32 | items) for non-empty children */
+    uint32_t* big;              /* [HM_RS_BIG_MAX] children with many runs (k_rs_copy_big) */
+    uint32_t* nbig;             /* their count */
+    uint64_t big_min;           /* runs above which a child is listed */
 };
+#define HM_RS_BIG_MAX 4096
+#define HM_RS_BIG 2048              /* default big_min (HM_RS_BIG_MIN in the environment overrides) */
 
 
 struct HmCompactArgs {

@@ -60,3 +60,35 @@ def test_default_plans(gpu, monkeypatch):
     got = device.count(lat, lon, None, 0, 18)
     assert int(got.stage_us[7]) == 2
     _same(got, oracle.count(lat, lon, None, 0, 18))
+
+
+@pytest.mark.parametrize("big_min", [None, "1000000", "0"])
+def test_hot_children_many_runs(gpu, monkeypatch, big_min):
+    """Children with many runs -- one run per work item of their parent, the
+    hot tiles of a skewed cloud -- are copied by every wave of k_rs_copy_big
+    when they hold more than HM_RS_BIG_MIN runs (2048 by default: the three
+    hot zoom-18 tiles here, ~5100 runs each); also with none listed (one wave
+    per child) and with every child listed (the 4096-entry list overflows, the
+    rest are copied in place).  A zoom-5 parent of ~5100 work items plus a
+    uniform background."""
+    if big_min is None:
+        monkeypatch.delenv("HM_RS_BIG_MIN", raising=False)
+    else:
+        monkeypatch.setenv("HM_RS_BIG_MIN", big_min)
+    from conftest import cells_digest
+    rng = np.random.default_rng(21)
+    Z = 18
+    hot = [(70001, 130003), (70100, 130050), (71000, 131000)]   # one zoom-5 tile (>> 13)
+    rows = [np.full(14_000_000, r, np.int64) for r, _ in hot]
+    cols = [np.full(14_000_000, c, np.int64) for _, c in hot]
+    rows.append(rng.integers(0, 1 << Z, 6_000_000))
+    cols.append(rng.integers(0, 1 << Z, 6_000_000))
+    rows = np.concatenate(rows)
+    cols = np.concatenate(cols)
+    perm = rng.permutation(rows.size)
+    rows, cols = rows[perm], cols[perm]
+    got = device.count(rows, cols, None, 0, Z, tiles=True)
+    ref = oracle.count_tiles(rows, cols, 0, Z)
+    assert got.zoom.size == ref["zoom"].size
+    assert cells_digest(got.zoom, got.row, got.col, got.count) == \
+        cells_digest(ref["zoom"], ref["row"], ref["col"], ref["count"])
