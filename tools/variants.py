@@ -44,6 +44,8 @@ VARIANTS = {
     "ta64k": ["HM_TA=65536"],
     "ta128k": ["HM_TA=131072"],
     "lz3": ["HM_LEVEL_ZOOMS=3"],            # levels z5, z8, z11 (zmax 18)
+    "split256": ["HM_SPW_SPLIT=256"],       # narrow small-bucket instantiation up to 256 keys
+    "sp1024": ["HM_SP_MAX=1024"],           # buckets of 1025-2048 keys to k_aggregate
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
