@@ -8,10 +8,17 @@ pyramid for zooms 0..18 (heatmap.py:107-111 semantics), every non-empty cell
 written to HBM as (key, count).
 
     python bench.py                                   # 1 GPU, 1e9 points (config 2)
+    python bench.py --gpus N                          # spawns N ranks itself
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
         # N GPUs, 1.25e9 points per GPU (config 3 at N=8: 1e10), weak scaling:
         # each rank bins its shard, then the sparse cells are hash-partitioned
         # by heatmap row over RCCL all-to-all and merged
+
+`--gpus N` with no WORLD_SIZE in the environment starts N worker processes
+(one per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_* set) before anything touches
+HIP, and exits with the first failing rank's status.  A launcher's WORLD_SIZE
+that differs from --gpus, or fewer visible GPUs than ranks, is an error (exit
+status 2): the line would otherwise claim a node it did not measure.
 
 With N > 1 ranks the steps are pipelined: step k's exchange and merge run on a
 second HIP stream (and host thread) while step k+1 counts, so the per-step time
@@ -65,16 +72,78 @@ def parse():
     return ap.parse_args()
 
 
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def spawn(args):
+    """--gpus N without a launcher: start N ranks of this script (no HIP call
+    in this process: torch.cuda.device_count() does not initialise the GPU),
+    wait for all, and stop the others as soon as one fails (its peers would
+    block in a collective)."""
+    import subprocess
+
+    dry = os.environ.get("HM_BENCH_DRY") == "1"     # CPU test of the spawn itself
+    if not dry:
+        import torch
+
+        nd = torch.cuda.device_count()
+        if nd < args.gpus:
+            print("bench.py: --gpus %d needs %d visible GPUs, found %d" % (args.gpus, args.gpus, nd),
+                  file=sys.stderr, flush=True)
+            return 2
+    port = os.environ.get("MASTER_PORT") or str(_free_port())
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            c = p.poll()
+            if c is None:
+                continue
+            live.remove(p)
+            if c != 0 and rc == 0:
+                rc = c
+                for q in live:
+                    q.kill()          # the exact child processes this call started
+        if live:
+            time.sleep(0.2)
+    return rc
+
+
 def dist_init(args):
     ws = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if ws != args.gpus:
+        print("bench.py: WORLD_SIZE=%d but --gpus %d" % (ws, args.gpus), file=sys.stderr, flush=True)
+        sys.exit(2)
+    if os.environ.get("HM_BENCH_DRY") == "1":
+        print(json.dumps({"rank": rank, "local_rank": local, "world_size": ws}), flush=True)
+        sys.exit(0)
     args.dist = ws > 1 or args.force_dist
+    import torch
+
+    nd = torch.cuda.device_count()
+    if local >= nd:
+        print("bench.py: rank %d (local %d) has no GPU: %d visible" % (rank, local, nd), file=sys.stderr, flush=True)
+        sys.exit(2)
     if args.dist:
         import torch.distributed as dist
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl")
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     return ws, rank, local
 
 
@@ -88,19 +157,20 @@ def barrier(ws):
 
 
 def profile_traffic(workload_tag):
-    """HBM bytes of one hm_count step from the committed PMC summary."""
+    """HBM bytes of one hm_count step and the executed fp64 VALU operations
+    per point, from the committed PMC summary (tools/pmc_traffic.py)."""
     path = os.path.join(REPO, "profiles", "pmc_summary.json")
     if not os.path.exists(path):
-        return None, None
+        return None, None, None
     try:
         with open(path) as f:
             d = json.load(f)
         e = d.get(workload_tag)
         if not e:
-            return None, None
-        return e.get("hbm_bytes_per_step"), os.path.relpath(path, REPO)
+            return None, None, None
+        return e.get("hbm_bytes_per_step"), os.path.relpath(path, REPO), e.get("fp64")
     except Exception:
-        return None, None
+        return None, None, None
 
 
 def cpu_baseline(args, lat_dev=None, lon_dev=None):
@@ -128,8 +198,33 @@ def cpu_baseline(args, lat_dev=None, lon_dev=None):
                       % (n, args.kind, args.seed, args.zmin, args.zmax, int(r["threads"]), dt)}
 
 
+def measured_peak(torch, nbytes=4 << 30, reps=5):
+    """STREAM-like copy rate on this GPU (bytes read + written per second):
+    torch's device copy of a 4 GiB buffer, the best of `reps`."""
+    a = torch.empty(nbytes // 8, dtype=torch.float64, device="cuda")
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    b.copy_(a)
+    best = 0.0
+    for _ in range(reps):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        b.copy_(a)
+        e1.record()
+        e1.synchronize()
+        best = max(best, 2.0 * nbytes / (e0.elapsed_time(e1) * 1e-3) / 1e9)
+    del a, b
+    torch.cuda.empty_cache()
+    return best
+
+
 def main():
     args = parse()
+    if args.gpus < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr)
+        sys.exit(2)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn(args))
     ws, rank, local = dist_init(args)
     import torch
 
@@ -146,16 +241,29 @@ def main():
     ctx = device.context(local)
 
     def step():
-        m, b = device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=bufs)
-        if args.dist:
-            m = multigpu.merge_cells(b, m, ws, rank)
-        return m, b
+        return device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=bufs)
 
+    dist_info = None
     if args.dist:
+        import torch.distributed as dist
+
+        # the same per-GPU workload without the exchange: what one rank alone
+        # takes per step (the weak-scaling reference at this per-GPU size)
+        for _ in range(args.warmup):
+            m_local, bufs = step()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(args.steps):
+            m_local, bufs = step()
+        e1.record()
+        e1.synchronize()
+        local_ms = e0.elapsed_time(e1) / args.steps
         # steps pipelined over two buffer sets: step k's exchange and merge
         # (RCCL + merge kernels, their own HIP stream and host thread) run
         # while step k+1 counts; every step's merge ends inside the timed region
         bufsets = [bufs, device.CountBuffers(64 << 20)]
+        merge_ms = []
         m, stages, _ = multigpu.pipelined_steps(
             lambda b: device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=b),
             bufsets, args.warmup, ws, rank, ctx)
@@ -164,16 +272,28 @@ def main():
         t0 = time.perf_counter()
         m, stages, bufs = multigpu.pipelined_steps(
             lambda b: device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=b),
-            bufsets, args.steps, ws, rank, ctx)
+            bufsets, args.steps, ws, rank, ctx, merge_ms=merge_ms)
         torch.cuda.synchronize()
         barrier(ws)
         dt = time.perf_counter() - t0
-        step_ms_ev = dt / args.steps * 1e3     # host clock: the steps overlap across two streams
+        t = torch.tensor([dt, float(m), local_ms, float(np.mean(merge_ms)) if merge_ms else 0.0, float(m_local)],
+                         dtype=torch.float64, device="cuda")
+        tmax = t.clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        dt, cells = float(tmax[0]), int(t[1])
+        step_ms_ev = dt / args.steps * 1e3     # host clock, max over ranks: the steps overlap on two streams
+        cells_rank = int(t[4]) // ws           # cells one rank's count emits (before the exchange)
+        dist_info = {"points_per_gpu": per, "local_ms_per_step": float(tmax[2]),
+                     "merge_ms_per_step": float(tmax[3]), "merge_ms_mean_over_ranks": float(t[3]) / ws,
+                     "efficiency_vs_local": float(tmax[2]) / step_ms_ev,
+                     "note": "local = the same count on this rank's shard with no exchange (max over ranks); "
+                             "merge = route + RCCL reduce/all-to-all + owner merge of one step, host clock on the "
+                             "merge thread, overlapped with the next step's count"}
     else:
         for _ in range(args.warmup):
             m, bufs = step()
         torch.cuda.synchronize()
-        barrier(ws)
         stages = []
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
@@ -184,18 +304,9 @@ def main():
             stages.append(us[:5])
         ev1.record()
         torch.cuda.synchronize()
-        barrier(ws)
         dt = time.perf_counter() - t0
         step_ms_ev = ev0.elapsed_time(ev1) / args.steps
-    if args.dist:
-        import torch.distributed as dist
-
-        t = torch.tensor([dt, float(m)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t[:1], op=dist.ReduceOp.MAX)
-        dist.all_reduce(t[1:], op=dist.ReduceOp.SUM)
-        dt, cells = float(t[0]), int(t[1])
-    else:
-        cells = int(m)
+        cells = cells_rank = int(m)
     check = None
     if not args.no_check:
         # every zoom's counts sum to the number of points (over all ranks' owned cells)
@@ -210,8 +321,9 @@ def main():
     total_points = per * ws
     st = np.mean(np.array(stages), axis=0)
     tag = "%s_%d_z%d-%d" % (args.kind, per, args.zmin, args.zmax)
-    traffic, traffic_src = profile_traffic(tag)
-    alg_step = ALG_BYTES_PER_POINT * per + ALG_BYTES_PER_CELL * (cells // ws)      # one rank's step
+    traffic, traffic_src, fp64 = profile_traffic(tag)
+    peak_meas = measured_peak(torch)
+    alg_step = ALG_BYTES_PER_POINT * per + ALG_BYTES_PER_CELL * cells_rank      # one rank's step
     achieved = alg_step / (step_ms_ev * 1e-3) / 1e9
     kernels = {
         "k_project_partition": {"us": float(st[0]), "alg_bytes": ALG_BYTES_PER_POINT * per,
@@ -242,10 +354,15 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "hm_count step (all pipeline kernels, one rank)",
                      "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "traffic_source": traffic_src, "avg_launch_us": step_ms_ev * 1e3,
-                     "alg_bytes_per_launch": alg_step, "cells_per_step": cells // ws},
+                     "alg_bytes_per_launch": alg_step, "cells_per_step": cells_rank,
+                     "measured_peak": {"GBps": peak_meas, "frac": achieved / peak_meas,
+                                       "how": "torch device copy of 4 GiB, (read + write bytes) / time, best of 5"},
+                     "fp64": fp64},
         "kernels": kernels,
         "pipeline": {"slow_path_points": ctx.last_stats()[0], "check": check},
     }
+    if dist_info is not None:
+        out["distributed"] = dist_info
     if rank == 0:
         out["cpu_baseline"] = cpu_baseline(args, lat, lon)
         print(json.dumps(out), flush=True)

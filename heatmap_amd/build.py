@@ -19,7 +19,8 @@ CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libheatmap_amd.so")
 SOURCES = ["hm_kernels.hip", "hm_general.hip", "hm_stream.hip", "hm_merge.hip", "hm_api.cpp"]
-HEADERS = ["hm_common.h", "hm_device.h", "hm_glibc_emul.h", "hm_project.h", "hm_pipeline.h", "hm_ytab.h", "hm_table.h"]
+HEADERS = ["hm_common.h", "hm_device.h", "hm_glibc_emul.h", "hm_branred.h", "hm_project.h", "hm_pipeline.h",
+           "hm_ytab.h", "hm_table.h"]
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
 FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=" + ARCH,
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unknown-pragmas",
@@ -44,14 +45,17 @@ def build(force: bool = False, verbose: bool = True, out: str = None, defines=()
         return LIB
     os.makedirs(os.path.dirname(lib), exist_ok=True)
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-    objs = []
-    for src in SOURCES:
+    objs, procs = [], []
+    for src in SOURCES:   # the translation units compile in parallel
         obj = os.path.join(os.path.dirname(lib), os.path.basename(lib) + "." + src.rsplit(".", 1)[0] + ".o")
         cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(src_dir, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
-        subprocess.check_call(cmd)
+        procs.append((subprocess.Popen(cmd), cmd))
         objs.append(obj)
+    for p, cmd in procs:
+        if p.wait() != 0:
+            raise subprocess.CalledProcessError(p.returncode, cmd)
     cmd = [hipcc, "--offload-arch=" + ARCH, "-shared", "-fPIC", *objs, "-o", lib + ".tmp"]
     if verbose:
         print(" ".join(cmd), flush=True)

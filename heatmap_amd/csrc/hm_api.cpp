@@ -41,6 +41,9 @@ struct Level {
 
 }  // namespace
 
+#define HM_SPREAD_MIN_KEYS (1u << 19)
+#define HM_SPREAD_ZOOMS 3
+
 /* per-call stage events: [0..4] stage boundaries, [5..] pairs around the
  * level >= 2 partition launches */
 #define HM_NEV 12
@@ -58,6 +61,10 @@ struct hm_ctx {
     int64_t last_slow = 0;
     double stage_us[8] = {0};
     hipEvent_t ev[HM_NEV];
+    /* plan-tuning knobs, read once from the environment at hm_ctx_create
+     * (INTEGRATION.md): HM_SPREAD_MIN_KEYS, HM_RS_BIG_MIN */
+    double spread_min_keys = 0;
+    uint64_t rs_big_min = 0;
 };
 
 enum {
@@ -169,6 +176,10 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     c->stream = (hipStream_t)stream;
     c->bufs.resize(B_COUNT);
     for (int i = 0; i < HM_NEV; i++) c->ev[i] = nullptr;
+    c->spread_min_keys = HM_SPREAD_MIN_KEYS;
+    if (const char* e = getenv("HM_SPREAD_MIN_KEYS")) c->spread_min_keys = atof(e);
+    c->rs_big_min = HM_RS_BIG;
+    if (const char* e = getenv("HM_RS_BIG_MIN")) c->rs_big_min = (uint64_t)atoll(e);
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -431,9 +442,7 @@ static int count_fallback(hm_ctx* ctx, const double* lat, const double* lon, con
  * when level 1's sampled histogram is flat -- no digit above 4x the mean --
  * and the mean level-1 bucket holds >= HM_SPREAD_MIN_KEYS keys; the
  * environment variable of that name overrides the threshold). */
-#define HM_SPREAD_MIN_KEYS (1u << 19)
-#define HM_SPREAD_ZOOMS 3
-static void spread_replan(const uint32_t* h, int F, int64_t n, int zb, int* zs, int* L)
+static void spread_replan(const uint32_t* h, int F, int64_t n, int zb, int* zs, int* L, double min_keys)
 {
     uint64_t tot = 0, mx = 0;
     int ne = 0;
@@ -442,8 +451,6 @@ static void spread_replan(const uint32_t* h, int F, int64_t n, int zb, int* zs, 
         mx = std::max<uint64_t>(mx, h[i]);
         ne += h[i] != 0;
     }
-    double min_keys = HM_SPREAD_MIN_KEYS;
-    if (const char* e = getenv("HM_SPREAD_MIN_KEYS")) min_keys = atof(e);
     if (ne == 0 || (double)n < min_keys * ne || (double)mx * ne > 4.0 * (double)tot) return;
     int step = HM_SPREAD_ZOOMS;
     while (zs[0] + step * (HM_MAX_LEVELS - 1) < zb) step++;
@@ -723,7 +730,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             if ((st = read_state(ctx))) return st;
             /* levels 2.. may take the spread plan (the level-1 pass is the
              * same under both: its output is u32 keys whenever L > 1) */
-            if (L > 1) spread_replan(ctx->host_aux, F, n, zb, zs, &L);
+            if (L > 1) spread_replan(ctx->host_aux, F, n, zb, zs, &L, ctx->spread_min_keys);
             ctx->last_levels = L;
             V.count = (uint32_t)(down[0] >> 32);
             V.items = (uint32_t)(down[0] & 0xFFFFFFFFull);
@@ -834,8 +841,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ra.excl = excl;
         ENSURE(B_RS_BIG, (HM_RS_BIG_MAX + 1) * sizeof(uint32_t), ra.big);
         ra.nbig = ra.big + HM_RS_BIG_MAX;
-        ra.big_min = HM_RS_BIG;
-        if (const char* e = getenv("HM_RS_BIG_MIN")) ra.big_min = (uint64_t)atoll(e);
+        ra.big_min = ctx->rs_big_min;
         HIPCHK(hipMemsetAsync(ra.nbig, 0, sizeof(uint32_t), s));
         hm_launch_rs_copy(s, ra);
         hm_launch_scan(s, ra.cnt, nflat, partial, excl, tot + 1);

@@ -335,7 +335,7 @@ def cells_to_table(cells: Cells):
 
     d = cells.delta
     if len(cells) == 0:
-        return pa.table({"id": pa.array([], pa.string()), "heatmap": pa.array([], pa.string())})
+        return pa.table({"id": pa.array([], pa.large_string()), "heatmap": pa.array([], pa.large_string())})
     tz, tr, tc = cells.zoom - d, cells.row >> d, cells.col >> d
     o = np.lexsort((cells.col, cells.row, cells.zoom, tc, tr, tz, cells.span, cells.label))
     lab, sp, z, r, c, v = cells.label[o], cells.span[o], cells.zoom[o], cells.row[o], cells.col[o], cells.value[o]
@@ -344,26 +344,29 @@ def cells_to_table(cells: Cells):
     head[1:] = ((lab[1:] != lab[:-1]) | (sp[1:] != sp[:-1]) | (tz[1:] != tz[:-1]) | (tr[1:] != tr[:-1]) |
                 (tc[1:] != tc[:-1]))
     starts = np.flatnonzero(head)
-    s = lambda a: pc.cast(pa.array(a), pa.string())  # noqa: E731
+    s = lambda a: pc.cast(pa.array(a), pa.large_string())  # noqa: E731
+    t = lambda x: pa.scalar(x, pa.large_string())  # noqa: E731
     # float repr of integer-valued counts below 1e16 is "<int>.0"; others via repr
     vi = v.astype(np.int64)
     small = (v == vi) & (np.abs(v) < 1e16)
-    vs = pc.binary_join_element_wise(s(vi), pa.scalar(".0"), "")
+    vs = pc.binary_join_element_wise(s(vi), t(".0"), t(""))
     if not small.all():
         vs = vs.to_pylist()
         for i in np.flatnonzero(~small).tolist():
             vs[i] = repr(float(v[i]))
-        vs = pa.array(vs, pa.string())
-    bins = pc.binary_join_element_wise(s(z), s(r), s(c), "_")
-    pieces = pc.binary_join_element_wise(pa.scalar('"'), bins, pa.scalar('": '), vs, "")
-    offsets = np.append(starts, lab.size).astype(np.int32)
-    joined = pc.binary_join(pa.ListArray.from_arrays(pa.array(offsets), pieces), ", ")
-    heat = pc.binary_join_element_wise(pa.scalar("{"), joined, pa.scalar("}"), "")
-    names = pa.array(cells.labels, pa.string()).take(pa.array(lab[starts]))
-    spans = pa.array(cells.spans, pa.string()).take(pa.array(sp[starts]))
+        vs = pa.array(vs, pa.large_string())
+    bins = pc.binary_join_element_wise(s(z), s(r), s(c), t("_"))
+    pieces = pc.binary_join_element_wise(t('"'), bins, t('": '), vs, t(""))
+    # 64-bit offsets throughout: a batch can hold more than 2^31 bins or 2 GiB
+    # of JSON text (int32 offsets would wrap silently)
+    offsets = np.append(starts, lab.size).astype(np.int64)
+    joined = pc.binary_join(pa.LargeListArray.from_arrays(pa.array(offsets, pa.int64()), pieces), t(", "))
+    heat = pc.binary_join_element_wise(t("{"), joined, t("}"), t(""))
+    names = pa.array(cells.labels, pa.large_string()).take(pa.array(lab[starts]))
+    spans = pa.array(cells.spans, pa.large_string()).take(pa.array(sp[starts]))
     ids = pc.binary_join_element_wise(names, spans,
-                                      pc.binary_join_element_wise(s(tz[starts]), s(tr[starts]), s(tc[starts]), "_"),
-                                      KEY_SEPERATOR)
+                                      pc.binary_join_element_wise(s(tz[starts]), s(tr[starts]), s(tc[starts]), t("_")),
+                                      t(KEY_SEPERATOR))
     return pa.table({"id": ids, "heatmap": heat})
 
 

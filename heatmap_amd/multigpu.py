@@ -150,7 +150,8 @@ def merge_exotic(cells: torch.Tensor, ws: int, rank: int) -> torch.Tensor:
     return torch.cat([u, tot[:, None]], 1)
 
 
-def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, dense_zmax: int = 10):
+def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, dense_zmax: int = 10,
+                    merge_ms=None):
     """Run `steps` count + merge steps with step k's merge overlapping step
     k+1's count: count(buffers) -> (m, buffers) runs on the calling thread
     (its hm context, the current stream); merge_cells runs on a helper thread
@@ -158,9 +159,11 @@ def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, de
     collectives (in step order, as on every rank).  bufsets: >= 2 CountBuffers
     used in turn; a set is counted into again only after its merge finished.
     Returns (cells owned after the last merge, per-step stage timings of the
-    counts, the last step's buffers)."""
+    counts, the last step's buffers); merge_ms (a list): each merge's host
+    time on the merge thread is appended."""
     import queue
     import threading
+    import time
 
     todo, free = queue.Queue(), queue.Queue()
     for b in bufsets:
@@ -176,8 +179,11 @@ def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, de
                     if item is None:
                         return
                     m, b = item
+                    t0 = time.perf_counter()
                     owned.append(merge_cells(b, m, ws, rank, dense_zmax))
                     side.synchronize()
+                    if merge_ms is not None:
+                        merge_ms.append((time.perf_counter() - t0) * 1e3)
                     last[0] = b
                     free.put(b)
         except BaseException as e:   # surfaced on the calling thread
@@ -222,6 +228,14 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)
     rl = recv.tolist()
+    # the owned cells are at most the received ones plus (rank 0) the dense
+    # grid's: grow this rank's buffers first (a local decision -- a rank that
+    # raised here instead would leave its peers blocked in the next collective)
+    need = sum(rl) + (grid.numel() if dense_zmax >= 0 and rank == 0 else 0)
+    if need > buffers.keys.numel():
+        buffers.keys = torch.empty(need, dtype=torch.int64, device=keys.device)
+        buffers.counts = torch.empty_like(buffers.keys)
+        buffers.capacity = need
     nk = torch.empty(sum(rl), dtype=torch.int64, device=keys.device)
     nc = torch.empty_like(nk)
     dist.all_to_all_single(nk, sk, rl, sent)
@@ -245,8 +259,6 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         k = torch.cat(parts_k)
         c = torch.cat(parts_c)
         n = k.numel()
-        if n > buffers.keys.numel():
-            raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (n, buffers.keys.numel()))
         buffers.keys[:n] = k
         buffers.counts[:n] = c
     nx = int(getattr(buffers, "nx", 0))

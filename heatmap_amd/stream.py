@@ -102,6 +102,7 @@ class StreamingHeatmap:
         self.device_index = device_index
         self.zmin, self.zmax, self.base_hour = int(zmin), int(zmax), int(base_hour)
         self.labels = ["all"]          # group id -> row-key group (0: the literal user id 'all')
+        self._explicit_max = -1        # largest group id passed as group= (those have no label)
         self._index = {"all": 0}
         # cells outside [0, 2^zmax)^2: (group, hour or UNDATED_HOUR, zoom, row, col, count)
         self._x = np.zeros((0, 6), dtype=np.int64)
@@ -159,6 +160,13 @@ class StreamingHeatmap:
             raise ValueError("pass user_id or group, not both")
         if user_id is not None:
             group = self._groups(user_id, keep, n)
+        elif group is not None:
+            # explicit ids: NOGROUP / ALLGROUPS are the table's own markers
+            gmax = int((group.to(torch.int64) & 0xFFFFFFFF).max().item()) if isinstance(group, torch.Tensor) and \
+                group.numel() else (int(np.asarray(group, dtype=np.uint32).max()) if np.size(group) else 0)
+            if gmax >= NOGROUP:
+                raise ValueError("group ids must be < 0x%X (0xFFFFFFFE/0xFFFFFFFF are reserved)" % NOGROUP)
+            self._explicit_max = max(self._explicit_max, gmax)
 
         def u32(x, what):
             if x is None:
@@ -193,8 +201,11 @@ class StreamingHeatmap:
         row = torch.empty(n, dtype=torch.int64, device=la.device)
         col = torch.empty(n, dtype=torch.int64, device=la.device)
         st = torch.empty(n, dtype=torch.uint8, device=la.device)
-        self.ctx.L.hm_project(self.ctx.ptr, device._ptr(la), device._ptr(lo), n, self.zmax, device._ptr(row),
-                              device._ptr(col), device._ptr(st))
+        rc = self.ctx.L.hm_project(self.ctx.ptr, device._ptr(la), device._ptr(lo), n, self.zmax, device._ptr(row),
+                                   device._ptr(col), device._ptr(st))
+        if rc != _lib.HM_OK:      # before anything is inserted: the batch stays atomic
+            idx, kind = self.ctx.last_error()
+            _lib.raise_for(rc, idx)
         lim = 1 << self.zmax
         out = (st == 0) & ((row < 0) | (row >= lim) | (col < 0) | (col >= lim))
         if kp is not None:
@@ -325,6 +336,9 @@ class StreamingHeatmap:
             raise ValueError("rows need zooms %d..%d; the stream holds %d..%d" % (d + 1, mz + d, self.zmin, self.zmax))
         if timespan not in ("alltime", "year", "month", "day"):
             raise ValueError("timespan must be 'alltime', 'year', 'month' or 'day'")
+        if self._explicit_max >= len(self.labels):
+            raise ValueError("rows need a label per group: group id %d was passed as group= and has none "
+                             "(feed the stream with user_id= to build rows)" % self._explicit_max)
         _, ap, az, ar, ac, an = self.rollup(timespan, merge_groups=True)
         gg, gp, gz, gr, gc, gn = self.rollup(timespan, merge_groups=False)
         grouped = gg != NOGROUP
