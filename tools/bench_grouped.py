@@ -1,0 +1,142 @@
+#!/usr/bin/env python3
+"""The row-producing path (reference heatmap.py:64-75,111-112,120-129): per-user
+counts in one device pass (hm_count_grouped) and heatmap_table end to end.
+
+  device   one step = one hm_count_grouped over N device-resident hotspot
+           points, each with one of U user groups (a hash of its index): the
+           exact projection of every point, 128-bit (group, super-tile, Morton)
+           keys, the LSD radix sort and the RLE zoom cascade (hm_general.hip),
+           every (group, zoom, row, col, count) record written to HBM.
+  table    heatmap_table on a host batch of M points with string user ids
+           (factorize, two device passes, combine_cells, pyarrow rows), timed
+           by phase.
+
+    python tools/bench_grouped.py --points 1e8 --users 10000 --zmin 6 --zmax 21
+Prints one JSON line per part.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from heatmap_amd import _lib, device  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0
+
+
+def bench_device(a):
+    n = int(a.points)
+    lat = torch.empty(n, dtype=torch.float64, device="cuda")
+    lon = torch.empty(n, dtype=torch.float64, device="cuda")
+    device.synth(a.kind, lat, lon, seed=a.seed)
+    grp = ((torch.arange(n, device="cuda", dtype=torch.int64) * 2654435761) >> 7) % a.users
+    grp = grp.to(torch.int32)
+    ctx = device.context(0)
+    buf = {"cap": int(a.cap_factor * n) + 1024}
+    buf["cells"] = torch.empty(5 * buf["cap"], dtype=torch.int64, device="cuda")
+    nout = ctypes.c_int64(0)
+    p = device._ptr
+
+    def step():
+        while True:
+            rc = ctx.L.hm_count_grouped(ctx.ptr, p(lat), p(lon), ctypes.c_void_p(0), p(grp), n, a.zmin, a.zmax,
+                                        p(buf["cells"]), buf["cap"], ctypes.byref(nout))
+            if rc != _lib.HM_E_CAPACITY:
+                break
+            buf["cap"] = int(nout.value * 1.05) + 1024      # warm-up only: the timed steps fit
+            buf["cells"] = torch.empty(5 * buf["cap"], dtype=torch.int64, device="cuda")
+        if rc != _lib.HM_OK:
+            _lib.raise_for(rc)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    e0.record()
+    for _ in range(a.steps):
+        step()
+    e1.record()
+    e1.synchronize()
+    dt = time.perf_counter() - t0
+    ms = e0.elapsed_time(e1) / a.steps
+    m = nout.value
+    cells = buf["cells"]
+    tot = int(cells[:5 * m].reshape(-1, 5)[:, 4].sum().item())
+    alg = 16 * n + 4 * n + 40 * m
+    out = {"part": "hm_count_grouped", "value": n / (ms * 1e-3), "unit": "points/s", "ms_per_step": ms,
+           "host_ms_per_step": dt * 1e3 / a.steps, "points": n, "users": a.users, "kind": a.kind,
+           "zooms": [a.zmin, a.zmax], "records": m,
+           "check": "ok" if tot == n * (a.zmax - a.zmin + 1) else "FAIL sum %d" % tot,
+           "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved_GBps": alg / (ms * 1e-3) / 1e9,
+                        "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                        "alg_bytes_note": "16 B lat/lon + 4 B group per point read, 40 B per output record"}}
+    print(json.dumps(out), flush=True)
+    del lat, lon, grp, cells
+    torch.cuda.empty_cache()
+
+
+def bench_table(a):
+    from heatmap_amd import heatmap as hm
+    from heatmap_amd import synth
+
+    n = int(a.table_points)
+    lat, lon = synth.generate(a.kind, n, seed=a.seed)
+    g = ((np.arange(n, dtype=np.int64) * 2654435761) >> 7) % a.users
+    names = np.array(["u%d" % i for i in range(a.users)], dtype=object)
+    user = names[g]
+    user[g % 7 == 3] = "x-anon"          # 'x*' ids: counted in 'all' only (heatmap.py:64-70)
+    keep = (np.arange(n) % 5 != 2)       # background rows (heatmap.py:28-29)
+    ph = {}
+    hm.heatmap_table(lat[:10000], lon[:10000], user[:10000], keep[:10000], a.zmax - 5, 5)   # warm-up
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    plan = hm.group_plan(user, keep)
+    ph["group_plan"] = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    c = device.count(lat, lon, keep.astype(np.uint8), 6, a.zmax)
+    ph["count_all (device + copy)"] = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    gc = device.count_grouped(lat, lon, plan.gid, plan.grouped.astype(np.uint8), 6, a.zmax)
+    ph["count_grouped (device + copy)"] = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    cells = hm.combine_cells(plan.labels, (c.zoom, c.row, c.col, c.count),
+                             (gc.group, gc.zoom, gc.row, gc.col, gc.count), a.zmax, 5)
+    ph["combine_cells"] = time.perf_counter() - t1
+    t1 = time.perf_counter()
+    tab = hm.cells_to_table(cells)
+    ph["cells_to_table"] = time.perf_counter() - t1
+    tot = time.perf_counter() - t0
+    print(json.dumps({"part": "heatmap_table", "value": n / tot, "unit": "points/s", "seconds": tot,
+                      "points": n, "users": a.users, "rows": tab.num_rows, "bins": len(cells),
+                      "detail_zooms": [6, a.zmax], "phases_s": ph}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--points", type=float, default=1e8)
+    ap.add_argument("--table-points", type=float, default=1e7)
+    ap.add_argument("--users", type=int, default=10000)
+    ap.add_argument("--kind", default="hotspots")
+    ap.add_argument("--zmin", type=int, default=6)
+    ap.add_argument("--zmax", type=int, default=21)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--cap-factor", type=float, default=2.0, help="first record capacity per point")
+    ap.add_argument("--no-table", action="store_true")
+    a = ap.parse_args()
+    bench_device(a)
+    if not a.no_table:
+        bench_table(a)
+
+
+if __name__ == "__main__":
+    main()
