@@ -24,10 +24,10 @@ HM_E_CAPACITY = 17
 HM_E_HIP = 18
 HM_E_NOMEM = 19
 HM_COUNT_MAX_ZOOM = 21
-HM_ABI_VERSION = 3
+HM_ABI_VERSION = 4
 HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4
 
-EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy",
+EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy", "hm_ctx_tune",
            "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
@@ -82,6 +82,7 @@ def load() -> ctypes.CDLL:
         L.hm_ctx_create.argtypes = [P(vp), c.c_int, vp]
         L.hm_ctx_set_stream.argtypes = [vp, vp]
         L.hm_ctx_destroy.argtypes = [vp]
+        L.hm_ctx_tune.argtypes = [vp, c.c_char_p, c.c_double, P(c.c_double)]
         L.hm_project.argtypes = [vp, vp, vp, c.c_int64, c.c_int, vp, vp, vp]
         L.hm_count.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64),
                                vp, c.c_int64, P(c.c_int64)]

@@ -65,6 +65,11 @@ struct hm_ctx {
      * (INTEGRATION.md): HM_SPREAD_MIN_KEYS, HM_RS_BIG_MIN */
     double spread_min_keys = 0;
     uint64_t rs_big_min = 0;
+    /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
+     * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
+    int hot = 1;
+    double hot_inv_share = 2048;
+    double hot_min_keys = 65536;
 };
 
 enum {
@@ -77,6 +82,7 @@ enum {
     ST_REDO_OUT = 6,
     ST_XCURSOR = 7,
     ST_OVERFLOW = 8,
+    ST_NHOT = 9,          /* hot tiles of this call (k_hot_select; low 32 bits) */
     ST_COUNT = 16
 };
 
@@ -108,6 +114,7 @@ enum {
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
+    B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B,
     B_COUNT
 };
 
@@ -180,6 +187,9 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     if (const char* e = getenv("HM_SPREAD_MIN_KEYS")) c->spread_min_keys = atof(e);
     c->rs_big_min = HM_RS_BIG;
     if (const char* e = getenv("HM_RS_BIG_MIN")) c->rs_big_min = (uint64_t)atoll(e);
+    if (const char* e = getenv("HM_HOT")) c->hot = atoi(e);
+    if (const char* e = getenv("HM_HOT_INV_SHARE")) c->hot_inv_share = atof(e);
+    if (const char* e = getenv("HM_HOT_MIN_KEYS")) c->hot_min_keys = atof(e);
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -187,7 +197,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     } else if (hipHostMalloc(&c->host_state, 4 * ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->host_state = nullptr;
         st = HM_E_NOMEM;
-    } else if (hipHostMalloc(&c->host_aux, (2 + 2 * HM_L1_SHARDS) * HM_MAX_F1 * sizeof(uint32_t)) != hipSuccess) {
+    } else if (hipHostMalloc(&c->host_aux, (2 + 2 * HM_L1_SHARDS) * HM_D1 * sizeof(uint32_t)) != hipSuccess) {
         c->host_aux = nullptr;
         st = HM_E_NOMEM;
     }
@@ -209,6 +219,33 @@ int hm_ctx_set_stream(hm_ctx* c, void* stream)
 {
     if (!c) return HM_E_ARG;
     c->stream = (hipStream_t)stream;
+    return HM_OK;
+}
+
+int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
+{
+    if (!c || !name) return HM_E_ARG;
+    double prev;
+    if (!strcmp(name, "HM_SPREAD_MIN_KEYS")) {
+        prev = c->spread_min_keys;
+        c->spread_min_keys = value;
+    } else if (!strcmp(name, "HM_RS_BIG_MIN")) {
+        prev = (double)c->rs_big_min;
+        c->rs_big_min = (uint64_t)(value < 0 ? 0 : value);
+    } else if (!strcmp(name, "HM_HOT")) {
+        prev = c->hot;
+        c->hot = value != 0;
+    } else if (!strcmp(name, "HM_HOT_INV_SHARE")) {
+        if (!(value >= 1)) return HM_E_ARG;
+        prev = c->hot_inv_share;
+        c->hot_inv_share = value;
+    } else if (!strcmp(name, "HM_HOT_MIN_KEYS")) {
+        prev = c->hot_min_keys;
+        c->hot_min_keys = value;
+    } else {
+        return HM_E_ARG;
+    }
+    if (old) *old = prev;
     return HM_OK;
 }
 
@@ -529,6 +566,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     int npart = 0;              /* level >= 2 partition launches timed (ev[5..]) */
 
     uint32_t* seg1 = nullptr;   /* level-1 items' run tables (k_partition_fr) */
+    bool hot_on = false;        /* hot tiles sampled and looked up by level 1 */
+    uint32_t nhot = 0;          /* hot tiles found */
+    HmHotRunArgs hr;            /* hot tiles as level-2 children */
+    memset(&hr, 0, sizeof(hr));
     for (int l = 0; l < L; l++) {
         Level& V = lv[l];
         V.zc = zs[l];
@@ -541,14 +582,18 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         if (l == 0) {
             /* ---- level 1: projection + partition into per-digit regions ---- */
             const int F = 1 << V.dbits;
-            const int FS = F * HM_L1_SHARDS;
+            /* digit slots: F cold digits, hot tile h at HM_MAX_F1 + h */
+            const int FS = HM_D1 * HM_L1_SHARDS;
             uint32_t *fill, *rbase, *rcap, *hist;
             uint8_t* smask;
             ENSURE(B_L1_FILL, FS * 4, fill);
             ENSURE(B_L1_RBASE, FS * 4, rbase);
             ENSURE(B_L1_RCAP, FS * 4, rcap);
-            ENSURE(B_L1_HIST, F * 4, hist);
-            ENSURE(B_L1_SMASK, F, smask);
+            ENSURE(B_L1_HIST, HM_D1 * 4, hist);
+            ENSURE(B_L1_SMASK, HM_D1, smask);
+            /* hot tiles need the two-level plan (level 1 at z1, the last at
+             * zb), a dense zoom-zb sample histogram of <= 4^11 tiles */
+            hot_on = ctx->hot && L == 2 && zb <= 11 && zs[0] == HM_Z1 && n > 0 && V.dbits == 2 * HM_Z1;
             uint32_t* redo_idx = nullptr;
             int64_t *redo_rows = nullptr, *redo_cols = nullptr;
             if (!from_tiles) {
@@ -581,21 +626,63 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             /* region sizes: a sampled digit histogram with a generous margin */
             /* ~256K samples below 2^28 points (launch-bound batches), ~1M above */
             const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> ((uint64_t)n < (1ull << 28) ? 18 : 20));
-            HIPCHK(hipMemsetAsync(hist, 0, F * 4, s));
-            if (n > 0) hm_launch_sample_digits(s, a, stride, hist);
+            HIPCHK(hipMemsetAsync(hist, 0, HM_D1 * 4, s));
+            uint32_t* hot_counts = nullptr;
+            uint32_t* hot_tiles = nullptr;
+            uint32_t* hot_hash = nullptr;
+            uint8_t* hot_parent = nullptr;
+            uint32_t* hot_n = (uint32_t*)(ctx->state + ST_NHOT);
+            if (hot_on) {
+                ENSURE(B_HOT_COUNTS, (4ull << (2 * zb)), hot_counts);
+                ENSURE(B_HOT, (HM_MAX_HOT + HM_HOT_SLOTS) * 4, hot_tiles);
+                ENSURE(B_HOT_PARENT, HM_MAX_F1, hot_parent);
+                hot_hash = hot_tiles + HM_MAX_HOT;
+                HIPCHK(hipMemsetAsync(hot_counts, 0, 4ull << (2 * zb), s));
+                HIPCHK(hipMemsetAsync(hot_parent, 0, HM_MAX_F1, s));
+                a.hot_z = zb;
+                a.hot_hash = hot_hash;
+                a.hot_n = hot_n;
+            } else {
+                a.hot_z = -1;
+            }
+            if (n > 0) hm_launch_sample_digits(s, a, stride, hist, hot_counts);
             HIPCHK(hipGetLastError());
+            if (hot_on) {
+                hr.tiles = hot_tiles;
+                hr.n = hot_n;
+                hr.zb = zb;
+                hr.z1 = zs[0];
+                hr.fill = fill;
+                hr.rbase = rbase;
+                HmHotArgs ha;
+                ha.counts = hot_counts;
+                ha.zb = zb;
+                ha.z1 = zs[0];
+                const uint64_t m = ((uint64_t)n + stride - 1) / stride;
+                ha.thresh = (uint32_t)std::max<double>(
+                    {1.0, ceil((double)m / ctx->hot_inv_share), ceil(ctx->hot_min_keys / (double)stride)});
+                ha.tiles = hot_tiles;
+                ha.hist = hist;
+                ha.hotparent = hot_parent;
+                ha.n = hot_n;
+                ha.hash = hot_hash;
+                hm_launch_hot_select(s, ha);
+                HIPCHK(hipGetLastError());
+            }
             /* pinned host scratch (the overflow retry): caps [FS] | bases [FS] */
-            uint32_t* hc = ctx->host_aux + HM_MAX_F1;
-            uint32_t* hb = hc + HM_MAX_F1 * HM_L1_SHARDS;
+            uint32_t* hc = ctx->host_aux + HM_D1;
+            uint32_t* hb = hc + HM_D1 * HM_L1_SHARDS;
             /* the region sizes are computed on the device (k_l1_sizes); the key
              * buffer takes the host's bound of their total: est sums to at
-             * most nn, at most M (digit, shard) entries are non-empty, and
-             * sum sqrt(e stride) <= sqrt(M nn stride) (Cauchy-Schwarz) */
-            const double nn = (double)n + (double)F * (double)stride;
-            const double M = F + std::min((double)F, nn / (64.0 * HM_T1)) * (HM_L1_SHARDS - 1);
+             * most nn (a hot tile's samples leave its cold digit), at most M
+             * (digit, shard) entries are non-empty, and sum sqrt(e stride) <=
+             * sqrt(M nn stride) (Cauchy-Schwarz) */
+            const double nn = (double)n + (double)(F + (hot_on ? HM_MAX_HOT : 0)) * (double)stride;
+            const double M = F + std::min((double)F, nn / (64.0 * HM_T1)) * (HM_L1_SHARDS - 1) +
+                             (hot_on ? (double)HM_MAX_HOT * HM_L1_SHARDS : 0.0);
             const double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 + 1024.0;
             if (bound >= (double)0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
-            hm_launch_l1_sizes(s, hist, F, stride, rcap, rbase, smask);
+            hm_launch_l1_sizes(s, hist, F, hot_on ? hot_n : nullptr, stride, rcap, rbase, smask);
             HIPCHK(hipGetLastError());
             void* kout = nullptr;
             uint64_t total_cap = (uint64_t)bound;
@@ -612,6 +699,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 }
                 ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (total_cap + 8) * (V.out16 ? 2 : 4), kout);
                 a.keys_out = kout;
+                if (hot_on) {
+                    /* hot keys: u16, straight into the last level's key array
+                     * (level 2 writes the cold keys' positions of it) */
+                    void* kh = nullptr;
+                    ENSURE(slot_k ? B_KEYS_A : B_KEYS_B, (total_cap + 8) * 2, kh);
+                    a.keys_hot = kh;
+                }
                 HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
                 HIPCHK(hipMemsetAsync(ctx->state + ST_OVERFLOW, 0, 8, s));
                 HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, 16, s));   /* ST_REDO, ST_REDO_OUT */
@@ -715,6 +809,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             ba.item_keys = (L == 1) ? HM_TA : HM_TN;
             ba.sparse_max = (L == 1) ? HM_SP_MAX : 0u;
             ba.total = tot;
+            nhot = hot_on ? (uint32_t)(ctx->host_state[ST_NHOT] & 0xFFFFFFFFull) : 0u;
+            if (nhot) {
+                uint32_t* d2b;
+                ENSURE(B_D2B, HM_MAX_F1 * 4, d2b);
+                ba.hotparent = hr.tiles ? (const uint8_t*)ctx->bufs[B_HOT_PARENT].p : nullptr;
+                ba.d2b = d2b;
+                hr.d2b = d2b;
+            }
             if (L == 1) {
                 ENSURE(B_SLOTS, cap * 4, slots);
                 ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
@@ -730,7 +832,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             if ((st = read_state(ctx))) return st;
             /* levels 2.. may take the spread plan (the level-1 pass is the
              * same under both: its output is u32 keys whenever L > 1) */
-            if (L > 1) spread_replan(ctx->host_aux, F, n, zb, zs, &L, ctx->spread_min_keys);
+            if (L > 1 && !nhot) spread_replan(ctx->host_aux, F, n, zb, zs, &L, ctx->spread_min_keys);
             ctx->last_levels = L;
             V.count = (uint32_t)(down[0] >> 32);
             V.items = (uint32_t)(down[0] & 0xFFFFFFFFull);
@@ -825,6 +927,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
         ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
         hm_launch_rs_count(s, ra);
+        const bool hot_level = nhot && l == 1;   /* hot tiles are children of level 2 */
+        if (hot_level) {
+            hr.dbits = V.dbits;
+            hr.nr = ra.nr;
+            hm_launch_hot_nr(s, hr);
+        }
         hm_launch_scan(s, ra.nr, V.nchildren, partial, runbase, tot + 0);
         HIPCHK(hipGetLastError());
         unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
@@ -844,6 +952,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ra.big_min = ctx->rs_big_min;
         HIPCHK(hipMemsetAsync(ra.nbig, 0, sizeof(uint32_t), s));
         hm_launch_rs_copy(s, ra);
+        if (hot_level) {
+            hr.runbase = runbase;
+            hr.flat = flat;
+            hr.cnt = ra.cnt;
+            hm_launch_hot_runs(s, hr);
+        }
         hm_launch_scan(s, ra.cnt, nflat, partial, excl, tot + 1);
         ra.total_keys = tot + 1;
         uint32_t* cnkeys;
@@ -1005,6 +1119,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         (void)hipEventElapsedTime(&ms, ev[5 + 2 * (l - 1)], ev[6 + 2 * (l - 1)]);
         ctx->stage_us[4] += ms * 1000.0;
     }
+    ctx->stage_us[6] = (double)nhot;   /* hm_last_stats: hot tiles of the call */
     const unsigned long long nc = ctx->host_state[ST_CURSOR];
     *n_out = (int64_t)nc;
     /* cells outside the square: the general path over the exotic list */

@@ -113,16 +113,27 @@ __device__ __forceinline__ void hm_exotic_append(const HmExotic& x, bool p, int6
 template <typename OutT, int MODE, bool FULL>
 __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partition(HmPart1Args a)
 {
-    __shared__ uint32_t cur[HM_MAX_F1 + 64];   /* + 64 dummy words (hm_lds_count) */
-    __shared__ OutT stage[HM_T1 + 64];
-    /* digit of each staged key, and per digit (region position - stage offset) */
-    __shared__ uint16_t sdig[HM_T1 + 64];
-    __shared__ uint32_t dbase[HM_MAX_F1];
+    __shared__ uint32_t cur[HM_D1 + 64];   /* + 64 dummy words (hm_lds_count) */
+    /* the staged keys; until the projection is done it holds the hot-tile hash */
+    __shared__ __attribute__((aligned(16))) OutT stage[HM_T1 + 64];
+    /* digit of each staged key; until the count is done it holds each
+     * digit's region (base, capacity << 1 | sharded) for this tile */
+    __shared__ __attribute__((aligned(8))) uint16_t sdig[HM_T1 + 64];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
+    /* the projection's polynomial table; after the projection it holds, per
+     * digit, (region position - stage offset) */
     __shared__ double tab[HM_YTAB_N];
+    static_assert(sizeof(OutT) * HM_T1 >= HM_HOT_SLOTS * 4, "the hot-tile hash lives in the stage");
+    static_assert(sizeof(double) * HM_YTAB_N >= HM_D1 * 4, "dbase lives in the polynomial table");
+    uint32_t* const hsh = (uint32_t*)stage;
+    uint32_t* const dbase = (uint32_t*)tab;
+    uint2* const rinfo = (uint2*)sdig;
+    static_assert(sizeof(uint16_t) * HM_T1 >= HM_D1 * sizeof(uint2), "region info lives in sdig");
     constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
+    /* hot tiles of this call (block-uniform; the count is an L2-hot word) */
+    const uint32_t H = a.hot_z >= 0 ? *a.hot_n : 0u;
     const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;   /* first input point */
     /* the resolved-redo launch is sized for the list's capacity; its length
      * is read here (no host round trip) */
@@ -169,17 +180,28 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
      * both candidates are fetched and the mask picks one later.  (Waiting for
      * the mask before the dependent loads would wait for every point load
      * issued before it.) */
-    constexpr int PERD = HM_MAX_F1 / HM_P1_THREADS;
+    constexpr int PERD = HM_D1 / HM_P1_THREADS;
+    static_assert(HM_D1 % HM_P1_THREADS == 0, "digit slots per thread");
+    /* digit slot d is live: a cold digit (d < F) or one of the H hot tiles */
+    auto live = [&](int d) { return d < F || (d >= HM_MAX_F1 && (uint32_t)(d - HM_MAX_F1) < H); };
     uint32_t smk[PERD], rcap2[PERD][2], rbase2[PERD][2];
 #pragma unroll
     for (int q = 0; q < PERD; q++) {
         const int d = tid * PERD + q;
         const uint32_t s0 = (uint32_t)d * HM_L1_SHARDS, s1 = s0 + (blockIdx.x & (HM_L1_SHARDS - 1));
-        smk[q] = d < F ? a.smask[d] : 0u;
-        rcap2[q][0] = d < F ? a.rcap[s0] : 0u;
-        rcap2[q][1] = d < F ? a.rcap[s1] : 0u;
-        rbase2[q][0] = d < F ? a.rbase[s0] : 0u;
-        rbase2[q][1] = d < F ? a.rbase[s1] : 0u;
+        const bool lv = live(d);
+        smk[q] = lv ? a.smask[d] : 0u;
+        rcap2[q][0] = lv ? a.rcap[s0] : 0u;
+        rcap2[q][1] = lv ? a.rcap[s1] : 0u;
+        rbase2[q][0] = lv ? a.rbase[s0] : 0u;
+        rbase2[q][1] = lv ? a.rbase[s1] : 0u;
+    }
+    /* the hot-tile hash, also ahead of the points (stored to LDS below) */
+    constexpr int HPT = HM_HOT_SLOTS / HM_P1_THREADS;
+    uint32_t hv[HPT];
+    if (H) {
+#pragma unroll
+        for (int q = 0; q < HPT; q++) hv[q] = a.hot_hash[q * HM_P1_THREADS + tid];
     }
     __builtin_amdgcn_sched_barrier(0);
     /* issue every load of the tile before any arithmetic: 16 points x 16 B per
@@ -228,7 +250,19 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         }
     }
     /* LDS set-up after the loads are issued */
-    for (int i = tid; i < F; i += HM_P1_THREADS) cur[i] = 0;
+    for (int i = tid; i < HM_D1; i += HM_P1_THREADS) cur[i] = 0;
+    /* this tile's region of each digit: the registers are free again for
+     * the projection, the count reads it back */
+#pragma unroll
+    for (int q = 0; q < PERD; q++) {
+        const int d = tid * PERD + q;
+        const uint32_t sh = smk[q] != 0;
+        rinfo[d] = make_uint2(sh ? rbase2[q][1] : rbase2[q][0], ((sh ? rcap2[q][1] : rcap2[q][0]) << 1) | sh);
+    }
+    if (H) {
+#pragma unroll
+        for (int q = 0; q < HPT; q++) hsh[q * HM_P1_THREADS + tid] = hv[q];
+    }
     if (!FROM_TILES) {
 #pragma unroll
         for (int q = 0; q < TPT; q++) {
@@ -238,15 +272,6 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     }
     __syncthreads();
     if (MODE == 0) HM_STAMP_M(2, 1);
-    uint32_t slot[PERD], rcap[PERD], rbase[PERD];
-#pragma unroll
-    for (int q = 0; q < PERD; q++) {
-        const int d = tid * PERD + q;
-        const int hot = smk[q] != 0;
-        slot[q] = (uint32_t)d * HM_L1_SHARDS + (hot ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u);
-        rcap[q] = hot ? rcap2[q][1] : rcap2[q][0];
-        rbase[q] = hot ? rbase2[q][1] : rbase2[q][0];
-    }
     /* fast path for every point, branch-free; points the fast path cannot
      * settle (guard band, polar/out-of-range/non-finite input) are marked in
      * `redo` and resolved afterwards in one ballot-guarded pass */
@@ -340,6 +365,31 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         const uint32_t ws = hm_wave_sum((uint32_t)nslow);
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
+    if (H) {
+        /* points in a hot tile: digit HM_MAX_F1 + h, key = the zoom-Z offset
+         * inside the tile (u16); the tile is found in the LDS hash */
+        const int hs = a.Z - a.hot_z;                 /* offset bits per coordinate */
+        const uint32_t hm = (1u << hs) - 1u;
+        const uint32_t wm = (1u << wd) - 1u;
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT; k++) {
+            const bool v = dig[k] != 0xFFFFFFFFu;
+            const uint32_t r = ((dig[k] >> wd) << hb) | (rest[k] >> hb);
+            const uint32_t c = ((dig[k] & wm) << hb) | (rest[k] & lowm);
+            const uint32_t t = ((r >> hs) << a.hot_z) | (c >> hs);
+            uint32_t slot = (t * 2654435761u) >> (32 - 11);
+            static_assert(HM_HOT_SLOTS == 1 << 11, "hash slots");
+            uint32_t e = hsh[slot];
+            while (v && e != HM_HOT_EMPTY && (e >> 10) != t) {
+                slot = (slot + 1) & (HM_HOT_SLOTS - 1);
+                e = hsh[slot];
+            }
+            if (v && e != HM_HOT_EMPTY) {
+                dig[k] = HM_MAX_F1 + (e & 1023u);
+                rest[k] = ((r & hm) << hs) | (c & hm);
+            }
+        }
+    }
     /* one returning atomic per point: the digit histogram and the point's
      * rank within its digit (its slot is the digit's offset + rank) */
     uint32_t rank[HM_P1_PPT];
@@ -349,7 +399,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         uint32_t old[HM_P1_GROUP];
 #pragma unroll
         for (int u = 0; u < HM_P1_GROUP; u++) {
-            gm[u] = hm_merge_prep(hm_cur_slot(dig[k0 + u], wd), dig[k0 + u] != 0xFFFFFFFFu, HM_MAX_F1);
+            gm[u] = hm_merge_prep(hm_cur_slot(dig[k0 + u], wd), dig[k0 + u] != 0xFFFFFFFFu, HM_D1);
             old[u] = atomicAdd(&cur[gm[u].idx], gm[u].inc);
         }
 #pragma unroll
@@ -361,16 +411,21 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
      * non-empty digit), issued as soon as the histogram is known; the results
      * are consumed only after the scan and the claim below, so the atomic
      * latency hides behind LDS work */
-    constexpr int PER = HM_MAX_F1 / HM_P1_THREADS;
+    constexpr int PER = PERD;
     uint32_t cnt[PER];
     uint32_t gpos[PER];
+    uint32_t rcap[PER], rbase[PER];
     uint32_t s = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        cnt[q] = d < F ? cur[hm_cur_slot(d, wd)] : 0u;
+        const uint2 ri = rinfo[d];
+        rbase[q] = ri.x;
+        rcap[q] = ri.y >> 1;
+        const uint32_t slot = (uint32_t)d * HM_L1_SHARDS + ((ri.y & 1u) ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u);
+        cnt[q] = live(d) ? cur[hm_cur_slot(d, wd)] : 0u;
         gpos[q] = 0;
-        if (d < F && cnt[q]) gpos[q] = atomicAdd(&a.fill[slot[q]], cnt[q]);
+        if (cnt[q]) gpos[q] = atomicAdd(&a.fill[slot], cnt[q]);
         s += cnt[q];
     }
     /* exclusive scan of the digit histogram */
@@ -385,7 +440,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F) cur[hm_cur_slot(d, wd)] = offq[q];
+        if (live(d)) cur[hm_cur_slot(d, wd)] = offq[q];
     }
     __syncthreads();
     if (MODE == 0) HM_STAMP_M(2, 4);
@@ -405,7 +460,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = tid * PER + q;
-        if (d < F) {
+        if (live(d)) {
             const bool fits = cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q];
             over |= cnt[q] && !fits;
             dbase[d] = fits ? rbase[q] + gpos[q] - offq[q] : 0xFFFFFFFFu;
@@ -417,9 +472,16 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     if (MODE == 0) HM_STAMP_M(2, 6);
     {
         OutT* out = (OutT*)a.keys_out;
+        uint16_t* hout = (uint16_t*)a.keys_hot;
         for (uint32_t i = tid; i < total; i += HM_P1_THREADS) {
-            const uint32_t b = dbase[sdig[i]];
-            if (b != 0xFFFFFFFFu) out[b + i] = stage[i];
+            const uint32_t d = sdig[i];
+            const uint32_t b = dbase[d];
+            if (b != 0xFFFFFFFFu) {
+                if (d < HM_MAX_F1)
+                    out[b + i] = stage[i];
+                else
+                    hout[b + i] = (uint16_t)stage[i];
+            }
         }
     }
     if (MODE == 0) HM_STAMP_M(2, 7);
@@ -427,15 +489,26 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
 
 /* Sampled digit histogram of level 1 (every stride-th point, fast projection
  * only): sizes the per-digit key regions k_project_partition fills. */
-template <bool FROM_TILES>
-__global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t stride_pts, uint32_t* hist)
+#define HM_SAMPLE_HSLOTS 4096   /* per-block hash of sampled hot-zoom tiles */
+template <bool FROM_TILES, bool HOT>
+__global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t stride_pts, uint32_t* hist,
+                                                       uint32_t* hot_counts)
 {
     __shared__ uint32_t h[HM_MAX_F1 + 64];
     __shared__ double tab[HM_YTAB_N];
+    /* HOT: the block's samples per zoom-hot_z tile, pre-aggregated in LDS
+     * (a hot tile gets one global atomic per block, not one per sample) */
+    __shared__ uint32_t hk[HOT ? HM_SAMPLE_HSLOTS : 1], hc[HOT ? HM_SAMPLE_HSLOTS : 1];
     const int F = 1 << a.dbits;
     for (int i = threadIdx.x; i < F; i += 256) h[i] = 0;
+    if (HOT)
+        for (int i = threadIdx.x; i < HM_SAMPLE_HSLOTS; i += 256) {
+            hk[i] = HM_HOT_EMPTY;
+            hc[i] = 0;
+        }
     if (!FROM_TILES) hm_load_ytab(tab);
     __syncthreads();
+    uint32_t hlost = 0;   /* samples the (full) LDS hash could not take: counted directly */
     const double scale = hm_exp2i(a.Z);
     const double kz = HM_INV360 * scale;
     const uint32_t lim = 1u << a.Z;
@@ -461,69 +534,175 @@ __global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t s
         }
         const uint32_t d = ((((uint32_t)r) >> hb) << wd) | (((uint32_t)c) >> hb);
         hm_lds_count(h, HM_MAX_F1, d, v);
+        if (HOT && v) {
+            const int hs = a.Z - a.hot_z;
+            const uint32_t t = ((((uint32_t)r) >> hs) << a.hot_z) | (((uint32_t)c) >> hs);
+            uint32_t sl = (t * 2654435761u) >> (32 - 12);
+            static_assert(HM_SAMPLE_HSLOTS == 1 << 12, "sample hash slots");
+            int probes = 0;
+            for (;;) {
+                const uint32_t o = atomicCAS(&hk[sl], HM_HOT_EMPTY, t);
+                if (o == HM_HOT_EMPTY || o == t) {
+                    atomicAdd(&hc[sl], 1u);
+                    break;
+                }
+                sl = (sl + 1) & (HM_SAMPLE_HSLOTS - 1);
+                if (++probes == HM_SAMPLE_HSLOTS) {
+                    atomicAdd(&hot_counts[t], 1u);
+                    hlost++;
+                    break;
+                }
+            }
+        }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < F; i += 256)
         if (h[i]) atomicAdd(&hist[i], h[i]);
+    if (HOT)
+        for (int i = threadIdx.x; i < HM_SAMPLE_HSLOTS; i += 256)
+            if (hc[i]) atomicAdd(&hot_counts[hk[i]], hc[i]);
+    (void)hlost;
+}
+
+/* Hot tiles: every zoom-zb tile with >= thresh sampled points (at most
+ * HM_MAX_HOT, first come), their sampled counts as level-1 histogram entries
+ * HM_MAX_F1 + h, and the z1 digits that hold them. */
+__global__ __launch_bounds__(256) void k_hot_select(HmHotArgs a)
+{
+    const uint64_t ntiles = 1ull << (2 * a.zb);
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < ntiles; t += stride) {
+        const uint32_t c = a.counts[t];
+        if (c >= a.thresh) {
+            const uint32_t h = atomicAdd(a.n, 1u);
+            if (h < HM_MAX_HOT) {
+                a.tiles[h] = (uint32_t)t;
+                a.hist[HM_MAX_F1 + h] = c;
+                const int s = a.zb - a.z1;
+                const uint32_t tr = (uint32_t)(t >> a.zb), tc = (uint32_t)(t & ((1ull << a.zb) - 1));
+                const uint32_t d = ((tr >> s) << a.z1) | (tc >> s);
+                a.hotparent[d] = 1;
+                atomicSub(&a.hist[d], c);   /* those samples' keys leave the cold digit */
+            }
+        }
+    }
+}
+
+/* the LDS hash image k_project_partition looks hot tiles up in; clamps the
+ * count to HM_MAX_HOT.  One block. */
+__global__ __launch_bounds__(256) void k_hot_hash(HmHotArgs a)
+{
+    __shared__ uint32_t hsh[HM_HOT_SLOTS];
+    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 256) hsh[i] = HM_HOT_EMPTY;
+    __syncthreads();
+    const uint32_t H = min(*a.n, (uint32_t)HM_MAX_HOT);
+    for (uint32_t h = threadIdx.x; h < H; h += 256) {
+        const uint32_t t = a.tiles[h];
+        uint32_t sl = (t * 2654435761u) >> (32 - 11);
+        while (atomicCAS(&hsh[sl], HM_HOT_EMPTY, (t << 10) | h) != HM_HOT_EMPTY) sl = (sl + 1) & (HM_HOT_SLOTS - 1);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 256) a.hash[i] = hsh[i];
+    if (threadIdx.x == 0) *a.n = H;
+}
+
+void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a)
+{
+    const uint64_t ntiles = 1ull << (2 * a.zb);
+    uint64_t blocks = (ntiles + 4095) / 4096;
+    if (blocks > 1024) blocks = 1024;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_hot_select, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hot_hash, dim3(1), dim3(256), 0, s, a);
 }
 
 /* Level-1 region sizes from the sampled histogram, on the device (no host
  * round trip): per digit est = hist * stride; a digit above 64 tiles gets
  * HM_L1_SHARDS shards; per shard cap = e + e/16 + 8 sqrt(e * stride) + 2 T1
- * (e = est / shards); bases = exclusive prefix over (digit, shard).  The same
- * formula as the host's retry path.  One block of 1024 threads. */
-__global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ hist, int F, uint64_t stride,
+ * (e = est / shards); bases = exclusive prefix over (digit, shard), the F
+ * cold digits first, then the hot tiles' digits HM_MAX_F1 + h (h < *hot_n),
+ * one position space.  The same formula as the host's retry path.  One block
+ * of 1024 threads: thread t sizes cold digit t and hot digit HM_MAX_F1 + t. */
+__device__ __forceinline__ uint32_t hm_l1_cap(uint32_t hist, uint64_t stride, int* ns)
+{
+    const double est = (double)hist * (double)stride;
+    *ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
+    const double e = est / *ns;
+    return (uint32_t)fmin(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) + 2.0 * HM_T1);
+}
+
+__global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ hist, int F,
+                                                   const uint32_t* __restrict__ hot_n, uint64_t stride,
                                                    uint32_t* __restrict__ rcap, uint32_t* __restrict__ rbase,
                                                    uint8_t* __restrict__ smask)
 {
     __shared__ unsigned long long wsum[1024 / 64];
-    const int d = threadIdx.x;
-    const int lane = d & 63, w = d >> 6;
-    uint32_t c = 0;
-    int ns = 1;
-    if (d < F) {
-        const double est = (double)hist[d] * (double)stride;
-        ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
-        const double e = est / ns;
-        c = (uint32_t)fmin(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) + 2.0 * HM_T1);
-        smask[d] = (uint8_t)(ns - 1);
-    }
-    const unsigned long long mine = d < F ? (unsigned long long)c * (unsigned long long)ns : 0ull;
-    unsigned long long incl = mine;
-    for (int o = 1; o < 64; o <<= 1) {
-        const unsigned long long y = __shfl_up(incl, o, 64);
-        if (lane >= o) incl += y;
-    }
-    if (lane == 63) wsum[w] = incl;
-    __syncthreads();
-    unsigned long long before = 0;
-    for (int i = 0; i < w; i++) before += wsum[i];
-    unsigned long long pos = before + incl - mine;
-    if (d < F)
-        for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
-            const uint32_t cs = sh < ns ? c : 0u;
-            rcap[d * HM_L1_SHARDS + sh] = cs;
-            rbase[d * HM_L1_SHARDS + sh] = (uint32_t)pos;   /* total < 2^32: the host's bound */
-            pos += cs;
+    static_assert(HM_MAX_HOT <= 1024 && HM_MAX_F1 <= 1024, "one digit of each kind per thread");
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const uint32_t H = hot_n ? min(*hot_n, (uint32_t)HM_MAX_HOT) : 0u;
+    unsigned long long base = 0;
+    for (int kind = 0; kind < 2; kind++) {
+        const int d = kind ? HM_MAX_F1 + t : t;
+        const bool live = kind ? (uint32_t)t < H : t < F;
+        uint32_t c = 0;
+        int ns = 1;
+        if (live) {
+            c = hm_l1_cap(hist[d], stride, &ns);
+            smask[d] = (uint8_t)(ns - 1);
         }
+        const unsigned long long mine = live ? (unsigned long long)c * (unsigned long long)ns : 0ull;
+        unsigned long long incl = mine;
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned long long y = __shfl_up(incl, o, 64);
+            if (lane >= o) incl += y;
+        }
+        __syncthreads();
+        if (lane == 63) wsum[w] = incl;
+        __syncthreads();
+        unsigned long long before = 0, all = 0;
+        for (int i = 0; i < 1024 / 64; i++) {
+            before += i < w ? wsum[i] : 0ull;
+            all += wsum[i];
+        }
+        unsigned long long pos = base + before + incl - mine;
+        if (live)
+            for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
+                const uint32_t cs = sh < ns ? c : 0u;
+                rcap[d * HM_L1_SHARDS + sh] = cs;
+                rbase[d * HM_L1_SHARDS + sh] = (uint32_t)pos;   /* total < 2^32: the host's bound */
+                pos += cs;
+            }
+        base += all;
+    }
 }
 
-void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, uint64_t stride, uint32_t* rcap, uint32_t* rbase,
-                        uint8_t* smask)
+void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, const uint32_t* hot_n, uint64_t stride,
+                        uint32_t* rcap, uint32_t* rbase, uint8_t* smask)
 {
-    hipLaunchKernelGGL(k_l1_sizes, dim3(1), dim3(1024), 0, s, hist, F, stride, rcap, rbase, smask);
+    hipLaunchKernelGGL(k_l1_sizes, dim3(1), dim3(1024), 0, s, hist, F, hot_n, stride, rcap, rbase, smask);
 }
 
-void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist)
+void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist,
+                             uint32_t* hot_counts)
 {
     const uint64_t m = ((uint64_t)a.n + stride_pts - 1) / stride_pts;
     uint64_t blocks = (m + 1023) / 1024;
-    if (blocks > 2048) blocks = 2048;
+    /* with the hot-tile counts: fewer, fuller blocks (one global atomic per
+     * block and tile) */
+    const uint64_t cap = hot_counts ? 256 : 2048;
+    if (blocks > cap) blocks = cap;
     if (blocks < 1) blocks = 1;
-    if (a.rows_in)
-        hipLaunchKernelGGL(k_sample_digits<true>, dim3((unsigned)blocks), dim3(256), 0, s, a, stride_pts, hist);
-    else
-        hipLaunchKernelGGL(k_sample_digits<false>, dim3((unsigned)blocks), dim3(256), 0, s, a, stride_pts, hist);
+#define HM_SD(T, H) hipLaunchKernelGGL((k_sample_digits<T, H>), dim3((unsigned)blocks), dim3(256), 0, s, a, stride_pts, \
+                                       hist, hot_counts)
+    if (a.rows_in) {
+        if (hot_counts) HM_SD(true, true);
+        else HM_SD(true, false);
+    } else {
+        if (hot_counts) HM_SD(false, true);
+        else HM_SD(false, false);
+    }
+#undef HM_SD
 }
 
 /* Level-1 buckets from the filled regions: one flat run per non-empty digit
@@ -542,12 +721,15 @@ __global__ __launch_bounds__(1024) void k_level1_buckets(HmL1Args a)
         nk += f[sh];
         nr += f[sh] != 0;
     }
-    const uint32_t ne = nk > 0;
-    const uint32_t nit = ne ? (nk <= a.sparse_max ? 0u : (nk + a.item_keys - 1) / a.item_keys) : 0u;
+    /* a digit whose points all went to its hot tiles is still a bucket: the
+     * parent of those tiles at level 2 (no keys, no items of its own) */
+    const uint32_t ne = nk > 0 || (a.hotparent && d < a.F && a.hotparent[d]);
+    const uint32_t nit = nk ? (nk <= a.sparse_max ? 0u : (nk + a.item_keys - 1) / a.item_keys) : 0u;
     uint32_t count, items, runs;
     const uint32_t idx = hm_block_excl_scan<1024>(ne, scr, &count);
     const uint32_t ib = hm_block_excl_scan<1024>(nit, scr, &items);
     const uint32_t r0 = hm_block_excl_scan<1024>(nr, scr, &runs);
+    if (a.d2b && d < a.F) a.d2b[d] = ne ? idx : 0xFFFFFFFFu;
     if (ne) {
         /* logical key positions of the bucket: [region base, + nk), its
          * non-empty shards' keys one after the other */
@@ -1286,8 +1468,11 @@ __global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
             h.incl = hm_wave_incl_scan(h.n);
             const uint64_t nr = __shfl(nrl, i, 64);
             const uint64_t rb = __shfl(rbl, i, 64);
-            /* a sparse level's children hold a few runs: one 64-run step */
-            if (nr <= 64)
+            /* a sparse level's children hold a few runs: one 64-run step;
+             * a hot tile has runs but no sharded ones (k_hot_runs lists them) */
+            if (__shfl(h.incl, 63, 64) == 0)
+                ;
+            else if (nr <= 64)
                 hm_rs_slice<1>(a, h, nr, rb, 0);
             else if (nr <= 256)
                 hm_rs_slice<4>(a, h, nr, rb, 0);
@@ -1350,6 +1535,64 @@ __global__ __launch_bounds__(256) void k_rs_keys(HmRsArgs a)
         const uint32_t nit = nk <= a.sparse_max ? 0u : (nk + a.item_keys - 1) / a.item_keys;
         a.vals[c] = (1ull << 32) | (uint64_t)nit;
     }
+}
+
+/* Hot tiles as level-2 children: child (bucket of its z1 digit, its digit
+ * below it); its runs are its non-empty level-1 region shards, whose keys K1
+ * wrote in the final (u16) form into the level-2 key array.  k_hot_nr sets
+ * the children's run counts before the run scan, k_hot_runs lists the runs at
+ * their flat positions after it (k_rs_copy skips the children). */
+__device__ __forceinline__ uint64_t hm_hot_child(const HmHotRunArgs& a, uint32_t t)
+{
+    const int s = a.zb - a.z1;
+    const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
+    const uint32_t m = (1u << s) - 1u;
+    const uint64_t p = a.d2b[((tr >> s) << a.z1) | (tc >> s)];
+    return (p << a.dbits) | (((tr & m) << s) | (tc & m));
+}
+
+__global__ __launch_bounds__(256) void k_hot_nr(HmHotRunArgs a)
+{
+    const uint32_t H = *a.n;
+    for (uint32_t h = blockIdx.x * 256 + threadIdx.x; h < H; h += gridDim.x * 256) {
+        uint32_t nr = 0;
+#pragma unroll
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) nr += a.fill[(HM_MAX_F1 + h) * HM_L1_SHARDS + sh] != 0;
+        if (nr) a.nr[hm_hot_child(a, a.tiles[h])] = nr;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_hot_runs(HmHotRunArgs a)
+{
+    const uint32_t H = *a.n;
+    for (uint32_t h = blockIdx.x * 256 + threadIdx.x; h < H; h += gridDim.x * 256) {
+        uint64_t j = 0;
+        bool any = false;
+#pragma unroll
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) any |= a.fill[(HM_MAX_F1 + h) * HM_L1_SHARDS + sh] != 0;
+        if (!any) continue;
+        const uint64_t rb = a.runbase[hm_hot_child(a, a.tiles[h])];
+#pragma unroll
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
+            const uint32_t k = (HM_MAX_F1 + h) * HM_L1_SHARDS + sh;
+            const uint32_t f = a.fill[k];
+            if (f) {
+                a.flat[rb + j] = make_uint2(a.rbase[k], f);
+                a.cnt[rb + j] = f;
+                j++;
+            }
+        }
+    }
+}
+
+void hm_launch_hot_nr(hipStream_t s, const HmHotRunArgs& a)
+{
+    hipLaunchKernelGGL(k_hot_nr, dim3(HM_MAX_HOT / 256), dim3(256), 0, s, a);
+}
+
+void hm_launch_hot_runs(hipStream_t s, const HmHotRunArgs& a)
+{
+    hipLaunchKernelGGL(k_hot_runs, dim3(HM_MAX_HOT / 256), dim3(256), 0, s, a);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -23,6 +23,14 @@
 #define HM_L1_SHARDS 8                      /* sub-regions of a hot level-1 digit */
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
+/* hot tiles: zoom-zb tiles (the last level's bucket zoom) that a sample shows
+ * to hold >= 1/2048 of the points each.  Level 1 gives each its own digit
+ * HM_MAX_F1 + h and writes its keys (u16, zb-relative) straight into the
+ * final level's key array, so they skip every intermediate partition pass. */
+#define HM_MAX_HOT 512
+#define HM_D1 (HM_MAX_F1 + HM_MAX_HOT)      /* level-1 digit slots: cold z1 digits, then hot tiles */
+#define HM_HOT_SLOTS 2048                   /* hot-tile hash (load <= 1/4) */
+#define HM_HOT_EMPTY 0xFFFFFFFFu
 /* levels >= 2 */
 #ifndef HM_PN_THREADS
 #define HM_PN_THREADS 1024
@@ -190,6 +198,38 @@ struct HmPart1Args {
     unsigned long long* err_word;
     HmExotic x;
     unsigned long long* slow_count;
+    /* hot tiles (hot_z >= 0): keys of hot tile h go to the u16 array keys_hot
+     * at the regions of digit HM_MAX_F1 + h (same position space as keys_out) */
+    int hot_z;
+    void* keys_hot;
+    const uint32_t* hot_hash;   /* [HM_HOT_SLOTS]: tile id << 10 | h, HM_HOT_EMPTY */
+    const uint32_t* hot_n;      /* device word: number of hot tiles */
+};
+
+/* hot-tile selection from the sampled zoom-zb counts (k_hot_select) */
+struct HmHotArgs {
+    uint32_t* counts;           /* [4^zb] sampled points per zoom-zb tile (zeroed before sampling) */
+    int zb, z1;
+    uint32_t thresh;            /* sampled points a hot tile needs */
+    uint32_t* tiles;            /* [HM_MAX_HOT] tile id (row << zb | col) */
+    uint32_t* hist;             /* [HM_D1] level-1 sampled histogram: hot h at HM_MAX_F1 + h */
+    uint8_t* hotparent;         /* [HM_MAX_F1] z1 digits that hold a hot tile */
+    uint32_t* n;                /* device word: hot tiles found (<= HM_MAX_HOT) */
+    uint32_t* hash;             /* [HM_HOT_SLOTS] */
+};
+
+/* hot tiles as children of the level-2 run scan (k_hot_nr / k_hot_runs) */
+struct HmHotRunArgs {
+    const uint32_t* tiles;
+    const uint32_t* n;
+    int zb, z1, dbits;
+    const uint32_t* fill;       /* level-1 [HM_D1 * HM_L1_SHARDS] */
+    const uint32_t* rbase;
+    const uint32_t* d2b;        /* [HM_MAX_F1] z1 digit -> level-1 bucket */
+    uint64_t* nr;               /* runs per level-2 child */
+    const uint64_t* runbase;
+    uint2* flat;
+    uint64_t* cnt;
 };
 
 /* level-1 buckets (k_level1_buckets) from the filled regions */
@@ -207,6 +247,8 @@ struct HmL1Args {
     int32_t* slots;            /* last level only */
     uint32_t* nslots;
     uint32_t* slot_bucket;
+    const uint8_t* hotparent;  /* digits that are buckets for their hot children alone (or null) */
+    uint32_t* d2b;             /* digit -> bucket index (or null) */
 };
 
 struct HmPartNArgs {
@@ -302,9 +344,15 @@ void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int6
                        int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow);
 /* mode: 0 fast path + redo list, 1 tile input (exact row/col given), 2 fused exact (fallback) */
 void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool out16, int mode);
-void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist);
-void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, uint64_t stride, uint32_t* rcap, uint32_t* rbase,
-                        uint8_t* smask);
+/* hot_counts (or null): sampled points per zoom-a.hot_z tile, dense */
+void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist,
+                             uint32_t* hot_counts);
+void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a);
+/* region sizes of the F cold digits and (hot_n) the hot tiles' digits */
+void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, const uint32_t* hot_n, uint64_t stride,
+                        uint32_t* rcap, uint32_t* rbase, uint8_t* smask);
+void hm_launch_hot_nr(hipStream_t s, const HmHotRunArgs& a);
+void hm_launch_hot_runs(hipStream_t s, const HmHotRunArgs& a);
 void hm_launch_level1_buckets(hipStream_t s, const HmL1Args& a);
 struct HmRedoArgs {
     const double* lat;

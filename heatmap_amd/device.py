@@ -57,6 +57,15 @@ class Context:
         self.L.hm_last_stats(self.ptr, ctypes.byref(slow), us, 8)
         return slow.value, list(us)
 
+    def tune(self, name: str, value: float) -> float:
+        """Set one plan-tuning knob (include/heatmap_amd.h hm_ctx_tune);
+        returns the previous value."""
+        old = ctypes.c_double(0)
+        rc = self.L.hm_ctx_tune(self.ptr, name.encode(), float(value), ctypes.byref(old))
+        if rc != _lib.HM_OK:
+            raise ValueError("unknown tuning knob %r" % name)
+        return old.value
+
     def __del__(self):  # pragma: no cover
         try:
             if getattr(self, "ptr", None):
@@ -73,6 +82,29 @@ def context(device: int = 0) -> Context:
             c = _CTX[key] = Context(device)
     c.bind_stream()
     return c
+
+
+class tuned:
+    """Context manager: plan-tuning knobs of this thread's context for the
+    block (tests force plans at parity sizes), restored afterwards.
+
+        with device.tuned(HM_HOT_MIN_KEYS=0): ...
+    """
+
+    def __init__(self, device: int = 0, **knobs):
+        self.device, self.knobs, self.old = device, knobs, {}
+
+    def __enter__(self):
+        ctx = context(self.device)
+        for k, v in self.knobs.items():
+            self.old[k] = ctx.tune(k, v)
+        return ctx
+
+    def __exit__(self, *exc):
+        ctx = context(self.device)
+        for k, v in self.old.items():
+            ctx.tune(k, v)
+        return False
 
 
 def _dev(x, dtype, device):

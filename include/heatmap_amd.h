@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 3
+#define HM_ABI_VERSION 4
 
 /* status / per-point error kinds */
 #define HM_OK 0
@@ -92,6 +92,21 @@ const char* hm_status_string(int status);
 int hm_ctx_create(hm_ctx** out, int device, void* stream);
 int hm_ctx_set_stream(hm_ctx* ctx, void* stream);
 int hm_ctx_destroy(hm_ctx* ctx);
+
+/* Plan tuning of one context (no effect on results, only on which kernels
+ * count them).  hm_ctx_create reads each from the environment variable of the
+ * same name once; this sets it afterwards.  HM_E_ARG for an unknown name.
+ *   HM_SPREAD_MIN_KEYS  mean level-1 bucket (keys) of a flat histogram above
+ *                       which levels 2.. take 3 zooms (default 2^19)
+ *   HM_RS_BIG_MIN       runs above which a level child is copied by every
+ *                       wave of the run scan (default 2048)
+ *   HM_HOT              1 (default): hot tiles skip the intermediate
+ *                       partition passes; 0: off
+ *   HM_HOT_INV_SHARE    a tile is hot with >= 1/this of the sampled points
+ *                       (default 2048)
+ *   HM_HOT_MIN_KEYS     ... and >= this many estimated points (default 65536)
+ * Returns the previous value in *old (if not NULL). */
+int hm_ctx_tune(hm_ctx* ctx, const char* name, double value, double* old);
 
 /* Project n points at one zoom (-30..30; negative zooms scale by 2^zoom, as
  * Python's 2 ** zoom does for Tile.parent_id at zoom 0, tile.py:60-61).  row/col: int64[n]; status: uint8[n]
@@ -150,6 +165,7 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
  *       compactions (incl. host reads; contains [4])
  *   [2] final aggregation (k_aggregate, sparse/small/merged buckets)
  *   [3] k_pool levels   [4] the level >= 2 k_partition launches alone
+ *   [6] hot tiles of the call (their points skipped levels 2..)
  *   [7] partition levels of the pipeline plan (0 if the call took the
  *       general path); 3 zooms per level for dense, evenly spread clouds */
 int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_stages);

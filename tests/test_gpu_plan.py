@@ -3,7 +3,8 @@
 Dense, evenly spread clouds switch levels 2.. from 6 to 3 zooms per level
 (z5 -> z8 -> z11 at zmax 18).  At parity-test sizes the switch is forced by
 lowering HM_SPREAD_MIN_KEYS (the mean level-1 bucket size it requires,
-2^19 keys by default: the 1e9-point uniform bench).  The partition level
+2^19 keys by default: the 1e9-point uniform bench) through hm_ctx_tune
+(device.tuned).  The partition level
 count is read back from hm_last_stats' slot 7.  Expected counts: the oracle
 (heatmap.py:109-111's per-zoom reduceByKey).
 """
@@ -24,57 +25,53 @@ def _same(got, ref):
 
 
 @pytest.mark.parametrize("Z,levels,n", [(18, 3, 1_500_000), (21, 4, 150_000), (16, 3, 1_500_000), (14, 2, 800_000)])
-def test_spread_plan_tiles(gpu, monkeypatch, Z, levels, n):
+def test_spread_plan_tiles(gpu, Z, levels, n):
     """(n stays small at zoom 21: the last level's dense child space, 64 per
     non-empty zoom-11 parent, must fit HM_SCAN_LIMIT or the call takes the
     general path)"""
-    monkeypatch.setenv("HM_SPREAD_MIN_KEYS", "1")
     rng = np.random.default_rng(Z)
     rows = rng.integers(0, 1 << Z, n).astype(np.int64)
     cols = rng.integers(0, 1 << Z, n).astype(np.int64)
-    got = device.count(rows, cols, None, 0, Z, tiles=True)
+    with device.tuned(HM_SPREAD_MIN_KEYS=1):
+        got = device.count(rows, cols, None, 0, Z, tiles=True)
     assert int(got.stage_us[7]) == levels
     _same(got, oracle.count_tiles(rows, cols, 0, Z))
 
 
 @pytest.mark.parametrize("zmin", [0, 9])
-def test_spread_plan_latlon(gpu, monkeypatch, zmin):
-    monkeypatch.setenv("HM_SPREAD_MIN_KEYS", "1")
+def test_spread_plan_latlon(gpu, zmin):
     lat, lon = synth.generate("uniform", 2_000_000, seed=3)
     keep = (np.arange(lat.size) % 7 != 3).astype(np.uint8)
-    got = device.count(lat, lon, keep, zmin, 18)
+    with device.tuned(HM_SPREAD_MIN_KEYS=1):
+        got = device.count(lat, lon, keep, zmin, 18)
     assert int(got.stage_us[7]) == 3
     _same(got, oracle.count(lat, lon, keep, zmin, 18))
 
 
-def test_default_plans(gpu, monkeypatch):
+def test_default_plans(gpu):
     """Without the override: parity-size uniform clouds and any hotspot cloud
     keep 6 zooms per level (a hotspot histogram is never flat)."""
-    monkeypatch.delenv("HM_SPREAD_MIN_KEYS", raising=False)
     lat, lon = synth.generate("uniform", 1_000_000, seed=4)
     got = device.count(lat, lon, None, 0, 18)
     assert int(got.stage_us[7]) == 2
     _same(got, oracle.count(lat, lon, None, 0, 18))
-    monkeypatch.setenv("HM_SPREAD_MIN_KEYS", "1")
     lat, lon = synth.generate("hotspots", 1_000_000, seed=4)
-    got = device.count(lat, lon, None, 0, 18)
+    with device.tuned(HM_SPREAD_MIN_KEYS=1):
+        got = device.count(lat, lon, None, 0, 18)
     assert int(got.stage_us[7]) == 2
     _same(got, oracle.count(lat, lon, None, 0, 18))
 
 
-@pytest.mark.parametrize("big_min", [None, "1000000", "0"])
-def test_hot_children_many_runs(gpu, monkeypatch, big_min):
+@pytest.mark.parametrize("big_min", [None, 1000000, 0])
+def test_hot_children_many_runs(gpu, big_min):
     """Children with many runs -- one run per work item of their parent, the
     hot tiles of a skewed cloud -- are copied by every wave of k_rs_copy_big
     when they hold more than HM_RS_BIG_MIN runs (2048 by default: the three
     hot zoom-18 tiles here, ~5100 runs each); also with none listed (one wave
     per child) and with every child listed (the 4096-entry list overflows, the
     rest are copied in place).  A zoom-5 parent of ~5100 work items plus a
-    uniform background."""
-    if big_min is None:
-        monkeypatch.delenv("HM_RS_BIG_MIN", raising=False)
-    else:
-        monkeypatch.setenv("HM_RS_BIG_MIN", big_min)
+    uniform background.  Hot tiles off: with them the three tiles' keys skip
+    level 2 (tests/test_gpu_hot.py runs the same cloud that way)."""
     from conftest import cells_digest
     rng = np.random.default_rng(21)
     Z = 18
@@ -87,7 +84,10 @@ def test_hot_children_many_runs(gpu, monkeypatch, big_min):
     cols = np.concatenate(cols)
     perm = rng.permutation(rows.size)
     rows, cols = rows[perm], cols[perm]
-    got = device.count(rows, cols, None, 0, Z, tiles=True)
+    knobs = {"HM_HOT": 0} if big_min is None else {"HM_HOT": 0, "HM_RS_BIG_MIN": big_min}
+    with device.tuned(**knobs):
+        got = device.count(rows, cols, None, 0, Z, tiles=True)
+    assert int(got.stage_us[6]) == 0
     ref = oracle.count_tiles(rows, cols, 0, Z)
     assert got.zoom.size == ref["zoom"].size
     assert cells_digest(got.zoom, got.row, got.col, got.count) == \
