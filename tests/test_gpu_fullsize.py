@@ -1,0 +1,107 @@
+"""Parity at the bench sizes: 1e9-point clouds (BASELINE configs 2 and 4) and
+a 20-batch x 10M-point stream (config 5), cell for cell through the
+order-free digest of tests/conftest.py, computed on the device and compared
+with tests/golden/big_digests.json (the C oracle, tests/golden/make_bigdigest.py).
+
+These are the sizes at which paths switch on that smaller tests reach only
+with tuned thresholds: hot tiles at their default share, the region-sized
+level 1 with its sampled margins, many-run children copied by k_rs_copy_big
+(skew with hot tiles off: ~110k runs in one child), multi-item buckets merged
+through global slots.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import GOLDEN
+from heatmap_amd import device
+
+pytestmark = pytest.mark.gpu
+
+M29 = (1 << 29) - 1
+_U = (1 << 64) - 1
+
+
+def _s64(v):
+    return v - (1 << 64) if v >= 1 << 63 else v
+
+
+def device_digest(torch, keys, counts):
+    """tests/conftest.py cells_digest of HM_KEY cells, on the device (int64
+    arithmetic wraps like the uint64 original; right shifts made logical)."""
+    z = keys >> 58
+    r = (keys >> 29) & M29
+    c = keys & M29
+
+    def lsr(x, k):
+        return (x >> k) & ((1 << (64 - k)) - 1)
+
+    x = (z * _s64(0x9E3779B97F4A7C15)) ^ r
+    x = (x * _s64(0xBF58476D1CE4E5B9)) ^ c
+    x = (x * _s64(0x94D049BB133111EB)) ^ counts
+    x = x ^ lsr(x, 31)
+    x = x * _s64(0xD6E8FEB86659FD93)
+    x = x ^ lsr(x, 32)
+    s = int(x.sum().item()) & _U
+    while x.numel() > 1:
+        h = x.numel() // 2
+        y = x[:h] ^ x[h:2 * h]
+        x = torch.cat([y, x[2 * h:]]) if x.numel() & 1 else y
+    xr = (int(x[0].item()) & _U) if x.numel() else 0
+    return [int(keys.numel()), int(counts.sum().item()), s, xr]
+
+
+def _golden(name):
+    path = os.path.join(GOLDEN, "big_digests.json")
+    d = json.load(open(path))
+    if name not in d:
+        pytest.skip("%s not in big_digests.json" % name)
+    return d[name]
+
+
+@pytest.mark.parametrize("name,hot", [("hotspots_1e9_z0-18", 1), ("hotspots_1e9_z0-18", 0),
+                                      ("skew_1e9_z0-18", 1), ("skew_1e9_z0-18", 0)])
+def test_fullsize_cloud(gpu, name, hot):
+    torch = gpu
+    g = _golden(name)
+    n = g["n"]
+    lat = torch.empty(n, dtype=torch.float64, device="cuda")
+    lon = torch.empty(n, dtype=torch.float64, device="cuda")
+    device.synth(g["kind"], lat, lon, seed=g["seed"], start=g["start"])
+    with device.tuned(HM_HOT=hot):
+        m, buf = device.count_device(lat, lon, None, g["zmin"], g["zmax"])
+        st = device.context(0).last_stats()[1]
+    del lat, lon
+    assert buf.nx == 0
+    if hot and name.startswith("skew"):
+        assert int(st[6]) == 1
+    if not hot:
+        assert int(st[6]) == 0
+    assert device_digest(torch, buf.keys[:m], buf.counts[:m]) == g["digest"]
+
+
+def test_fullsize_stream(gpu):
+    """20 batches of 10M points, one epoch hour each, folded into a resident
+    heatmap: the alltime cells equal the oracle's count of all 200M points,
+    and three hours' cells equal their batches' counts."""
+    torch = gpu
+    from heatmap_amd.stream import ALLTIME, StreamingHeatmap
+
+    base = 480000
+    g = _golden("hotspots_2e8_z0-18_stream20x10M")
+    b = 10_000_000
+    s = StreamingHeatmap(0, 18, base_hour=base, initial_cells=1 << 26)
+    lat = torch.empty(b, dtype=torch.float64, device="cuda")
+    lon = torch.empty(b, dtype=torch.float64, device="cuda")
+    for k in range(20):
+        device.synth("hotspots", lat, lon, seed=0, start=k * b)
+        s.add(lat, lon, hour=torch.full((b,), base + k, dtype=torch.int32, device="cuda"))
+    n, keys, counts = s.extract_device(ALLTIME)[:3]
+    assert device_digest(torch, keys[:n], counts[:n]) == g["digest"]
+    for k, name in ((0, "hotspots_1e7_start0_z0-18"), (7, "hotspots_1e7_start70M_z0-18"),
+                    (19, "hotspots_1e7_start190M_z0-18")):
+        n, keys, counts = s.extract_device(base + k)[:3]
+        assert device_digest(torch, keys[:n], counts[:n]) == _golden(name)["digest"], name
+    s.close()
