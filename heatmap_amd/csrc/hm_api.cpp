@@ -114,7 +114,7 @@ enum {
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
-    B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B,
+    B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS,
     B_COUNT
 };
 
@@ -1291,6 +1291,45 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
     if (n == 0) return HM_OK;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
+    unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+    {
+        /* bucketed LDS merge (hm_merge.hip): <= 4096 hash buckets of ~2048+
+         * cells, one block each */
+        HmMergeArgs a;
+        memset(&a, 0, sizeof(a));
+        int lb = 0;
+        while (lb < 12 && ((uint64_t)n >> lb) > 2048) lb++;
+        a.keys = keys;
+        a.counts = counts;
+        a.n = (uint64_t)n;
+        a.lb = lb;
+        a.nblocks = (uint32_t)std::min<uint64_t>(512, ((uint64_t)n + 65535) / 65536);
+        const uint64_t m = ((uint64_t)1 << lb) * a.nblocks;
+        ENSURE(B_MB_CNT, m * 8, a.bcnt);
+        ENSURE(B_MB_OFF, (m + 1) * 8, a.boff);
+        ENSURE(B_MB_KEYS, (uint64_t)n * 8, a.pkeys);
+        ENSURE(B_MB_COUNTS, (uint64_t)n * 8, a.pcounts);
+        unsigned long long* st;
+        ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), st);
+        uint64_t* partial;
+        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+        HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
+        a.keys_out = keys_out;
+        a.counts_out = counts_out;
+        a.cap = (uint64_t)capacity;
+        a.cursor = st;
+        a.overflow = st + 1;
+        hm_launch_merge_buckets(s, a, partial);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(down, st, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        HIPCHK(hipStreamSynchronize(s));
+        if (!down[1]) {
+            *n_out = (int64_t)down[0];
+            return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+        }
+        /* a bucket's table filled up (adversarial hash collisions): the
+         * global hash table below takes the whole merge again */
+    }
     uint64_t cap = 1024;
     while (cap < 2 * (uint64_t)n) cap <<= 1;
     HmsTable t;
@@ -1311,7 +1350,6 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
     }
     hm_launch_table_extract(s, t, keys_out, counts_out, (uint64_t)capacity, t.state + HMS_ST_CURSOR);
     HIPCHK(hipGetLastError());
-    unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
     HIPCHK(hipMemcpyAsync(down, t.state, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;   /* cannot happen: load factor <= 1/2 */

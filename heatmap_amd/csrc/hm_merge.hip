@@ -224,6 +224,127 @@ __global__ __launch_bounds__(256) void k_dense_extract(const uint64_t* __restric
     }
 }
 
+/* ---- bucketed merge (hm_cells_merge / hm_cells_merge_runs) ----
+ * The owner of a multi-GPU exchange receives every rank's cells of its rows,
+ * one run per sender (~28M cells at 1.25e9 points per rank).  Inserting them
+ * one by one into a 1 GB global hash table is a random read-modify-write per
+ * cell; here the cells are first hash-partitioned into buckets of ~2048
+ * (two streaming passes), then one block per bucket sums equal keys in LDS
+ * and writes the distinct cells with one output reservation. */
+__device__ __forceinline__ uint32_t hm_mb_bucket(uint64_t k, int lb)
+{
+    return lb ? (uint32_t)(hms_hash(k) >> (64 - lb)) : 0u;
+}
+
+template <bool SCATTER>
+__global__ __launch_bounds__(256) void k_mb_part(HmMergeArgs a)
+{
+    /* dynamic LDS: SCATTER: u64 base[2^lb] then u32 hist[2^lb]; else hist only */
+    extern __shared__ unsigned long long dyn[];
+    const uint32_t NB = 1u << a.lb;
+    uint64_t* base = (uint64_t*)dyn;
+    uint32_t* hist = SCATTER ? (uint32_t*)(dyn + NB) : (uint32_t*)dyn;
+    const uint32_t blk = blockIdx.x;
+    for (uint32_t i = threadIdx.x; i < NB; i += 256) hist[i] = 0;
+    __syncthreads();
+    const uint64_t per = (a.n + a.nblocks - 1) / a.nblocks;
+    const uint64_t b0 = (uint64_t)blk * per, b1 = min(b0 + per, a.n);
+    if (!SCATTER) {
+        for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) atomicAdd(&hist[hm_mb_bucket(a.keys[i], a.lb)], 1u);
+        __syncthreads();
+        for (uint32_t b = threadIdx.x; b < NB; b += 256) a.bcnt[(uint64_t)b * a.nblocks + blk] = hist[b];
+    } else {
+        /* this chunk's slots of each bucket start at boff[b * nblocks + blk] */
+        for (uint32_t b = threadIdx.x; b < NB; b += 256) base[b] = a.boff[(uint64_t)b * a.nblocks + blk];
+        __syncthreads();
+        for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) {
+            const uint64_t k = a.keys[i];
+            const uint32_t b = hm_mb_bucket(k, a.lb);
+            const uint64_t q = base[b] + atomicAdd(&hist[b], 1u);
+            a.pkeys[q] = k;
+            a.pcounts[q] = a.counts[i];
+        }
+    }
+}
+
+/* one bucket per block: its cells into an LDS table (P sub-passes by hash
+ * bits when the bucket is large, so a table never holds more than ~half its
+ * slots), distinct cells out */
+__global__ __launch_bounds__(HM_MB_THREADS) void k_mb_merge(HmMergeArgs a)
+{
+    __shared__ unsigned long long tk[HM_MB_TS];
+    __shared__ unsigned long long tc[HM_MB_TS];
+    __shared__ uint32_t scr[HM_MB_THREADS / 64 + 1];
+    __shared__ unsigned long long sbase;
+    __shared__ uint32_t full;
+    const uint32_t b = blockIdx.x;
+    const uint64_t e0 = a.boff[(uint64_t)b * a.nblocks], e1 = a.boff[(uint64_t)(b + 1) * a.nblocks];
+    if (e1 == e0) return;
+    const uint64_t size = e1 - e0;
+    const uint32_t P = (uint32_t)((size + HM_MB_TS / 2 - 1) / (HM_MB_TS / 2));
+    constexpr int SPT = HM_MB_TS / HM_MB_THREADS;
+    for (uint32_t pass = 0; pass < P; pass++) {
+        for (int j = 0; j < SPT; j++) {
+            tk[j * HM_MB_THREADS + threadIdx.x] = HMS_EMPTY;
+            tc[j * HM_MB_THREADS + threadIdx.x] = 0;
+        }
+        if (threadIdx.x == 0) full = 0;
+        __syncthreads();
+        for (uint64_t i = e0 + threadIdx.x; i < e1; i += HM_MB_THREADS) {
+            const uint64_t k = a.pkeys[i];
+            const uint64_t h = hms_hash(k);
+            if ((uint32_t)((h >> 32) % P) != pass) continue;
+            uint32_t sl = (uint32_t)h & (HM_MB_TS - 1);
+            int probes = 0;
+            for (;;) {
+                const unsigned long long o = atomicCAS(&tk[sl], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
+                if (o == HMS_EMPTY || o == k) {
+                    atomicAdd(&tc[sl], (unsigned long long)a.pcounts[i]);
+                    break;
+                }
+                sl = (sl + 1) & (HM_MB_TS - 1);
+                if (++probes == HM_MB_TS) {
+                    full = 1;
+                    break;
+                }
+            }
+        }
+        __syncthreads();
+        if (full) {
+            if (threadIdx.x == 0) atomicOr(a.overflow, 1ull);
+            return;
+        }
+        uint32_t c = 0;
+        for (int j = 0; j < SPT; j++) c += tk[threadIdx.x * SPT + j] != HMS_EMPTY;
+        uint32_t tot;
+        uint32_t off = hm_block_excl_scan<HM_MB_THREADS>(c, scr, &tot);
+        if (threadIdx.x == 0) sbase = atomicAdd(a.cursor, (unsigned long long)tot);
+        __syncthreads();
+        const uint64_t base = sbase;
+        for (int j = 0; j < SPT; j++) {
+            const uint32_t sl = threadIdx.x * SPT + j;
+            if (tk[sl] != HMS_EMPTY) {
+                const uint64_t q = base + off++;
+                if (q < a.cap) {
+                    a.keys_out[q] = tk[sl];
+                    a.counts_out[q] = tc[sl];
+                }
+            }
+        }
+        __syncthreads();
+    }
+}
+
+void hm_launch_merge_buckets(hipStream_t s, const HmMergeArgs& a, uint64_t* partial)
+{
+    const uint32_t NB = 1u << a.lb;
+    const uint64_t m = (uint64_t)NB * a.nblocks;
+    hipLaunchKernelGGL(k_mb_part<false>, dim3(a.nblocks), dim3(256), NB * 4, s, a);
+    hm_launch_scan(s, a.bcnt, m, partial, a.boff, a.boff + m);
+    hipLaunchKernelGGL(k_mb_part<true>, dim3(a.nblocks), dim3(256), NB * 12, s, a);
+    hipLaunchKernelGGL(k_mb_merge, dim3(NB), dim3(HM_MB_THREADS), 0, s, a);
+}
+
 static unsigned hm_mgrid(uint64_t n, unsigned cap)
 {
     uint64_t b = (n + 255) / 256;

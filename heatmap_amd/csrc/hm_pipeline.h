@@ -541,6 +541,28 @@ struct HmRouteArgs {
     uint64_t* counts_out;
 };
 unsigned hm_route_blocks(uint64_t n);
+/* bucketed merge of (key, count) cells: hash-partition into 2^lb buckets
+ * (count + scatter passes over nblocks input chunks), then one block per
+ * bucket sums equal keys in an LDS table and writes the distinct cells */
+#define HM_MB_TS 8192                 /* LDS table slots per merge block */
+#define HM_MB_THREADS 1024
+struct HmMergeArgs {
+    const uint64_t* keys;
+    const uint64_t* counts;
+    uint64_t n;
+    int lb;
+    uint32_t nblocks;
+    uint64_t* bcnt;            /* [2^lb * nblocks] cells per (bucket, chunk), bucket-major */
+    uint64_t* boff;            /* its exclusive scan, total at [2^lb * nblocks] */
+    uint64_t* pkeys;           /* partitioned cells */
+    uint64_t* pcounts;
+    uint64_t* keys_out;
+    uint64_t* counts_out;
+    uint64_t cap;
+    unsigned long long* cursor;
+    unsigned long long* overflow;   /* an LDS table filled up: the caller falls back */
+};
+void hm_launch_merge_buckets(hipStream_t s, const HmMergeArgs& a, uint64_t* partial);
 void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter);
 void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t);
 void hm_launch_cells_merge_unique(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n,

@@ -46,6 +46,8 @@ CASES = {
     "hotspots_1e9_z0-18": ("hotspots", 0, 0, 1_000_000_000, 0, 18),
     "skew_1e9_z0-18": ("skew", 0, 0, 1_000_000_000, 0, 18),
     "hotspots_2e8_z0-18_stream20x10M": ("hotspots", 0, 0, 200_000_000, 0, 18),
+    # >= 2^19 keys per level-1 bucket: the 3-zoom spread plan at its default threshold
+    "uniform_6e8_z0-18": ("uniform", 0, 0, 600_000_000, 0, 18),
     "hotspots_1e7_start0_z0-18": ("hotspots", 0, 0, 10_000_000, 0, 18),
     "hotspots_1e7_start70M_z0-18": ("hotspots", 0, 70_000_000, 10_000_000, 0, 18),
     "hotspots_1e7_start190M_z0-18": ("hotspots", 0, 190_000_000, 10_000_000, 0, 18),

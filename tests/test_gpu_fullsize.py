@@ -62,7 +62,7 @@ def _golden(name):
 
 
 @pytest.mark.parametrize("name,hot", [("hotspots_1e9_z0-18", 1), ("hotspots_1e9_z0-18", 0),
-                                      ("skew_1e9_z0-18", 1), ("skew_1e9_z0-18", 0)])
+                                      ("skew_1e9_z0-18", 1), ("skew_1e9_z0-18", 0), ("uniform_6e8_z0-18", 1)])
 def test_fullsize_cloud(gpu, name, hot):
     torch = gpu
     g = _golden(name)
@@ -79,6 +79,8 @@ def test_fullsize_cloud(gpu, name, hot):
         assert int(st[6]) == 1
     if not hot:
         assert int(st[6]) == 0
+    if name.startswith("uniform"):
+        assert int(st[7]) == 3       # the spread plan, by default at this size
     assert device_digest(torch, buf.keys[:m], buf.counts[:m]) == g["digest"]
 
 
