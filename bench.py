@@ -194,7 +194,7 @@ def cpu_baseline(args, lat_dev=None, lon_dev=None):
     assert r["status"] == 0
     return {"value": n / dt, "unit": "points/s", "cores": int(r["threads"]), "kind": "port",
             "sample": "first %d of the %s points (seed %d), zooms %d-%d; C oracle (glibc projection, OpenMP x%d; "
-                      "serial radix sort + RLE cascade), %.1f s"
+                      "OpenMP LSD radix sort + RLE zoom cascade), %.1f s"
                       % (n, args.kind, args.seed, args.zmin, args.zmax, int(r["threads"]), dt)}
 
 
