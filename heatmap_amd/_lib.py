@@ -18,6 +18,7 @@ HM_E_NAN = 1
 HM_E_DOMAIN = 2
 HM_E_INF = 3
 HM_E_RANGE = 8
+HM_BIGCOL = 10        # hm_project: column beyond int64, returned as an integer-valued double's bits
 HM_E_EXOTIC = 9
 HM_E_ARG = 16
 HM_E_CAPACITY = 17

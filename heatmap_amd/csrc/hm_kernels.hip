@@ -78,11 +78,20 @@ __global__ __launch_bounds__(256) void k_project(const double* __restrict__ lat,
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
         int64_t r = 0, c = 0;
         int slow = 0;
-        const int st = hm_project_point(lat[i], lon[i], zoom, &r, &c, &slow, tab);
-        row[i] = st == HM_OK ? r : 0;
-        col[i] = st == HM_OK ? c : 0;
+        int st = hm_project_point(lat[i], lon[i], zoom, &r, &c, &slow, tab);
+        if (HM_UNLIKELY(st == HM_E_RANGE)) {
+            /* the row projected (its errors come first), the column is beyond
+             * int64: return it exactly, as an integer-valued double */
+            if (hm_row(lat[i], zoom, &r, &slow, tab) == HM_OK) {
+                c = __double_as_longlong(floor((lon[i] + 180.0) / 360.0 * hm_exp2i(zoom)));
+                st = HM_BIGCOL;
+            }
+        }
+        const bool good = st == HM_OK || st == HM_BIGCOL;
+        row[i] = good ? r : 0;
+        col[i] = good ? c : 0;
         status[i] = (uint8_t)st;
-        if (HM_UNLIKELY(st != HM_OK)) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+        if (HM_UNLIKELY(!good)) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
         const uint64_t sm = __ballot(slow);
         if (sm && hm_lane() == __ffsll((unsigned long long)sm) - 1) atomicAdd(slow_count, (unsigned long long)__popcll(sm));
     }

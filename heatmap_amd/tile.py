@@ -32,6 +32,24 @@ def _scalar_project(lat, lon, zoom):
     return p
 
 
+def _cols(p):
+    """Columns of a projection as Python ints: those beyond int64 (status
+    HM_BIGCOL) come back as integer-valued doubles, exact (tile.py:21 prints
+    them as unbounded ints)."""
+    big = p.status == _lib.HM_BIGCOL
+    if not big.any():
+        return p.col
+    out = p.col.astype(object)
+    for i in np.flatnonzero(big).tolist():
+        out[i] = int(np.array([p.col[i]], np.int64).view(np.float64)[0])
+    return out
+
+
+def _status(p, i=0):
+    st = int(p.status[i])
+    return _lib.HM_OK if st == _lib.HM_BIGCOL else st
+
+
 class Tile:
     MAX_ZOOM = 16
     MIN_ZOOM = 0
@@ -41,10 +59,10 @@ class Tile:
     def tile_id_from_lat_long(cls, latitude, longitude, zoom):
         """tile.py:9-13: "z_row_col"; row is evaluated (and raises) first."""
         p = _scalar_project(latitude, longitude, zoom)
-        st = int(p.status[0])
+        st = _status(p)
         if st != _lib.HM_OK:
             _lib.raise_for(st)
-        return Tile.tile_id_from_row_column(int(p.row[0]), int(p.col[0]), zoom)
+        return Tile.tile_id_from_row_column(int(p.row[0]), int(_cols(p)[0]), zoom)
 
     @classmethod
     def row_from_latitude(cls, latitude, zoom):
@@ -59,10 +77,10 @@ class Tile:
     def column_from_longitude(cls, longitude, zoom):
         """tile.py:19-21."""
         p = _scalar_project(0.0, longitude, zoom)
-        st = int(p.status[0])
+        st = _status(p)
         if st != _lib.HM_OK:
             _lib.raise_for(st)
-        return int(p.col[0])
+        return int(_cols(p)[0])
 
     # vectorised forms: one device call for many points
     @classmethod
@@ -75,13 +93,13 @@ class Tile:
     def columns_from_longitudes(cls, longitudes, zoom):
         lon = np.asarray(longitudes, dtype=np.float64)
         p = device.project(np.zeros_like(lon), lon, zoom, raise_errors=True)
-        return p.col
+        return _cols(p)      # int64, or Python ints when a column passes int64
 
     @classmethod
     def tile_ids_from_lat_longs(cls, latitudes, longitudes, zoom):
         p = device.project(np.asarray(latitudes, np.float64), np.asarray(longitudes, np.float64), zoom,
                            raise_errors=True)
-        return ["%d_%d_%d" % (zoom, r, c) for r, c in zip(p.row.tolist(), p.col.tolist())]
+        return ["%d_%d_%d" % (zoom, r, c) for r, c in zip(p.row.tolist(), list(_cols(p)))]
 
     # --- ids ------------------------------------------------------------------
     @classmethod

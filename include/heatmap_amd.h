@@ -58,7 +58,8 @@ extern "C" {
 #define HM_E_DOMAIN 2    /* ValueError("math domain error")  tan(+-inf) / log(<=0), tile.py:17 */
 #define HM_E_INF 3       /* OverflowError("cannot convert float infinity to integer") tile.py:21 */
 #define HM_E_RANGE 8     /* representable by the reference but not by this path:
-                            |col| >= 2^63, or (cells outside the square) a
+                            hm_count*: |col| >= 2^63 (hm_project returns those
+                            columns, HM_BIGCOL), or (cells outside the square) a
                             zoom-0 tile row outside [-16, 16) / column outside
                             [-2^47, 2^47).  (Latitudes of any magnitude are
                             projected: glibc's Payne-Hanek reduction is
@@ -70,6 +71,12 @@ extern "C" {
                             host side (heatmap_amd/stream.py) then splits the
                             batch and counts those points with hm_count_grouped;
                             hm_count* bin such points directly. */
+#define HM_BIGCOL 10     /* hm_project only, not an error: the point projected
+                            and its column is beyond int64 (|lon| > ~1.6e15 deg
+                            at zoom 21); col holds the column as the bits of
+                            an IEEE double -- floor((lon + 180.0) / 360.0 *
+                            2^z), integer-valued and exact, which the reference
+                            prints as a Python int (tile.py:21) */
 #define HM_E_ARG 16      /* bad argument (zoom range, null pointer, n < 0) */
 #define HM_E_CAPACITY 17 /* output arrays too small; *n_out holds the size needed */
 #define HM_E_HIP 18      /* HIP runtime error (no device, launch failure) */

@@ -13,16 +13,40 @@ pytestmark = pytest.mark.gpu
 
 
 def test_project_kat(gpu):
+    """All 30k reference KATs; a column beyond int64 (KAT status 8) comes back
+    exactly (HM_BIGCOL: an integer-valued double) and equals the reference's
+    Python int (projection_kat_bigcols.json)."""
+    from heatmap_amd import _lib
+
     d = np.load(os.path.join(GOLDEN, "projection_kat.npz"))
+    big = {int(k): int(v) for k, v in json.load(open(os.path.join(GOLDEN, "projection_kat_bigcols.json"))).items()}
     bad = 0
+    nbig = 0
     for z in np.unique(d["zoom"]):
-        m = d["zoom"] == z
+        m = np.flatnonzero(d["zoom"] == z)
         p = device.project(d["lat"][m], d["lon"][m], int(z))
         re_, ce = d["row_err"][m], d["col_err"][m]
-        exp = np.where(re_ != 0, re_, np.where(ce == 8, 8, ce))
+        exp = np.where(re_ != 0, re_, np.where(ce == 8, _lib.HM_BIGCOL, ce))
         ok = (p.status == exp) & ((exp != 0) | ((p.row == d["row"][m]) & (p.col == d["col"][m])))
+        for j in np.flatnonzero(exp == _lib.HM_BIGCOL).tolist():
+            i = int(m[j])
+            got = int(np.array([p.col[j]], np.int64).view(np.float64)[0])
+            ok[j] = ok[j] and p.row[j] == d["row"][i] and i in big and got == big[i]
+            nbig += 1
         bad += int((~ok).sum())
     assert bad == 0
+    assert nbig == len(big)
+
+
+def test_tile_big_column_ids(gpu):
+    """Tile.tile_id_from_lat_long prints a column beyond int64 as the
+    reference does (tests/golden/tile_ids.json holds such ids)."""
+    from heatmap_amd.tile import Tile
+
+    for la, lo, z, want in json.load(open(os.path.join(GOLDEN, "tile_ids.json"))):
+        if "Error" in want:
+            continue
+        assert Tile.tile_id_from_lat_long(float(la), float(lo), z) == want, (la, lo, z)
 
 
 @pytest.mark.parametrize("kind,n,zmin,zmax", [("uniform", 20000, 0, 14), ("hotspots", 200000, 0, 18),
