@@ -35,7 +35,7 @@ def test_project_kat(gpu):
             nbig += 1
         bad += int((~ok).sum())
     assert bad == 0
-    assert nbig == len(big)
+    assert nbig == sum(1 for i in big if d["row_err"][i] == 0)   # (a row error wins, tile.py:10-11)
 
 
 def test_tile_big_column_ids(gpu):
