@@ -688,11 +688,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             uint64_t total_cap = (uint64_t)bound;
             for (int attempt = 0;; attempt++) {
                 if (attempt > 0) {
+                    /* a digit's shards stay consecutive: its keys' logical
+                     * positions are one range (k_level1_buckets) */
                     total_cap = 0;
-                    for (int i = 0; i < FS; i++) {
-                        hb[i] = (uint32_t)total_cap;
-                        total_cap += hc[i];
-                    }
+                    for (int d = 0; d < HM_D1; d++)
+                        for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
+                            hb[hm_l1i(d, sh)] = (uint32_t)total_cap;
+                            total_cap += hc[hm_l1i(d, sh)];
+                        }
                     if (total_cap >= 0xFFF00000ull) return HM_FALLBACK;
                     HIPCHK(hipMemcpyAsync(rcap, hc, FS * 4, hipMemcpyHostToDevice, s));
                     HIPCHK(hipMemcpyAsync(rbase, hb, FS * 4, hipMemcpyHostToDevice, s));

@@ -102,6 +102,28 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
     return r;
 }
 
+template <int THREADS>
+__device__ __forceinline__ uint64_t hm_block_excl_scan64(uint64_t v, unsigned long long* scratch, uint64_t* total)
+{
+    constexpr int NW = THREADS / 64;
+    const int lane = hm_lane();
+    const int w = threadIdx.x >> 6;
+    const uint64_t inc = hm_wave_incl_scan64(v);
+    if (lane == 63) scratch[w] = inc;
+    __syncthreads();
+    if (w == 0) {
+        const uint64_t s = lane < NW ? scratch[lane] : 0ull;
+        const uint64_t si = hm_wave_incl_scan64(s);
+        if (lane < NW) scratch[lane] = si - s;
+        if (lane == NW - 1) scratch[NW] = si;
+    }
+    __syncthreads();
+    const uint64_t r = scratch[w] + inc - v;
+    *total = scratch[NW];
+    __syncthreads();
+    return r;
+}
+
 /* LDS histogram increment / slot reservation, branch-free.  The lanes whose
  * key equals the first active lane's are added by one atomic of their first
  * lane (the skew case, SURVEY.md section 7 hard part 3: a wave of one key

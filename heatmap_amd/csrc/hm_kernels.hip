@@ -128,7 +128,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     /* digit of each staged key; until the count is done it holds each
      * digit's region (base, capacity << 1 | sharded) for this tile */
     __shared__ __attribute__((aligned(8))) uint16_t sdig[HM_T1 + 64];
-    __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
+    __shared__ unsigned long long scr[HM_P1_THREADS / 64 + 1];
     /* the projection's polynomial table; after the projection it holds, per
      * digit, (region position - stage offset) */
     __shared__ double tab[HM_YTAB_N];
@@ -196,8 +196,8 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     uint32_t smk[PERD], rcap2[PERD][2], rbase2[PERD][2];
 #pragma unroll
     for (int q = 0; q < PERD; q++) {
-        const int d = tid * PERD + q;
-        const uint32_t s0 = (uint32_t)d * HM_L1_SHARDS, s1 = s0 + (blockIdx.x & (HM_L1_SHARDS - 1));
+        const int d = q * HM_P1_THREADS + tid;
+        const uint32_t s0 = hm_l1i(d, 0), s1 = hm_l1i(d, blockIdx.x & (HM_L1_SHARDS - 1));
         const bool lv = live(d);
         smk[q] = lv ? a.smask[d] : 0u;
         rcap2[q][0] = lv ? a.rcap[s0] : 0u;
@@ -264,7 +264,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
      * the projection, the count reads it back */
 #pragma unroll
     for (int q = 0; q < PERD; q++) {
-        const int d = tid * PERD + q;
+        const int d = q * HM_P1_THREADS + tid;
         const uint32_t sh = smk[q] != 0;
         rinfo[d] = make_uint2(sh ? rbase2[q][1] : rbase2[q][0], ((sh ? rcap2[q][1] : rcap2[q][0]) << 1) | sh);
     }
@@ -425,30 +425,36 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     uint32_t gpos[PER];
     uint32_t rcap[PER], rbase[PER];
     uint32_t s = 0;
+    /* thread t holds digits q * T + t: a wave's lanes reserve for
+     * consecutive digits (coalesced atomics on the shard-major fill words) */
+    uint64_t packed = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * HM_P1_THREADS + tid;
         const uint2 ri = rinfo[d];
         rbase[q] = ri.x;
         rcap[q] = ri.y >> 1;
-        const uint32_t slot = (uint32_t)d * HM_L1_SHARDS + ((ri.y & 1u) ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u);
+        const uint32_t slot = hm_l1i(d, (ri.y & 1u) ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u);
         cnt[q] = live(d) ? cur[hm_cur_slot(d, wd)] : 0u;
         gpos[q] = 0;
         if (cnt[q]) gpos[q] = atomicAdd(&a.fill[slot], cnt[q]);
-        s += cnt[q];
+        packed |= (uint64_t)cnt[q] << (21 * q);
     }
-    /* exclusive scan of the digit histogram */
-    uint32_t total;
-    uint32_t off = hm_block_excl_scan<HM_P1_THREADS>(s, scr, &total);
+    static_assert(PER <= 3 && HM_T1 < (1 << 21), "three 21-bit digit counts per scanned word");
+    /* exclusive scan in digit order (q major, then thread): one scan of the
+     * three counts packed in 21-bit fields */
+    uint64_t tot64;
+    const uint64_t off64 = hm_block_excl_scan64<HM_P1_THREADS>(packed, (unsigned long long*)scr, &tot64);
     uint32_t offq[PER];
+    uint32_t total = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        offq[q] = off;
-        off += cnt[q];
+        offq[q] = total + (uint32_t)((off64 >> (21 * q)) & 0x1FFFFFu);
+        total += (uint32_t)((tot64 >> (21 * q)) & 0x1FFFFFu);
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * HM_P1_THREADS + tid;
         if (live(d)) cur[hm_cur_slot(d, wd)] = offq[q];
     }
     __syncthreads();
@@ -468,7 +474,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     bool over = false;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * HM_P1_THREADS + tid;
         if (live(d)) {
             const bool fits = cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q];
             over |= cnt[q] && !fits;
@@ -678,8 +684,8 @@ __global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ 
         if (live)
             for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
                 const uint32_t cs = sh < ns ? c : 0u;
-                rcap[d * HM_L1_SHARDS + sh] = cs;
-                rbase[d * HM_L1_SHARDS + sh] = (uint32_t)pos;   /* total < 2^32: the host's bound */
+                rcap[hm_l1i(d, sh)] = cs;
+                rbase[hm_l1i(d, sh)] = (uint32_t)pos;   /* total < 2^32: the host's bound */
                 pos += cs;
             }
         base += all;
@@ -726,7 +732,7 @@ __global__ __launch_bounds__(1024) void k_level1_buckets(HmL1Args a)
     const int ns = d < a.F ? a.smask[d] + 1 : 0;
 #pragma unroll
     for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
-        f[sh] = sh < ns ? a.fill[d * HM_L1_SHARDS + sh] : 0u;
+        f[sh] = sh < ns ? a.fill[hm_l1i(d, sh)] : 0u;
         nk += f[sh];
         nr += f[sh] != 0;
     }
@@ -742,7 +748,7 @@ __global__ __launch_bounds__(1024) void k_level1_buckets(HmL1Args a)
     if (ne) {
         /* logical key positions of the bucket: [region base, + nk), its
          * non-empty shards' keys one after the other */
-        const uint32_t kb = a.rbase[d * HM_L1_SHARDS];
+        const uint32_t kb = a.rbase[hm_l1i(d, 0)];
         a.out.nkeys[idx] = nk;
         a.out.nruns[idx] = nr;
         a.out.rbase[idx] = r0;
@@ -755,7 +761,7 @@ __global__ __launch_bounds__(1024) void k_level1_buckets(HmL1Args a)
 #pragma unroll
         for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
             if (f[sh]) {
-                a.runs[j] = make_uint2(a.rbase[d * HM_L1_SHARDS + sh], f[sh]);
+                a.runs[j] = make_uint2(a.rbase[hm_l1i(d, sh)], f[sh]);
                 a.excl[j] = at;
                 at += f[sh];
                 j++;
@@ -1566,7 +1572,7 @@ __global__ __launch_bounds__(256) void k_hot_nr(HmHotRunArgs a)
     for (uint32_t h = blockIdx.x * 256 + threadIdx.x; h < H; h += gridDim.x * 256) {
         uint32_t nr = 0;
 #pragma unroll
-        for (int sh = 0; sh < HM_L1_SHARDS; sh++) nr += a.fill[(HM_MAX_F1 + h) * HM_L1_SHARDS + sh] != 0;
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) nr += a.fill[hm_l1i(HM_MAX_F1 + h, sh)] != 0;
         if (nr) a.nr[hm_hot_child(a, a.tiles[h])] = nr;
     }
 }
@@ -1578,12 +1584,12 @@ __global__ __launch_bounds__(256) void k_hot_runs(HmHotRunArgs a)
         uint64_t j = 0;
         bool any = false;
 #pragma unroll
-        for (int sh = 0; sh < HM_L1_SHARDS; sh++) any |= a.fill[(HM_MAX_F1 + h) * HM_L1_SHARDS + sh] != 0;
+        for (int sh = 0; sh < HM_L1_SHARDS; sh++) any |= a.fill[hm_l1i(HM_MAX_F1 + h, sh)] != 0;
         if (!any) continue;
         const uint64_t rb = a.runbase[hm_hot_child(a, a.tiles[h])];
 #pragma unroll
         for (int sh = 0; sh < HM_L1_SHARDS; sh++) {
-            const uint32_t k = (HM_MAX_F1 + h) * HM_L1_SHARDS + sh;
+            const uint32_t k = hm_l1i(HM_MAX_F1 + h, sh);
             const uint32_t f = a.fill[k];
             if (f) {
                 a.flat[rb + j] = make_uint2(a.rbase[k], f);

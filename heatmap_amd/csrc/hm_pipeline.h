@@ -31,6 +31,10 @@
 #define HM_D1 (HM_MAX_F1 + HM_MAX_HOT)      /* level-1 digit slots: cold z1 digits, then hot tiles */
 #define HM_HOT_SLOTS 2048                   /* hot-tile hash (load <= 1/4) */
 #define HM_HOT_EMPTY 0xFFFFFFFFu
+/* level-1 (digit, shard) arrays (fill, rbase, rcap) are shard-major: the
+ * digits one wave reserves for sit in consecutive words, so its returning
+ * atomics coalesce into a few 64-B requests instead of one per digit */
+__host__ __device__ inline uint32_t hm_l1i(uint32_t d, uint32_t sh) { return sh * HM_D1 + d; }
 /* levels >= 2 */
 #ifndef HM_PN_THREADS
 #define HM_PN_THREADS 1024
@@ -190,9 +194,9 @@ struct HmPart1Args {
     unsigned long long* redo_count;
     uint64_t redo_cap;
     void* keys_out;
-    uint32_t* fill;           /* [F * HM_L1_SHARDS] per (digit, shard) */
-    const uint32_t* rbase;    /* [F * HM_L1_SHARDS] */
-    const uint32_t* rcap;     /* [F * HM_L1_SHARDS] */
+    uint32_t* fill;           /* [HM_D1 * HM_L1_SHARDS] per (digit, shard): hm_l1i */
+    const uint32_t* rbase;    /* [HM_D1 * HM_L1_SHARDS] */
+    const uint32_t* rcap;     /* [HM_D1 * HM_L1_SHARDS] */
     const uint8_t* smask;     /* [F]: shards of digit d - 1 (0 or HM_L1_SHARDS - 1) */
     unsigned long long* overflow;
     unsigned long long* err_word;
