@@ -70,6 +70,7 @@ struct hm_ctx {
     int hot = 1;
     double hot_inv_share = 2048;
     double hot_min_keys = 65536;
+    int run_shard_bits = -1;   /* HM_RUN_SHARD_BITS: level >= 2 run-counter shards (-1: by plan) */
 };
 
 enum {
@@ -190,6 +191,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     if (const char* e = getenv("HM_HOT")) c->hot = atoi(e);
     if (const char* e = getenv("HM_HOT_INV_SHARE")) c->hot_inv_share = atof(e);
     if (const char* e = getenv("HM_HOT_MIN_KEYS")) c->hot_min_keys = atof(e);
+    if (const char* e = getenv("HM_RUN_SHARD_BITS")) c->run_shard_bits = atoi(e);
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -242,6 +244,10 @@ int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
     } else if (!strcmp(name, "HM_HOT_MIN_KEYS")) {
         prev = c->hot_min_keys;
         c->hot_min_keys = value;
+    } else if (!strcmp(name, "HM_RUN_SHARD_BITS")) {
+        if (value > 5) return HM_E_ARG;
+        prev = c->run_shard_bits;
+        c->run_shard_bits = value < 0 ? -1 : (int)value;
     } else {
         return HM_E_ARG;
     }
@@ -567,6 +573,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
 
     uint32_t* seg1 = nullptr;   /* level-1 items' run tables (k_partition_fr) */
     bool hot_on = false;        /* hot tiles sampled and looked up by level 1 */
+    bool spread = false;        /* levels 2.. take fewer zooms (spread_replan) */
     uint32_t nhot = 0;          /* hot tiles found */
     HmHotRunArgs hr;            /* hot tiles as level-2 children */
     memset(&hr, 0, sizeof(hr));
@@ -836,6 +843,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             /* levels 2.. may take the spread plan (the level-1 pass is the
              * same under both: its output is u32 keys whenever L > 1) */
             if (L > 1 && !nhot) spread_replan(ctx->host_aux, F, n, zb, zs, &L, ctx->spread_min_keys);
+            spread = L > 2 && zs[1] - zs[0] < HM_LEVEL_ZOOMS;
             ctx->last_levels = L;
             V.count = (uint32_t)(down[0] >> 32);
             V.items = (uint32_t)(down[0] & 0xFFFFFFFFull);
@@ -873,7 +881,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         /* run-counter shards: up to 32 (a hot child takes one returning atomic
          * per parent work item; one counter per child made k_partition 16%
          * slower), fewer when the dense child space is large; <= 2^25 */
-        int sb = HM_RUN_SHARD_BITS;
+        /* with hot tiles (their children skip this level) or the spread plan,
+         * no child is hot: one counter per child, and the partition kernels'
+         * run-slot atomics coalesce (lanes own consecutive digits) */
+        int sb = ctx->run_shard_bits >= 0 ? ctx->run_shard_bits : ((nhot || spread) ? 0 : HM_RUN_SHARD_BITS);
         while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
         const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
         if (run_cap >= (1ull << 32)) return HM_E_NOMEM;

@@ -124,6 +124,30 @@ __device__ __forceinline__ uint64_t hm_block_excl_scan64(uint64_t v, unsigned lo
     return r;
 }
 
+/* Digit slots d = q * THREADS + t of thread t (q < PER): a wave's lanes own
+ * consecutive digits, so per-digit global counters they update coalesce.
+ * Exclusive offsets in digit order (q major, then thread) from ONE 64-bit
+ * block scan of the PER counts packed in 64/PER-bit fields (each count, and
+ * the block's total per q, must stay below 2^(64/PER)). */
+template <int THREADS, int PER>
+__device__ __forceinline__ void hm_digit_offsets(const uint32_t (&cnt)[PER], uint32_t (&off)[PER],
+                                                 unsigned long long* scratch)
+{
+    constexpr int FB = 64 / PER;
+    constexpr uint64_t FM = (FB == 64) ? ~0ull : ((1ull << FB) - 1);
+    uint64_t packed = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) packed |= (uint64_t)cnt[q] << (FB * q);
+    uint64_t tot;
+    const uint64_t o = hm_block_excl_scan64<THREADS>(packed, scratch, &tot);
+    uint32_t base = 0;
+#pragma unroll
+    for (int q = 0; q < PER; q++) {
+        off[q] = base + (uint32_t)((o >> (FB * q)) & FM);
+        base += (uint32_t)((tot >> (FB * q)) & FM);
+    }
+}
+
 /* LDS histogram increment / slot reservation, branch-free.  The lanes whose
  * key equals the first active lane's are added by one atomic of their first
  * lane (the skew case, SURVEY.md section 7 hard part 3: a wave of one key

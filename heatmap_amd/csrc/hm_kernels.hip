@@ -1081,6 +1081,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     __shared__ __attribute__((aligned(16))) uint32_t stage[HM_TN + 64];
     __shared__ uint32_t cur[HM_MAX_FN + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ uint32_t scr[HM_PN_THREADS / 64 + 1];
+    __shared__ unsigned long long scr64[HM_PN_THREADS / 64 + 1];
     __shared__ HmRunLds<512> L;
     HM_STAMP(0);
     const int tid = threadIdx.x;
@@ -1127,16 +1128,15 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     HM_STAMP(7);
     const uint32_t total = it.b - it.a;
     constexpr int PER = HM_MAX_FN / HM_PN_THREADS;
+    static_assert(HM_TN < (1 << (64 / PER)), "packed digit counts");
     uint32_t cnt[PER];
-    uint32_t s = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * HM_PN_THREADS + tid;
         cnt[q] = d < F ? cur[hm_cur_slot(d, ww)] : 0u;
-        s += cnt[q];
     }
-    uint32_t tot2;
-    uint32_t off = hm_block_excl_scan<HM_PN_THREADS>(s, scr, &tot2);
+    uint32_t offq[PER];
+    hm_digit_offsets<HM_PN_THREADS, PER>(cnt, offq, scr64);
     HM_STAMP(8);
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
     const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
@@ -1144,19 +1144,16 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     /* run-slot atomics are issued here and their results consumed only after
      * the scatter, so their latency hides behind it */
     uint32_t idx[PER];
-    uint32_t offq[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
-        offq[q] = off;
+        const int d = q * HM_PN_THREADS + tid;
         idx[q] = 0;
         if (d < F && cnt[q])
             idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
-        off += cnt[q];
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * HM_PN_THREADS + tid;
         if (d < F) cur[hm_cur_slot(d, ww)] = offq[q];
     }
     constexpr int KPT = HM_TN / HM_PN_THREADS;
@@ -1191,7 +1188,7 @@ __global__ __launch_bounds__(HM_PN_THREADS, 8) void k_partition(HmPartNArgs a)
     for (uint32_t i = tid; i < total; i += HM_PN_THREADS) out[i] = so[i];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * HM_PN_THREADS + tid;
         if (d < F && cnt[q]) {
             const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
             a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);
@@ -1219,7 +1216,7 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     /* key e of the item at stage[sh + e], sh = it.a mod V: the copy-out then
      * moves 16-B vectors aligned on both sides */
     __shared__ __attribute__((aligned(16))) OutT stage[HM_TN + 64 + V];
-    __shared__ uint32_t scr[T / 64 + 1];
+    __shared__ unsigned long long scr[T / 64 + 1];
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
     const uint32_t g = hm_block_id();
@@ -1274,32 +1271,31 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     HM_STAMP_M(3, 2);
     __syncthreads();
     HM_STAMP_M(3, 3);
+    static_assert(HM_TN < (1 << (64 / PER)), "packed digit counts");
     uint32_t cnt[PER];
-    uint32_t s = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * T + tid;
         cnt[q] = d < F ? cur[hm_cur_slot(d, ww)] : 0u;
-        s += cnt[q];
     }
-    uint32_t tot2;
-    uint32_t off = hm_block_excl_scan<T>(s, scr, &tot2);
+    uint32_t offq[PER];
+    hm_digit_offsets<T, PER>(cnt, offq, scr);
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
     const uint32_t sh = it.j & ((1u << a.shard_bits) - 1u);
     const uint64_t cap = ((uint64_t)it.nitems + (1u << a.shard_bits) - 1) >> a.shard_bits;
-    uint32_t idx[PER], offq[PER];
+    /* lanes own consecutive digits: with one run counter per child
+     * (shard_bits 0) a wave's run-slot atomics coalesce */
+    uint32_t idx[PER];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
-        offq[q] = off;
+        const int d = q * T + tid;
         idx[q] = 0;
         if (d < F && cnt[q])
             idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
-        off += cnt[q];
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * T + tid;
         if (d < F) cur[hm_cur_slot(d, ww)] = offq[q];
     }
     __syncthreads();
@@ -1330,7 +1326,7 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
-        const int d = tid * PER + q;
+        const int d = q * T + tid;
         if (d < F && cnt[q]) {
             const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, a.shard_bits);
             a.runs_out[rb + sh * cap + idx[q]] = make_uint2(it.a + offq[q], cnt[q]);

@@ -112,6 +112,8 @@ int hm_ctx_destroy(hm_ctx* ctx);
  *   HM_HOT_INV_SHARE    a tile is hot with >= 1/this of the sampled points
  *                       (default 2048)
  *   HM_HOT_MIN_KEYS     ... and >= this many estimated points (default 65536)
+ *   HM_RUN_SHARD_BITS   log2 run counters per level-2+ child (0..5; default
+ *                       -1: 0 with hot tiles or the spread plan, else 4)
  * Returns the previous value in *old (if not NULL). */
 int hm_ctx_tune(hm_ctx* ctx, const char* name, double value, double* old);
 
