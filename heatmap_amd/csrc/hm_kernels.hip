@@ -295,19 +295,21 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
         int64_t r, c;
         int ok;
+        bool dom;
         if (FROM_TILES) {
             r = __double_as_longlong(pa);
             c = __double_as_longlong(po);
             ok = 1;
+            dom = ((uint64_t)r < lim) & ((uint64_t)c < lim);
         } else {
             int32_t r32, c32;
             ok = hm_project_fast(pa, po, scale, kz, &r32, &c32, tab);
             r = r32;
             c = c32;
+            dom = ((uint32_t)r32 < lim) & ((uint32_t)c32 < lim);   /* lim <= 2^21: 32-bit tests */
         }
-        const bool inb = i < n;
+        const bool inb = FULLT || i < n;   /* a whole tile is in range */
         const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
-        const bool dom = ((uint64_t)r < lim) & ((uint64_t)c < lim);
         redo |= (uint32_t)(inb & !(ok & dom)) << k;
         const bool v = inb & ok & dom & kept;
         dig[k] = v ? ((((uint32_t)r >> hb) << wd) | ((uint32_t)c >> hb)) : 0xFFFFFFFFu;
