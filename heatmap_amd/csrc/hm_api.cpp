@@ -84,6 +84,7 @@ enum {
     ST_XCURSOR = 7,
     ST_OVERFLOW = 8,
     ST_NHOT = 9,          /* hot tiles of this call (k_hot_select; low 32 bits) */
+    ST_L1TOTAL = 10,      /* level-1 regions' total capacity (k_l1_sizes) */
     ST_COUNT = 16
 };
 
@@ -137,6 +138,20 @@ static int ensure(hm_ctx* c, int slot, size_t bytes, void** out)
     }
     *out = b.p;
     return HM_OK;
+}
+
+/* the arena is a cache: after an allocation failure every buffer is
+ * released at the API boundary (nothing of the failed call is in flight
+ * past the synchronisation) so the next call starts from an empty arena */
+static void arena_release(hm_ctx* c)
+{
+    (void)hipStreamSynchronize(c->stream);
+    for (auto& b : c->bufs) {
+        if (b.p) (void)hipFree(b.p);
+        b.p = nullptr;
+        b.cap = 0;
+    }
+    (void)hipGetLastError();
 }
 
 #define ENSURE(slot, bytes, ptr)                                         \
@@ -687,10 +702,17 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             const double nn = (double)n + (double)(F + (hot_on ? HM_MAX_HOT : 0)) * (double)stride;
             const double M = F + std::min((double)F, nn / (64.0 * HM_T1)) * (HM_L1_SHARDS - 1) +
                              (hot_on ? (double)HM_MAX_HOT * HM_L1_SHARDS : 0.0);
-            const double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 + 1024.0;
-            if (bound >= (double)0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
-            hm_launch_l1_sizes(s, hist, F, hot_on ? hot_n : nullptr, stride, rcap, rbase, smask);
+            double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 + 1024.0;
+            hm_launch_l1_sizes(s, hist, F, hot_on ? hot_n : nullptr, stride, rcap, rbase, smask,
+                               ctx->state + ST_L1TOTAL);
             HIPCHK(hipGetLastError());
+            if (bound >= (double)0xFFF00000ull) {
+                /* the bound passes the u32 key positions (n above ~1.5e9):
+                 * read the exact total of the sized regions instead */
+                if ((st = read_state(ctx))) return st;
+                bound = (double)ctx->host_state[ST_L1TOTAL] + 1024.0;
+                if (bound >= (double)0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
+            }
             void* kout = nullptr;
             uint64_t total_cap = (uint64_t)bound;
             for (int attempt = 0;; attempt++) {
@@ -1157,11 +1179,16 @@ extern "C" int hm_count(hm_ctx* ctx, const double* lat, const double* lon, const
                         int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
     if (n > 0 && (!lat || !lon)) return HM_E_ARG;
-    int st = count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
+    int st = HM_OK;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        st = count_impl(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
                         xcells_out, xcapacity, nx_out);
-    if (st == HM_FALLBACK)
-        st = count_fallback(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity,
-                            n_out, xcells_out, xcapacity, nx_out);
+        if (st == HM_FALLBACK)
+            st = count_fallback(ctx, lat, lon, nullptr, nullptr, keep, n, zmin, zmax, keys_out, counts_out, capacity,
+                                n_out, xcells_out, xcapacity, nx_out);
+        if (st != HM_E_NOMEM) break;
+        arena_release(ctx);   /* cached buffers of earlier calls may be what is missing */
+    }
     return st;
 }
 
@@ -1170,11 +1197,16 @@ extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* co
                               int64_t* n_out, int64_t* xcells_out, int64_t xcapacity, int64_t* nx_out)
 {
     if (n > 0 && (!row || !col)) return HM_E_ARG;
-    int st = count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
+    int st = HM_OK;
+    for (int attempt = 0; attempt < 2; attempt++) {
+        st = count_impl(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity, n_out,
                         xcells_out, xcapacity, nx_out);
-    if (st == HM_FALLBACK)
-        st = count_fallback(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity,
-                            n_out, xcells_out, xcapacity, nx_out);
+        if (st == HM_FALLBACK)
+            st = count_fallback(ctx, nullptr, nullptr, row, col, keep, n, zmin, zmax, keys_out, counts_out, capacity,
+                                n_out, xcells_out, xcapacity, nx_out);
+        if (st != HM_E_NOMEM) break;
+        arena_release(ctx);
+    }
     return st;
 }
 
@@ -1222,7 +1254,12 @@ extern "C" int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lo
                                 int64_t capacity, int64_t* n_out)
 {
     if (n > 0 && (!lat || !lon)) return HM_E_ARG;
-    return grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    int st = grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    if (st == HM_E_NOMEM) {
+        arena_release(ctx);
+        st = grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    }
+    return st;
 }
 
 extern "C" int hm_count_grouped_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep,
@@ -1230,7 +1267,12 @@ extern "C" int hm_count_grouped_tiles(hm_ctx* ctx, const int64_t* row, const int
                                       int64_t capacity, int64_t* n_out)
 {
     if (n > 0 && (!row || !col)) return HM_E_ARG;
-    return grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    int st = grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    if (st == HM_E_NOMEM) {
+        arena_release(ctx);
+        st = grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    }
+    return st;
 }
 
 /* ------------------------------------------------------------------------ */

@@ -651,7 +651,7 @@ __device__ __forceinline__ uint32_t hm_l1_cap(uint32_t hist, uint64_t stride, in
 __global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ hist, int F,
                                                    const uint32_t* __restrict__ hot_n, uint64_t stride,
                                                    uint32_t* __restrict__ rcap, uint32_t* __restrict__ rbase,
-                                                   uint8_t* __restrict__ smask)
+                                                   uint8_t* __restrict__ smask, unsigned long long* total)
 {
     __shared__ unsigned long long wsum[1024 / 64];
     static_assert(HM_MAX_HOT <= 1024 && HM_MAX_F1 <= 1024, "one digit of each kind per thread");
@@ -692,12 +692,13 @@ __global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ 
             }
         base += all;
     }
+    if (t == 0 && total) *total = base;
 }
 
 void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, const uint32_t* hot_n, uint64_t stride,
-                        uint32_t* rcap, uint32_t* rbase, uint8_t* smask)
+                        uint32_t* rcap, uint32_t* rbase, uint8_t* smask, unsigned long long* total)
 {
-    hipLaunchKernelGGL(k_l1_sizes, dim3(1), dim3(1024), 0, s, hist, F, hot_n, stride, rcap, rbase, smask);
+    hipLaunchKernelGGL(k_l1_sizes, dim3(1), dim3(1024), 0, s, hist, F, hot_n, stride, rcap, rbase, smask, total);
 }
 
 void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist,

@@ -352,9 +352,10 @@ void hm_launch_part1(hipStream_t s, const HmPart1Args& a, uint32_t grid, bool ou
 void hm_launch_sample_digits(hipStream_t s, const HmPart1Args& a, uint64_t stride_pts, uint32_t* hist,
                              uint32_t* hot_counts);
 void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a);
-/* region sizes of the F cold digits and (hot_n) the hot tiles' digits */
+/* region sizes of the F cold digits and (hot_n) the hot tiles' digits; their
+ * total -> *total */
 void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, const uint32_t* hot_n, uint64_t stride,
-                        uint32_t* rcap, uint32_t* rbase, uint8_t* smask);
+                        uint32_t* rcap, uint32_t* rbase, uint8_t* smask, unsigned long long* total);
 void hm_launch_hot_nr(hipStream_t s, const HmHotRunArgs& a);
 void hm_launch_hot_runs(hipStream_t s, const HmHotRunArgs& a);
 void hm_launch_level1_buckets(hipStream_t s, const HmL1Args& a);
