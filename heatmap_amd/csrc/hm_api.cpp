@@ -656,10 +656,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             uint32_t* hot_n = (uint32_t*)(ctx->state + ST_NHOT);
             if (hot_on) {
                 ENSURE(B_HOT_COUNTS, (4ull << (2 * zb)), hot_counts);
-                ENSURE(B_HOT, (HM_MAX_HOT + HM_HOT_SLOTS) * 4, hot_tiles);
+                ENSURE(B_HOT, (HM_MAX_HOT + HM_HOT_SLOTS + 2 * HM_HOT_CAND + 1) * 4, hot_tiles);
                 ENSURE(B_HOT_PARENT, HM_MAX_F1, hot_parent);
                 hot_hash = hot_tiles + HM_MAX_HOT;
                 HIPCHK(hipMemsetAsync(hot_counts, 0, 4ull << (2 * zb), s));
+                HIPCHK(hipMemsetAsync(hot_hash + HM_HOT_SLOTS + 2 * HM_HOT_CAND, 0, 4, s));   /* candidates */
                 HIPCHK(hipMemsetAsync(hot_parent, 0, HM_MAX_F1, s));
                 a.hot_z = zb;
                 a.hot_hash = hot_hash;
@@ -688,6 +689,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 ha.hotparent = hot_parent;
                 ha.n = hot_n;
                 ha.hash = hot_hash;
+                ha.cand = hot_hash + HM_HOT_SLOTS;
                 hm_launch_hot_select(s, ha);
                 HIPCHK(hipGetLastError());
             }

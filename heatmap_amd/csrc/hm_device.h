@@ -186,6 +186,36 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t dummy, 
     return same ? base + r : old;
 }
 
+/* hm_lds_claim split in two, so several claims can be in flight: prep, the
+ * atomic (atomicAdd(&cur[g.idx], g.inc)), then pos.  The lanes whose key
+ * equals lane 0's (straight-line code: every lane active) are one atomic of
+ * lane 0; if lane 0 holds no valid key none merge.  `dummy_lane` = the
+ * caller's private dummy word of this lane. */
+struct HmClaim {
+    bool same;
+    uint32_t r, idx, inc;
+};
+
+__device__ __forceinline__ HmClaim hm_claim_prep(uint32_t key, bool valid, uint32_t dummy_lane)
+{
+    HmClaim g;
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    g.same = valid & (key == k0);
+    const uint64_t m = __ballot(g.same);
+    g.r = hm_mbcnt(m);
+    const bool lead = g.same & (g.r == 0);
+    const bool own = valid & !g.same;
+    g.idx = (lead | own) ? key : dummy_lane;
+    g.inc = lead ? (uint32_t)__popcll(m) : (uint32_t)own;
+    return g;
+}
+
+__device__ __forceinline__ uint32_t hm_claim_pos(const HmClaim& g, uint32_t old)
+{
+    /* a non-empty group holds lane 0, which added for it */
+    return g.same ? __builtin_amdgcn_readfirstlane(old) + g.r : old;
+}
+
 /* Multi-round wave aggregation for LDS histograms and slot claims.  Round r
  * takes the first lane not yet grouped, and every lane holding its key joins
  * that group; after HM_MERGE_ROUNDS rounds the remaining lanes go alone.  The
@@ -270,3 +300,7 @@ __device__ __forceinline__ uint32_t hm_skew(uint32_t d, int w)
 #define HM_SKEW_CUR 1
 #endif
 __device__ __forceinline__ uint32_t hm_cur_slot(uint32_t d, int w) { return HM_SKEW_CUR ? hm_skew(d, w) : d; }
+
+/* level-1 digit slot: cold digits (< HM_MAX_F1, a 2-D grid) skewed as
+ * hm_cur_slot, hot-tile digits as they are (no 2-D structure) */
+__device__ __forceinline__ uint32_t hm_dslot(uint32_t d, int w) { return d < 1024u ? hm_cur_slot(d, w) : d; }

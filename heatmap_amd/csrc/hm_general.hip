@@ -278,28 +278,41 @@ __global__ __launch_bounds__(256) void k_rle_emit(HmGenEmit e, const ulonglong2*
     }
 }
 
-/* grouped counts from tiles (hm_count_grouped_tiles): list the kept ones */
+/* grouped counts from tiles (hm_count_grouped_tiles): list the kept ones,
+ * one output reservation per block step of 256 * HM_TL_PPT points (as
+ * k_project_list: a per-wave reservation on one counter saturates it) */
+#define HM_TL_PPT 16
 __global__ __launch_bounds__(256) void k_tiles_list(const int64_t* __restrict__ rows, const int64_t* __restrict__ cols,
                                                     const uint8_t* __restrict__ keep, const uint32_t* __restrict__ group,
                                                     int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
                                                     unsigned long long* count)
 {
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t n_up = (n + 63) & ~63ll;   /* whole waves stay in the loop */
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
-        const bool p = i < n && (!keep || keep[i]);
-        const uint64_t m = __ballot(p);
-        if (!m) continue;
-        const int lead = __ffsll((unsigned long long)m) - 1;
-        unsigned long long b = 0;
-        if (hm_lane() == lead) b = atomicAdd(count, (unsigned long long)__popcll(m));
-        b = __shfl(b, lead, 64);
-        if (p) {
-            const uint64_t q = b + hm_mbcnt(m);
-            row[q] = rows[i];
-            col[q] = cols[i];
-            grp[q] = group ? group[i] : 0u;
-            idx[q] = i;
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long base_s;
+    constexpr int64_t TILE = 256 * HM_TL_PPT;
+    for (int64_t t0 = (int64_t)blockIdx.x * TILE; t0 < n; t0 += (int64_t)gridDim.x * TILE) {
+        uint32_t pm = 0;
+#pragma unroll
+        for (int k = 0; k < HM_TL_PPT; k++) {
+            const int64_t i = t0 + (int64_t)k * 256 + threadIdx.x;
+            pm |= (uint32_t)(i < n && (!keep || keep[i])) << k;
+        }
+        uint32_t tot;
+        uint32_t pos = hm_block_excl_scan<256>((uint32_t)__popc(pm), scr, &tot);
+        if (threadIdx.x == 0) base_s = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        const unsigned long long b = base_s;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < HM_TL_PPT; k++) {
+            if ((pm >> k) & 1u) {
+                const int64_t i = t0 + (int64_t)k * 256 + threadIdx.x;
+                const uint64_t q = b + pos++;
+                row[q] = rows[i];
+                col[q] = cols[i];
+                grp[q] = group ? group[i] : 0u;
+                idx[q] = i;
+            }
         }
     }
 }
@@ -356,6 +369,6 @@ void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* col
                           const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
                           unsigned long long* count)
 {
-    hipLaunchKernelGGL(k_tiles_list, dim3(hm_ggrid((uint64_t)n, 256, 8192)), dim3(256), 0, s, rows, cols, keep, group,
+    hipLaunchKernelGGL(k_tiles_list, dim3(hm_ggrid((uint64_t)n, 256 * HM_TL_PPT, 4096)), dim3(256), 0, s, rows, cols, keep, group,
                        n, row, col, grp, idx, count);
 }

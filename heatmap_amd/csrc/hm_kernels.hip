@@ -132,9 +132,9 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     /* the projection's polynomial table; after the projection it holds, per
      * digit, (region position - stage offset) */
     __shared__ double tab[HM_YTAB_N];
-    static_assert(sizeof(OutT) * HM_T1 >= HM_HOT_SLOTS * 4, "the hot-tile hash lives in the stage");
+    static_assert(sizeof(OutT) * HM_T1 >= HM_HOT_SLOTS * 4, "the hot-tile table lives in the stage");
     static_assert(sizeof(double) * HM_YTAB_N >= HM_D1 * 4, "dbase lives in the polynomial table");
-    uint32_t* const hsh = (uint32_t*)stage;
+    uint4* const hsh4 = (uint4*)stage;
     uint32_t* const dbase = (uint32_t*)tab;
     uint2* const rinfo = (uint2*)sdig;
     static_assert(sizeof(uint16_t) * HM_T1 >= HM_D1 * sizeof(uint2), "region info lives in sdig");
@@ -205,12 +205,12 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         rbase2[q][0] = lv ? a.rbase[s0] : 0u;
         rbase2[q][1] = lv ? a.rbase[s1] : 0u;
     }
-    /* the hot-tile hash, also ahead of the points (stored to LDS below) */
-    constexpr int HPT = HM_HOT_SLOTS / HM_P1_THREADS;
-    uint32_t hv[HPT];
+    /* the hot-tile table, also ahead of the points (stored to LDS below) */
+    static_assert(HM_HOT_BUCKETS == 2 * HM_P1_THREADS && HM_HOT_WAYS == 4, "two uint4 buckets per thread");
+    uint4 hv0 = make_uint4(0u, 0u, 0u, 0u), hv1 = hv0;   /* (no array: it would live in scratch) */
     if (H) {
-#pragma unroll
-        for (int q = 0; q < HPT; q++) hv[q] = a.hot_hash[q * HM_P1_THREADS + tid];
+        hv0 = ((const uint4*)a.hot_hash)[tid];
+        hv1 = ((const uint4*)a.hot_hash)[HM_P1_THREADS + tid];
     }
     __builtin_amdgcn_sched_barrier(0);
     /* issue every load of the tile before any arithmetic: 16 points x 16 B per
@@ -269,8 +269,8 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         rinfo[d] = make_uint2(sh ? rbase2[q][1] : rbase2[q][0], ((sh ? rcap2[q][1] : rcap2[q][0]) << 1) | sh);
     }
     if (H) {
-#pragma unroll
-        for (int q = 0; q < HPT; q++) hsh[q * HM_P1_THREADS + tid] = hv[q];
+        hsh4[tid] = hv0;
+        hsh4[HM_P1_THREADS + tid] = hv1;
     }
     if (!FROM_TILES) {
 #pragma unroll
@@ -287,6 +287,30 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     const int hb = a.restbits >> 1;      /* offset bits per coordinate in rest */
     const int wd = a.dbits >> 1;         /* digit bits per coordinate */
     const uint32_t lowm = (1u << hb) - 1u;
+    const int hs = a.Z - a.hot_z;        /* hot keys: offset bits per coordinate */
+    const uint32_t hm = (1u << hs) - 1u;
+    /* a tile's digit slot (the skewed LDS slot of its digit, hm_cur_slot: one
+     * bijection used for every digit table of the block) and key.  A point in
+     * a hot tile (one 16-B read of its table bucket: the entry's tile bits
+     * cancel in the XOR, so the minimum is h exactly when the tile is there)
+     * takes digit HM_MAX_F1 + h and its zoom-Z offset inside the tile. */
+    const uint32_t wm = (1u << wd) - 1u;
+    auto key_of = [&](uint32_t r, uint32_t c, bool v, uint32_t& dslot, uint32_t& key) {
+        const uint32_t rd = r >> hb, cd = c >> hb;
+        /* = hm_dslot(rd << wd | cd): the column digit rotated by 8 rows */
+        uint32_t dg = (rd << wd) | (HM_SKEW_CUR ? ((cd + (rd << 3)) & wm) : cd);
+        key = ((r & lowm) << hb) | (c & lowm);
+        if (H) {   /* block-uniform */
+            const uint32_t t = ((r >> hs) << a.hot_z) | (c >> hs);
+            const uint4 e = hsh4[hm_hot_bucket(t)];
+            const uint32_t tk = t << 9;
+            const uint32_t x = min(min(e.x ^ tk, e.y ^ tk), min(e.z ^ tk, e.w ^ tk));
+            const bool hot = x < 512u;
+            dg = hot ? HM_MAX_F1 + x : dg;
+            key = hot ? (((r & hm) << hs) | (c & hm)) : key;
+        }
+        dslot = v ? dg : 0xFFFFFFFFu;
+    };
     uint32_t redo = 0;
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT; k++) {
@@ -312,8 +336,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;
         redo |= (uint32_t)(inb & !(ok & dom)) << k;
         const bool v = inb & ok & dom & kept;
-        dig[k] = v ? ((((uint32_t)r >> hb) << wd) | ((uint32_t)c >> hb)) : 0xFFFFFFFFu;
-        rest[k] = (((uint32_t)r & lowm) << hb) | ((uint32_t)c & lowm);
+        key_of((uint32_t)r, (uint32_t)c, v, dig[k], rest[k]);
         /* pin the key: without it the compiler keeps every point's
          * projection temporaries alive past this point (158 VGPRs, 1 block/CU) */
         asm volatile("" : "+v"(dig[k]), "+v"(rest[k]));
@@ -326,6 +349,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         /* defer: k_redo resolves these with the exact chain and feeds them
          * back as extra tiles (keeps the exact path out of this kernel's
          * register allocation) */
+        if (__ballot(redo != 0))
 #pragma unroll
         for (int k = 0; k < HM_P1_PPT; k++) {
             const bool rd = (redo >> k) & 1u;
@@ -366,55 +390,28 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
             const bool good = rd & (st == HM_OK) & kept;
             const bool outside = good & (((uint64_t)r >= lim) | ((uint64_t)c >= lim));
             hm_exotic_append(a.x, outside, r, c, i);
-            if (good & !outside) {
-                dig[k] = (((uint32_t)r >> hb) << wd) | ((uint32_t)c >> hb);
-                rest[k] = (((uint32_t)r & lowm) << hb) | ((uint32_t)c & lowm);
-            }
+            if (good & !outside) key_of((uint32_t)r, (uint32_t)c, true, dig[k], rest[k]);
         }
     }
     if (!FROM_TILES) {
         const uint32_t ws = hm_wave_sum((uint32_t)nslow);
         if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
     }
-    if (H) {
-        /* points in a hot tile: digit HM_MAX_F1 + h, key = the zoom-Z offset
-         * inside the tile (u16); the tile is found in the LDS hash */
-        const int hs = a.Z - a.hot_z;                 /* offset bits per coordinate */
-        const uint32_t hm = (1u << hs) - 1u;
-        const uint32_t wm = (1u << wd) - 1u;
-#pragma unroll
-        for (int k = 0; k < HM_P1_PPT; k++) {
-            const bool v = dig[k] != 0xFFFFFFFFu;
-            const uint32_t r = ((dig[k] >> wd) << hb) | (rest[k] >> hb);
-            const uint32_t c = ((dig[k] & wm) << hb) | (rest[k] & lowm);
-            const uint32_t t = ((r >> hs) << a.hot_z) | (c >> hs);
-            uint32_t slot = (t * 2654435761u) >> (32 - 11);
-            static_assert(HM_HOT_SLOTS == 1 << 11, "hash slots");
-            uint32_t e = hsh[slot];
-            while (v && e != HM_HOT_EMPTY && (e >> 10) != t) {
-                slot = (slot + 1) & (HM_HOT_SLOTS - 1);
-                e = hsh[slot];
-            }
-            if (v && e != HM_HOT_EMPTY) {
-                dig[k] = HM_MAX_F1 + (e & 1023u);
-                rest[k] = ((r & hm) << hs) | (c & hm);
-            }
-        }
-    }
     /* one returning atomic per point: the digit histogram and the point's
      * rank within its digit (its slot is the digit's offset + rank) */
+    const uint32_t dummy = HM_D1 + (uint32_t)hm_lane();
     uint32_t rank[HM_P1_PPT];
 #pragma unroll
     for (int k0 = 0; k0 < HM_P1_PPT; k0 += HM_P1_GROUP) {
-        HmMerge gm[HM_P1_GROUP];
+        HmClaim gm[HM_P1_GROUP];
         uint32_t old[HM_P1_GROUP];
 #pragma unroll
         for (int u = 0; u < HM_P1_GROUP; u++) {
-            gm[u] = hm_merge_prep(hm_cur_slot(dig[k0 + u], wd), dig[k0 + u] != 0xFFFFFFFFu, HM_D1);
+            gm[u] = hm_claim_prep(dig[k0 + u], dig[k0 + u] != 0xFFFFFFFFu, dummy);
             old[u] = atomicAdd(&cur[gm[u].idx], gm[u].inc);
         }
 #pragma unroll
-        for (int u = 0; u < HM_P1_GROUP; u++) rank[k0 + u] = hm_merge_pos(gm[u], old[u]);
+        for (int u = 0; u < HM_P1_GROUP; u++) rank[k0 + u] = hm_claim_pos(gm[u], old[u]);
     }
     __syncthreads();
     if (MODE == 0) HM_STAMP_M(2, 3);
@@ -425,8 +422,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     constexpr int PER = PERD;
     uint32_t cnt[PER];
     uint32_t gpos[PER];
-    uint32_t rcap[PER], rbase[PER];
-    uint32_t s = 0;
+    uint32_t rcap[PER], rbase[PER], dsl[PER];
     /* thread t holds digits q * T + t: a wave's lanes reserve for
      * consecutive digits (coalesced atomics on the shard-major fill words) */
     uint64_t packed = 0;
@@ -436,41 +432,46 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         const uint2 ri = rinfo[d];
         rbase[q] = ri.x;
         rcap[q] = ri.y >> 1;
+        dsl[q] = hm_dslot(d, wd);
         const uint32_t slot = hm_l1i(d, (ri.y & 1u) ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u);
-        cnt[q] = live(d) ? cur[hm_cur_slot(d, wd)] : 0u;
+        cnt[q] = live(d) ? cur[dsl[q]] : 0u;
         gpos[q] = 0;
         if (cnt[q]) gpos[q] = atomicAdd(&a.fill[slot], cnt[q]);
         packed |= (uint64_t)cnt[q] << (21 * q);
     }
     static_assert(PER <= 3 && HM_T1 < (1 << 21), "three 21-bit digit counts per scanned word");
+    static_assert(HM_MAX_F1 % HM_P1_THREADS == 0, "cold digits fill whole q rows");
     /* exclusive scan in digit order (q major, then thread): one scan of the
-     * three counts packed in 21-bit fields */
+     * three counts packed in 21-bit fields.  Cold digits come first, so the
+     * stage holds the cold keys in [0, cold) and the hot tiles' after them */
     uint64_t tot64;
     const uint64_t off64 = hm_block_excl_scan64<HM_P1_THREADS>(packed, (unsigned long long*)scr, &tot64);
     uint32_t offq[PER];
-    uint32_t total = 0;
+    uint32_t total = 0, cold = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
+        if (q * HM_P1_THREADS == HM_MAX_F1) cold = total;
         offq[q] = total + (uint32_t)((off64 >> (21 * q)) & 0x1FFFFFu);
         total += (uint32_t)((tot64 >> (21 * q)) & 0x1FFFFFu);
     }
+    if (PER * HM_P1_THREADS == HM_MAX_F1) cold = total;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = q * HM_P1_THREADS + tid;
-        if (live(d)) cur[hm_cur_slot(d, wd)] = offq[q];
+        if (live(d)) cur[dsl[q]] = offq[q];
     }
     __syncthreads();
     if (MODE == 0) HM_STAMP_M(2, 4);
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT; k++) {
         const bool v = dig[k] != 0xFFFFFFFFu;
-        const uint32_t pos = v ? cur[hm_cur_slot(v ? dig[k] : 0u, wd)] + rank[k] : HM_T1 + hm_lane();
+        const uint32_t pos = v ? cur[v ? dig[k] : 0u] + rank[k] : HM_T1 + hm_lane();
         stage[pos] = (OutT)rest[k];
         sdig[pos] = (uint16_t)dig[k];
     }
-    /* lane-parallel copy-out: staged key i of digit d goes to region
-     * position dbase[d] + i (= rbase + gpos + i - offset of d), so a wave
-     * stores 64 consecutive staged keys (one or a few digits' runs).  A
+    /* lane-parallel copy-out: staged key i of digit slot s goes to region
+     * position dbase[s] + i (= rbase + gpos + i - offset of its digit), so a
+     * wave stores 64 consecutive staged keys (one or a few digits' runs).  A
      * reservation past the region's capacity is dropped and flagged (the host
      * re-runs the level with exact sizes). */
     bool over = false;
@@ -480,7 +481,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         if (live(d)) {
             const bool fits = cnt[q] && (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rcap[q];
             over |= cnt[q] && !fits;
-            dbase[d] = fits ? rbase[q] + gpos[q] - offq[q] : 0xFFFFFFFFu;
+            dbase[dsl[q]] = fits ? rbase[q] + gpos[q] - offq[q] : 0xFFFFFFFFu;
         }
     }
     if (MODE == 0) HM_STAMP_M(2, 5);
@@ -488,16 +489,28 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     __syncthreads();
     if (MODE == 0) HM_STAMP_M(2, 6);
     {
+        /* every LDS read first (a thread copies <= HM_P1_PPT staged keys),
+         * then the stores: no load-use round trip per key */
         OutT* out = (OutT*)a.keys_out;
         uint16_t* hout = (uint16_t*)a.keys_hot;
-        for (uint32_t i = tid; i < total; i += HM_P1_THREADS) {
-            const uint32_t d = sdig[i];
-            const uint32_t b = dbase[d];
-            if (b != 0xFFFFFFFFu) {
-                if (d < HM_MAX_F1)
-                    out[b + i] = stage[i];
+        uint32_t sv[HM_P1_PPT], sb[HM_P1_PPT];
+#pragma unroll
+        for (int j = 0; j < HM_P1_PPT; j++) {
+            const uint32_t i = j * HM_P1_THREADS + tid;
+            const uint32_t ic = i < total ? i : 0u;
+            sb[j] = sdig[ic];
+            sv[j] = (uint32_t)stage[ic];
+        }
+#pragma unroll
+        for (int j = 0; j < HM_P1_PPT; j++) sb[j] = dbase[sb[j]];
+#pragma unroll
+        for (int j = 0; j < HM_P1_PPT; j++) {
+            const uint32_t i = j * HM_P1_THREADS + tid;
+            if (i < total && sb[j] != 0xFFFFFFFFu) {
+                if (i < cold)
+                    out[sb[j] + i] = (OutT)sv[j];
                 else
-                    hout[b + i] = (uint16_t)stage[i];
+                    hout[sb[j] + i] = (uint16_t)sv[j];
             }
         }
     }
@@ -581,46 +594,59 @@ __global__ __launch_bounds__(256) void k_sample_digits(HmPart1Args a, uint64_t s
     (void)hlost;
 }
 
-/* Hot tiles: every zoom-zb tile with >= thresh sampled points (at most
- * HM_MAX_HOT, first come), their sampled counts as level-1 histogram entries
- * HM_MAX_F1 + h, and the z1 digits that hold them. */
+/* Hot-tile candidates: every zoom-zb tile with >= thresh sampled points (at
+ * most HM_HOT_CAND, first come), listed with its sampled count. */
 __global__ __launch_bounds__(256) void k_hot_select(HmHotArgs a)
 {
     const uint64_t ntiles = 1ull << (2 * a.zb);
     const uint64_t stride = (uint64_t)gridDim.x * 256;
+    uint32_t* const ncand = a.cand + 2 * HM_HOT_CAND;
     for (uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x; t < ntiles; t += stride) {
         const uint32_t c = a.counts[t];
         if (c >= a.thresh) {
-            const uint32_t h = atomicAdd(a.n, 1u);
-            if (h < HM_MAX_HOT) {
-                a.tiles[h] = (uint32_t)t;
-                a.hist[HM_MAX_F1 + h] = c;
-                const int s = a.zb - a.z1;
-                const uint32_t tr = (uint32_t)(t >> a.zb), tc = (uint32_t)(t & ((1ull << a.zb) - 1));
-                const uint32_t d = ((tr >> s) << a.z1) | (tc >> s);
-                a.hotparent[d] = 1;
-                atomicSub(&a.hist[d], c);   /* those samples' keys leave the cold digit */
+            const uint32_t j = atomicAdd(ncand, 1u);
+            if (j < HM_HOT_CAND) {
+                a.cand[2 * j] = (uint32_t)t;
+                a.cand[2 * j + 1] = c;
             }
         }
     }
 }
 
-/* the LDS hash image k_project_partition looks hot tiles up in; clamps the
- * count to HM_MAX_HOT.  One block. */
-__global__ __launch_bounds__(256) void k_hot_hash(HmHotArgs a)
+/* The hot tiles and the table image k_project_partition looks them up in.  A
+ * candidate becomes hot tile h (< HM_MAX_HOT) when its bucket has a free way;
+ * otherwise it stays cold (any set of hot tiles gives the same counts).  Hot
+ * tile h: its sampled count as level-1 histogram entry HM_MAX_F1 + h, taken
+ * off its z1 digit, which is flagged as a hot parent.  One block. */
+__global__ __launch_bounds__(1024) void k_hot_hash(HmHotArgs a)
 {
-    __shared__ uint32_t hsh[HM_HOT_SLOTS];
-    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 256) hsh[i] = HM_HOT_EMPTY;
+    __shared__ uint32_t tab[HM_HOT_SLOTS];
+    __shared__ uint32_t fill[HM_HOT_BUCKETS];
+    __shared__ uint32_t nh;
+    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 1024) tab[i] = HM_HOT_EMPTY;
+    for (int i = threadIdx.x; i < HM_HOT_BUCKETS; i += 1024) fill[i] = 0;
+    if (threadIdx.x == 0) nh = 0;
     __syncthreads();
-    const uint32_t H = min(*a.n, (uint32_t)HM_MAX_HOT);
-    for (uint32_t h = threadIdx.x; h < H; h += 256) {
-        const uint32_t t = a.tiles[h];
-        uint32_t sl = (t * 2654435761u) >> (32 - 11);
-        while (atomicCAS(&hsh[sl], HM_HOT_EMPTY, (t << 10) | h) != HM_HOT_EMPTY) sl = (sl + 1) & (HM_HOT_SLOTS - 1);
+    const uint32_t nc = min(a.cand[2 * HM_HOT_CAND], (uint32_t)HM_HOT_CAND);
+    for (uint32_t j = threadIdx.x; j < nc; j += 1024) {
+        const uint32_t t = a.cand[2 * j], c = a.cand[2 * j + 1];
+        const uint32_t b = hm_hot_bucket(t);
+        const uint32_t w = atomicAdd(&fill[b], 1u);
+        if (w >= HM_HOT_WAYS) continue;
+        const uint32_t h = atomicAdd(&nh, 1u);
+        if (h >= HM_MAX_HOT) continue;   /* its way stays empty */
+        tab[b * HM_HOT_WAYS + w] = (t << 9) | h;
+        a.tiles[h] = t;
+        a.hist[HM_MAX_F1 + h] = c;
+        const int s = a.zb - a.z1;
+        const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
+        const uint32_t d = ((tr >> s) << a.z1) | (tc >> s);
+        a.hotparent[d] = 1;
+        atomicSub(&a.hist[d], c);   /* those samples' keys leave the cold digit */
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 256) a.hash[i] = hsh[i];
-    if (threadIdx.x == 0) *a.n = H;
+    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 1024) a.hash[i] = tab[i];
+    if (threadIdx.x == 0) *a.n = min(nh, (uint32_t)HM_MAX_HOT);
 }
 
 void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a)
@@ -630,7 +656,7 @@ void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a)
     if (blocks > 1024) blocks = 1024;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_hot_select, dim3((unsigned)blocks), dim3(256), 0, s, a);
-    hipLaunchKernelGGL(k_hot_hash, dim3(1), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_hot_hash, dim3(1), dim3(1024), 0, s, a);
 }
 
 /* Level-1 region sizes from the sampled histogram, on the device (no host
@@ -2421,35 +2447,52 @@ void hm_launch_collect_exotic(hipStream_t s, const double* lat, const double* lo
 
 /* grouped counts: exact tile of every point (errors in input order), and a
  * list of the kept ones with their group and input index */
+/* Kept points as a (row, col, group, index) list for the general path.  A
+ * block takes HM_PL_PPT * 256 consecutive points per step: projections in
+ * registers, one block scan, ONE output reservation per step (one reservation
+ * per wave on a single counter saturated it: ~88 per us, 18.8 ms per 1e8
+ * points).  The list is in no particular order. */
+#define HM_PL_PPT 16
 __global__ __launch_bounds__(256) void k_project_list(const double* lat, const double* lon, const uint8_t* keep,
                                                       const uint32_t* group, int64_t n, int Z, int64_t* row,
                                                       int64_t* col, uint32_t* grp, int64_t* idx,
                                                       unsigned long long* count, unsigned long long* err_word)
 {
     __shared__ double tab[HM_YTAB_N];
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long base_s;
     hm_load_ytab(tab);
     __syncthreads();
-    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    const int64_t n_up = (n + 63) & ~63ll;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_up; i += stride) {
-        int64_t r = 0, c = 0;
-        int st = HM_E_ARG;
-        if (i < n) {
-            int slow = 0;
-            st = hm_project_point(lat[i], lon[i], Z, &r, &c, &slow, tab);
-            if (st != HM_OK) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+    constexpr int64_t TILE = 256 * HM_PL_PPT;
+    for (int64_t t0 = (int64_t)blockIdx.x * TILE; t0 < n; t0 += (int64_t)gridDim.x * TILE) {
+        int64_t r[HM_PL_PPT], c[HM_PL_PPT];
+        uint32_t pm = 0;
+#pragma unroll
+        for (int k = 0; k < HM_PL_PPT; k++) {
+            const int64_t i = t0 + (int64_t)k * 256 + threadIdx.x;
+            r[k] = 0;
+            c[k] = 0;
+            int st = HM_E_ARG;
+            if (i < n) {
+                int slow = 0;
+                st = hm_project_point(lat[i], lon[i], Z, &r[k], &c[k], &slow, tab);
+                if (st != HM_OK) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+            }
+            pm |= (uint32_t)(i < n && st == HM_OK && (!keep || keep[i])) << k;
         }
-        const bool p = i < n && st == HM_OK && (!keep || keep[i]);
-        const uint64_t m = __ballot(p);
-        if (m) {
-            const int lead = __ffsll((unsigned long long)m) - 1;
-            unsigned long long b = 0;
-            if (hm_lane() == lead) b = atomicAdd(count, (unsigned long long)__popcll(m));
-            b = __shfl(b, lead, 64);
-            if (p) {
-                const uint64_t q = b + hm_mbcnt(m);
-                row[q] = r;
-                col[q] = c;
+        uint32_t tot;
+        uint32_t pos = hm_block_excl_scan<256>((uint32_t)__popc(pm), scr, &tot);
+        if (threadIdx.x == 0) base_s = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        const unsigned long long b = base_s;
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < HM_PL_PPT; k++) {
+            if ((pm >> k) & 1u) {
+                const int64_t i = t0 + (int64_t)k * 256 + threadIdx.x;
+                const uint64_t q = b + pos++;
+                row[q] = r[k];
+                col[q] = c[k];
                 grp[q] = group ? group[i] : 0u;
                 idx[q] = i;
             }
@@ -2461,8 +2504,8 @@ void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon,
                             const uint32_t* group, int64_t n, int Z, int64_t* row, int64_t* col, uint32_t* grp,
                             int64_t* idx, unsigned long long* count, unsigned long long* err_word)
 {
-    int64_t blocks = (n + 255) / 256;
-    if (blocks > 8192) blocks = 8192;
+    int64_t blocks = (n + 256 * HM_PL_PPT - 1) / (256 * HM_PL_PPT);
+    if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_project_list, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, row, col,
                        grp, idx, count, err_word);

@@ -29,8 +29,21 @@
  * final level's key array, so they skip every intermediate partition pass. */
 #define HM_MAX_HOT 512
 #define HM_D1 (HM_MAX_F1 + HM_MAX_HOT)      /* level-1 digit slots: cold z1 digits, then hot tiles */
-#define HM_HOT_SLOTS 2048                   /* hot-tile hash (load <= 1/4) */
+/* hot-tile table: HM_HOT_BUCKETS buckets of HM_HOT_WAYS entries (one 16-B LDS
+ * read per lookup, no probe loop); entry = tile << 9 | h, HM_HOT_EMPTY.  A
+ * candidate whose bucket is full stays cold (k_hot_hash). */
+#define HM_HOT_BUCKETS 1024
+#define HM_HOT_WAYS 4
+#define HM_HOT_SLOTS (HM_HOT_BUCKETS * HM_HOT_WAYS)
+#define HM_HOT_CAND 4096                    /* candidates k_hot_select may list */
 #define HM_HOT_EMPTY 0xFFFFFFFFu
+static_assert(HM_MAX_HOT <= 512, "h takes the low 9 bits of a table entry");
+/* bucket of zoom-zb tile t (t < 2^22: zb <= 11) */
+__host__ __device__ inline uint32_t hm_hot_bucket(uint32_t t)
+{
+    return ((t & 0xFFFFFFu) * 0x9E3779u) >> 22;   /* 24-bit product: v_mul_u32_u24, full rate */
+}
+static_assert(HM_HOT_BUCKETS == 1 << 10, "hm_hot_bucket takes 10 bits");
 /* level-1 (digit, shard) arrays (fill, rbase, rcap) are shard-major: the
  * digits one wave reserves for sit in consecutive words, so its returning
  * atomics coalesce into a few 64-B requests instead of one per digit */
@@ -206,7 +219,7 @@ struct HmPart1Args {
      * at the regions of digit HM_MAX_F1 + h (same position space as keys_out) */
     int hot_z;
     void* keys_hot;
-    const uint32_t* hot_hash;   /* [HM_HOT_SLOTS]: tile id << 10 | h, HM_HOT_EMPTY */
+    const uint32_t* hot_hash;   /* [HM_HOT_SLOTS]: bucketed table, tile id << 9 | h, HM_HOT_EMPTY */
     const uint32_t* hot_n;      /* device word: number of hot tiles */
 };
 
@@ -220,6 +233,7 @@ struct HmHotArgs {
     uint8_t* hotparent;         /* [HM_MAX_F1] z1 digits that hold a hot tile */
     uint32_t* n;                /* device word: hot tiles found (<= HM_MAX_HOT) */
     uint32_t* hash;             /* [HM_HOT_SLOTS] */
+    uint32_t* cand;             /* [2 * HM_HOT_CAND + 1]: (tile, count) candidates, then their number */
 };
 
 /* hot tiles as children of the level-2 run scan (k_hot_nr / k_hot_runs) */

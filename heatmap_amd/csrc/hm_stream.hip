@@ -287,8 +287,9 @@ __global__ __launch_bounds__(256) void k_stream_convert(const int64_t* __restric
         keys[i] = in ? ((uint64_t)r[0] << cb) | (hms_pyr_off(z) + ((uint64_t)row << z) + (uint64_t)col) : HMS_EMPTY;
         counts[i] = (uint64_t)r[4];
     }
-    const uint64_t b = hms_wave_sum(bad);
-    if ((threadIdx.x & 63) == 0 && b) atomicAdd(&state[HMS_ST_EXOTIC], (unsigned long long)b);
+    uint64_t v[1] = {bad};
+    hms_block_sums(v);
+    if (threadIdx.x == 0 && v[0]) atomicAdd(&state[HMS_ST_EXOTIC], (unsigned long long)v[0]);
 }
 
 /* Fold n cells into the table.  FROM_COUNT: hm_count keys of one bucket
@@ -305,11 +306,11 @@ __global__ __launch_bounds__(256) void k_stream_insert(const uint64_t* __restric
         const uint64_t k = FROM_COUNT ? prefix | hms_cell(keys[i]) : keys[i];
         claimed += hms_insert_unique(t, k, counts[i], &overflow);   /* a batch's cells are distinct */
     }
-    claimed = hms_wave_sum(claimed);
-    const uint64_t of = hms_wave_sum(overflow);
-    if ((threadIdx.x & 63) == 0) {
-        if (claimed) atomicAdd(&t.state[HMS_ST_OCCUPIED], (unsigned long long)claimed);
-        if (of) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)of);
+    uint64_t v[2] = {claimed, overflow};
+    hms_block_sums(v);
+    if (threadIdx.x == 0) {
+        if (v[0]) atomicAdd(&t.state[HMS_ST_OCCUPIED], (unsigned long long)v[0]);
+        if (v[1]) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)v[1]);
     }
 }
 
@@ -324,11 +325,11 @@ __global__ __launch_bounds__(256) void k_stream_rehash(HmsTable from, HmsTable t
         const ulonglong2 sl = ((const ulonglong2*)from.slots)[i];
         if (sl.x != HMS_EMPTY) claimed += hms_insert_unique(to, sl.x, sl.y, &overflow);
     }
-    claimed = hms_wave_sum(claimed);
-    const uint64_t of = hms_wave_sum(overflow);
-    if ((threadIdx.x & 63) == 0) {
-        if (claimed) atomicAdd(&to.state[HMS_ST_OCCUPIED], (unsigned long long)claimed);
-        if (of) atomicAdd(&to.state[HMS_ST_OVERFLOW], (unsigned long long)of);
+    uint64_t v[2] = {claimed, overflow};
+    hms_block_sums(v);
+    if (threadIdx.x == 0) {
+        if (v[0]) atomicAdd(&to.state[HMS_ST_OCCUPIED], (unsigned long long)v[0]);
+        if (v[1]) atomicAdd(&to.state[HMS_ST_OVERFLOW], (unsigned long long)v[1]);
     }
 }
 
@@ -418,15 +419,13 @@ __global__ __launch_bounds__(256) void k_stream_rollup(HmsRollupArgs a)
         }
         claimed += hms_insert(a.to, ((uint64_t)b << a.cb) | (sl.x & cmask), sl.y, &overflow);
     }
-    claimed = hms_wave_sum(claimed);
-    const uint64_t of = hms_wave_sum(overflow);
-    const uint64_t bc = hms_wave_sum(bclaimed);
-    const uint64_t fl = hms_wave_sum(full);
-    if ((threadIdx.x & 63) == 0) {
-        if (claimed) atomicAdd(&a.to.state[HMS_ST_OCCUPIED], (unsigned long long)claimed);
-        if (of) atomicAdd(&a.to.state[HMS_ST_OVERFLOW], (unsigned long long)of);
-        if (bc) atomicAdd(&a.state[HMS_ST_BUCKETS], (unsigned long long)bc);
-        if (fl) atomicAdd(&a.state[HMS_ST_BFULL], (unsigned long long)fl);
+    uint64_t v[4] = {claimed, overflow, bclaimed, full};
+    hms_block_sums(v);
+    if (threadIdx.x == 0) {
+        if (v[0]) atomicAdd(&a.to.state[HMS_ST_OCCUPIED], (unsigned long long)v[0]);
+        if (v[1]) atomicAdd(&a.to.state[HMS_ST_OVERFLOW], (unsigned long long)v[1]);
+        if (v[2]) atomicAdd(&a.state[HMS_ST_BUCKETS], (unsigned long long)v[2]);
+        if (v[3]) atomicAdd(&a.state[HMS_ST_BFULL], (unsigned long long)v[3]);
     }
 }
 
@@ -474,7 +473,7 @@ __global__ __launch_bounds__(256) void k_stream_emit(HmsEmitArgs a)
 static dim3 hms_grid(uint64_t n)
 {
     uint64_t b = (n + 255) / 256;
-    if (b > 8192) b = 8192;
+    if (b > 2048) b = 2048;   /* 8 blocks per CU; one state atomic per block */
     return dim3((unsigned)(b ? b : 1));
 }
 

@@ -26,6 +26,25 @@ __device__ __forceinline__ uint64_t hms_wave_sum(uint64_t v)
     return v;
 }
 
+/* Sums of NV per-thread values over a 256-thread block, valid in thread 0
+ * (every thread calls): the kernels' state counters then take one atomic per
+ * block, not one per wave (a few thousand same-address atomics already cost
+ * ~0.1 ms: one word takes ~88 per us) */
+template <int NV>
+__device__ __forceinline__ void hms_block_sums(uint64_t (&v)[NV])
+{
+    __shared__ unsigned long long s[NV][4];
+#pragma unroll
+    for (int q = 0; q < NV; q++) v[q] = hms_wave_sum(v[q]);
+    if ((threadIdx.x & 63) == 0)
+#pragma unroll
+        for (int q = 0; q < NV; q++) s[q][threadIdx.x >> 6] = v[q];
+    __syncthreads();
+    if (threadIdx.x == 0)
+#pragma unroll
+        for (int q = 0; q < NV; q++) v[q] = s[q][0] + s[q][1] + s[q][2] + s[q][3];
+}
+
 /* Insert-or-add; returns 1 if this call claimed a new slot. */
 __device__ __forceinline__ uint32_t hms_insert(const HmsTable& t, uint64_t k, uint64_t c, uint32_t* overflow)
 {
