@@ -206,7 +206,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         rbase2[q][1] = lv ? a.rbase[s1] : 0u;
     }
     /* the hot-tile table, also ahead of the points (stored to LDS below) */
-    static_assert(HM_HOT_BUCKETS == 2 * HM_P1_THREADS && HM_HOT_WAYS == 4, "two uint4 buckets per thread");
+    static_assert(HM_HOT_SLOTS == 8 * HM_P1_THREADS, "the table is two uint4 per thread");
     uint4 hv0 = make_uint4(0u, 0u, 0u, 0u), hv1 = hv0;   /* (no array: it would live in scratch) */
     if (H) {
         hv0 = ((const uint4*)a.hot_hash)[tid];
@@ -302,9 +302,14 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         key = ((r & lowm) << hb) | (c & lowm);
         if (H) {   /* block-uniform */
             const uint32_t t = ((r >> hs) << a.hot_z) | (c >> hs);
-            const uint4 e = hsh4[hm_hot_bucket(t)];
             const uint32_t tk = t << 9;
+#if HM_HOT_WAYS == 4
+            const uint4 e = hsh4[hm_hot_bucket(t)];
             const uint32_t x = min(min(e.x ^ tk, e.y ^ tk), min(e.z ^ tk, e.w ^ tk));
+#else
+            const uint2 e = ((const uint2*)hsh4)[hm_hot_bucket(t)];
+            const uint32_t x = min(e.x ^ tk, e.y ^ tk);
+#endif
             const bool hot = x < 512u;
             dg = hot ? HM_MAX_F1 + x : dg;
             key = hot ? (((r & hm) << hs) | (c & hm)) : key;
@@ -1946,27 +1951,28 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
     __syncthreads();
     if (hm_block_id() >= a.items) return;   /* block-uniform */
     const HmItem it = hm_item(a.B, hm_block_id());
-    /* counted at skewed slots (hm_skew), un-skewed before the pyramid
-     * (measured neutral on hotspot data; kept for the column-clustered case) */
+    /* HM_AG_SKEW: counted at skewed slots (hm_skew), un-skewed before the
+     * pyramid (for column-clustered keys) */
     struct {
         uint32_t* grid;
         uint32_t dummy;
         int lg;
-        __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { hm_lds_count(grid, dummy, hm_skew(k, lg), v); }
+        __device__ __forceinline__ uint32_t sl(uint32_t k) { return HM_AG_SKEW ? hm_skew(k, lg) : k; }
+        __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { hm_lds_count(grid, dummy, sl(k), v); }
         __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t)
         {
-            hm_lds_count(grid, dummy, hm_skew(x.x & 0xFFFFu, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.x >> 16, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.y & 0xFFFFu, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.y >> 16, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.z & 0xFFFFu, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.z >> 16, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.w & 0xFFFFu, lg), v);
-            hm_lds_count(grid, dummy, hm_skew(x.w >> 16, lg), v);
+            hm_lds_count(grid, dummy, sl(x.x & 0xFFFFu), v);
+            hm_lds_count(grid, dummy, sl(x.x >> 16), v);
+            hm_lds_count(grid, dummy, sl(x.y & 0xFFFFu), v);
+            hm_lds_count(grid, dummy, sl(x.y >> 16), v);
+            hm_lds_count(grid, dummy, sl(x.z & 0xFFFFu), v);
+            hm_lds_count(grid, dummy, sl(x.z >> 16), v);
+            hm_lds_count(grid, dummy, sl(x.w & 0xFFFFu), v);
+            hm_lds_count(grid, dummy, sl(x.w >> 16), v);
         }
     } f{grid, HM_AG_CELLS, a.lg};
     hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);
-    {
+    if (HM_AG_SKEW) {
         constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;
         uint32_t x[CPT];
 #pragma unroll

@@ -32,18 +32,21 @@
 /* hot-tile table: HM_HOT_BUCKETS buckets of HM_HOT_WAYS entries (one 16-B LDS
  * read per lookup, no probe loop); entry = tile << 9 | h, HM_HOT_EMPTY.  A
  * candidate whose bucket is full stays cold (k_hot_hash). */
-#define HM_HOT_BUCKETS 1024
-#define HM_HOT_WAYS 4
-#define HM_HOT_SLOTS (HM_HOT_BUCKETS * HM_HOT_WAYS)
+#ifndef HM_HOT_WAYS
+#define HM_HOT_WAYS 2                       /* 2 or 4 (one 8- or 16-B read): 2 measured 0.13 ms faster */
+#endif
+#define HM_HOT_SLOTS 4096
+#define HM_HOT_BUCKETS (HM_HOT_SLOTS / HM_HOT_WAYS)
+#define HM_HOT_BBITS (HM_HOT_WAYS == 4 ? 10 : 11)
 #define HM_HOT_CAND 4096                    /* candidates k_hot_select may list */
 #define HM_HOT_EMPTY 0xFFFFFFFFu
 static_assert(HM_MAX_HOT <= 512, "h takes the low 9 bits of a table entry");
 /* bucket of zoom-zb tile t (t < 2^22: zb <= 11) */
 __host__ __device__ inline uint32_t hm_hot_bucket(uint32_t t)
 {
-    return ((t & 0xFFFFFFu) * 0x9E3779u) >> 22;   /* 24-bit product: v_mul_u32_u24, full rate */
+    return ((t & 0xFFFFFFu) * 0x9E3779u) >> (32 - HM_HOT_BBITS);   /* 24-bit product: v_mul_u32_u24, full rate */
 }
-static_assert(HM_HOT_BUCKETS == 1 << 10, "hm_hot_bucket takes 10 bits");
+static_assert(HM_HOT_BUCKETS == 1 << HM_HOT_BBITS && (HM_HOT_WAYS == 2 || HM_HOT_WAYS == 4), "hot-tile table");
 /* level-1 (digit, shard) arrays (fill, rbase, rcap) are shard-major: the
  * digits one wave reserves for sit in consecutive words, so its returning
  * atomics coalesce into a few 64-B requests instead of one per digit */
@@ -77,6 +80,9 @@ __host__ __device__ inline uint32_t hm_l1i(uint32_t d, uint32_t sh) { return sh 
 #define HM_AG_THREADS 1024
 #define HM_AG_CELLS 16384
 #define HM_AG_LG 7
+#ifndef HM_AG_SKEW
+#define HM_AG_SKEW 0                        /* 1: k_aggregate counts at hm_skew slots (0 measured 0.09 ms faster on hotspots, neutral on skew) */
+#endif
 #ifndef HM_TA
 #define HM_TA (1u << 18)                    /* keys per aggregation work item */
 #endif

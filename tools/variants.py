@@ -46,6 +46,9 @@ VARIANTS = {
     "lz3": ["HM_LEVEL_ZOOMS=3"],            # levels z5, z8, z11 (zmax 18)
     "split256": ["HM_SPW_SPLIT=256"],       # narrow small-bucket instantiation up to 256 keys
     "sp1024": ["HM_SP_MAX=1024"],           # buckets of 1025-2048 keys to k_aggregate
+    "hot2": ["HM_HOT_WAYS=2"],              # 2-way hot-tile buckets (8-B read)
+    "agns": ["HM_AG_SKEW=0"],               # k_aggregate without the skewed slots
+    "hot2agns": ["HM_HOT_WAYS=2", "HM_AG_SKEW=0"],
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
