@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-EXCLUDE = ("k_synth", "at::native")
+EXCLUDE = ("k_synth", "at::native", "__amd_rocclr_copyBuffer")   # copies: the bench's measured-peak pass
 
 
 def per_kernel(d, counter):

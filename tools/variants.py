@@ -49,6 +49,9 @@ VARIANTS = {
     "hot2": ["HM_HOT_WAYS=2"],              # 2-way hot-tile buckets (8-B read)
     "agns": ["HM_AG_SKEW=0"],               # k_aggregate without the skewed slots
     "hot2agns": ["HM_HOT_WAYS=2", "HM_AG_SKEW=0"],
+    "agslow": ["HM_AG_FAST=0"],             # k_aggregate with the lane-0 merge on every key
+    "agm4": ["HM_MERGE_MIN=4"],
+    "agm16": ["HM_MERGE_MIN=16"],
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
