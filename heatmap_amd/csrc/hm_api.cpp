@@ -116,7 +116,8 @@ enum {
     B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
-    B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS,
+    B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS, B_MB_CNT2, B_MB_OFF2,
+    B_MB_KEYS2, B_MB_COUNTS2,
     B_COUNT
 };
 
@@ -1351,33 +1352,88 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
     hipStream_t s = ctx->stream;
     unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
     {
-        /* bucketed LDS merge (hm_merge.hip): <= 4096 hash buckets of ~2048+
-         * cells, one block each */
+        /* bucketed LDS merge (hm_merge.hip): 2^lb hash buckets of <= ~1800
+         * cells (one LDS table pass each), one block per bucket; the cells are
+         * hash-partitioned by the top lb bits in one or two coalesced passes
+         * of <= 7 bits */
         HmMergeArgs a;
         memset(&a, 0, sizeof(a));
         int lb = 0;
-        while (lb < 12 && ((uint64_t)n >> lb) > 2048) lb++;
+        while (lb < 14 && ((uint64_t)n >> lb) > 1800) lb++;
+        const int b1 = lb <= 7 ? lb : (lb + 1) / 2, b2 = lb - b1;
+        auto chunks = [](uint64_t cells, uint64_t per, uint32_t cap) {
+            return (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(cap, (cells + per - 1) / per));
+        };
+        HmMbPass p1;
+        memset(&p1, 0, sizeof(p1));
+        p1.kin = keys;
+        p1.cin = counts;
+        p1.n = (uint64_t)n;
+        p1.nseg = 1;
+        p1.C = chunks((uint64_t)n, 65536, 512);
+        p1.shift = 64 - b1;
+        p1.bits = b1;
+        const uint64_t m1 = ((uint64_t)1 << b1) * p1.C;
+        uint64_t *cnt1, *off1, *pk, *pc;
+        ENSURE(B_MB_CNT, m1 * 8, cnt1);
+        ENSURE(B_MB_OFF, (m1 + 1) * 8, off1);
+        ENSURE(B_MB_KEYS, (uint64_t)n * 8, pk);
+        ENSURE(B_MB_COUNTS, (uint64_t)n * 8, pc);
+        uint64_t* partial;
+        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+        p1.cnt = cnt1;
+        p1.off = off1;
+        p1.kout = pk;
+        p1.cout = pc;
+        hm_launch_mb_pass(s, p1, false);
+        hm_launch_scan(s, cnt1, m1, partial, off1, off1 + m1);
+        hm_launch_mb_pass(s, p1, true);
+        a.pkeys = pk;
+        a.pcounts = pc;
+        a.boff = off1;
+        a.nblocks = p1.C;
+        if (b2 > 0) {
+            /* second pass: each first-pass bucket (a segment) by the next b2 bits */
+            HmMbPass p2 = p1;
+            p2.kin = pk;
+            p2.cin = pc;
+            p2.segoff = off1;
+            p2.segstride = p1.C;
+            p2.nseg = 1u << b1;
+            p2.C = chunks((uint64_t)n >> b1, 32768, 64);
+            p2.shift = 64 - lb;
+            p2.bits = b2;
+            const uint64_t m2 = ((uint64_t)1 << lb) * p2.C;
+            uint64_t *cnt2, *off2, *qk, *qc;
+            ENSURE(B_MB_CNT2, m2 * 8, cnt2);
+            ENSURE(B_MB_OFF2, (m2 + 1) * 8, off2);
+            ENSURE(B_MB_KEYS2, (uint64_t)n * 8, qk);
+            ENSURE(B_MB_COUNTS2, (uint64_t)n * 8, qc);
+            p2.cnt = cnt2;
+            p2.off = off2;
+            p2.kout = qk;
+            p2.cout = qc;
+            hm_launch_mb_pass(s, p2, false);
+            hm_launch_scan(s, cnt2, m2, partial, off2, off2 + m2);
+            hm_launch_mb_pass(s, p2, true);
+            a.pkeys = qk;
+            a.pcounts = qc;
+            a.boff = off2;
+            a.nblocks = p2.C;
+        }
         a.keys = keys;
         a.counts = counts;
         a.n = (uint64_t)n;
         a.lb = lb;
-        a.nblocks = (uint32_t)std::min<uint64_t>(512, ((uint64_t)n + 65535) / 65536);
-        const uint64_t m = ((uint64_t)1 << lb) * a.nblocks;
-        ENSURE(B_MB_CNT, m * 8, a.bcnt);
-        ENSURE(B_MB_OFF, (m + 1) * 8, a.boff);
-        ENSURE(B_MB_KEYS, (uint64_t)n * 8, a.pkeys);
-        ENSURE(B_MB_COUNTS, (uint64_t)n * 8, a.pcounts);
         unsigned long long* st;
         ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), st);
-        uint64_t* partial;
-        ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
         HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
         a.keys_out = keys_out;
         a.counts_out = counts_out;
         a.cap = (uint64_t)capacity;
         a.cursor = st;
         a.overflow = st + 1;
-        hm_launch_merge_buckets(s, a, partial);
+        hm_launch_mb_merge(s, a);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(down, st, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
         HIPCHK(hipStreamSynchronize(s));

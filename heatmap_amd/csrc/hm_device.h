@@ -48,15 +48,20 @@ __device__ __forceinline__ uint32_t hm_mbcnt(uint64_t mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
-/* inclusive wave prefix sum */
+/* inclusive wave prefix sum: DPP row shifts 1, 2, 4, 8 scan each row of 16
+ * lanes (out-of-row sources read 0), then row_bcast:15 / row_bcast:31 carry
+ * rows 0 -> 1, 2 -> 3 and rows 0-1 -> 2-3 (6 VALU, no LDS permutes).  Every
+ * lane must be active. */
+#define HM_DPP_ADD(v, ctrl, rows) \
+    (v) += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(v), (ctrl), (rows), 0xF, false)
 __device__ __forceinline__ uint32_t hm_wave_incl_scan(uint32_t v)
 {
-    const int lane = hm_lane();
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t t = __shfl_up(v, o, 64);
-        if (lane >= o) v += t;
-    }
+    HM_DPP_ADD(v, 0x111, 0xF);   /* row_shr:1 */
+    HM_DPP_ADD(v, 0x112, 0xF);   /* row_shr:2 */
+    HM_DPP_ADD(v, 0x114, 0xF);   /* row_shr:4 */
+    HM_DPP_ADD(v, 0x118, 0xF);   /* row_shr:8 */
+    HM_DPP_ADD(v, 0x142, 0xA);   /* row_bcast:15 into rows 1, 3 */
+    HM_DPP_ADD(v, 0x143, 0xC);   /* row_bcast:31 into rows 2, 3 */
     return v;
 }
 
@@ -184,6 +189,29 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t dummy, 
     const uint32_t old = atomicAdd(&cur[i], inc);
     const uint32_t base = __builtin_amdgcn_readlane(old, m ? __ffsll((unsigned long long)m) - 1 : 0);
     return same ? base + r : old;
+}
+
+/* LDS histogram increment that merges only when it pays: when more than
+ * HM_MERGE_MIN valid lanes hold lane 0's key (wave-uniform test) those are one
+ * atomic of their first lane; otherwise every valid lane adds 1 on its own
+ * (the LDS serialises the few same-address lanes of a spread-out wave for
+ * less than the merge's VALU work costs).  `dummy_lane`: this lane's private
+ * dummy word. */
+#ifndef HM_MERGE_MIN
+#define HM_MERGE_MIN 8
+#endif
+__device__ __forceinline__ void hm_lds_count_fast(uint32_t* hist, uint32_t dummy_lane, uint32_t key, bool valid)
+{
+    const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
+    const uint64_t m = __ballot(valid & (key == k0));
+    if (__popcll(m) > HM_MERGE_MIN) {
+        const int l = __ffsll((unsigned long long)m) - 1;
+        const bool same = (m >> hm_lane()) & 1ull;
+        const bool lead = hm_lane() == l;
+        atomicAdd(&hist[(valid & (!same | lead)) ? key : dummy_lane], lead ? (uint32_t)__popcll(m) : 1u);
+    } else {
+        atomicAdd(&hist[valid ? key : dummy_lane], 1u);
+    }
 }
 
 /* hm_lds_claim split in two, so several claims can be in flight: prep, the

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     uint32_t rcap[PER], rbase[PER], dsl[PER];
     /* thread t holds digits q * T + t: a wave's lanes reserve for
      * consecutive digits (coalesced atomics on the shard-major fill words) */
-    uint64_t packed = 0;
+    uint32_t tsum = 0;
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = q * HM_P1_THREADS + tid;
@@ -442,24 +442,16 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         cnt[q] = live(d) ? cur[dsl[q]] : 0u;
         gpos[q] = 0;
         if (cnt[q]) gpos[q] = atomicAdd(&a.fill[slot], cnt[q]);
-        packed |= (uint64_t)cnt[q] << (21 * q);
+        tsum += cnt[q];
     }
-    static_assert(PER <= 3 && HM_T1 < (1 << 21), "three 21-bit digit counts per scanned word");
-    static_assert(HM_MAX_F1 % HM_P1_THREADS == 0, "cold digits fill whole q rows");
-    /* exclusive scan in digit order (q major, then thread): one scan of the
-     * three counts packed in 21-bit fields.  Cold digits come first, so the
-     * stage holds the cold keys in [0, cold) and the hot tiles' after them */
-    uint64_t tot64;
-    const uint64_t off64 = hm_block_excl_scan64<HM_P1_THREADS>(packed, (unsigned long long*)scr, &tot64);
+    /* stage ranges in thread order (a thread's digits q = 0.. adjacent): one
+     * 32-bit block scan.  Any disjoint ranges do: the copy-out finds each
+     * staged key's region through its digit slot */
+    uint32_t total;
     uint32_t offq[PER];
-    uint32_t total = 0, cold = 0;
+    offq[0] = hm_block_excl_scan<HM_P1_THREADS>(tsum, (uint32_t*)scr, &total);
 #pragma unroll
-    for (int q = 0; q < PER; q++) {
-        if (q * HM_P1_THREADS == HM_MAX_F1) cold = total;
-        offq[q] = total + (uint32_t)((off64 >> (21 * q)) & 0x1FFFFFu);
-        total += (uint32_t)((tot64 >> (21 * q)) & 0x1FFFFFu);
-    }
-    if (PER * HM_P1_THREADS == HM_MAX_F1) cold = total;
+    for (int q = 1; q < PER; q++) offq[q] = offq[q - 1] + cnt[q - 1];
 #pragma unroll
     for (int q = 0; q < PER; q++) {
         const int d = q * HM_P1_THREADS + tid;
@@ -498,21 +490,21 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
          * then the stores: no load-use round trip per key */
         OutT* out = (OutT*)a.keys_out;
         uint16_t* hout = (uint16_t*)a.keys_hot;
-        uint32_t sv[HM_P1_PPT], sb[HM_P1_PPT];
+        uint32_t sv[HM_P1_PPT], sl[HM_P1_PPT], sb[HM_P1_PPT];
 #pragma unroll
         for (int j = 0; j < HM_P1_PPT; j++) {
             const uint32_t i = j * HM_P1_THREADS + tid;
             const uint32_t ic = i < total ? i : 0u;
-            sb[j] = sdig[ic];
+            sl[j] = sdig[ic];
             sv[j] = (uint32_t)stage[ic];
         }
 #pragma unroll
-        for (int j = 0; j < HM_P1_PPT; j++) sb[j] = dbase[sb[j]];
+        for (int j = 0; j < HM_P1_PPT; j++) sb[j] = dbase[sl[j]];
 #pragma unroll
         for (int j = 0; j < HM_P1_PPT; j++) {
             const uint32_t i = j * HM_P1_THREADS + tid;
             if (i < total && sb[j] != 0xFFFFFFFFu) {
-                if (i < cold)
+                if (sl[j] < HM_MAX_F1)
                     out[sb[j] + i] = (OutT)sv[j];
                 else
                     hout[sb[j] + i] = (uint16_t)sv[j];
@@ -1282,25 +1274,27 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     HM_STAMP_M(3, 1);
     const int sw = a.restbits >> 1, ww = a.dbits >> 1, sp = sw + ww;
     const uint32_t m = (1u << sw) - 1u;
-    /* re-encode each key as (digit << 2s) | rest, then count and rank */
+    /* re-encode each key as (digit slot << 2s) | rest (the slot: the digit's
+     * hm_cur_slot, a bijection), then count and rank */
     uint32_t rank[KPT];
+    const uint32_t dummy = HM_MAX_FN + (uint32_t)hm_lane();
     /* HM_FR_GROUP atomics in flight per thread (more costs registers) */
 #pragma unroll
     for (int k0 = 0; k0 < KPT; k0 += HM_FR_GROUP) {
-        HmMerge gm[HM_FR_GROUP];
+        HmClaim gm[HM_FR_GROUP];
         uint32_t old[HM_FR_GROUP];
 #pragma unroll
         for (int u = 0; u < HM_FR_GROUP; u++) {
             const int k = k0 + u;
             const uint32_t r = kv[k] >> sp, c = kv[k] & ((1u << sp) - 1u);
-            const uint32_t d = ((r >> sw) << ww) | (c >> sw);
-            kv[k] = (d << (2 * sw)) | ((r & m) << sw) | (c & m);
+            const uint32_t ds = hm_cur_slot(((r >> sw) << ww) | (c >> sw), ww);
+            kv[k] = (ds << (2 * sw)) | ((r & m) << sw) | (c & m);
             const bool v = (uint32_t)(k * T + tid) < total;
-            gm[u] = hm_merge_prep(hm_cur_slot(d, ww), v, HM_MAX_FN);
+            gm[u] = hm_claim_prep(ds, v, dummy);
             old[u] = atomicAdd(&cur[gm[u].idx], gm[u].inc);
         }
 #pragma unroll
-        for (int u = 0; u < HM_FR_GROUP; u++) rank[k0 + u] = hm_merge_pos(gm[u], old[u]);
+        for (int u = 0; u < HM_FR_GROUP; u++) rank[k0 + u] = hm_claim_pos(gm[u], old[u]);
     }
     HM_STAMP_M(3, 2);
     __syncthreads();
@@ -1339,8 +1333,8 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
         const bool v = (uint32_t)(k * T + tid) < total;
-        const uint32_t d = kv[k] >> a.restbits;
-        const uint32_t pos = v ? sh0 + cur[hm_cur_slot(v ? d : 0u, ww)] + rank[k] : (uint32_t)HM_TN + V + (uint32_t)(tid & 63);
+        const uint32_t ds = kv[k] >> a.restbits;   /* digit slot */
+        const uint32_t pos = v ? sh0 + cur[v ? ds : 0u] + rank[k] : (uint32_t)HM_TN + V + (uint32_t)(tid & 63);
         stage[pos] = (OutT)(kv[k] & restmask);
     }
     __syncthreads();
@@ -1958,17 +1952,24 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
         uint32_t dummy;
         int lg;
         __device__ __forceinline__ uint32_t sl(uint32_t k) { return HM_AG_SKEW ? hm_skew(k, lg) : k; }
-        __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { hm_lds_count(grid, dummy, sl(k), v); }
+        __device__ __forceinline__ void cnt(uint32_t k, bool v)
+        {
+            if (HM_AG_FAST)
+                hm_lds_count_fast(grid, dummy + (uint32_t)hm_lane(), sl(k), v);
+            else
+                hm_lds_count(grid, dummy, sl(k), v);
+        }
+        __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { cnt(k, v); }
         __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t)
         {
-            hm_lds_count(grid, dummy, sl(x.x & 0xFFFFu), v);
-            hm_lds_count(grid, dummy, sl(x.x >> 16), v);
-            hm_lds_count(grid, dummy, sl(x.y & 0xFFFFu), v);
-            hm_lds_count(grid, dummy, sl(x.y >> 16), v);
-            hm_lds_count(grid, dummy, sl(x.z & 0xFFFFu), v);
-            hm_lds_count(grid, dummy, sl(x.z >> 16), v);
-            hm_lds_count(grid, dummy, sl(x.w & 0xFFFFu), v);
-            hm_lds_count(grid, dummy, sl(x.w >> 16), v);
+            cnt(x.x & 0xFFFFu, v);
+            cnt(x.x >> 16, v);
+            cnt(x.y & 0xFFFFu, v);
+            cnt(x.y >> 16, v);
+            cnt(x.z & 0xFFFFu, v);
+            cnt(x.z >> 16, v);
+            cnt(x.w & 0xFFFFu, v);
+            cnt(x.w >> 16, v);
         }
     } f{grid, HM_AG_CELLS, a.lg};
     hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);

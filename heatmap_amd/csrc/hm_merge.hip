@@ -236,35 +236,97 @@ __device__ __forceinline__ uint32_t hm_mb_bucket(uint64_t k, int lb)
     return lb ? (uint32_t)(hms_hash(k) >> (64 - lb)) : 0u;
 }
 
+/* Hash partition of (key, count) cells, one pass (HmMbPass).  The count
+ * pass histograms each chunk's digits; the scatter pass takes a chunk 4096
+ * cells at a time, orders them by digit in LDS and writes every digit's
+ * cells as one contiguous run at its running offset (a wave's stores are
+ * consecutive words: a direct 4096-way scatter wrote one partial line per
+ * cell and took 1.2 ms for 28M cells). */
+#define HM_MB_PPT 16
+#define HM_MB_TILE (256 * HM_MB_PPT)
+#define HM_MB_MAXD 128
 template <bool SCATTER>
-__global__ __launch_bounds__(256) void k_mb_part(HmMergeArgs a)
+__global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
 {
-    /* dynamic LDS: SCATTER: u64 base[2^lb] then u32 hist[2^lb]; else hist only */
-    extern __shared__ unsigned long long dyn[];
-    const uint32_t NB = 1u << a.lb;
-    uint64_t* base = (uint64_t*)dyn;
-    uint32_t* hist = SCATTER ? (uint32_t*)(dyn + NB) : (uint32_t*)dyn;
-    const uint32_t blk = blockIdx.x;
-    for (uint32_t i = threadIdx.x; i < NB; i += 256) hist[i] = 0;
-    __syncthreads();
-    const uint64_t per = (a.n + a.nblocks - 1) / a.nblocks;
-    const uint64_t b0 = (uint64_t)blk * per, b1 = min(b0 + per, a.n);
-    if (!SCATTER) {
-        for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) atomicAdd(&hist[hm_mb_bucket(a.keys[i], a.lb)], 1u);
-        __syncthreads();
-        for (uint32_t b = threadIdx.x; b < NB; b += 256) a.bcnt[(uint64_t)b * a.nblocks + blk] = hist[b];
-    } else {
-        /* this chunk's slots of each bucket start at boff[b * nblocks + blk] */
-        for (uint32_t b = threadIdx.x; b < NB; b += 256) base[b] = a.boff[(uint64_t)b * a.nblocks + blk];
-        __syncthreads();
-        for (uint64_t i = b0 + threadIdx.x; i < b1; i += 256) {
-            const uint64_t k = a.keys[i];
-            const uint32_t b = hm_mb_bucket(k, a.lb);
-            const uint64_t q = base[b] + atomicAdd(&hist[b], 1u);
-            a.pkeys[q] = k;
-            a.pcounts[q] = a.counts[i];
-        }
+    __shared__ uint32_t hist[HM_MB_MAXD];
+    __shared__ uint32_t toff[HM_MB_MAXD];
+    __shared__ unsigned long long gb[HM_MB_MAXD];
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long sk[SCATTER ? HM_MB_TILE : 1], sc[SCATTER ? HM_MB_TILE : 1];
+    __shared__ uint8_t sd[SCATTER ? HM_MB_TILE : 1];
+    const int tid = threadIdx.x;
+    const uint32_t s = blockIdx.x / a.C, c = blockIdx.x % a.C;
+    const uint32_t nd = 1u << a.bits, dm = nd - 1u;
+    const uint64_t s0 = a.segoff ? a.segoff[(uint64_t)s * a.segstride] : 0ull;
+    const uint64_t s1 = a.segoff ? a.segoff[(uint64_t)(s + 1) * a.segstride] : a.n;
+    const uint64_t len = s1 - s0;
+    const uint64_t c0 = s0 + len * c / a.C, c1 = s0 + len * (c + 1) / a.C;
+    const uint64_t cbase = ((uint64_t)s << a.bits) * a.C + c;   /* + d * C */
+    for (uint32_t d = tid; d < nd; d += 256) {
+        hist[d] = 0;
+        if (SCATTER) gb[d] = a.off[cbase + (uint64_t)d * a.C];
     }
+    __syncthreads();
+    if (!SCATTER) {
+        for (uint64_t i = c0 + tid; i < c1; i += 256) atomicAdd(&hist[(uint32_t)(hms_hash(a.kin[i]) >> a.shift) & dm], 1u);
+        __syncthreads();
+        for (uint32_t d = tid; d < nd; d += 256) a.cnt[cbase + (uint64_t)d * a.C] = hist[d];
+        return;
+    }
+    for (uint64_t t0 = c0; t0 < c1; t0 += HM_MB_TILE) {
+        const uint32_t tn = (uint32_t)min((uint64_t)HM_MB_TILE, c1 - t0);
+        uint64_t k[HM_MB_PPT], cc[HM_MB_PPT];
+        uint32_t d[HM_MB_PPT], r[HM_MB_PPT];
+#pragma unroll
+        for (int j = 0; j < HM_MB_PPT; j++) {
+            const uint32_t i = j * 256 + tid;
+            const bool v = i < tn;
+            k[j] = v ? a.kin[t0 + i] : 0ull;
+            cc[j] = v ? a.cin[t0 + i] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < HM_MB_PPT; j++) {
+            const bool v = (uint32_t)(j * 256 + tid) < tn;
+            d[j] = (uint32_t)(hms_hash(k[j]) >> a.shift) & dm;
+            r[j] = v ? atomicAdd(&hist[d[j]], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t tot;
+        const uint32_t o = hm_block_excl_scan<256>(tid < (int)nd ? hist[tid] : 0u, scr, &tot);
+        if (tid < (int)nd) toff[tid] = o;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < HM_MB_PPT; j++) {
+            if ((uint32_t)(j * 256 + tid) < tn) {
+                const uint32_t pos = toff[d[j]] + r[j];
+                sk[pos] = k[j];
+                sc[pos] = cc[j];
+                sd[pos] = (uint8_t)d[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < tn; i += 256) {
+            const uint32_t dd = sd[i];
+            const uint64_t dst = gb[dd] + (i - toff[dd]);
+            a.kout[dst] = sk[i];
+            a.cout[dst] = sc[i];
+        }
+        __syncthreads();
+        if (tid < (int)nd) {
+            gb[tid] += hist[tid];
+            hist[tid] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+void hm_launch_mb_pass(hipStream_t s, const HmMbPass& a, bool scatter)
+{
+    const unsigned g = a.nseg * a.C;
+    if (scatter)
+        hipLaunchKernelGGL(k_mb_pass<true>, dim3(g), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_mb_pass<false>, dim3(g), dim3(256), 0, s, a);
 }
 
 /* one bucket per block: its cells into an LDS table (P sub-passes by hash
@@ -335,14 +397,9 @@ __global__ __launch_bounds__(HM_MB_THREADS) void k_mb_merge(HmMergeArgs a)
     }
 }
 
-void hm_launch_merge_buckets(hipStream_t s, const HmMergeArgs& a, uint64_t* partial)
+void hm_launch_mb_merge(hipStream_t s, const HmMergeArgs& a)
 {
-    const uint32_t NB = 1u << a.lb;
-    const uint64_t m = (uint64_t)NB * a.nblocks;
-    hipLaunchKernelGGL(k_mb_part<false>, dim3(a.nblocks), dim3(256), NB * 4, s, a);
-    hm_launch_scan(s, a.bcnt, m, partial, a.boff, a.boff + m);
-    hipLaunchKernelGGL(k_mb_part<true>, dim3(a.nblocks), dim3(256), NB * 12, s, a);
-    hipLaunchKernelGGL(k_mb_merge, dim3(NB), dim3(HM_MB_THREADS), 0, s, a);
+    hipLaunchKernelGGL(k_mb_merge, dim3(1u << a.lb), dim3(HM_MB_THREADS), 0, s, a);
 }
 
 static unsigned hm_mgrid(uint64_t n, unsigned cap)

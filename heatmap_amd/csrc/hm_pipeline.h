@@ -80,6 +80,9 @@ __host__ __device__ inline uint32_t hm_l1i(uint32_t d, uint32_t sh) { return sh 
 #define HM_AG_THREADS 1024
 #define HM_AG_CELLS 16384
 #define HM_AG_LG 7
+#ifndef HM_AG_FAST
+#define HM_AG_FAST 1                        /* k_aggregate: hm_lds_count_fast (merge only wave-heavy keys) */
+#endif
 #ifndef HM_AG_SKEW
 #define HM_AG_SKEW 0                        /* 1: k_aggregate counts at hm_skew slots (0 measured 0.09 ms faster on hotspots, neutral on skew) */
 #endif
@@ -569,7 +572,7 @@ unsigned hm_route_blocks(uint64_t n);
 /* bucketed merge of (key, count) cells: hash-partition into 2^lb buckets
  * (count + scatter passes over nblocks input chunks), then one block per
  * bucket sums equal keys in an LDS table and writes the distinct cells */
-#define HM_MB_TS 8192                 /* LDS table slots per merge block */
+#define HM_MB_TS 4096                 /* LDS table slots per merge block (buckets of <= ~1800 cells: one pass) */
 #define HM_MB_THREADS 1024
 struct HmMergeArgs {
     const uint64_t* keys;
@@ -587,7 +590,25 @@ struct HmMergeArgs {
     unsigned long long* cursor;
     unsigned long long* overflow;   /* an LDS table filled up: the caller falls back */
 };
-void hm_launch_merge_buckets(hipStream_t s, const HmMergeArgs& a, uint64_t* partial);
+/* one hash-partition pass of the bucketed merge (k_mb_pass): segment s of
+ * the input (all of it when segoff is null, else [segoff[s * segstride],
+ * segoff[(s + 1) * segstride])) is cut into C chunks, one block each; digit
+ * = (hms_hash(key) >> shift) & (2^bits - 1); cnt/off index ((s << bits) + d)
+ * * C + c, so their scan is in (segment, digit, chunk) order */
+struct HmMbPass {
+    const uint64_t* kin;
+    const uint64_t* cin;
+    uint64_t n;
+    const uint64_t* segoff;
+    uint32_t segstride, nseg, C;
+    int shift, bits;
+    uint64_t* cnt;
+    const uint64_t* off;
+    uint64_t* kout;
+    uint64_t* cout;
+};
+void hm_launch_mb_pass(hipStream_t s, const HmMbPass& a, bool scatter);
+void hm_launch_mb_merge(hipStream_t s, const HmMergeArgs& a);
 void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter);
 void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t);
 void hm_launch_cells_merge_unique(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n,

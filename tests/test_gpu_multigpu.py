@@ -59,6 +59,21 @@ def test_merge_kernel_sums_duplicates(gpu):
     assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
 
 
+@pytest.mark.parametrize("n", [1, 100, 1801, 300_000, 6_000_000])
+def test_merge_partition_passes(gpu, n):
+    """hm_cells_merge at sizes that take zero, one and two hash-partition
+    passes (2^lb buckets of <= ~1800 cells), keys repeated up to 3 times."""
+    g = torch.Generator().manual_seed(n)
+    base = torch.randint(0, 1 << 62, (n,), generator=g, dtype=torch.int64)
+    k = torch.cat([base, base[::2], base[::5]])
+    c = torch.randint(1, 1 << 31, (k.numel(),), generator=g, dtype=torch.int64)
+    p = torch.randperm(k.numel(), generator=g)
+    uk, uc = multigpu.DeviceOps(0).merge(k[p].cuda(), c[p].cuda())
+    ek, ec = TorchOps.merge(k, c)
+    o = torch.argsort(uk.cpu())
+    assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
+
+
 def test_merge_runs_of_distinct_keys(gpu):
     """hm_cells_merge_runs: three runs (one per sending rank), each of distinct
     keys, overlapping across runs; an empty run in between."""
