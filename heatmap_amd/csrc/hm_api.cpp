@@ -554,6 +554,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
 
     hipEvent_t* ev = ctx->ev;
     int nev = 0;
+    /* stage timings (hm_last_stats) for calls of >= 2^24 points: each event
+     * record is an API call, and small calls (stream batches) are bound by
+     * the host's issue rate */
+    const bool timing = n >= (1ll << 24);
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
     ctx->last_levels = L;
 
@@ -716,6 +720,45 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 bound = (double)ctx->host_state[ST_L1TOTAL] + 1024.0;
                 if (bound >= (double)0xFFF00000ull) return HM_FALLBACK;   /* key positions are u32 */
             }
+            /* the non-empty digits are the level's buckets, one run each */
+            HmL1Args ba;
+            memset(&ba, 0, sizeof(ba));
+            const uint64_t cap = (uint64_t)F + 1;
+            ENSURE(B_BK0 + 0, cap * 4, ba.out.nkeys);
+            ENSURE(B_BK0 + 1, cap * 4, ba.out.nruns);
+            ENSURE(B_BK0 + 2, cap * 4, ba.out.rbase);
+            ENSURE(B_BK0 + 3, cap * 4, ba.out.item_begin);
+            ENSURE(B_BK0 + 4, cap * 4, ba.out.digit);
+            ENSURE(B_BK0 + 5, cap * 8, ba.out.coord);
+            ENSURE(B_BK0 + 6, cap * 4, ba.out.keybase);
+            ENSURE(B_FLAT_A, (uint64_t)FS * sizeof(uint2) + 8, ba.runs);
+            ENSURE(B_EXCL_A, (uint64_t)FS * sizeof(uint64_t) + 8, ba.excl);
+            ENSURE(B_CHILD0, 2 * 4, ba.child_begin);
+            uint64_t* tot;
+            ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+            ba.F = F;
+            ba.dbits = V.dbits;
+            ba.fill = fill;
+            ba.rbase = rbase;
+            ba.smask = smask;
+            ba.item_keys = (L == 1) ? HM_TA : HM_TN;
+            ba.sparse_max = (L == 1) ? HM_SP_MAX : 0u;
+            ba.total = tot;
+            if (hot_on) {   /* hot parents all zero when no tile turned out hot */
+                uint32_t* d2b;
+                ENSURE(B_D2B, HM_MAX_F1 * 4, d2b);
+                ba.hotparent = hr.tiles ? (const uint8_t*)ctx->bufs[B_HOT_PARENT].p : nullptr;
+                ba.d2b = d2b;
+                hr.d2b = d2b;
+            }
+            if (L == 1) {
+                ENSURE(B_SLOTS, cap * 4, slots);
+                ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
+                ba.slots = slots;
+                ba.nslots = (uint32_t*)(ctx->state + ST_NSLOTS);
+                ba.slot_bucket = slot_bucket;
+            }
+            unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
             void* kout = nullptr;
             uint64_t total_cap = (uint64_t)bound;
             for (int attempt = 0;; attempt++) {
@@ -742,14 +785,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     a.keys_hot = kh;
                 }
                 HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
-                HIPCHK(hipMemsetAsync(ctx->state + ST_OVERFLOW, 0, 8, s));
-                HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, 16, s));   /* ST_REDO, ST_REDO_OUT */
-                HIPCHK(hipMemsetAsync(ctx->state + ST_SLOW, 0, 8, s));
-                HIPCHK(hipMemsetAsync(xl.count, 0, 8, s));
-                HIPCHK(hipEventRecord(ev[0], s));
+                /* ST_XCOUNT .. ST_OVERFLOW (XCOUNT, SLOW, REDO, REDO_OUT, OVERFLOW;
+                 * CURSOR, NSLOTS, XCURSOR are still 0 here) in one memset */
+                static_assert(ST_XCOUNT == 1 && ST_OVERFLOW == 8 && ST_NHOT > ST_OVERFLOW, "level-1 words");
+                HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, 8 * 8, s));
+                if (timing) HIPCHK(hipEventRecord(ev[0], s));
                 hm_launch_part1(s, a, tiles_in, V.out16, from_tiles ? 1 : 0);
                 HIPCHK(hipGetLastError());
-                HIPCHK(hipEventRecord(ev[1], s));
+                if (timing) HIPCHK(hipEventRecord(ev[1], s));
                 nev = 2;
                 if (!from_tiles) {
                     HmRedoArgs ra;
@@ -783,7 +826,18 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     hm_launch_part1(s, b, (uint32_t)((redo_cap + HM_T1 - 1) / HM_T1), V.out16, 1);
                     HIPCHK(hipGetLastError());
                 }
-                if ((st = read_state(ctx))) return st;
+                /* the level's buckets from the filled regions, launched before
+                 * the one host sync of level 1 (its results are used only if
+                 * the level turns out clean: no error, no redo or region
+                 * overflow) */
+                auto buckets1 = [&]() -> int {
+                    hm_launch_level1_buckets(s, ba);
+                    HIPCHK(hipGetLastError());
+                    HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+                    if (L > 1) HIPCHK(hipMemcpyAsync(ctx->host_aux, hist, F * 4, hipMemcpyDeviceToHost, s));
+                    return read_state(ctx);
+                };
+                if ((st = buckets1())) return st;
                 if ((st = take_error(ctx))) return st;
                 const uint64_t nredo = ctx->host_state[ST_REDO];
                 ctx->last_slow = (int64_t)nredo;
@@ -793,9 +847,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
                     HIPCHK(hipMemsetAsync(ctx->state + ST_OVERFLOW, 0, 8, s));
                     HIPCHK(hipMemsetAsync(xl.count, 0, 8, s));
+                    HIPCHK(hipMemsetAsync(ctx->state + ST_NSLOTS, 0, 8, s));   /* buckets1 again */
                     hm_launch_part1(s, a, tiles_in, V.out16, 2);
                     HIPCHK(hipGetLastError());
-                    if ((st = read_state(ctx))) return st;
+                    if ((st = buckets1())) return st;
                     if ((st = take_error(ctx))) return st;
                 }
                 if (!ctx->host_state[ST_OVERFLOW]) break;
@@ -820,51 +875,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 nx = ctx->host_state[ST_XCOUNT];
                 if (nx > xl.cap) return HM_E_HIP;   /* cannot happen: the same points */
             }
-            /* the non-empty digits are the level's buckets, one run each */
-            HmL1Args ba;
-            memset(&ba, 0, sizeof(ba));
-            const uint64_t cap = (uint64_t)F + 1;
-            ENSURE(B_BK0 + 0, cap * 4, ba.out.nkeys);
-            ENSURE(B_BK0 + 1, cap * 4, ba.out.nruns);
-            ENSURE(B_BK0 + 2, cap * 4, ba.out.rbase);
-            ENSURE(B_BK0 + 3, cap * 4, ba.out.item_begin);
-            ENSURE(B_BK0 + 4, cap * 4, ba.out.digit);
-            ENSURE(B_BK0 + 5, cap * 8, ba.out.coord);
-            ENSURE(B_BK0 + 6, cap * 4, ba.out.keybase);
-            ENSURE(B_FLAT_A, (uint64_t)FS * sizeof(uint2) + 8, ba.runs);
-            ENSURE(B_EXCL_A, (uint64_t)FS * sizeof(uint64_t) + 8, ba.excl);
-            ENSURE(B_CHILD0, 2 * 4, ba.child_begin);
-            uint64_t* tot;
-            ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
-            ba.F = F;
-            ba.dbits = V.dbits;
-            ba.fill = fill;
-            ba.rbase = rbase;
-            ba.smask = smask;
-            ba.item_keys = (L == 1) ? HM_TA : HM_TN;
-            ba.sparse_max = (L == 1) ? HM_SP_MAX : 0u;
-            ba.total = tot;
             nhot = hot_on ? (uint32_t)(ctx->host_state[ST_NHOT] & 0xFFFFFFFFull) : 0u;
-            if (nhot) {
-                uint32_t* d2b;
-                ENSURE(B_D2B, HM_MAX_F1 * 4, d2b);
-                ba.hotparent = hr.tiles ? (const uint8_t*)ctx->bufs[B_HOT_PARENT].p : nullptr;
-                ba.d2b = d2b;
-                hr.d2b = d2b;
-            }
-            if (L == 1) {
-                ENSURE(B_SLOTS, cap * 4, slots);
-                ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
-                ba.slots = slots;
-                ba.nslots = (uint32_t*)(ctx->state + ST_NSLOTS);
-                ba.slot_bucket = slot_bucket;
-            }
-            hm_launch_level1_buckets(s, ba);
-            HIPCHK(hipGetLastError());
-            unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
-            HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-            if (L > 1) HIPCHK(hipMemcpyAsync(ctx->host_aux, hist, F * 4, hipMemcpyDeviceToHost, s));
-            if ((st = read_state(ctx))) return st;
             /* levels 2.. may take the spread plan (the level-1 pass is the
              * same under both: its output is u32 keys whenever L > 1) */
             if (L > 1 && !nhot) spread_replan(ctx->host_aux, F, n, zb, zs, &L, ctx->spread_min_keys);
@@ -939,10 +950,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.runs_out = runs_sh;
             a.items = lv[l - 1].items;
             a.seg = l == 1 ? seg1 : nullptr;
-            HIPCHK(hipEventRecord(ev[5 + 2 * (l - 1)], s));
+            if (timing) HIPCHK(hipEventRecord(ev[5 + 2 * (l - 1)], s));
             hm_launch_partN(s, a, lv[l - 1].items, V.out16, l == 1 && seg1 != nullptr);
             HIPCHK(hipGetLastError());
-            HIPCHK(hipEventRecord(ev[6 + 2 * (l - 1)], s));
+            if (timing) HIPCHK(hipEventRecord(ev[6 + 2 * (l - 1)], s));
             npart = l;
         }
 
@@ -1081,7 +1092,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         nparents = V.count;
         slot_k ^= 1;
     }
-    HIPCHK(hipEventRecord(ev[nev++], s));
+    if (timing) HIPCHK(hipEventRecord(ev[nev], s));
+    nev++;
 
     /* final aggregation over B_L */
     HmOut o;
@@ -1127,7 +1139,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         hm_launch_small(s, a, partial);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(ev[nev++], s));
+    if (timing) HIPCHK(hipEventRecord(ev[nev], s));
+    nev++;
     /* pooling: level l children -> parents in B_{l-1} (root for l = 0) */
     for (int l = L - 1; l >= 0; l--) {
         HmPoolArgs pa;
@@ -1146,14 +1159,15 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         hm_launch_pool(s, pa, lv[l].nparents);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(ev[nev++], s));
+    if (timing) HIPCHK(hipEventRecord(ev[nev], s));
+    nev++;
     if ((st = read_state(ctx))) return st;
-    for (int i = 0; i + 1 < nev; i++) {
+    for (int i = 0; timing && i + 1 < nev; i++) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, ev[i], ev[i + 1]);
         ctx->stage_us[i] = ms * 1000.0;
     }
-    for (int l = 1; l <= npart; l++) {
+    for (int l = 1; timing && l <= npart; l++) {
         float ms = 0;
         (void)hipEventElapsedTime(&ms, ev[5 + 2 * (l - 1)], ev[6 + 2 * (l - 1)]);
         ctx->stage_us[4] += ms * 1000.0;
@@ -1521,75 +1535,31 @@ extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int
 struct hm_stream {
     hm_ctx* ctx = nullptr;
     int zmin = 0, zmax = 0;
-    int cb = 0;                           /* cell bits of a table key */
+    int cb = 0;                           /* cell bits of a log key */
     uint32_t base = 0;
-    HmsTable t{};                         /* cells */
+    unsigned long long* state = nullptr;  /* device HMS_ST_* words */
     HmsBuckets bk{};                      /* (group, period) buckets */
     uint32_t *bflag = nullptr, *blist = nullptr, *bloc = nullptr; /* per bucket: last batch, list, run */
     uint32_t epoch = 0;
-    uint64_t occupied = 0, nbuckets = 0;  /* occupied: exact, or an upper bound while stale */
-    bool stale = false;
-    unsigned long long* hstate = nullptr; /* pinned mirror of t.state */
-    Buf bids, rec, bkeys, bcounts;        /* per-batch scratch */
+    /* the cell log: llen cells of lcap; alt: the compaction target */
+    uint64_t *lkeys = nullptr, *lcounts = nullptr, *akeys = nullptr, *acounts = nullptr;
+    uint64_t lcap = 0, llen = 0;
+    bool compact = true;                  /* the log holds distinct keys */
+    uint64_t nbuckets = 0;
+    unsigned long long* hstate = nullptr; /* pinned mirror of state */
+    Buf bids, rec;                        /* per-batch scratch */
     Buf plat, plon, pkeep, pstart, pcnt;  /* partition path: bucket-contiguous batch */
-    int64_t bcap = 0, rcap = 0;           /* cells bkeys/bcounts, records rec hold */
-    Buf rslots;                           /* rollup table */
+    int64_t rcap = 0;                     /* records rec holds */
+    Buf rk, rc, mk, mc;                   /* rollup scratch: relabeled and merged cells */
 };
 
 static int stream_sync_state(hm_stream* s)
 {
-    HIPCHK(hipMemcpyAsync(s->hstate, s->t.state, HMS_ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
+    HIPCHK(hipMemcpyAsync(s->hstate, s->state, HMS_ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                           s->ctx->stream));
     HIPCHK(hipStreamSynchronize(s->ctx->stream));
-    s->occupied = s->hstate[HMS_ST_OCCUPIED];
     s->nbuckets = s->hstate[HMS_ST_BUCKETS];
-    s->stale = false;
-    return s->hstate[HMS_ST_OVERFLOW] ? HM_E_CAPACITY : HM_OK;
-}
-
-/* after an insert of m cells: the occupancy grows by at most m; the exact
- * count is read at the next sync (no host round trip per batch) */
-static int stream_inserted(hm_stream* s, uint64_t m)
-{
-    s->occupied += m;
-    s->stale = true;
     return HM_OK;
-}
-
-static int stream_alloc_table(hm_stream* s, uint64_t cap, HmsTable* t)
-{
-    t->mask = cap - 1;
-    t->state = s->t.state;
-    if (hipMalloc((void**)&t->slots, cap * 16) != hipSuccess) {
-        (void)hipGetLastError();
-        t->slots = nullptr;
-        return HM_E_NOMEM;
-    }
-    hm_launch_stream_init(s->ctx->stream, *t);
-    HIPCHK(hipGetLastError());
-    return HM_OK;
-}
-
-/* keep the load factor <= 5/8 after inserting `incoming` more cells */
-static int stream_reserve(hm_stream* s, uint64_t incoming)
-{
-    uint64_t cap = s->t.mask + 1;
-    if ((s->occupied + incoming) * 8 <= cap * 5) return HM_OK;
-    int st;
-    if (s->stale && (st = stream_sync_state(s))) return st;   /* the exact count */
-    const uint64_t need = s->occupied + incoming;
-    if (need * 8 <= cap * 5) return HM_OK;
-    while (need * 8 > cap * 5) cap <<= 1;
-    HmsTable nt;
-    st = stream_alloc_table(s, cap, &nt);
-    if (st) return st;
-    HIPCHK(hipMemsetAsync(s->t.state, 0, 2 * sizeof(unsigned long long), s->ctx->stream));
-    hm_launch_stream_rehash(s->ctx->stream, s->t, nt);
-    HIPCHK(hipGetLastError());
-    st = stream_sync_state(s);
-    HIPCHK(hipFree(s->t.slots));
-    s->t = nt;
-    return st;
 }
 
 static int stream_buf(hm_stream* s, Buf& b, size_t bytes)
@@ -1607,38 +1577,96 @@ static int stream_buf(hm_stream* s, Buf& b, size_t bytes)
     return HM_OK;
 }
 
-static int stream_cells_buf(hm_stream* s, int64_t want)
+static int stream_alloc2(uint64_t n, uint64_t** k, uint64_t** c)
 {
-    if (s->bcap >= want) return HM_OK;
-    int st;
-    if ((st = stream_buf(s, s->bkeys, (size_t)want * 8)) || (st = stream_buf(s, s->bcounts, (size_t)want * 8)))
-        return st;
-    s->bcap = want;
+    *k = nullptr;
+    *c = nullptr;
+    if (hipMalloc((void**)k, n * 8) != hipSuccess || hipMalloc((void**)c, n * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        if (*k) (void)hipFree(*k);
+        *k = nullptr;
+        *c = nullptr;
+        return HM_E_NOMEM;
+    }
     return HM_OK;
 }
 
-/* a batch of one bucket: hm_count's pyramid, folded in under that bucket */
+/* sum the log's equal keys (the bucketed LDS merge) into the alternate
+ * arrays, then swap them in */
+static int stream_compact(hm_stream* s)
+{
+    if (s->compact || s->llen == 0) {
+        s->compact = true;
+        return HM_OK;
+    }
+    int st;
+    if (!s->akeys && (st = stream_alloc2(s->lcap, &s->akeys, &s->acounts))) return st;
+    int64_t m = 0;
+    if ((st = cells_merge(s->ctx, s->lkeys, s->lcounts, (int64_t)s->llen, nullptr, 0, s->akeys, s->acounts,
+                          (int64_t)s->lcap, &m)))
+        return st;
+    std::swap(s->lkeys, s->akeys);
+    std::swap(s->lcounts, s->acounts);
+    s->llen = (uint64_t)m;
+    s->compact = true;
+    return HM_OK;
+}
+
+/* room for `need` more cells at the log's tail: compact first, then grow */
+static int stream_room(hm_stream* s, uint64_t need)
+{
+    if (s->lcap - s->llen >= need) return HM_OK;
+    int st;
+    if ((st = stream_compact(s))) return st;
+    if (s->lcap - s->llen >= need) return HM_OK;
+    uint64_t cap = s->lcap ? s->lcap : 1024;
+    while (cap - s->llen < need) cap <<= 1;
+    uint64_t *k, *c;
+    if ((st = stream_alloc2(cap, &k, &c))) return st;
+    hipStream_t q = s->ctx->stream;
+    if (s->llen) {
+        HIPCHK(hipMemcpyAsync(k, s->lkeys, s->llen * 8, hipMemcpyDeviceToDevice, q));
+        HIPCHK(hipMemcpyAsync(c, s->lcounts, s->llen * 8, hipMemcpyDeviceToDevice, q));
+    }
+    HIPCHK(hipStreamSynchronize(q));
+    for (uint64_t* p : {s->lkeys, s->lcounts, s->akeys, s->acounts})
+        if (p) (void)hipFree(p);
+    s->lkeys = k;
+    s->lcounts = c;
+    s->akeys = s->acounts = nullptr;   /* the compaction target, at the new size when needed */
+    s->lcap = cap;
+    return HM_OK;
+}
+
+/* m cells appended at the tail */
+static void stream_appended(hm_stream* s, uint64_t m)
+{
+    if (m) s->compact = s->compact && s->llen == 0;   /* one count's cells are distinct */
+    s->llen += m;
+}
+
+/* a batch of one bucket: hm_count's cells written at the log's tail, keyed
+ * under that bucket */
 static int stream_fold_one(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
                            uint32_t bucket)
 {
     int64_t m = 0;
     int st;
-    if ((st = stream_cells_buf(s, 2 * n + 1024))) return st; /* typical batches: fewer cells than 2 per point */
+    if ((st = stream_room(s, 2 * (uint64_t)n + 1024))) return st; /* typical batches: fewer cells than 2 per point */
     for (;;) {
         int64_t nx = 0;
-        st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, (uint64_t*)s->bkeys.p, (uint64_t*)s->bcounts.p,
-                      s->bcap, &m, nullptr, 0, &nx);
-        /* the resident table's keys hold tiles inside [0, 2^z)^2 only */
+        st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, s->lkeys + s->llen, s->lcounts + s->llen,
+                      (int64_t)(s->lcap - s->llen), &m, nullptr, 0, &nx);
+        /* the log's keys hold tiles inside [0, 2^z)^2 only */
         if (nx > 0) return HM_E_EXOTIC;
         if (st != HM_E_CAPACITY) break;
-        if ((st = stream_cells_buf(s, m + m / 4 + 1024))) return st;
+        if ((st = stream_room(s, (uint64_t)(m + m / 4 + 1024)))) return st;
     }
     if (st) return st;
-    if ((st = stream_reserve(s, (uint64_t)m))) return st;
-    hm_launch_stream_insert(s->ctx->stream, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m,
-                            true, (uint64_t)bucket << s->cb, s->t);
+    hm_launch_stream_rekey(s->ctx->stream, s->lkeys + s->llen, (uint64_t)m, (uint64_t)bucket << s->cb);
     HIPCHK(hipGetLastError());
-    return stream_inserted(s, (uint64_t)m);
+    stream_appended(s, (uint64_t)m);
+    return HM_OK;
 }
 
 /* a batch of several buckets: one grouped pass with the bucket as group */
@@ -1660,24 +1688,23 @@ static int stream_fold_grouped(hm_stream* s, const double* lat, const double* lo
         s->rcap = want;
     }
     if (st) return st;
-    if ((st = stream_cells_buf(s, m + 1))) return st;
+    if ((st = stream_room(s, (uint64_t)m + 1))) return st;
     hipStream_t q = s->ctx->stream;
-    HIPCHK(hipMemsetAsync(s->t.state + HMS_ST_EXOTIC, 0, 8, q));
-    hm_launch_stream_convert(q, (const int64_t*)s->rec.p, (uint64_t)m, s->cb, (uint64_t*)s->bkeys.p,
-                             (uint64_t*)s->bcounts.p, s->t.state);
+    HIPCHK(hipMemsetAsync(s->state + HMS_ST_EXOTIC, 0, 8, q));
+    hm_launch_stream_convert(q, (const int64_t*)s->rec.p, (uint64_t)m, s->cb, s->lkeys + s->llen,
+                             s->lcounts + s->llen, s->state);
     HIPCHK(hipGetLastError());
     if ((st = stream_sync_state(s))) return st;
-    if (s->hstate[HMS_ST_EXOTIC]) return HM_E_EXOTIC;   /* checked before anything is inserted */
-    if ((st = stream_reserve(s, (uint64_t)m))) return st;
-    hm_launch_stream_insert(q, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, (uint64_t)m, false, 0, s->t);
-    HIPCHK(hipGetLastError());
-    return stream_inserted(s, (uint64_t)m);
+    if (s->hstate[HMS_ST_EXOTIC]) return HM_E_EXOTIC;   /* checked before the cells join the log */
+    stream_appended(s, (uint64_t)m);
+    return HM_OK;
 }
 
 /* a batch of a few buckets: gathered into one run per bucket (+ one run of
- * the points not kept), one hm_count per run, all counted before anything is
- * inserted.  Errors: the batch is re-counted as a whole so the reported point
- * is the first failing one in input order, as hm_count's. */
+ * the points not kept), one hm_count per run written at the log's tail, all
+ * counted before the tail joins the log.  Errors: the batch is re-counted as
+ * a whole so the reported point is the first failing one in input order, as
+ * hm_count's. */
 static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
                              uint32_t nparts)
 {
@@ -1725,7 +1752,7 @@ static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon,
         if ((st = stream_buf(s, s->pkeep, (size_t)nun))) return st;
         HIPCHK(hipMemsetAsync(s->pkeep.p, 0, nun, q));
     }
-    if ((st = stream_cells_buf(s, 2 * (int64_t)kept + 1024))) return st;
+    if ((st = stream_room(s, 2 * kept + 1024))) return st;
     for (;;) {
         uint64_t off = 0;
         bool grow = false;
@@ -1733,19 +1760,20 @@ static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon,
             const uint64_t nj = (j < nparts ? start[j + 1] : (uint64_t)n) - start[j];
             if (!nj) continue;
             int64_t m = 0, nx = 0;
+            uint64_t* tk = s->lkeys + s->llen + off;
+            uint64_t* tc = s->lcounts + s->llen + off;
             st = hm_count(ctx, (const double*)s->plat.p + start[j], (const double*)s->plon.p + start[j],
-                          j < nparts ? nullptr : (const uint8_t*)s->pkeep.p, (int64_t)nj, s->zmin, s->zmax,
-                          (uint64_t*)s->bkeys.p + off, (uint64_t*)s->bcounts.p + off, s->bcap - (int64_t)off, &m,
-                          nullptr, 0, &nx);
-            /* the resident table's keys hold tiles inside [0, 2^z)^2 only (and
-             * with no record buffer given, hm_count reports them as capacity) */
+                          j < nparts ? nullptr : (const uint8_t*)s->pkeep.p, (int64_t)nj, s->zmin, s->zmax, tk, tc,
+                          (int64_t)(s->lcap - s->llen - off), &m, nullptr, 0, &nx);
+            /* the log's keys hold tiles inside [0, 2^z)^2 only (and with no
+             * record buffer given, hm_count reports them as capacity) */
             if (nx > 0) return HM_E_EXOTIC;
             if (st == HM_E_CAPACITY) {
-                if ((st = stream_cells_buf(s, (int64_t)(off + m) * 5 / 4 + 1024))) return st;
+                if ((st = stream_room(s, (off + (uint64_t)m) * 5 / 4 + 1024))) return st;
                 grow = true;
                 break;
             }
-            if (st != HM_OK && st != HM_E_CAPACITY) {
+            if (st != HM_OK) {
                 /* the first failing point in input order */
                 int64_t m2 = 0, nx2 = 0;
                 const int st2 = hm_count(ctx, lat, lon, keep, n, s->zmin, s->zmax, nullptr, nullptr, 0, &m2, nullptr,
@@ -1753,16 +1781,15 @@ static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon,
                 return st2 != HM_OK && st2 != HM_E_CAPACITY ? st2 : st;
             }
             if (j < nparts) {
-                hm_launch_stream_rekey(q, (uint64_t*)s->bkeys.p + off, (uint64_t)m, (uint64_t)hb[j] << s->cb);
+                hm_launch_stream_rekey(q, tk, (uint64_t)m, (uint64_t)hb[j] << s->cb);
                 HIPCHK(hipGetLastError());
                 off += (uint64_t)m;
             }
         }
         if (grow) continue;
-        if ((st = stream_reserve(s, off))) return st;
-        hm_launch_stream_insert(q, (const uint64_t*)s->bkeys.p, (const uint64_t*)s->bcounts.p, off, false, 0, s->t);
-        HIPCHK(hipGetLastError());
-        return stream_inserted(s, off);
+        /* several buckets' cells: distinct only across buckets, still a fresh log's */
+        stream_appended(s, off);
+        return HM_OK;
     }
 }
 
@@ -1786,19 +1813,18 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
     const uint64_t want = max_buckets ? (uint64_t)max_buckets : (1ull << 20);
     while (nb < want + want / 4 && nb < (1ull << bb)) nb <<= 1;
     s->bk.mask = nb - 1;
-    uint64_t cap = 1024;
-    while (cap * 5 < (uint64_t)initial_cells * 8) cap <<= 1;
-    if (hipMalloc((void**)&s->t.state, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
+    s->lcap = std::max<uint64_t>(1024, (uint64_t)initial_cells);
+    int st = HM_OK;
+    if (hipMalloc((void**)&s->state, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc((void**)&s->hstate, 2 * HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&s->bk.keys, nb * 8) != hipSuccess || hipMalloc((void**)&s->bflag, nb * 4) != hipSuccess ||
-        hipMalloc((void**)&s->blist, nb * 4) != hipSuccess || hipMalloc((void**)&s->bloc, nb * 4) != hipSuccess) {
+        hipMalloc((void**)&s->blist, nb * 4) != hipSuccess || hipMalloc((void**)&s->bloc, nb * 4) != hipSuccess ||
+        stream_alloc2(s->lcap, &s->lkeys, &s->lcounts) != HM_OK) {
         (void)hipGetLastError();
         hm_stream_destroy(s);
         return HM_E_NOMEM;
     }
-    int st = stream_alloc_table(s, cap, &s->t);
-    if (st == HM_OK)
-        st = hip_fail(hipMemsetAsync(s->t.state, 0, HMS_ST_COUNT * sizeof(unsigned long long), ctx->stream), "memset");
+    st = hip_fail(hipMemsetAsync(s->state, 0, HMS_ST_COUNT * sizeof(unsigned long long), ctx->stream), "memset");
     if (st == HM_OK) {
         hm_launch_stream_fill(ctx->stream, s->bk.keys, nb, HMS_EMPTY);
         st = hip_fail(hipGetLastError(), "fill");
@@ -1823,7 +1849,7 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
     hipStream_t q = ctx->stream;
     int st;
     /* buckets of the kept points (interned; a failing batch may leave unused
-     * buckets behind, never counts) */
+     * buckets behind, never cells) */
     /* reset BFULL, EXOTIC, BMM, NLIST, ERR in one copy */
     unsigned long long* init = s->hstate + HMS_ST_COUNT;
     init[0] = 0;                                    /* BFULL */
@@ -1831,7 +1857,7 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
     init[2] = 0;                                    /* BMM */
     init[3] = 0;                                    /* NLIST */
     init[4] = ~0ull;                                /* ERR */
-    HIPCHK(hipMemcpyAsync(s->t.state + HMS_ST_BFULL, init, 5 * 8, hipMemcpyHostToDevice, q));
+    HIPCHK(hipMemcpyAsync(s->state + HMS_ST_BFULL, init, 5 * 8, hipMemcpyHostToDevice, q));
     const bool per_point = group || hour;
     if (per_point && (st = stream_buf(s, s->bids, (size_t)n * 4))) return st;
     HmsBucketArgs a;
@@ -1846,10 +1872,10 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
     a.bflag = s->bflag;
     a.epoch = s->epoch;
     a.list = s->blist;
-    a.state = s->t.state;
-    a.err_word = s->t.state + HMS_ST_ERR;
+    a.state = s->state;
+    a.err_word = s->state + HMS_ST_ERR;
     hm_launch_stream_buckets(q, a);
-    hm_launch_stream_collect(q, s->bflag, s->bk.mask + 1, s->epoch, s->blist, s->t.state);
+    hm_launch_stream_collect(q, s->bflag, s->bk.mask + 1, s->epoch, s->blist, s->state);
     HIPCHK(hipGetLastError());
     if ((st = stream_sync_state(s))) return st;
     const uint32_t nparts = (uint32_t)s->hstate[HMS_ST_NLIST];
@@ -1870,14 +1896,18 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
 extern "C" int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity, int64_t* buckets)
 {
     if (!s) return HM_E_ARG;
-    if (s->stale) {
-        HIPCHK(hipSetDevice(s->ctx->device));
-        const int st = stream_sync_state(s);
-        if (st) return st;
+    HIPCHK(hipSetDevice(s->ctx->device));
+    int st;
+    if (cells) {
+        /* distinct (bucket, cell) pairs: the log compacted */
+        if ((st = stream_compact(s))) return st;
+        *cells = (int64_t)s->llen;
     }
-    if (cells) *cells = (int64_t)s->occupied;
-    if (capacity) *capacity = (int64_t)(s->t.mask + 1);
-    if (buckets) *buckets = (int64_t)s->nbuckets;
+    if (capacity) *capacity = (int64_t)s->lcap;
+    if (buckets) {
+        if ((st = stream_sync_state(s))) return st;
+        *buckets = (int64_t)s->nbuckets;
+    }
     return HM_OK;
 }
 
@@ -1889,33 +1919,48 @@ extern "C" int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_
         (capacity > 0 && (!keys_out || !counts_out)))
         return HM_E_ARG;
     *n_out = 0;
-    HIPCHK(hipSetDevice(s->ctx->device));
-    hipStream_t q = s->ctx->stream;
+    hm_ctx* ctx = s->ctx;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t q = ctx->stream;
     int st;
-    if (s->occupied == 0) return HM_OK;
-    /* scratch table: at most every cell slot, load <= 1/2; its own state words */
-    uint64_t cap = 1024;
-    while (cap < 2 * s->occupied) cap <<= 1;
-    if ((st = stream_buf(s, s->rslots, cap * 16 + 64))) return st;
-    HmsTable r;
-    r.slots = (uint64_t*)s->rslots.p;
-    r.mask = cap - 1;
-    r.state = (unsigned long long*)((char*)s->rslots.p + cap * 16);
-    HIPCHK(hipMemsetAsync(r.state, 0, 64, q));
-    hm_launch_stream_init(q, r);
-    HmsRollupArgs a;
-    a.from = s->t;
-    a.to = r;
+    if (s->llen == 0) return HM_OK;
+    /* the log's cells of the rollup, re-keyed to label buckets */
+    if ((st = stream_buf(s, s->rk, s->llen * 8)) || (st = stream_buf(s, s->rc, s->llen * 8))) return st;
+    unsigned long long* cur = s->state + HMS_ST_CURSOR;
+    HIPCHK(hipMemsetAsync(cur, 0, 8, q));
+    HIPCHK(hipMemsetAsync(s->state + HMS_ST_BFULL, 0, 8, q));
+    HmsRelabelArgs a;
+    a.keys = s->lkeys;
+    a.counts = s->lcounts;
+    a.n = s->llen;
     a.buckets = s->bk;
     a.cb = s->cb;
     a.span = span;
     a.merge = merge_groups ? 1 : 0;
     a.base = s->base;
     a.select = select;
-    a.state = s->t.state;
-    hm_launch_stream_rollup(q, a);
+    a.keys_out = (uint64_t*)s->rk.p;
+    a.counts_out = (uint64_t*)s->rc.p;
+    a.cursor = cur;
+    a.state = s->state;
+    hm_launch_stream_relabel(q, a);
+    HIPCHK(hipGetLastError());
+    if ((st = stream_sync_state(s))) return st;
+    if (s->hstate[HMS_ST_BFULL]) return HM_E_CAPACITY;   /* no bucket left for a rollup label */
+    const uint64_t m = s->hstate[HMS_ST_CURSOR];
+    if (m == 0) return HM_OK;
+    /* equal label cells summed */
+    if ((st = stream_buf(s, s->mk, m * 8)) || (st = stream_buf(s, s->mc, m * 8))) return st;
+    int64_t nd = 0;
+    if ((st = cells_merge(ctx, (const uint64_t*)s->rk.p, (const uint64_t*)s->rc.p, (int64_t)m, nullptr, 0,
+                          (uint64_t*)s->mk.p, (uint64_t*)s->mc.p, (int64_t)m, &nd)))
+        return st;
+    *n_out = nd;
+    if (nd > capacity) return HM_E_CAPACITY;
     HmsEmitArgs e;
-    e.t = r;
+    e.keys = (const uint64_t*)s->mk.p;
+    e.counts = (const uint64_t*)s->mc.p;
+    e.n = (uint64_t)nd;
     e.buckets = s->bk;
     e.cb = s->cb;
     e.zmin = s->zmin;
@@ -1925,17 +1970,9 @@ extern "C" int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_
     e.counts_out = counts_out;
     e.groups_out = groups_out;
     e.periods_out = periods_out;
-    e.cap = (uint64_t)capacity;
-    e.cursor = r.state + HMS_ST_CURSOR;
     hm_launch_stream_emit(q, e);
     HIPCHK(hipGetLastError());
-    unsigned long long* down = s->ctx->host_state + 2 * ST_COUNT;
-    HIPCHK(hipMemcpyAsync(down, r.state, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, q));
-    if ((st = stream_sync_state(s))) return st;
-    if (s->hstate[HMS_ST_BFULL]) return HM_E_CAPACITY;   /* no bucket left for a rollup label */
-    if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;         /* cannot happen: load <= 1/2 */
-    *n_out = (int64_t)down[HMS_ST_CURSOR];
-    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+    return HM_OK;
 }
 
 extern "C" int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out, uint64_t* counts_out,
@@ -1955,9 +1992,9 @@ extern "C" int hm_stream_destroy(hm_stream* s)
     if (!s) return HM_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
-    for (void* p : {(void*)s->t.slots, (void*)s->t.state, (void*)s->bk.keys, (void*)s->bflag, (void*)s->blist,
-                    (void*)s->bloc, s->bids.p, s->rec.p, s->bkeys.p, s->bcounts.p, s->rslots.p, s->plat.p, s->plon.p,
-                    s->pkeep.p, s->pstart.p, s->pcnt.p})
+    for (void* p : {(void*)s->state, (void*)s->bk.keys, (void*)s->bflag, (void*)s->blist, (void*)s->bloc,
+                    (void*)s->lkeys, (void*)s->lcounts, (void*)s->akeys, (void*)s->acounts, s->bids.p, s->rec.p,
+                    s->plat.p, s->plon.p, s->pkeep.p, s->pstart.p, s->pcnt.p, s->rk.p, s->rc.p, s->mk.p, s->mc.p})
         if (p) (void)hipFree(p);
     if (s->hstate) (void)hipHostFree(s->hstate);
     delete s;

@@ -479,16 +479,25 @@ struct HmsScatterArgs {
     double* lat_out;
     double* lon_out;
 };
-struct HmsRollupArgs {
-    HmsTable from, to;
+/* a rollup's cells: the log's, relabeled (k_stream_relabel) */
+struct HmsRelabelArgs {
+    const uint64_t* keys;    /* the log */
+    const uint64_t* counts;
+    uint64_t n;
     HmsBuckets buckets;
     int cb, span, merge;
     uint32_t base;
     int64_t select;          /* -1, or the one period value kept */
+    uint64_t* keys_out;      /* label bucket << cb | cell */
+    uint64_t* counts_out;
+    unsigned long long* cursor;   /* cells written */
     unsigned long long* state;
 };
+/* merged label cells -> caller's arrays (k_stream_emit) */
 struct HmsEmitArgs {
-    HmsTable t;
+    const uint64_t* keys;
+    const uint64_t* counts;
+    uint64_t n;
     HmsBuckets buckets;
     int cb, zmin, zmax;
     uint32_t base;
@@ -496,8 +505,6 @@ struct HmsEmitArgs {
     uint64_t* counts_out;
     uint32_t* groups_out;
     uint32_t* periods_out;
-    uint64_t cap;
-    unsigned long long* cursor;
 };
 void hm_launch_stream_buckets(hipStream_t s, const HmsBucketArgs& a);
 void hm_launch_stream_batch_list(hipStream_t s, const uint32_t* list, uint32_t nlist, uint32_t* loc);
@@ -508,12 +515,9 @@ void hm_launch_stream_scatter(hipStream_t s, const HmsScatterArgs& a);
 void hm_launch_stream_rekey(hipStream_t s, uint64_t* keys, uint64_t m, uint64_t prefix);
 void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int cb, uint64_t* keys, uint64_t* counts,
                               unsigned long long* state);
-void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, bool from_count,
-                             uint64_t prefix, const HmsTable& t);
 void hm_launch_stream_init(hipStream_t s, const HmsTable& t);
 void hm_launch_stream_fill(hipStream_t s, uint64_t* p, uint64_t n, uint64_t v);
-void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to);
-void hm_launch_stream_rollup(hipStream_t s, const HmsRollupArgs& a);
+void hm_launch_stream_relabel(hipStream_t s, const HmsRelabelArgs& a);
 void hm_launch_stream_emit(hipStream_t s, const HmsEmitArgs& a);
 
 /* general count path (hm_general.hip): sort of 128-bit cell keys + zoom cascade */

@@ -3,27 +3,28 @@
  *
  * The reference recomputes its whole pyramid per Spark job (heatmap.py:152-158)
  * and keys every bin by user group and timespan label (heatmap.py:54-55,62-75).
- * A stream instead folds each micro-batch's cells into tables that stay in HBM:
+ * A stream instead keeps every micro-batch's cells in HBM, log-structured:
  *
  *   bucket table  u64 keys {group u32 | period u32}, open addressing; a
  *                 bucket's id is its SLOT INDEX, so interning needs one CAS on
- *                 the key word and no value word (no second write another
- *                 thread would have to wait for).  Periods: an epoch hour
+ *                 the key word and no value word.  Periods: an epoch hour
  *                 relative to the stream's base, "undated", or (rollup outputs)
  *                 a day / month / year / alltime label.
- *   cell table    16-B slots {u64 key, u64 count}: key = bucket << cb | cell,
- *                 cell = the pyramid index (4^z - 1)/3 + row * 2^z + col of a
- *                 tile of zoom z (cb bits: 43 at zmax 21).  One insert per
- *                 batch cell; every label (alltime, year, month, day) is a
- *                 rollup of the hour buckets at query time.
+ *   cell log      {u64 key, u64 count} arrays: key = bucket << cb | cell, cell =
+ *                 the pyramid index (4^z - 1)/3 + row * 2^z + col of a tile of
+ *                 zoom z (cb bits: 43 at zmax 21).  A batch's count pass writes
+ *                 its cells straight at the log's tail and k_stream_rekey adds
+ *                 the bucket: ingest is an append (no hash-table probe per cell;
+ *                 a 4 GB table insert took 0.4 ms per 10M-point batch).
  *
  * Per batch: k_stream_buckets interns each kept point's (group, hour) and
  * writes its bucket id; one count pass (hm_count when the batch has one
- * bucket, else the grouped general path with the bucket as group) gives the
- * batch's cells; k_stream_convert checks them (tiles outside the square are
- * refused before anything is inserted) and k_stream_insert folds them in.
- * Rollups (k_stream_rollup) re-key every cell slot to (group or all groups,
- * label) in a scratch table and k_stream_emit lists it.
+ * bucket, one per bucket for a few, else the grouped general path with the
+ * bucket as group) writes the batch's cells at the tail.  Queries (rollups:
+ * hour, day, month, year, alltime) relabel the log's cells to (group or all
+ * groups, label) buckets (k_stream_relabel), sum equal keys with the bucketed
+ * LDS merge (hm_cells_merge) and list them (k_stream_emit).  The log is
+ * compacted (the same merge) when it fills up or its exact size is asked for.
  */
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -292,47 +293,6 @@ __global__ __launch_bounds__(256) void k_stream_convert(const int64_t* __restric
     if (threadIdx.x == 0 && v[0]) atomicAdd(&state[HMS_ST_EXOTIC], (unsigned long long)v[0]);
 }
 
-/* Fold n cells into the table.  FROM_COUNT: hm_count keys of one bucket
- * (prefix = bucket << cb); else cell-table keys as k_stream_convert made them. */
-template <bool FROM_COUNT>
-__global__ __launch_bounds__(256) void k_stream_insert(const uint64_t* __restrict__ keys,
-                                                       const uint64_t* __restrict__ counts, uint64_t n,
-                                                       uint64_t prefix, HmsTable t)
-{
-    uint64_t claimed = 0;
-    uint32_t overflow = 0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const uint64_t k = FROM_COUNT ? prefix | hms_cell(keys[i]) : keys[i];
-        claimed += hms_insert_unique(t, k, counts[i], &overflow);   /* a batch's cells are distinct */
-    }
-    uint64_t v[2] = {claimed, overflow};
-    hms_block_sums(v);
-    if (threadIdx.x == 0) {
-        if (v[0]) atomicAdd(&t.state[HMS_ST_OCCUPIED], (unsigned long long)v[0]);
-        if (v[1]) atomicAdd(&t.state[HMS_ST_OVERFLOW], (unsigned long long)v[1]);
-    }
-}
-
-/* Re-insert every occupied slot of `from` into `to` (table growth). */
-__global__ __launch_bounds__(256) void k_stream_rehash(HmsTable from, HmsTable to)
-{
-    uint64_t claimed = 0;
-    uint32_t overflow = 0;
-    const uint64_t n = from.mask + 1;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const ulonglong2 sl = ((const ulonglong2*)from.slots)[i];
-        if (sl.x != HMS_EMPTY) claimed += hms_insert_unique(to, sl.x, sl.y, &overflow);
-    }
-    uint64_t v[2] = {claimed, overflow};
-    hms_block_sums(v);
-    if (threadIdx.x == 0) {
-        if (v[0]) atomicAdd(&to.state[HMS_ST_OCCUPIED], (unsigned long long)v[0]);
-        if (v[1]) atomicAdd(&to.state[HMS_ST_OVERFLOW], (unsigned long long)v[1]);
-    }
-}
-
 __global__ __launch_bounds__(256) void k_stream_init(HmsTable t)
 {
     const uint64_t n = t.mask + 1;
@@ -386,87 +346,88 @@ __device__ __forceinline__ uint32_t hms_period_value(uint32_t pw, uint32_t base)
     return pw & 0x0FFFFFFFu;
 }
 
-__global__ __launch_bounds__(256) void k_stream_rollup(HmsRollupArgs a)
+/* log key -> rollup label key (group or HMS_ALLGROUPS, label period word),
+ * or ~0: not in the rollup */
+__device__ __forceinline__ uint64_t hms_relabel_key(const HmsRelabelArgs& a, uint64_t k)
 {
-    uint64_t claimed = 0;
-    uint32_t overflow = 0, bclaimed = 0, full = 0;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint64_t n = a.from.mask + 1;
+    const uint64_t bk = a.buckets.keys[k >> a.cb];
+    const uint32_t pw = (uint32_t)bk;
+    if ((pw >> 28) != 0 && pw != HMS_UNDATED) return ~0ull;   /* not a raw bucket (cannot happen) */
+    const uint32_t lp = hms_label(pw, a.base, a.span);
+    if (lp == HMS_SKIP) return ~0ull;
+    if (a.select >= 0 && (int64_t)hms_period_value(lp, a.base) != a.select) return ~0ull;
+    const uint32_t g = a.merge ? HMS_ALLGROUPS : (uint32_t)(bk >> 32);
+    return ((uint64_t)g << 32) | lp;
+}
+
+/* The log's cells of a rollup, re-keyed to their label buckets (interned) and
+ * compacted: a block takes 256 * HMS_RL_PPT cells at a time, counts the ones
+ * in the rollup, reserves their room with one atomic and writes them.  The
+ * lanes sharing lane 0's label intern it once (a merged rollup is one label
+ * per period); the rest probe alone. */
+#define HMS_RL_PPT 32
+__global__ __launch_bounds__(256) void k_stream_relabel(HmsRelabelArgs a)
+{
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long sbase;
+    const int tid = threadIdx.x;
     const uint64_t cmask = (1ull << a.cb) - 1ull;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        const ulonglong2 sl = ((const ulonglong2*)a.from.slots)[i];
-        if (sl.x == HMS_EMPTY) continue;
-        const uint64_t bk = a.buckets.keys[sl.x >> a.cb];
-        const uint32_t pw = (uint32_t)bk;
-        if ((pw >> 28) != 0 && pw != HMS_UNDATED) continue;   /* not a raw bucket (cannot happen) */
-        const uint32_t lp = hms_label(pw, a.base, a.span);
-        if (lp == HMS_SKIP) continue;
-        if (a.select >= 0 && (int64_t)hms_period_value(lp, a.base) != a.select) continue;
-        const uint32_t g = a.merge ? HMS_ALLGROUPS : (uint32_t)(bk >> 32);
-        const uint64_t key = ((uint64_t)g << 32) | lp;
-        /* the lanes sharing the first lane's label bucket intern it once (a
-         * merged rollup is one label for the whole wave); the rest probe alone */
-        const uint64_t k0 = __builtin_amdgcn_readfirstlane(key);
-        const uint64_t same = __ballot(key == k0);
-        uint32_t b = 0;
-        if (lane == (uint32_t)(__ffsll((unsigned long long)same) - 1)) b = hms_intern(a.buckets, k0, &bclaimed);
-        b = __shfl(b, __ffsll((unsigned long long)same) - 1, 64);
-        if (key != k0) b = hms_intern(a.buckets, key, &bclaimed);
-        if (b == HMS_NO_BUCKET) {
-            full = 1;
-            continue;
+    uint32_t bclaimed = 0, full = 0;
+    constexpr uint64_t CH = 256 * HMS_RL_PPT;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * CH; c0 < a.n; c0 += (uint64_t)gridDim.x * CH) {
+        uint32_t cnt = 0;
+        for (int j = 0; j < HMS_RL_PPT; j++) {
+            const uint64_t i = c0 + (uint64_t)j * 256 + tid;
+            if (i < a.n) cnt += hms_relabel_key(a, a.keys[i]) != ~0ull;
         }
-        claimed += hms_insert(a.to, ((uint64_t)b << a.cb) | (sl.x & cmask), sl.y, &overflow);
+        uint32_t tot;
+        uint32_t pos = hm_block_excl_scan<256>(cnt, scr, &tot);
+        if (tid == 0) sbase = tot ? atomicAdd(a.cursor, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        const uint64_t base = sbase;
+        __syncthreads();
+        if (!tot) continue;
+        for (int j = 0; j < HMS_RL_PPT; j++) {
+            const uint64_t i = c0 + (uint64_t)j * 256 + tid;
+            const uint64_t k = i < a.n ? a.keys[i] : 0ull;
+            const uint64_t lk = i < a.n ? hms_relabel_key(a, k) : ~0ull;
+            const bool in = lk != ~0ull;
+            const uint64_t k0 = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(lk >> 32)) << 32) |
+                                __builtin_amdgcn_readfirstlane((uint32_t)lk);
+            const bool same = in & (lk == k0);
+            const uint64_t sm = __ballot(same);
+            uint32_t b = 0;
+            if (sm && hm_lane() == 0) b = hms_intern(a.buckets, k0, &bclaimed);   /* lane 0 is in the group */
+            b = __shfl(b, 0, 64);
+            if (in && !same) b = hms_intern(a.buckets, lk, &bclaimed);
+            if (in) {
+                full |= b == HMS_NO_BUCKET;   /* the caller discards the rollup */
+                const uint64_t q = base + pos++;
+                a.keys_out[q] = ((uint64_t)(b == HMS_NO_BUCKET ? 0u : b) << a.cb) | (k & cmask);
+                a.counts_out[q] = a.counts[i];
+            }
+        }
     }
-    uint64_t v[4] = {claimed, overflow, bclaimed, full};
+    uint64_t v[2] = {bclaimed, full};
     hms_block_sums(v);
-    if (threadIdx.x == 0) {
-        if (v[0]) atomicAdd(&a.to.state[HMS_ST_OCCUPIED], (unsigned long long)v[0]);
-        if (v[1]) atomicAdd(&a.to.state[HMS_ST_OVERFLOW], (unsigned long long)v[1]);
-        if (v[2]) atomicAdd(&a.state[HMS_ST_BUCKETS], (unsigned long long)v[2]);
-        if (v[3]) atomicAdd(&a.state[HMS_ST_BFULL], (unsigned long long)v[3]);
+    if (tid == 0) {
+        if (v[0]) atomicAdd(&a.state[HMS_ST_BUCKETS], (unsigned long long)v[0]);
+        if (v[1]) atomicAdd(&a.state[HMS_ST_BFULL], (unsigned long long)v[1]);
     }
 }
 
-/* occupied slots of a rollup table -> (group, period, hm_count key, count).
- * Each wave owns chunks of HMS_XCHUNK slots: it counts the occupied ones,
- * reserves its output with ONE atomic per chunk, then re-reads the (cache-hot)
- * chunk and writes in slot order.  Past `cap`: counted, not written. */
-#define HMS_XCHUNK (64 * 64)
+/* merged label cells -> (hm_count key, count, group, period) */
 __global__ __launch_bounds__(256) void k_stream_emit(HmsEmitArgs a)
 {
-    const uint64_t n = a.t.mask + 1;   /* power of two >= 1024 */
-    const uint32_t lane = threadIdx.x & 63;
     const uint64_t cmask = (1ull << a.cb) - 1ull;
-    const uint64_t wave = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint64_t waves = ((uint64_t)gridDim.x * blockDim.x) >> 6;
-    const ulonglong2* slots = (const ulonglong2*)a.t.slots;
-    for (uint64_t c0 = wave * HMS_XCHUNK; c0 < n; c0 += waves * HMS_XCHUNK) {
-        const uint64_t c1 = c0 + HMS_XCHUNK < n ? c0 + HMS_XCHUNK : n;
-        uint64_t cnt = 0;
-        for (uint64_t i = c0 + lane; i < c1; i += 64) cnt += slots[i].x != HMS_EMPTY;
-        cnt = hms_wave_sum(cnt);
-        if (!cnt) continue;
-        unsigned long long first = 0;
-        if (lane == 0) first = atomicAdd(a.cursor, (unsigned long long)cnt);
-        first = __shfl(first, 0, 64);
-        for (uint64_t j0 = c0; j0 < c1; j0 += 64) {
-            const ulonglong2 sl = slots[j0 + lane];
-            const bool m = sl.x != HMS_EMPTY;
-            const uint64_t bal = __ballot(m);
-            if (m) {
-                const uint64_t pos = first + hm_mbcnt(bal);
-                if (pos < a.cap) {
-                    const uint64_t bk = a.buckets.keys[sl.x >> a.cb];
-                    a.keys_out[pos] = hms_cell_key(sl.x & cmask, a.zmin, a.zmax);
-                    a.counts_out[pos] = sl.y;
-                    if (a.groups_out) a.groups_out[pos] = (uint32_t)(bk >> 32);
-                    if (a.periods_out) a.periods_out[pos] = hms_period_value((uint32_t)bk, a.base);
-                }
-            }
-            first += __popcll(bal);
-        }
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j < a.n; j += stride) {
+        const uint64_t k = a.keys[j];
+        const uint64_t bk = a.buckets.keys[k >> a.cb];
+        a.keys_out[j] = hms_cell_key(k & cmask, a.zmin, a.zmax);
+        a.counts_out[j] = a.counts[j];
+        if (a.groups_out) a.groups_out[j] = (uint32_t)(bk >> 32);
+        if (a.periods_out) a.periods_out[j] = hms_period_value((uint32_t)bk, a.base);
     }
 }
 
@@ -477,11 +438,31 @@ static dim3 hms_grid(uint64_t n)
     return dim3((unsigned)(b ? b : 1));
 }
 
+/* The keys of the batch's first and last kept-looking points, interned by one
+ * thread ahead of k_stream_buckets: a time-ordered batch brings a NEW hour, and
+ * every wave of the main kernel would otherwise find it missing at once and
+ * CAS the same key word (~5000 same-address atomics per 10M points, 55 us) */
+__global__ void k_stream_prime(HmsBucketArgs a)
+{
+    if (threadIdx.x != 0 || !a.hour) return;
+    uint32_t claimed = 0;
+    for (int e = 0; e < 2; e++) {
+        const uint64_t i = e ? a.n - 1 : 0;
+        if (a.keep && !a.keep[i]) continue;
+        const uint32_t h = a.hour[i];
+        if (h < a.base || h - a.base >= HMS_MAX_HOUR_OFFSET) continue;   /* k_stream_buckets reports it */
+        const uint32_t g = a.group ? a.group[i] : HMS_NOGROUP;
+        hms_intern(a.buckets, ((uint64_t)g << 32) | (h - a.base), &claimed);
+    }
+    if (claimed) atomicAdd(&a.state[HMS_ST_BUCKETS], (unsigned long long)claimed);
+}
+
 void hm_launch_stream_buckets(hipStream_t s, const HmsBucketArgs& a)
 {
     /* ~8+ steps of 256 points per wave: runs of one key stay in registers */
     uint64_t b = (a.n + 8192 - 1) / 8192;
     if (b > 2048) b = 2048;
+    if (a.n && a.hour) hipLaunchKernelGGL(k_stream_prime, dim3(1), dim3(64), 0, s, a);
     if (a.n) hipLaunchKernelGGL(k_stream_buckets, dim3((unsigned)(b ? b : 1)), dim3(256), 0, s, a);
 }
 
@@ -523,16 +504,6 @@ void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int
     if (m) hipLaunchKernelGGL(k_stream_convert, hms_grid(m), dim3(256), 0, s, rec, m, cb, keys, counts, state);
 }
 
-void hm_launch_stream_insert(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, bool from_count,
-                             uint64_t prefix, const HmsTable& t)
-{
-    if (!n) return;
-    if (from_count)
-        hipLaunchKernelGGL(k_stream_insert<true>, hms_grid(n), dim3(256), 0, s, keys, counts, n, prefix, t);
-    else
-        hipLaunchKernelGGL(k_stream_insert<false>, hms_grid(n), dim3(256), 0, s, keys, counts, n, prefix, t);
-}
-
 void hm_launch_stream_init(hipStream_t s, const HmsTable& t)
 {
     hipLaunchKernelGGL(k_stream_init, hms_grid(t.mask + 1), dim3(256), 0, s, t);
@@ -543,18 +514,13 @@ void hm_launch_stream_fill(hipStream_t s, uint64_t* p, uint64_t n, uint64_t v)
     if (n) hipLaunchKernelGGL(k_stream_fill, hms_grid(n), dim3(256), 0, s, p, n, v);
 }
 
-void hm_launch_stream_rehash(hipStream_t s, const HmsTable& from, const HmsTable& to)
+void hm_launch_stream_relabel(hipStream_t s, const HmsRelabelArgs& a)
 {
-    hipLaunchKernelGGL(k_stream_rehash, hms_grid(from.mask + 1), dim3(256), 0, s, from, to);
-}
-
-void hm_launch_stream_rollup(hipStream_t s, const HmsRollupArgs& a)
-{
-    hipLaunchKernelGGL(k_stream_rollup, hms_grid(a.from.mask + 1), dim3(256), 0, s, a);
+    const uint64_t chunks = (a.n + 256 * HMS_RL_PPT - 1) / (256 * HMS_RL_PPT);
+    if (a.n) hipLaunchKernelGGL(k_stream_relabel, dim3((unsigned)(chunks < 1024 ? chunks : 1024)), dim3(256), 0, s, a);
 }
 
 void hm_launch_stream_emit(hipStream_t s, const HmsEmitArgs& a)
 {
-    const uint64_t chunks = (a.t.mask + HMS_XCHUNK) / HMS_XCHUNK, blocks = (chunks + 3) / 4;
-    hipLaunchKernelGGL(k_stream_emit, dim3((unsigned)(blocks < 4096 ? blocks : 4096)), dim3(256), 0, s, a);
+    if (a.n) hipLaunchKernelGGL(k_stream_emit, hms_grid(a.n), dim3(256), 0, s, a);
 }

@@ -230,10 +230,18 @@ class StreamingHeatmap:
     # ---------------------------------------------------------------- queries
 
     def cells(self):
-        """(occupied cell-table slots, table capacity)"""
-        a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
-        self.ctx.L.hm_stream_cells(self.ptr, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c))
+        """(distinct (bucket, cell) pairs held, cell-log capacity); compacts
+        the log (one bucketed merge) when it holds repeated keys"""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        rc = self.ctx.L.hm_stream_cells(self.ptr, ctypes.byref(a), ctypes.byref(b), None)
+        if rc != _lib.HM_OK:
+            _lib.raise_for(rc)
         return a.value, b.value
+
+    def _log_capacity(self) -> int:
+        b = ctypes.c_int64(0)
+        self.ctx.L.hm_stream_cells(self.ptr, None, ctypes.byref(b), None)
+        return b.value
 
     def buckets(self) -> int:
         """(group, period) buckets in use, rollup labels included"""
@@ -247,7 +255,7 @@ class StreamingHeatmap:
         torch = self._torch
         self.ctx.bind_stream()
         span = SPANS[timespan]
-        cap = max(1024, self.cells()[0])
+        cap = max(1024, self._log_capacity())   # >= the log's cells >= the rollup's
         dev = "cuda:%d" % self.device_index
         while True:
             keys = torch.empty(cap, dtype=torch.int64, device=dev)

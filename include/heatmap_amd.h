@@ -168,7 +168,9 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
 
 /* Diagnostics of the last hm_project/hm_count call: points resolved by the
  * bit-exact glibc-restating slow path (guard band / out-of-window), and the
- * per-stage device time in microseconds of the last hm_count:
+ * per-stage device time in microseconds of the last hm_count (slots 0-4 are
+ * timed for calls of >= 2^24 points only, 0 otherwise: the event records are
+ * API calls, and a small call's time is the host's issue rate):
  *   [0] k_project_partition (projection + level-1 partition)
  *   [1] level-1 buckets, remaining partition levels, run scans and
  *       compactions (incl. host reads; contains [4])
@@ -187,7 +189,8 @@ int hm_last_stats(hm_ctx* ctx, int64_t* slow_points, double* stage_us, int n_sta
  * label -- hour, day, month, year (UTC calendar), alltime -- as a rollup.
  *   hm_stream_create  zooms [zmin, zmax] (zmax <= HM_MAX_ZOOM); hours
  *                     base_hour .. base_hour + 2^28 - 1; initial_cells sizes
- *                     the cell table (it grows); max_buckets (0: 2^20) bounds
+ *                     the cell log (batches append to it; it is compacted,
+ *                     then grown, when full); max_buckets (0: 2^20) bounds
  *                     the distinct (group, hour) and rollup-label buckets.
  *   hm_stream_add     hm_count semantics per point (projection errors, keep);
  *                     hour: uint32[n] (device) or NULL (undated: alltime
@@ -217,7 +220,8 @@ int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_hour, int64_
                      hm_stream** out);
 int hm_stream_add(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, const uint32_t* hour,
                   const uint32_t* group, int64_t n);
-/* occupied cell-table slots, the table capacity, and the buckets in use */
+/* distinct (bucket, cell) pairs held (cells != NULL compacts the log: one
+ * merge), the log's capacity in cells, and the buckets in use */
 int hm_stream_cells(hm_stream* s, int64_t* cells, int64_t* capacity, int64_t* buckets);
 int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_t select, uint64_t* keys_out,
                      uint64_t* counts_out, uint32_t* groups_out, uint32_t* periods_out, int64_t capacity,

@@ -20,37 +20,7 @@ from heatmap_amd import device
 
 pytestmark = pytest.mark.gpu
 
-M29 = (1 << 29) - 1
-_U = (1 << 64) - 1
-
-
-def _s64(v):
-    return v - (1 << 64) if v >= 1 << 63 else v
-
-
-def device_digest(torch, keys, counts):
-    """tests/conftest.py cells_digest of HM_KEY cells, on the device (int64
-    arithmetic wraps like the uint64 original; right shifts made logical)."""
-    z = keys >> 58
-    r = (keys >> 29) & M29
-    c = keys & M29
-
-    def lsr(x, k):
-        return (x >> k) & ((1 << (64 - k)) - 1)
-
-    x = (z * _s64(0x9E3779B97F4A7C15)) ^ r
-    x = (x * _s64(0xBF58476D1CE4E5B9)) ^ c
-    x = (x * _s64(0x94D049BB133111EB)) ^ counts
-    x = x ^ lsr(x, 31)
-    x = x * _s64(0xD6E8FEB86659FD93)
-    x = x ^ lsr(x, 32)
-    s = int(x.sum().item()) & _U
-    while x.numel() > 1:
-        h = x.numel() // 2
-        y = x[:h] ^ x[h:2 * h]
-        x = torch.cat([y, x[2 * h:]]) if x.numel() & 1 else y
-    xr = (int(x[0].item()) & _U) if x.numel() else 0
-    return [int(keys.numel()), int(counts.sum().item()), s, xr]
+from digest import device_digest  # noqa: E402
 
 
 def _golden(name):

@@ -8,9 +8,9 @@ TAG=${1:-stream}
 O="$R/gpurun_out/$TAG"
 mkdir -p "$O"
 cd "$R"
-timeout -k 10 300 python -u tools/bench_stream.py --batches 20 --warmup 2 > "$O/bench_stream.log" 2>&1 || { tail -30 "$O/bench_stream.log"; exit 1; }
+timeout -k 10 300 python -u tools/bench_stream.py --batches 18 --warmup 2 > "$O/bench_stream.log" 2>&1 || { tail -30 "$O/bench_stream.log"; exit 1; }
 tail -1 "$O/bench_stream.log"
-timeout -k 10 300 python -u tools/bench_stream.py --batches 20 --warmup 2 --hours 2 > "$O/bench_stream_h2.log" 2>&1 || { tail -30 "$O/bench_stream_h2.log"; exit 1; }
+timeout -k 10 300 python -u tools/bench_stream.py --batches 18 --warmup 2 --hours 2 > "$O/bench_stream_h2.log" 2>&1 || { tail -30 "$O/bench_stream_h2.log"; exit 1; }
 tail -1 "$O/bench_stream_h2.log"
 cd /tmp
 for h in 1 2; do
