@@ -335,7 +335,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
             ok = hm_project_fast(pa, po, scale, kz, &r32, &c32, tab);
             r = r32;
             c = c32;
-            dom = ((uint32_t)r32 < lim) & ((uint32_t)c32 < lim);   /* lim <= 2^21: 32-bit tests */
+            dom = true;   /* ok implies 0 <= r32, c32 < 2^Z (hm_project_fast) */
         }
         const bool inb = FULLT || i < n;   /* a whole tile is in range */
         const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFF) != 0;

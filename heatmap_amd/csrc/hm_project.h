@@ -146,10 +146,14 @@ HM_FN int hm_col(double lon, int zoom, int64_t* col)
 }
 
 /* Branch-free fast projection for the streaming kernels: returns 1 and the
- * tile (int32) when both fast paths are conclusive; 0 means "resolve this
- * point with the exact chain" (guard band, |lat| > 85.06, non-finite input,
- * |column| >= 2^31).  Identical results to hm_project_point whenever it
- * returns 1.  Per-launch constants: scale = 2^z, kz = RN(1/360) 2^z (exact). */
+ * tile (int32) when both fast paths are conclusive and the tile lies inside
+ * [0, 2^z)^2; 0 means "resolve this point with the exact chain" (guard band,
+ * |lat| > HM_LAT_SQ, non-finite input, a column outside [0, 2^z)).
+ * Identical results to hm_project_point whenever it returns 1 (then 0 <=
+ * row, col < 2^z: |lat| <= 85.05 < 85.0511 keeps Y inside (0, 1), so callers
+ * need no range test).  Per-launch constants: scale = 2^z, kz = RN(1/360) 2^z
+ * (exact). */
+#define HM_LAT_SQ 85.05
 HM_FN int hm_project_fast(double lat, double lon, double scale, double kz, int32_t* row, int32_t* col,
                           const double* tab)
 {
@@ -158,8 +162,8 @@ HM_FN int hm_project_fast(double lat, double lon, double scale, double kz, int32
     const double g = HM_Y_EPS * scale;
     const double y = (lon + 180.0) * kz;
     const double f2 = floor(y);
-    const double g2 = scale * 0x1p-49;   /* >= |y| 2^-49 on the accepted range |y| < 2^z */
-    const int ok = (fabs(lat) <= HM_LAT_FAST) & (fabs((R - f) - 0.5) < 0.5 - g) & (fabs(y) < scale) &
+    const double g2 = scale * 0x1p-49;   /* >= |y| 2^-49 on the accepted range 0 <= y < 2^z */
+    const int ok = (fabs(lat) <= HM_LAT_SQ) & (fabs((R - f) - 0.5) < 0.5 - g) & (y >= 0.0) & (y < scale) &
                    (fabs((y - f2) - 0.5) < 0.5 - g2);
     *row = (int32_t)(ok ? f : 0.0);
     *col = (int32_t)(ok ? f2 : 0.0);
