@@ -302,7 +302,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         key = ((r & lowm) << hb) | (c & lowm);
         if (H) {   /* block-uniform */
             const uint32_t t = ((r >> hs) << a.hot_z) | (c >> hs);
-            const uint32_t tk = t << 9;
+            const uint32_t tk = t << HM_HOT_HBITS;
 #if HM_HOT_WAYS == 4
             const uint4 e = hsh4[hm_hot_bucket(t)];
             const uint32_t x = min(min(e.x ^ tk, e.y ^ tk), min(e.z ^ tk, e.w ^ tk));
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
             const uint2 e = ((const uint2*)hsh4)[hm_hot_bucket(t)];
             const uint32_t x = min(e.x ^ tk, e.y ^ tk);
 #endif
-            const bool hot = x < 512u;
+            const bool hot = x < (uint32_t)HM_HOT_LIMIT;   /* an empty way leaves x >= HM_HOT_LIMIT */
             dg = hot ? HM_MAX_F1 + x : dg;
             key = hot ? (((r & hm) << hs) | (c & hm)) : key;
         }
@@ -613,40 +613,73 @@ __global__ __launch_bounds__(256) void k_hot_select(HmHotArgs a)
     }
 }
 
-/* The hot tiles and the table image k_project_partition looks them up in.  A
+/* The hot tiles and the table image k_project_partition looks them up in.
+ * The biggest candidates go first: a histogram of their sampled counts (8
+ * bins per octave) gives the cutoff bin above which fewer than HM_MAX_HOT
+ * candidates lie; those are placed, then the cutoff bin's first come.  A
  * candidate becomes hot tile h (< HM_MAX_HOT) when its bucket has a free way;
  * otherwise it stays cold (any set of hot tiles gives the same counts).  Hot
  * tile h: its sampled count as level-1 histogram entry HM_MAX_F1 + h, taken
  * off its z1 digit, which is flagged as a hot parent.  One block. */
+__device__ __forceinline__ uint32_t hm_hot_bin(uint32_t c)
+{
+    const uint32_t e = 31u - __clz(c | 1u);
+    return e < 3 ? c : (e << 3) | ((c >> (e - 3)) & 7u);   /* < 256 */
+}
+
 __global__ __launch_bounds__(1024) void k_hot_hash(HmHotArgs a)
 {
     __shared__ uint32_t tab[HM_HOT_SLOTS];
     __shared__ uint32_t fill[HM_HOT_BUCKETS];
-    __shared__ uint32_t nh;
-    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 1024) tab[i] = HM_HOT_EMPTY;
-    for (int i = threadIdx.x; i < HM_HOT_BUCKETS; i += 1024) fill[i] = 0;
-    if (threadIdx.x == 0) nh = 0;
+    __shared__ uint32_t bins[256];
+    __shared__ uint32_t nh, cut;
+    const int tid = threadIdx.x;
+    for (int i = tid; i < HM_HOT_SLOTS; i += 1024) tab[i] = HM_HOT_EMPTY;
+    for (int i = tid; i < HM_HOT_BUCKETS; i += 1024) fill[i] = 0;
+    for (int i = tid; i < 256; i += 1024) bins[i] = 0;
+    if (tid == 0) nh = 0;
     __syncthreads();
     const uint32_t nc = min(a.cand[2 * HM_HOT_CAND], (uint32_t)HM_HOT_CAND);
-    for (uint32_t j = threadIdx.x; j < nc; j += 1024) {
-        const uint32_t t = a.cand[2 * j], c = a.cand[2 * j + 1];
-        const uint32_t b = hm_hot_bucket(t);
-        const uint32_t w = atomicAdd(&fill[b], 1u);
-        if (w >= HM_HOT_WAYS) continue;
-        const uint32_t h = atomicAdd(&nh, 1u);
-        if (h >= HM_MAX_HOT) continue;   /* its way stays empty */
-        tab[b * HM_HOT_WAYS + w] = (t << 9) | h;
-        a.tiles[h] = t;
-        a.hist[HM_MAX_F1 + h] = c;
-        const int s = a.zb - a.z1;
-        const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
-        const uint32_t d = ((tr >> s) << a.z1) | (tc >> s);
-        a.hotparent[d] = 1;
-        atomicSub(&a.hist[d], c);   /* those samples' keys leave the cold digit */
+    for (uint32_t j = tid; j < nc; j += 1024) atomicAdd(&bins[hm_hot_bin(a.cand[2 * j + 1])], 1u);
+    __syncthreads();
+    if (tid < 64) {
+        /* cutoff: the highest bin at which the candidates from the top reach HM_MAX_HOT */
+        uint32_t acc = 0, c = 0;
+        if (tid == 0) {
+            for (int b = 255; b >= 0; b--) {
+                acc += bins[b];
+                if (acc >= HM_HOT_LIMIT) {
+                    c = (uint32_t)b;
+                    break;
+                }
+            }
+            cut = c;
+        }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < HM_HOT_SLOTS; i += 1024) a.hash[i] = tab[i];
-    if (threadIdx.x == 0) *a.n = min(nh, (uint32_t)HM_MAX_HOT);
+    for (int pass = 0; pass < 2; pass++) {
+        for (uint32_t j = tid; j < nc; j += 1024) {
+            const uint32_t t = a.cand[2 * j], c = a.cand[2 * j + 1];
+            const uint32_t bn = hm_hot_bin(c);
+            if (pass == 0 ? bn <= cut : bn != cut) continue;   /* pass 0: above the cutoff; 1: at it */
+            const uint32_t b = hm_hot_bucket(t);
+            const uint32_t w = atomicAdd(&fill[b], 1u);
+            if (w >= HM_HOT_WAYS) continue;
+            const uint32_t h = atomicAdd(&nh, 1u);
+            if (h >= HM_HOT_LIMIT) continue;   /* its way stays empty */
+            tab[b * HM_HOT_WAYS + w] = (t << HM_HOT_HBITS) | h;
+            a.tiles[h] = t;
+            a.hist[HM_MAX_F1 + h] = c;
+            const int s = a.zb - a.z1;
+            const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
+            const uint32_t d = ((tr >> s) << a.z1) | (tc >> s);
+            a.hotparent[d] = 1;
+            atomicSub(&a.hist[d], c);   /* those samples' keys leave the cold digit */
+        }
+        __syncthreads();
+    }
+    for (int i = tid; i < HM_HOT_SLOTS; i += 1024) a.hash[i] = tab[i];
+    if (tid == 0) *a.n = min(nh, (uint32_t)HM_HOT_LIMIT);
 }
 
 void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a)

@@ -24,13 +24,19 @@
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024
 /* hot tiles: zoom-zb tiles (the last level's bucket zoom) that a sample shows
- * to hold >= 1/2048 of the points each.  Level 1 gives each its own digit
+ * to hold >= 1/4096 (HM_HOT_INV_SHARE) of the points each.  Level 1 gives each its own digit
  * HM_MAX_F1 + h and writes its keys (u16, zb-relative) straight into the
  * final level's key array, so they skip every intermediate partition pass. */
+#ifndef HM_MAX_HOT
 #define HM_MAX_HOT 512
+#endif
+#define HM_HOT_HBITS (HM_MAX_HOT > 512 ? 10 : 9)   /* h's bits in a table entry */
+/* hot tiles a call may use: with 10-bit h, h = 1023 is left out so that no
+ * entry equals HM_HOT_EMPTY (tile 2^22 - 1 would) */
+#define HM_HOT_LIMIT (HM_HOT_HBITS == 10 ? 1023 : HM_MAX_HOT)
 #define HM_D1 (HM_MAX_F1 + HM_MAX_HOT)      /* level-1 digit slots: cold z1 digits, then hot tiles */
 /* hot-tile table: HM_HOT_BUCKETS buckets of HM_HOT_WAYS entries (one 16-B LDS
- * read per lookup, no probe loop); entry = tile << 9 | h, HM_HOT_EMPTY.  A
+ * read per lookup, no probe loop); entry = tile << HM_HOT_HBITS | h, HM_HOT_EMPTY.  A
  * candidate whose bucket is full stays cold (k_hot_hash). */
 #ifndef HM_HOT_WAYS
 #define HM_HOT_WAYS 2                       /* 2 or 4 (one 8- or 16-B read): 2 measured 0.13 ms faster */
@@ -40,7 +46,7 @@
 #define HM_HOT_BBITS (HM_HOT_WAYS == 4 ? 10 : 11)
 #define HM_HOT_CAND 4096                    /* candidates k_hot_select may list */
 #define HM_HOT_EMPTY 0xFFFFFFFFu
-static_assert(HM_MAX_HOT <= 512, "h takes the low 9 bits of a table entry");
+static_assert(HM_MAX_HOT <= 1024 && (HM_MAX_HOT & 255) == 0, "h takes the low 9 or 10 bits of a table entry");
 /* bucket of zoom-zb tile t (t < 2^22: zb <= 11) */
 __host__ __device__ inline uint32_t hm_hot_bucket(uint32_t t)
 {
@@ -228,7 +234,7 @@ struct HmPart1Args {
      * at the regions of digit HM_MAX_F1 + h (same position space as keys_out) */
     int hot_z;
     void* keys_hot;
-    const uint32_t* hot_hash;   /* [HM_HOT_SLOTS]: bucketed table, tile id << 9 | h, HM_HOT_EMPTY */
+    const uint32_t* hot_hash;   /* [HM_HOT_SLOTS]: bucketed table, tile id << HM_HOT_HBITS | h, HM_HOT_EMPTY */
     const uint32_t* hot_n;      /* device word: number of hot tiles */
 };
 

@@ -52,6 +52,10 @@ VARIANTS = {
     "agslow": ["HM_AG_FAST=0"],             # k_aggregate with the lane-0 merge on every key
     "agm4": ["HM_MERGE_MIN=4"],
     "agm16": ["HM_MERGE_MIN=16"],
+    "ta512k": ["HM_TA=524288"],
+    "ta1m": ["HM_TA=1048576"],
+    "hot1k": ["HM_MAX_HOT=1024"],
+    "hot1kta1m": ["HM_MAX_HOT=1024", "HM_TA=1048576"],
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
@@ -113,7 +117,8 @@ def one(name, points, steps, zmax):
     t0 = time.perf_counter()
     for _ in range(steps):
         m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
-        st.append(ctx.last_stats()[1][:4])
+        ls = ctx.last_stats()[1]
+        st.append(list(ls[:4]) + [ls[6]])   # stage times, hot tiles
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     tot = int(bufs.counts[:m].sum().item())
