@@ -42,6 +42,11 @@ struct Level {
 }  // namespace
 
 #define HM_SPREAD_MIN_KEYS (1u << 19)
+/* with hot tiles: the cold keys' mean level-1 bucket above which they take
+ * 3-zoom levels.  Off by default: measured slower (hotspots 6.6 -> 7.0 ms,
+ * skew 15.4 -> 24.7 ms: the middle level's run-streaming partition and a
+ * pool over 64K zoom-8 buckets cost more than the short runs they save) */
+#define HM_SPREAD_MIN_COLD 1e30
 #define HM_SPREAD_ZOOMS 3
 
 /* per-call stage events: [0..4] stage boundaries, [5..] pairs around the
@@ -64,6 +69,7 @@ struct hm_ctx {
     /* plan-tuning knobs, read once from the environment at hm_ctx_create
      * (INTEGRATION.md): HM_SPREAD_MIN_KEYS, HM_RS_BIG_MIN */
     double spread_min_keys = 0;
+    double spread_min_cold = 0;
     uint64_t rs_big_min = 0;
     /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
      * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
@@ -117,7 +123,7 @@ enum {
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
     B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS, B_MB_CNT2, B_MB_OFF2,
-    B_MB_KEYS2, B_MB_COUNTS2,
+    B_MB_KEYS2, B_MB_COUNTS2, B_KEYS_C, B_HOT_FORCE, B_C2B,
     B_COUNT
 };
 
@@ -202,6 +208,8 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     for (int i = 0; i < HM_NEV; i++) c->ev[i] = nullptr;
     c->spread_min_keys = HM_SPREAD_MIN_KEYS;
     if (const char* e = getenv("HM_SPREAD_MIN_KEYS")) c->spread_min_keys = atof(e);
+    c->spread_min_cold = HM_SPREAD_MIN_COLD;
+    if (const char* e = getenv("HM_SPREAD_MIN_COLD")) c->spread_min_cold = atof(e);
     c->rs_big_min = HM_RS_BIG;
     if (const char* e = getenv("HM_RS_BIG_MIN")) c->rs_big_min = (uint64_t)atoll(e);
     if (const char* e = getenv("HM_HOT")) c->hot = atoi(e);
@@ -247,6 +255,9 @@ int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
     if (!strcmp(name, "HM_SPREAD_MIN_KEYS")) {
         prev = c->spread_min_keys;
         c->spread_min_keys = value;
+    } else if (!strcmp(name, "HM_SPREAD_MIN_COLD")) {
+        prev = c->spread_min_cold;
+        c->spread_min_cold = value;
     } else if (!strcmp(name, "HM_RS_BIG_MIN")) {
         prev = (double)c->rs_big_min;
         c->rs_big_min = (uint64_t)(value < 0 ? 0 : value);
@@ -501,7 +512,8 @@ static int count_fallback(hm_ctx* ctx, const double* lat, const double* lon, con
  * when level 1's sampled histogram is flat -- no digit above 4x the mean --
  * and the mean level-1 bucket holds >= HM_SPREAD_MIN_KEYS keys; the
  * environment variable of that name overrides the threshold). */
-static void spread_replan(const uint32_t* h, int F, int64_t n, int zb, int* zs, int* L, double min_keys)
+static void spread_replan(const uint32_t* h, int F, double npts, int zb, int* zs, int* L, double min_keys,
+                          bool flat)
 {
     uint64_t tot = 0, mx = 0;
     int ne = 0;
@@ -510,7 +522,7 @@ static void spread_replan(const uint32_t* h, int F, int64_t n, int zb, int* zs, 
         mx = std::max<uint64_t>(mx, h[i]);
         ne += h[i] != 0;
     }
-    if (ne == 0 || (double)n < min_keys * ne || (double)mx * ne > 4.0 * (double)tot) return;
+    if (ne == 0 || npts < min_keys * ne || (flat && (double)mx * ne > 4.0 * (double)tot)) return;
     int step = HM_SPREAD_ZOOMS;
     while (zs[0] + step * (HM_MAX_LEVELS - 1) < zb) step++;
     if (step >= HM_LEVEL_ZOOMS) return;
@@ -651,8 +663,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.redo_count = ctx->state + ST_REDO;
             a.redo_cap = redo_cap;
             /* region sizes: a sampled digit histogram with a generous margin */
-            /* ~256K samples below 2^28 points (launch-bound batches), ~1M above */
-            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> ((uint64_t)n < (1ull << 28) ? 18 : 20));
+            /* ~256K samples (1M samples above 2^28 points took 90 us per 1e9-point
+             * count; the regions' 8-sigma margins scale with sqrt(stride)) */
+            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> 18);
             HIPCHK(hipMemsetAsync(hist, 0, HM_D1 * 4, s));
             uint32_t* hot_counts = nullptr;
             uint32_t* hot_tiles = nullptr;
@@ -878,7 +891,18 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             nhot = hot_on ? (uint32_t)(ctx->host_state[ST_NHOT] & 0xFFFFFFFFull) : 0u;
             /* levels 2.. may take the spread plan (the level-1 pass is the
              * same under both: its output is u32 keys whenever L > 1) */
-            if (L > 1 && !nhot) spread_replan(ctx->host_aux, F, n, zb, zs, &L, ctx->spread_min_keys);
+            if (L > 1 && !nhot) {
+                spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, true);
+            } else if (L > 1) {
+                /* with hot tiles the rest is the cloud's sparse background: 3
+                 * zooms per level unless it is tiny (a 6-zoom level scatters
+                 * each 8192-key item over 4096 children, runs of ~1 key); the
+                 * hot tiles then join at the last level.  (host_aux holds the
+                 * cold digits' sampled counts: the hot samples were taken off) */
+                double cold = 0;
+                for (int i = 0; i < F; i++) cold += ctx->host_aux[i];
+                spread_replan(ctx->host_aux, F, cold * (double)stride, zb, zs, &L, ctx->spread_min_cold, false);
+            }
             spread = L > 2 && zs[1] - zs[0] < HM_LEVEL_ZOOMS;
             ctx->last_levels = L;
             V.count = (uint32_t)(down[0] >> 32);
@@ -931,7 +955,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         uint2* runs_sh;
         uint32_t* nruns;
         const uint64_t nkeys_out = level_keys;
-        ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
+        /* with hot tiles the last level's keys go where level 1 put the hot
+         * tiles' (B); a 3-level plan's middle level then takes a third array */
+        const bool hot3 = nhot && L == 3;
+        const int kslot = hot3 ? (l == 1 ? B_KEYS_C : B_KEYS_B) : (slot_k ? B_KEYS_B : B_KEYS_A);
+        ENSURE(kslot, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
         ENSURE(B_RUNS_SH, run_cap * sizeof(uint2), runs_sh);
         ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
         HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
@@ -977,12 +1005,27 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
         ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
         hm_launch_rs_count(s, ra);
-        const bool hot_level = nhot && l == 1;   /* hot tiles are children of level 2 */
+        /* hot tiles are children of the last level: of their z5 bucket at
+         * level 2, of their zs[1] ancestor (kept as a bucket, below) at level 3 */
+        const bool hot_level = nhot && l == L - 1;
         if (hot_level) {
             hr.dbits = V.dbits;
             hr.nr = ra.nr;
+            hr.zp = zs[l - 1];
+            hr.c2b = (l == 2) ? (const uint32_t*)ctx->bufs[B_C2B].p : nullptr;
             hm_launch_hot_nr(s, hr);
         }
+        /* a 3-level plan with hot tiles: each hot tile's zs[1] ancestor must be
+         * a level-2 bucket (its parent at level 3) even without cold keys */
+        uint8_t* force = nullptr;
+        if (nhot && L == 3 && l == 1) {
+            ENSURE(B_HOT_FORCE, V.nchildren, force);
+            HIPCHK(hipMemsetAsync(force, 0, V.nchildren, s));
+            hr.dbits = V.dbits;
+            hr.zp = zs[1];
+            hm_launch_hot_force(s, hr, force);
+        }
+        ra.force = force;
         hm_launch_scan(s, ra.nr, V.nchildren, partial, runbase, tot + 0);
         HIPCHK(hipGetLastError());
         unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
@@ -1049,6 +1092,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ca.keybase = ckeybase;
         ca.parent_coord = parent_coord;
         ca.child_begin = child_begin;
+        if (nhot && L == 3 && l == 1) ENSURE(B_C2B, V.nchildren * 4, ca.c2b);   /* child -> bucket, for level 3 */
         if (l == L - 1) {
             ENSURE(B_SLOTS, cap * 4, slots);
             ENSURE(B_SLOTBKT, cap * 4, slot_bucket);

@@ -1596,7 +1596,9 @@ __global__ __launch_bounds__(256) void k_rs_keys(HmRsArgs a)
         if (nr == 0) {
             a.nkeys[c] = 0;
             a.keybase[c] = 0;
-            a.vals[c] = 0;
+            /* a forced child is a bucket without keys or items (a hot tile's
+             * ancestor: the tile joins it as a child one level down) */
+            a.vals[c] = (a.force && a.force[c]) ? (1ull << 32) : 0ull;
             continue;
         }
         const uint64_t rb = a.runbase[c];
@@ -1617,13 +1619,44 @@ __global__ __launch_bounds__(256) void k_rs_keys(HmRsArgs a)
  * wrote in the final (u16) form into the level-2 key array.  k_hot_nr sets
  * the children's run counts before the run scan, k_hot_runs lists the runs at
  * their flat positions after it (k_rs_copy skips the children). */
+__device__ __forceinline__ uint64_t hm_hot_parent(const HmHotRunArgs& a, uint32_t tr, uint32_t tc, int* s)
+{
+    const int s1 = a.zb - a.z1;
+    uint64_t p = a.d2b[((tr >> s1) << a.z1) | (tc >> s1)];   /* the z1 bucket */
+    *s = s1;
+    if (a.c2b) {
+        /* level 3: the zoom-zp ancestor's bucket among the z1 bucket's children */
+        const int sp = a.zb - a.zp, w = a.zp - a.z1;
+        const uint32_t m = (1u << w) - 1u;
+        p = a.c2b[(p << (2 * w)) | (((tr >> sp) & m) << w) | ((tc >> sp) & m)];
+        *s = sp;
+    }
+    return p;
+}
+
+/* the last-level child index of hot tile t */
 __device__ __forceinline__ uint64_t hm_hot_child(const HmHotRunArgs& a, uint32_t t)
 {
-    const int s = a.zb - a.z1;
     const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
+    int s;
+    const uint64_t p = hm_hot_parent(a, tr, tc, &s);
     const uint32_t m = (1u << s) - 1u;
-    const uint64_t p = a.d2b[((tr >> s) << a.z1) | (tc >> s)];
     return (p << a.dbits) | (((tr & m) << s) | (tc & m));
+}
+
+/* 3-level plan: flag each hot tile's zoom-zp ancestor among the level-2
+ * children (child = z1 bucket << dbits | ancestor digit), so it stays a bucket */
+__global__ __launch_bounds__(256) void k_hot_force(HmHotRunArgs a, uint8_t* force)
+{
+    const uint32_t H = *a.n;
+    for (uint32_t h = blockIdx.x * 256 + threadIdx.x; h < H; h += gridDim.x * 256) {
+        const uint32_t t = a.tiles[h];
+        const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
+        const int s1 = a.zb - a.z1, sp = a.zb - a.zp, w = a.zp - a.z1;
+        const uint64_t p = a.d2b[((tr >> s1) << a.z1) | (tc >> s1)];
+        const uint32_t m = (1u << w) - 1u;
+        force[(p << a.dbits) | (((tr >> sp) & m) << w) | ((tc >> sp) & m)] = 1;
+    }
 }
 
 __global__ __launch_bounds__(256) void k_hot_nr(HmHotRunArgs a)
@@ -1658,6 +1691,11 @@ __global__ __launch_bounds__(256) void k_hot_runs(HmHotRunArgs a)
             }
         }
     }
+}
+
+void hm_launch_hot_force(hipStream_t s, const HmHotRunArgs& a, uint8_t* force)
+{
+    hipLaunchKernelGGL(k_hot_force, dim3(HM_MAX_HOT / 256), dim3(256), 0, s, a, force);
 }
 
 void hm_launch_hot_nr(hipStream_t s, const HmHotRunArgs& a)
@@ -1792,6 +1830,7 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
         const uint64_t d = c & (F - 1);
         if (d == 0) a.child_begin[p] = idx;
         if (a.vals[c] >> 32) {
+            if (a.c2b) a.c2b[c] = idx;
             a.out.nkeys[idx] = a.nkeys[c];
             a.out.nruns[idx] = (uint32_t)a.nr[c];
             a.out.rbase[idx] = (uint32_t)a.runbase[c];

@@ -251,11 +251,15 @@ struct HmHotArgs {
     uint32_t* cand;             /* [2 * HM_HOT_CAND + 1]: (tile, count) candidates, then their number */
 };
 
-/* hot tiles as children of the level-2 run scan (k_hot_nr / k_hot_runs) */
+/* hot tiles as children of the last level's run scan (k_hot_nr / k_hot_runs):
+ * their parent is their z1 bucket (d2b) at level 2, or their zoom-zp
+ * ancestor's level-2 bucket (c2b) at level 3 */
 struct HmHotRunArgs {
     const uint32_t* tiles;
     const uint32_t* n;
     int zb, z1, dbits;
+    int zp;                     /* the parent level's zoom */
+    const uint32_t* c2b;        /* level 3: level-2 child -> bucket, else NULL */
     const uint32_t* fill;       /* level-1 [HM_D1 * HM_L1_SHARDS] */
     const uint32_t* rbase;
     const uint32_t* d2b;        /* [HM_MAX_F1] z1 digit -> level-1 bucket */
@@ -316,6 +320,7 @@ struct HmRsArgs {
     uint32_t* nkeys;            /* [nchildren] */
     uint32_t* keybase;          /* [nchildren] */
     uint64_t* vals;             /* [nchildren] (1 << 32 | items) for non-empty children */
+    const uint8_t* force;       /* [nchildren] or NULL: children kept as buckets without keys (hot ancestors) */
     uint32_t* big;              /* [HM_RS_BIG_MAX] children with many runs (k_rs_copy_big) */
     uint32_t* nbig;             /* their count */
     uint64_t big_min;           /* runs above which a child is listed */
@@ -338,6 +343,7 @@ struct HmCompactArgs {
     const uint64_t* parent_coord;
     HmCompactOut out;
     uint32_t* child_begin;
+    uint32_t* c2b;          /* [nchildren] or NULL: bucket index of each kept child */
     int32_t* slots;         /* last level only */
     uint32_t* nslots;
     uint32_t* slot_bucket;
@@ -386,6 +392,7 @@ void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a);
 void hm_launch_l1_sizes(hipStream_t s, const uint32_t* hist, int F, const uint32_t* hot_n, uint64_t stride,
                         uint32_t* rcap, uint32_t* rbase, uint8_t* smask, unsigned long long* total);
 void hm_launch_hot_nr(hipStream_t s, const HmHotRunArgs& a);
+void hm_launch_hot_force(hipStream_t s, const HmHotRunArgs& a, uint8_t* force);
 void hm_launch_hot_runs(hipStream_t s, const HmHotRunArgs& a);
 void hm_launch_level1_buckets(hipStream_t s, const HmL1Args& a);
 struct HmRedoArgs {

@@ -105,6 +105,10 @@ int hm_ctx_destroy(hm_ctx* ctx);
  * same name once; this sets it afterwards.  HM_E_ARG for an unknown name.
  *   HM_SPREAD_MIN_KEYS  mean level-1 bucket (keys) of a flat histogram above
  *                       which levels 2.. take 3 zooms (default 2^19)
+ *   HM_SPREAD_MIN_COLD  with hot tiles: mean level-1 bucket of the other
+ *                       (cold) keys above which levels 2.. take 3 zooms and
+ *                       the hot tiles join the last level (default off:
+ *                       1e30; measured slower on the bench clouds)
  *   HM_RS_BIG_MIN       runs above which a level child is copied by every
  *                       wave of the run scan (default 2048)
  *   HM_HOT              1 (default): hot tiles skip the intermediate

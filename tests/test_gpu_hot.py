@@ -1,5 +1,5 @@
 """Hot tiles (hm_pipeline.h): zoom-(Z-7) tiles that a
-sample shows to hold >= 1/2048 of the points get their own level-1 digit and
+sample shows to hold >= 1/4096 of the points get their own level-1 digit and
 go straight to the final aggregation, skipping the level-2 partition.  The
 counts must not change: every case is compared with the oracle (the per-zoom
 reduceByKey of heatmap.py:109-111) cell for cell, or, at tens of millions of
@@ -30,10 +30,26 @@ def _same(got, ref):
 def test_hot_latlon(gpu, kind, n, zmin, zmax):
     lat, lon = synth.generate(kind, n, seed=31)
     keep = (np.arange(n) % 11 != 5).astype(np.uint8)
-    with device.tuned(HM_HOT_MIN_KEYS=0):
+    with device.tuned(HM_HOT_MIN_KEYS=0, HM_SPREAD_MIN_COLD=1e12):
         got = device.count(lat, lon, keep, zmin, zmax)
     assert int(got.stage_us[6]) > 0, "no hot tiles"
     assert int(got.stage_us[7]) == 2
+    _same(got, oracle.count(lat, lon, keep, zmin, zmax))
+
+
+@pytest.mark.parametrize("kind,n,zmin,zmax", [("hotspots", 2_000_000, 0, 18), ("skew", 1_000_000, 0, 18),
+                                              ("hotspots", 1_000_000, 12, 18), ("hotspots", 1_000_000, 0, 16),
+                                              ("skew", 600_000, 0, 17)])
+def test_hot_with_spread_plan(gpu, kind, n, zmin, zmax):
+    """Hot tiles with the cold rest on 3-zoom levels (z5 -> z(Z-10) -> z(Z-7)):
+    the tiles join the last level as children of their level-2 ancestor, which
+    stays a bucket even without cold keys (forced)."""
+    lat, lon = synth.generate(kind, n, seed=37)
+    keep = (np.arange(n) % 13 != 4).astype(np.uint8)
+    with device.tuned(HM_HOT_MIN_KEYS=0, HM_SPREAD_MIN_COLD=0):
+        got = device.count(lat, lon, keep, zmin, zmax)
+    assert int(got.stage_us[6]) > 0, "no hot tiles"
+    assert int(got.stage_us[7]) == 3
     _same(got, oracle.count(lat, lon, keep, zmin, zmax))
 
 
