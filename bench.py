@@ -244,6 +244,7 @@ def main():
         return device.count_device(lat, lon, None, args.zmin, args.zmax, local, buffers=bufs)
 
     dist_info = None
+    reruns = None              # level-1 re-runs over the timed steps (single-rank path)
     if args.dist:
         import torch.distributed as dist
 
@@ -295,6 +296,7 @@ def main():
             m, bufs = step()
         torch.cuda.synchronize()
         stages = []
+        reruns = 0
         ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()
         ev0.record()
@@ -302,6 +304,7 @@ def main():
             m, bufs = step()
             _, us = ctx.last_stats()
             stages.append(us[:5])
+            reruns += int(us[5])
         ev1.record()
         torch.cuda.synchronize()
         dt = time.perf_counter() - t0
@@ -359,7 +362,7 @@ def main():
                                        "how": "torch device copy of 4 GiB, (read + write bytes) / time, best of 5"},
                      "fp64": fp64},
         "kernels": kernels,
-        "pipeline": {"slow_path_points": ctx.last_stats()[0], "check": check},
+        "pipeline": {"slow_path_points": ctx.last_stats()[0], "level1_reruns": reruns, "check": check},
     }
     if dist_info is not None:
         out["distributed"] = dist_info

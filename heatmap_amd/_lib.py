@@ -24,8 +24,9 @@ HM_E_ARG = 16
 HM_E_CAPACITY = 17
 HM_E_HIP = 18
 HM_E_NOMEM = 19
+HM_E_WIDE = 20        # hm_cells_route(count_bytes=4): a count needs 64 bits
 HM_COUNT_MAX_ZOOM = 21
-HM_ABI_VERSION = 4
+HM_ABI_VERSION = 5
 HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy", "hm_ctx_tune",
@@ -103,9 +104,10 @@ def load() -> ctypes.CDLL:
         L.hm_stream_destroy.argtypes = [vp]
         L.hm_dense_grid_size.argtypes = [c.c_int]
         L.hm_dense_grid_size.restype = c.c_int64
-        L.hm_cells_route.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, vp, vp, vp, P(c.c_int64)]
-        L.hm_cells_merge.argtypes = [vp, vp, vp, c.c_int64, vp, vp, c.c_int64, P(c.c_int64)]
-        L.hm_cells_merge_runs.argtypes = [vp, vp, vp, c.c_int64, P(c.c_int64), c.c_int, vp, vp, c.c_int64,
+        L.hm_cells_route.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, vp, vp, vp, c.c_int,
+                                     P(c.c_int64)]
+        L.hm_cells_merge.argtypes = [vp, vp, vp, c.c_int, c.c_int64, vp, vp, c.c_int64, P(c.c_int64)]
+        L.hm_cells_merge_runs.argtypes = [vp, vp, vp, c.c_int, c.c_int64, P(c.c_int64), c.c_int, vp, vp, c.c_int64,
                                           P(c.c_int64)]
         L.hm_dense_cells.argtypes = [vp, vp, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
         for name in EXPORTS:

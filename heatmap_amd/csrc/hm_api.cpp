@@ -70,6 +70,7 @@ struct hm_ctx {
      * (INTEGRATION.md): HM_SPREAD_MIN_KEYS, HM_RS_BIG_MIN */
     double spread_min_keys = 0;
     double spread_min_cold = 0;
+    int sample_log2 = 18;              /* level-1 region sizing: ~2^sample_log2 sampled points */
     uint64_t rs_big_min = 0;
     /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
      * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
@@ -184,6 +185,7 @@ const char* hm_status_string(int s)
     case HM_E_EXOTIC: return "the streaming heatmap holds tiles inside [0, 2^zmax)^2 only";
     case HM_E_ARG: return "invalid argument";
     case HM_E_CAPACITY: return "output capacity too small";
+    case HM_E_WIDE: return "a routed count needs 64 bits (route again with count_bytes = 8)";
     case HM_E_HIP: return "HIP runtime error";
     case HM_E_NOMEM: return "device allocation failed";
     default: return "unknown status";
@@ -216,6 +218,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     if (const char* e = getenv("HM_HOT_INV_SHARE")) c->hot_inv_share = atof(e);
     if (const char* e = getenv("HM_HOT_MIN_KEYS")) c->hot_min_keys = atof(e);
     if (const char* e = getenv("HM_RUN_SHARD_BITS")) c->run_shard_bits = atoi(e);
+    if (const char* e = getenv("HM_SAMPLE_LOG2")) c->sample_log2 = std::min(30, std::max(8, atoi(e)));
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -258,6 +261,10 @@ int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
     } else if (!strcmp(name, "HM_SPREAD_MIN_COLD")) {
         prev = c->spread_min_cold;
         c->spread_min_cold = value;
+    } else if (!strcmp(name, "HM_SAMPLE_LOG2")) {
+        if (!(value >= 8 && value <= 30)) return HM_E_ARG;
+        prev = c->sample_log2;
+        c->sample_log2 = (int)value;
     } else if (!strcmp(name, "HM_RS_BIG_MIN")) {
         prev = (double)c->rs_big_min;
         c->rs_big_min = (uint64_t)(value < 0 ? 0 : value);
@@ -607,6 +614,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     bool hot_on = false;        /* hot tiles sampled and looked up by level 1 */
     bool spread = false;        /* levels 2.. take fewer zooms (spread_replan) */
     uint32_t nhot = 0;          /* hot tiles found */
+    int l1_reruns = 0;          /* level-1 re-runs after a region overflow */
     HmHotRunArgs hr;            /* hot tiles as level-2 children */
     memset(&hr, 0, sizeof(hr));
     for (int l = 0; l < L; l++) {
@@ -665,7 +673,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             /* region sizes: a sampled digit histogram with a generous margin */
             /* ~256K samples (1M samples above 2^28 points took 90 us per 1e9-point
              * count; the regions' 8-sigma margins scale with sqrt(stride)) */
-            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> 18);
+            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> ctx->sample_log2);
             HIPCHK(hipMemsetAsync(hist, 0, HM_D1 * 4, s));
             uint32_t* hot_counts = nullptr;
             uint32_t* hot_tiles = nullptr;
@@ -870,6 +878,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 /* a region overflowed: fill[] now holds the exact sizes (the
                  * shard of every tile is fixed by its block id) */
                 if (attempt > 0) return HM_E_HIP;   /* cannot happen: the same points */
+                l1_reruns++;
                 HIPCHK(hipMemcpyAsync(hc, fill, FS * 4, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
                 for (int i = 0; i < FS; i++) hc[i] += 64;
@@ -1216,7 +1225,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         (void)hipEventElapsedTime(&ms, ev[5 + 2 * (l - 1)], ev[6 + 2 * (l - 1)]);
         ctx->stage_us[4] += ms * 1000.0;
     }
-    ctx->stage_us[6] = (double)nhot;   /* hm_last_stats: hot tiles of the call */
+    ctx->stage_us[5] = (double)l1_reruns;   /* hm_last_stats: level-1 re-runs (a region overflowed) */
+    ctx->stage_us[6] = (double)nhot;        /* hm_last_stats: hot tiles of the call */
     const unsigned long long nc = ctx->host_state[ST_CURSOR];
     *n_out = (int64_t)nc;
     /* cells outside the square: the general path over the exotic list */
@@ -1348,11 +1358,12 @@ extern "C" int64_t hm_dense_grid_size(int dense_zmax)
 }
 
 extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks,
-                              int delta, int dense_zmax, uint64_t* grid, uint64_t* keys_out, uint64_t* counts_out,
-                              int64_t* send_counts)
+                              int delta, int dense_zmax, uint64_t* grid, uint64_t* keys_out, void* counts_out,
+                              int count_bytes, int64_t* send_counts)
 {
     if (!ctx || n < 0 || nranks < 1 || nranks > 64 || delta < 0 || delta > 28 || dense_zmax > 14 ||
-        (dense_zmax >= 0 && !grid) || !send_counts || (n > 0 && (!keys || !counts || !keys_out || !counts_out)))
+        (count_bytes != 4 && count_bytes != 8) || (dense_zmax >= 0 && !grid) || !send_counts ||
+        (n > 0 && (!keys || !counts || !keys_out || !counts_out)))
         return HM_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -1366,7 +1377,7 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     memset(&a, 0, sizeof(a));
     ENSURE(B_RT_CNT, m * 8, a.block_cnt);
     uint64_t* off;
-    ENSURE(B_RT_OFF, (m + 1) * 8, off);
+    ENSURE(B_RT_OFF, (m + 2) * 8, off);    /* + the total, + the wide flag */
     uint64_t *partial, *tot;
     ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
     ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
@@ -1379,23 +1390,32 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     a.grid = grid;
     a.block_off = off;
     a.keys_out = keys_out;
-    a.counts_out = counts_out;
+    if (count_bytes == 4) {
+        a.counts_out32 = (uint32_t*)counts_out;
+        a.wide = (unsigned long long*)(off + m + 1);
+        HIPCHK(hipMemsetAsync(a.wide, 0, 8, s));
+    } else {
+        a.counts_out = (uint64_t*)counts_out;
+    }
     hm_launch_cells_route(s, a, false);
     hm_launch_scan(s, a.block_cnt, m, partial, off, off + m);
     hm_launch_cells_route(s, a, true);
     HIPCHK(hipGetLastError());
-    std::vector<uint64_t> h(m + 1);
-    HIPCHK(hipMemcpyAsync(h.data(), off, (m + 1) * 8, hipMemcpyDeviceToHost, s));
+    std::vector<uint64_t> h(m + 2);
+    HIPCHK(hipMemcpyAsync(h.data(), off, (m + 2) * 8, hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     for (int r = 0; r < nranks; r++)
         send_counts[r] = (int64_t)(h[(uint64_t)(r + 1) * blocks] - h[(uint64_t)r * blocks]);
-    return HM_OK;
+    return (count_bytes == 4 && h[m + 1]) ? HM_E_WIDE : HM_OK;
 }
 
-static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, const int64_t* runs,
-                       int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in, int count_bytes, int64_t n,
+                       const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
+                       int64_t* n_out)
 {
-    if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && (!keys || !counts)) ||
+    const uint64_t* counts = count_bytes == 8 ? (const uint64_t*)counts_in : nullptr;
+    const uint32_t* counts32 = count_bytes == 4 ? (const uint32_t*)counts_in : nullptr;
+    if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && !keys) || (n > 0 && !counts && !counts32) ||
         (capacity > 0 && (!keys_out || !counts_out)) || nruns < 0 || (nruns > 0 && !runs))
         return HM_E_ARG;
     int64_t sum = 0;
@@ -1409,6 +1429,7 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+    const uint64_t *pk_all = nullptr, *pc_all = nullptr;   /* the first partition pass's copy (u64 counts) */
     {
         /* bucketed LDS merge (hm_merge.hip): 2^lb hash buckets of <= ~1800
          * cells (one LDS table pass each), one block per bucket; the cells are
@@ -1426,10 +1447,11 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
         memset(&p1, 0, sizeof(p1));
         p1.kin = keys;
         p1.cin = counts;
+        p1.cin32 = counts32;
         p1.n = (uint64_t)n;
         p1.nseg = 1;
         p1.C = chunks((uint64_t)n, 65536, 512);
-        p1.shift = 64 - b1;
+        p1.shift = b1 ? 64 - b1 : 63;   /* b1 = 0: one bucket (digit mask 0; no shift by 64) */
         p1.bits = b1;
         const uint64_t m1 = ((uint64_t)1 << b1) * p1.C;
         uint64_t *cnt1, *off1, *pk, *pc;
@@ -1455,6 +1477,7 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
             HmMbPass p2 = p1;
             p2.kin = pk;
             p2.cin = pc;
+            p2.cin32 = nullptr;
             p2.segoff = off1;
             p2.segstride = p1.C;
             p2.nseg = 1u << b1;
@@ -1483,6 +1506,8 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
         a.counts = counts;
         a.n = (uint64_t)n;
         a.lb = lb;
+        pk_all = pk;
+        pc_all = pc;
         unsigned long long* st;
         ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), st);
         HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
@@ -1510,7 +1535,10 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
     t.mask = cap - 1;
     HIPCHK(hipMemsetAsync(t.state, 0, 8 * sizeof(unsigned long long), s));
     hm_launch_stream_init(s, t);
-    if (runs) {
+    if (counts32) {
+        /* u32 input counts: the partition pass's u64 copy, in partition order */
+        hm_launch_cells_merge(s, pk_all, pc_all, (uint64_t)n, t);
+    } else if (runs) {
         /* runs of distinct keys: no two threads of a launch insert one key */
         int64_t off = 0;
         for (int i = 0; i < nruns; i++) {
@@ -1529,17 +1557,19 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts
     return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
 }
 
-extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
+extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes, int64_t n,
                               uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
 {
-    return cells_merge(ctx, keys, counts, n, nullptr, 0, keys_out, counts_out, capacity, n_out);
+    if (count_bytes != 4 && count_bytes != 8) return HM_E_ARG;
+    return cells_merge(ctx, keys, counts, count_bytes, n, nullptr, 0, keys_out, counts_out, capacity, n_out);
 }
 
-extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
-                                   const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out,
-                                   int64_t capacity, int64_t* n_out)
+extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes,
+                                   int64_t n, const int64_t* runs, int nruns, uint64_t* keys_out,
+                                   uint64_t* counts_out, int64_t capacity, int64_t* n_out)
 {
-    return cells_merge(ctx, keys, counts, n, runs, nruns, keys_out, counts_out, capacity, n_out);
+    if (count_bytes != 4 && count_bytes != 8) return HM_E_ARG;
+    return cells_merge(ctx, keys, counts, count_bytes, n, runs, nruns, keys_out, counts_out, capacity, n_out);
 }
 
 extern "C" int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out,
@@ -1646,7 +1676,7 @@ static int stream_compact(hm_stream* s)
     int st;
     if (!s->akeys && (st = stream_alloc2(s->lcap, &s->akeys, &s->acounts))) return st;
     int64_t m = 0;
-    if ((st = cells_merge(s->ctx, s->lkeys, s->lcounts, (int64_t)s->llen, nullptr, 0, s->akeys, s->acounts,
+    if ((st = cells_merge(s->ctx, s->lkeys, s->lcounts, 8, (int64_t)s->llen, nullptr, 0, s->akeys, s->acounts,
                           (int64_t)s->lcap, &m)))
         return st;
     std::swap(s->lkeys, s->akeys);
@@ -1996,7 +2026,7 @@ extern "C" int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_
     /* equal label cells summed */
     if ((st = stream_buf(s, s->mk, m * 8)) || (st = stream_buf(s, s->mc, m * 8))) return st;
     int64_t nd = 0;
-    if ((st = cells_merge(ctx, (const uint64_t*)s->rk.p, (const uint64_t*)s->rc.p, (int64_t)m, nullptr, 0,
+    if ((st = cells_merge(ctx, (const uint64_t*)s->rk.p, (const uint64_t*)s->rc.p, 8, (int64_t)m, nullptr, 0,
                           (uint64_t*)s->mk.p, (uint64_t*)s->mc.p, (int64_t)m, &nd)))
         return st;
     *n_out = nd;

@@ -93,10 +93,13 @@ __global__ __launch_bounds__(HM_ROUTE_THREADS) void k_cells_route(HmRouteArgs a)
             if (sp) {
                 const uint64_t q = base[o] + pos;
                 a.keys_out[q] = k;
-                a.counts_out[q] = a.counts[i];
+                if (a.counts_out32) a.counts_out32[q] = (uint32_t)a.counts[i];
+                else a.counts_out[q] = a.counts[i];
             }
         } else {
             hm_lds_count(hist, HM_MAX_RANKS, o, sp);
+            if (a.counts_out32 && __any(sp && (a.counts[i] >> 32) != 0ull) && (tid & 63) == 0)
+                atomicOr(a.wide, 1ull);
         }
     }
     __syncthreads();
@@ -282,7 +285,7 @@ __global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
             const uint32_t i = j * 256 + tid;
             const bool v = i < tn;
             k[j] = v ? a.kin[t0 + i] : 0ull;
-            cc[j] = v ? a.cin[t0 + i] : 0ull;
+            cc[j] = v ? (a.cin32 ? (uint64_t)a.cin32[t0 + i] : a.cin[t0 + i]) : 0ull;
         }
 #pragma unroll
         for (int j = 0; j < HM_MB_PPT; j++) {

@@ -583,7 +583,9 @@ struct HmRouteArgs {
     uint64_t* block_cnt;       /* [nranks * blocks] pass 1 */
     const uint64_t* block_off; /* [nranks * blocks] exclusive scan of block_cnt */
     uint64_t* keys_out;
-    uint64_t* counts_out;
+    uint64_t* counts_out;      /* u64 counts, or */
+    uint32_t* counts_out32;    /* u32 counts (the exchange's 12 B/cell) */
+    unsigned long long* wide;  /* counts_out32: set when a sent count needs 64 bits */
 };
 unsigned hm_route_blocks(uint64_t n);
 /* bucketed merge of (key, count) cells: hash-partition into 2^lb buckets
@@ -615,6 +617,7 @@ struct HmMergeArgs {
 struct HmMbPass {
     const uint64_t* kin;
     const uint64_t* cin;
+    const uint32_t* cin32;      /* u32 input counts instead of cin (pass 1 of a merge of received cells) */
     uint64_t n;
     const uint64_t* segoff;
     uint32_t segstride, nseg, C;

@@ -163,8 +163,8 @@ HM_FN int hm_project_fast(double lat, double lon, double scale, double kz, int32
     const double y = (lon + 180.0) * kz;
     const double f2 = floor(y);
     const double g2 = scale * 0x1p-49;   /* >= |y| 2^-49 on the accepted range 0 <= y < 2^z */
-    const int ok = (fabs(lat) <= HM_LAT_SQ) & (fabs((R - f) - 0.5) < 0.5 - g) & (y >= 0.0) & (y < scale) &
-                   (fabs((y - f2) - 0.5) < 0.5 - g2);
+    const int ok = (int)(fabs(lat) <= HM_LAT_SQ) & (int)(fabs((R - f) - 0.5) < 0.5 - g) & (int)(y >= 0.0) &
+                   (int)(y < scale) & (int)(fabs((y - f2) - 0.5) < 0.5 - g2);   /* branch-free */
     *row = (int32_t)(ok ? f : 0.0);
     *col = (int32_t)(ok ? f2 : 0.0);
     return ok;

@@ -277,7 +277,7 @@ def _count_chunked(a, b, kp, n, zmin, zmax, device, tiles, chunk):
     cap = max(int(k.numel()), 1)
     out = CountBuffers(cap, device, 1024)
     nout = ctypes.c_int64(0)
-    rc = ctx.L.hm_cells_merge(ctx.ptr, _ptr(k), _ptr(c), int(k.numel()), _ptr(out.keys), _ptr(out.counts), cap,
+    rc = ctx.L.hm_cells_merge(ctx.ptr, _ptr(k), _ptr(c), 8, int(k.numel()), _ptr(out.keys), _ptr(out.counts), cap,
                               ctypes.byref(nout))
     if rc != _lib.HM_OK:
         _lib.raise_for(rc)

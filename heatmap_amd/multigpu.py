@@ -52,25 +52,35 @@ class DeviceOps:
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
 
-    def route(self, keys, counts, ws, dense_zmax):
+    def route(self, keys, counts, ws, dense_zmax, narrow=False):
+        """-> (dense grid, keys and counts grouped by owner, group sizes,
+        wide).  narrow: counts travel as int32 (12 B per cell) unless one
+        needs 64 bits -- then wide is True and the counts returned are of no
+        use (route again with narrow=False)."""
+        from . import _lib
+
         n = keys.numel()
         gsz = int(self.L.hm_dense_grid_size(dense_zmax))
         grid = torch.empty(max(gsz, 1), dtype=torch.int64, device=keys.device)
         ko = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
-        co = torch.empty_like(ko)
+        co = torch.empty(max(n, 1), dtype=torch.int32 if narrow else torch.int64, device=keys.device)
         send = (ctypes.c_int64 * ws)()
-        self._check(self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax,
-                                          self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko),
-                                          self._p(co), send))
+        rc = self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax,
+                                   self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko), self._p(co),
+                                   4 if narrow else 8, send)
+        wide = rc == _lib.HM_E_WIDE
+        if not wide:
+            self._check(rc)
         sent = list(send)
         m = sum(sent)
-        return grid[:gsz], ko[:m], co[:m], sent
+        return grid[:gsz], ko[:m], co[:m], sent, wide
 
     def merge(self, keys, counts, runs=None, out=None):
-        """Sum equal keys; runs (list of sizes): consecutive runs of distinct
-        keys (one sending rank's cells each), merged without count atomics.
-        out: (keys, counts) tensors to write into (their length is the
-        capacity; MemoryError if the merged cells do not fit)."""
+        """Sum equal keys (counts int32 or int64; the sums are int64); runs
+        (list of sizes): consecutive runs of distinct keys (one sending rank's
+        cells each), merged without count atomics.  out: (keys, counts)
+        tensors to write into (their length is the capacity; MemoryError if
+        the merged cells do not fit)."""
         from . import _lib
 
         n = keys.numel()
@@ -82,13 +92,16 @@ class DeviceOps:
             ko = torch.empty(cap, dtype=torch.int64, device=keys.device)
             co = torch.empty_like(ko)
         nout = ctypes.c_int64(0)
+        cb = counts.element_size()
+        if cb not in (4, 8):
+            raise TypeError("merge: counts must be int32 or int64")
         if runs is not None:
             ra = (ctypes.c_int64 * max(len(runs), 1))(*runs)
-            rc = self.L.hm_cells_merge_runs(self.ctx.ptr, self._p(keys), self._p(counts), n, ra, len(runs),
+            rc = self.L.hm_cells_merge_runs(self.ctx.ptr, self._p(keys), self._p(counts), cb, n, ra, len(runs),
                                             self._p(ko), self._p(co), cap, ctypes.byref(nout))
         else:
-            rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), n, self._p(ko), self._p(co),
-                                       cap, ctypes.byref(nout))
+            rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), cb, n, self._p(ko),
+                                       self._p(co), cap, ctypes.byref(nout))
         if rc == _lib.HM_E_CAPACITY and out is not None:
             raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (nout.value, cap))
         if rc != _lib.HM_OK:
@@ -221,13 +234,19 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         ops = DeviceOps(buffers.keys.device.index or 0)
     keys = buffers.keys[:m]
     counts = buffers.counts[:m]
-    grid, sk, sc, sent = ops.route(keys, counts, ws, dense_zmax)
-    if dense_zmax >= 0:
-        dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
-    send = torch.tensor(sent, dtype=torch.int64, device=keys.device)
+    # counts travel as int32 (12 B per cell, not 16) unless some rank holds a
+    # cell count >= 2^32: every rank's flag rides on the group-size exchange,
+    # so all ranks agree before the keys/counts all-to-all
+    grid, sk, sc, sent, wide = ops.route(keys, counts, ws, dense_zmax, narrow=True)
+    send = torch.tensor([[s, int(wide)] for s in sent], dtype=torch.int64, device=keys.device)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)
-    rl = recv.tolist()
+    recv = recv.cpu()
+    rl = recv[:, 0].tolist()
+    if bool(recv[:, 1].any()):
+        grid, sk, sc, sent, _ = ops.route(keys, counts, ws, dense_zmax, narrow=False)
+    if dense_zmax >= 0:
+        dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
     # the owned cells are at most the received ones plus (rank 0) the dense
     # grid's: grow this rank's buffers first (a local decision -- a rank that
     # raised here instead would leave its peers blocked in the next collective)
@@ -237,7 +256,7 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         buffers.counts = torch.empty_like(buffers.keys)
         buffers.capacity = need
     nk = torch.empty(sum(rl), dtype=torch.int64, device=keys.device)
-    nc = torch.empty_like(nk)
+    nc = torch.empty(sum(rl), dtype=sc.dtype, device=keys.device)
     dist.all_to_all_single(nk, sk, rl, sent)
     dist.all_to_all_single(nc, sc, rl, sent)
     if isinstance(ops, DeviceOps):

@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 4
+#define HM_ABI_VERSION 5
 
 /* status / per-point error kinds */
 #define HM_OK 0
@@ -81,6 +81,7 @@ extern "C" {
 #define HM_E_CAPACITY 17 /* output arrays too small; *n_out holds the size needed */
 #define HM_E_HIP 18      /* HIP runtime error (no device, launch failure) */
 #define HM_E_NOMEM 19    /* device allocation failed */
+#define HM_E_WIDE 20     /* hm_cells_route with count_bytes = 4: a count >= 2^32 (outputs complete otherwise) */
 
 /* Output cell key of hm_count: zoom in bits 58..63, row in 29..57, col in 0..28.
  * Sorting keys sorts by (zoom, row, col). */
@@ -109,12 +110,14 @@ int hm_ctx_destroy(hm_ctx* ctx);
  *                       (cold) keys above which levels 2.. take 3 zooms and
  *                       the hot tiles join the last level (default off:
  *                       1e30; measured slower on the bench clouds)
+ *   HM_SAMPLE_LOG2      level-1 regions are sized from ~2^this sampled
+ *                       points (8..30; default 18)
  *   HM_RS_BIG_MIN       runs above which a level child is copied by every
  *                       wave of the run scan (default 2048)
  *   HM_HOT              1 (default): hot tiles skip the intermediate
  *                       partition passes; 0: off
  *   HM_HOT_INV_SHARE    a tile is hot with >= 1/this of the sampled points
- *                       (default 2048)
+ *                       (default 4096)
  *   HM_HOT_MIN_KEYS     ... and >= this many estimated points (default 65536)
  *   HM_RUN_SHARD_BITS   log2 run counters per level-2+ child (0..5; default
  *                       -1: 0 with hot tiles or the spread plan, else 4)
@@ -180,6 +183,8 @@ int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);
  *       compactions (incl. host reads; contains [4])
  *   [2] final aggregation (k_aggregate, sparse/small/merged buckets)
  *   [3] k_pool levels   [4] the level >= 2 k_partition launches alone
+ *   [5] level-1 re-runs (a sampled region size was too small; slot 0 then
+ *       times the last run only)
  *   [6] hot tiles of the call (their points skipped levels 2..)
  *   [7] partition levels of the pipeline plan (0 if the call took the
  *       general path); 3 zooms per level for dense, evenly spread clouds */
@@ -245,19 +250,27 @@ int hm_stream_destroy(hm_stream* s);
  *                    (a hash of the heatmap row key (zoom, row >> delta,
  *                    col >> delta), so each output row has one owner);
  *                    send_counts (host int64[nranks]) receives the group sizes
- *                    for an RCCL all-to-all.  nranks <= 64.
- *   hm_cells_merge   sum the counts of equal keys over n received cells;
+ *                    for an RCCL all-to-all.  nranks <= 64.  count_bytes 4:
+ *                    counts_out is u32[n] (the exchange moves 12 B per cell,
+ *                    not 16); a count >= 2^32 returns HM_E_WIDE after filling
+ *                    everything else (the caller's ranks then agree to route
+ *                    again with count_bytes 8: a rank's cells count fewer
+ *                    points than it holds, so only > 2^32-point shards can).
+ *   hm_cells_merge   sum the counts of equal keys over n received cells
+ *                    (counts u32 or u64 per count_bytes; output u64);
  *   hm_cells_merge_runs  the same when the n cells are nruns consecutive runs
  *                    (host int64 sizes) each of distinct keys -- one rank's
  *                    cells each -- so only the key claim is atomic.
  *   hm_dense_cells   the non-empty cells of a (reduced) dense grid. */
 int64_t hm_dense_grid_size(int dense_zmax);
 int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks, int delta,
-                   int dense_zmax, uint64_t* grid, uint64_t* keys_out, uint64_t* counts_out, int64_t* send_counts);
-int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, uint64_t* keys_out,
-                   uint64_t* counts_out, int64_t capacity, int64_t* n_out);
-int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, const int64_t* runs,
-                        int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out);
+                   int dense_zmax, uint64_t* grid, uint64_t* keys_out, void* counts_out, int count_bytes,
+                   int64_t* send_counts);
+int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes, int64_t n,
+                   uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out);
+int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes, int64_t n,
+                        const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
+                        int64_t* n_out);
 int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out, uint64_t* counts_out,
                    int64_t capacity, int64_t* n_out);
 

@@ -25,13 +25,14 @@ def _cells(n, seed):
     return torch.from_numpy(keys), torch.from_numpy(c.count)
 
 
-@pytest.mark.parametrize("ws,dz", [(1, 10), (5, 8), (8, -1), (64, 4)])
-def test_route_kernel_contract(gpu, ws, dz):
+@pytest.mark.parametrize("ws,dz,narrow", [(1, 10, False), (5, 8, True), (8, -1, True), (64, 4, False)])
+def test_route_kernel_contract(gpu, ws, dz, narrow):
     keys, counts = _cells(300_000, ws)
     ops = multigpu.DeviceOps(0)
-    g, sk, sc, sent = ops.route(keys.cuda(), counts.cuda(), ws, dz)
-    rg, rk, rc, rsent = TorchOps.route(keys, counts, ws, dz)
-    assert sent == rsent
+    g, sk, sc, sent, wide = ops.route(keys.cuda(), counts.cuda(), ws, dz, narrow=narrow)
+    rg, rk, rc, rsent, rwide = TorchOps.route(keys, counts, ws, dz, narrow=narrow)
+    assert sent == rsent and not wide and not rwide
+    assert sc.dtype == (torch.int32 if narrow else torch.int64)
     assert torch.equal(g.cpu(), rg)
     sk, sc = sk.cpu(), sc.cpu()
     at = 0
@@ -46,6 +47,39 @@ def test_route_kernel_contract(gpu, ws, dz):
         ek, ec = TorchOps.dense_cells(rg, dz)
         o, eo = torch.argsort(dk.cpu()), torch.argsort(ek)
         assert torch.equal(dk.cpu()[o], ek[eo]) and torch.equal(dc.cpu()[o], ec[eo])
+
+
+def test_route_narrow_flags_wide_counts(gpu):
+    """narrow routing of a count >= 2^32 (a sparse zoom's cell): HM_E_WIDE
+    -> wide, with the group sizes still filled; routing again wide sends it."""
+    keys, counts = _cells(100_000, 9)
+    counts = counts.clone()
+    z = keys >> 58
+    i = int(torch.nonzero(z == 15)[0])
+    counts[i] = (1 << 33) + 7
+    ops = multigpu.DeviceOps(0)
+    _, _, _, sent, wide = ops.route(keys.cuda(), counts.cuda(), 4, 10, narrow=True)
+    assert wide and sum(sent) == int((z > 10).sum())
+    _, sk, sc, sent2, wide2 = ops.route(keys.cuda(), counts.cuda(), 4, 10, narrow=False)
+    assert not wide2 and sent2 == sent
+    assert int(sc.cpu()[sk.cpu() == keys[i]].item()) == (1 << 33) + 7
+
+
+def test_merge_narrow_counts(gpu):
+    """hm_cells_merge(_runs) of int32 counts (the exchange's width) sums into
+    int64, past 2^32 where many ranks' counts of one cell add up."""
+    g = torch.Generator().manual_seed(5)
+    base = torch.randint(0, 1 << 62, (400_000,), generator=g, dtype=torch.int64)
+    runs = [base, base[::2], base[::3], base[::2]]
+    k = torch.cat(runs)
+    c = torch.randint(1 << 30, (1 << 31) - 1, (k.numel(),), generator=g, dtype=torch.int64)
+    ek, ec = TorchOps.merge(k, c)
+    ops = multigpu.DeviceOps(0)
+    for r in (None, [x.numel() for x in runs]):
+        uk, uc = ops.merge(k.cuda(), c.to(torch.int32).cuda(), r)
+        o = torch.argsort(uk.cpu())
+        assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
+    assert int(ec.max()) >= 1 << 32
 
 
 def test_merge_kernel_sums_duplicates(gpu):

@@ -53,7 +53,7 @@ class TorchOps:
     hm_dense_cells (include/heatmap_amd.h)."""
 
     @staticmethod
-    def route(keys, counts, ws, dz):
+    def route(keys, counts, ws, dz, narrow=False):
         z, r, c = keys >> 58, (keys >> 29) & M29, keys & M29
         gsz = ((1 << (2 * (dz + 1))) - 1) // 3 if dz >= 0 else 0
         grid = torch.zeros(gsz, dtype=torch.int64)
@@ -66,13 +66,15 @@ class TorchOps:
         rec = torch.stack([sk >> 58, (sk >> 29) & M29, sk & M29], 1)
         own = multigpu.record_owner(rec, ws)
         o = torch.argsort(own, stable=True)
-        return grid, sk[o], sc[o], torch.bincount(own, minlength=ws).tolist()
+        wide = narrow and bool((sc >> 32).any())
+        sc = sc[o].to(torch.int32) if narrow else sc[o]
+        return grid, sk[o], sc, torch.bincount(own, minlength=ws).tolist(), wide
 
     @staticmethod
     def merge(keys, counts, runs=None):
         u, inv = torch.unique(keys, return_inverse=True)
         t = torch.zeros(u.numel(), dtype=torch.int64)
-        t.index_add_(0, inv, counts)
+        t.index_add_(0, inv, counts.to(torch.int64))
         return u, t
 
     @staticmethod
@@ -117,6 +119,12 @@ def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out):
     per = n // ws
     lat, lon = _cloud(kind, per, rank * per)
     k, c, x = _split(oracle.count(lat, lon, None, zmin, zmax))
+    if kind == "skew" and rank == 1:
+        # one rank's count of one sparse cell past 2^32: every rank routes its
+        # counts as int64 (the flag rides on the group-size exchange)
+        j = int(np.nonzero((k >> 58) > dense_zmax)[0][0])
+        c = c.copy()
+        c[j] += 1 << 32
     b = _Bufs(k, c, x, 4 * len(k) + 64)
     m = multigpu.merge_cells(b, len(k), ws, rank, dense_zmax=dense_zmax, ops=TorchOps())
     out[rank] = (b.keys[:m].numpy().copy(), b.counts[:m].numpy().copy(), b.xcells[:4 * b.nx].numpy().copy())
@@ -137,6 +145,9 @@ def test_merge_two_ranks(kind, zmax, dense_zmax):
     lat = np.concatenate([_cloud(kind, n // ws, r * (n // ws))[0] for r in range(ws)])
     lon = np.concatenate([_cloud(kind, n // ws, r * (n // ws))[1] for r in range(ws)])
     rk, rc, rx = _split(oracle.count(lat, lon, None, zmin, zmax))
+    if kind == "skew":                                  # the count rank 1 raised past 2^32
+        k1, _, _ = _split(oracle.count(*_cloud(kind, n // ws, n // ws), None, zmin, zmax))
+        rc[np.searchsorted(rk, k1[(k1 >> 58) > dense_zmax][0])] += 1 << 32
     o, ro = np.argsort(keys), np.argsort(rk)
     assert np.array_equal(keys[o], rk[ro])
     assert np.array_equal(counts[o], rc[ro])

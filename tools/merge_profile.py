@@ -46,7 +46,8 @@ def main():
         m, bufs = device.count_device(lat, lon, None, 0, 18, 0, buffers=bufs)
         t0 = mark("count", t0)
         keys, counts = bufs.keys[:m], bufs.counts[:m]
-        grid, sk, sc, sent = ops.route(keys, counts, 1, 10)
+        grid, sk, sc, sent, wide = ops.route(keys, counts, 1, 10, narrow=True)
+        assert not wide
         t0 = mark("route", t0)
         dist.reduce(grid, dst=0)
         t0 = mark("reduce", t0)
@@ -55,7 +56,7 @@ def main():
         dist.all_to_all_single(recv, send)
         rl = recv.tolist()
         nk = torch.empty(sum(rl), dtype=torch.int64, device="cuda")
-        nc = torch.empty_like(nk)
+        nc = torch.empty(sum(rl), dtype=sc.dtype, device="cuda")
         dist.all_to_all_single(nk, sk, rl, sent)
         dist.all_to_all_single(nc, sc, rl, sent)
         t0 = mark("all_to_all", t0)

@@ -118,7 +118,7 @@ def one(name, points, steps, zmax):
     for _ in range(steps):
         m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
         ls = ctx.last_stats()[1]
-        st.append(list(ls[:4]) + [ls[6]])   # stage times, hot tiles
+        st.append(list(ls[:4]) + [ls[6], ls[5]])   # stage times, hot tiles, level-1 re-runs
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / steps
     tot = int(bufs.counts[:m].sum().item())
