@@ -71,6 +71,7 @@ struct hm_ctx {
     double spread_min_keys = 0;
     double spread_min_cold = 0;
     int sample_log2 = 18;              /* level-1 region sizing: ~2^sample_log2 sampled points */
+    int debug_l1 = 0;                  /* HM_DEBUG_L1: report level-1 region overflows on stderr */
     uint64_t rs_big_min = 0;
     /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
      * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
@@ -219,6 +220,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     if (const char* e = getenv("HM_HOT_MIN_KEYS")) c->hot_min_keys = atof(e);
     if (const char* e = getenv("HM_RUN_SHARD_BITS")) c->run_shard_bits = atoi(e);
     if (const char* e = getenv("HM_SAMPLE_LOG2")) c->sample_log2 = std::min(30, std::max(8, atoi(e)));
+    if (const char* e = getenv("HM_DEBUG_L1")) c->debug_l1 = atoi(e);
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -730,7 +732,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             const double nn = (double)n + (double)(F + (hot_on ? HM_MAX_HOT : 0)) * (double)stride;
             const double M = F + std::min((double)F, nn / (64.0 * HM_T1)) * (HM_L1_SHARDS - 1) +
                              (hot_on ? (double)HM_MAX_HOT * HM_L1_SHARDS : 0.0);
-            double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 + 1024.0;
+            double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 +
+                           (double)(F + (hot_on ? HM_MAX_HOT : 0)) * HM_L1_ZERO_SAMPLES * (double)stride + 1024.0;
             hm_launch_l1_sizes(s, hist, F, hot_on ? hot_n : nullptr, stride, rcap, rbase, smask,
                                ctx->state + ST_L1TOTAL);
             HIPCHK(hipGetLastError());
@@ -880,7 +883,16 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 if (attempt > 0) return HM_E_HIP;   /* cannot happen: the same points */
                 l1_reruns++;
                 HIPCHK(hipMemcpyAsync(hc, fill, FS * 4, hipMemcpyDeviceToHost, s));
+                if (ctx->debug_l1) HIPCHK(hipMemcpyAsync(hb, rcap, FS * 4, hipMemcpyDeviceToHost, s));
                 HIPCHK(hipStreamSynchronize(s));
+                if (ctx->debug_l1) {
+                    /* HM_DEBUG_L1=1: the overflowing regions, and the sample behind them */
+                    for (int i = 0; i < FS; i++)
+                        if (hc[i] > hb[i])
+                            fprintf(stderr, "hm l1 overflow: digit %d shard %d fill %u cap %u hist %u stride %llu\n",
+                                    i % HM_D1, i / HM_D1, hc[i], hb[i], ctx->host_aux[i % HM_D1],
+                                    (unsigned long long)stride);
+                }
                 for (int i = 0; i < FS; i++) hc[i] += 64;
             }
             nx = ctx->host_state[ST_XCOUNT];

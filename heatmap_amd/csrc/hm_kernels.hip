@@ -704,7 +704,11 @@ __device__ __forceinline__ uint32_t hm_l1_cap(uint32_t hist, uint64_t stride, in
     const double est = (double)hist * (double)stride;
     *ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
     const double e = est / *ns;
-    return (uint32_t)fmin(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) + 2.0 * HM_T1);
+    /* + HM_L1_ZERO_SAMPLES strides per digit: a digit with few or no samples
+     * may still hold that many strides of points (P(0 samples | 24) = 4e-11);
+     * the region's unused tail is never read */
+    return (uint32_t)fmin(1.0e9, e + e / 16 + 8.0 * sqrt(e * (double)stride) +
+                                     (double)HM_L1_ZERO_SAMPLES * (double)stride / *ns + 2.0 * HM_T1);
 }
 
 __global__ __launch_bounds__(1024) void k_l1_sizes(const uint32_t* __restrict__ hist, int F,
@@ -2408,6 +2412,77 @@ __global__ __launch_bounds__(HM_POOL_THREADS) void k_pool(HmPoolArgs a)
     }
 }
 
+/* k_pool for levels of <= 64 children per parent (dbits <= 6): one wavefront
+ * per parent, HM_POOLW_WAVES parents per block and ONE output reservation per
+ * block.  (A block per parent took one same-address cursor atomic per emitted
+ * zoom -- 196K of them on the uniform cloud's z8 -> z11 level, ~2.2 ms at the
+ * L2's ~88 same-address atomics per microsecond.) */
+#define HM_POOLW_WAVES 16
+__global__ __launch_bounds__(64 * HM_POOLW_WAVES) void k_pool_waves(HmPoolArgs a)
+{
+    __shared__ unsigned long long lv[HM_POOLW_WAVES][64 + 16 + 4 + 1];
+    __shared__ uint32_t wtot[HM_POOLW_WAVES];
+    __shared__ unsigned long long sbase;
+    const uint32_t lane = hm_lane(), w = threadIdx.x >> 6;
+    const uint32_t p = hm_block_id() * HM_POOLW_WAVES + w;
+    const bool live = p < a.nparents;
+    const int lg = a.dbits / 2;
+    const uint32_t F = 1u << a.dbits;
+    unsigned long long* cur = lv[w];
+    if (lane < F) cur[lane] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const uint32_t c0 = live ? a.child_begin[p] : 0u, c1 = live ? a.child_begin[p + 1] : 0u;
+    if (c0 + lane < c1) cur[a.child_digit[c0 + lane]] = a.child_totals[c0 + lane];
+    __builtin_amdgcn_wave_barrier();
+    const uint64_t pm = (live && a.parent_coord) ? a.parent_coord[p] : 0ull;
+    /* levels k = 0 .. lg-1 (zooms z_child - k), each 4^(lg-k) row-major cells,
+     * stored one after another in the wave's LDS row */
+    unsigned long long val[3];
+    uint64_t bal[3];
+    uint32_t cnt = 0;
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        val[k] = 0;
+        bal[k] = 0;
+        if (k < lg) {
+            const uint32_t nk = 1u << (2 * (lg - k));
+            const unsigned long long x = lane < nk ? cur[lane] : 0ull;
+            const int z = a.z_child - k;
+            val[k] = x;
+            bal[k] = __ballot(live && z >= a.out.zmin && z <= a.out.zmax && x != 0ull);
+            cnt += (uint32_t)__popcll(bal[k]);
+            unsigned long long* nxt = cur + nk;
+            if (lane < nk / 4) nxt[lane] = hm_sum4<unsigned long long>(cur, lane, lg - k - 1);
+            __builtin_amdgcn_wave_barrier();
+            cur = nxt;
+        }
+    }
+    if (live && lane == 0 && a.parent_totals) a.parent_totals[p] = cur[0];
+    if (lane == 0) wtot[w] = cnt;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int i = 0; i < HM_POOLW_WAVES; i++) t += wtot[i];
+        sbase = t ? atomicAdd(a.out.cursor, (unsigned long long)t) : 0ull;
+    }
+    __syncthreads();
+    uint64_t base = sbase;
+    for (uint32_t i = 0; i < w; i++) base += wtot[i];
+#pragma unroll
+    for (int k = 0; k < 3; k++) {
+        if (k < lg) {
+            if ((bal[k] >> lane) & 1ull) {
+                const uint64_t pos = base + hm_mbcnt(bal[k]);
+                if (pos < a.out.capacity) {
+                    a.out.keys[pos] = hm_cell_key(a.z_child - k, pm, lg - k, lane);
+                    a.out.counts[pos] = val[k];
+                }
+            }
+            base += (uint64_t)__popcll(bal[k]);
+        }
+    }
+}
+
 /* ------------------------------------------------------------------------ */
 /* host launchers                                                            */
 /* ------------------------------------------------------------------------ */
@@ -2679,7 +2754,12 @@ void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
 }
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {
-    if (nparents) hipLaunchKernelGGL(k_pool, hm_grid2(nparents), dim3(HM_POOL_THREADS), 0, s, a);
+    if (!nparents) return;
+    if (!a.emit_root && a.dbits <= 6)
+        hipLaunchKernelGGL(k_pool_waves, hm_grid2((nparents + HM_POOLW_WAVES - 1) / HM_POOLW_WAVES),
+                           dim3(64 * HM_POOLW_WAVES), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_pool, hm_grid2(nparents), dim3(HM_POOL_THREADS), 0, s, a);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -1,0 +1,14 @@
+#!/bin/bash
+# stream batch timeline: kernel trace of tools/bench_stream.py (1-hour batches)
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+export TMPDIR=/tmp
+O="$R/gpurun_out/${1:-r03t}"
+mkdir -p "$O"
+cd /tmp
+timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -f csv -d "$O/trace" -o run -- python3 "$R/tools/bench_stream.py" --hours 1 --batches 8 --warmup 2 > "$O/trace.log" 2>&1 || { tail -30 "$O/trace.log"; exit 1; }
+tail -1 "$O/trace.log" | cut -c1-200
+g=$(find "$O/trace" -name "run_kernel_trace.csv" | head -1); cp "$g" "$O/kernel_trace.csv"
+g=$(find "$O/trace" -name "run_memory_copy_trace.csv" | head -1); [ -n "$g" ] && cp "$g" "$O/copy_trace.csv"
+g=$(find "$O/trace" -name "run_kernel_stats.csv" | head -1); cp "$g" "$O/kernel_stats.csv"
+echo "== done"
