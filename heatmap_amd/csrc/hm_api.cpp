@@ -16,6 +16,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -108,6 +109,32 @@ static int hip_fail(hipError_t e, const char* what)
         int _st = hip_fail((x), #x);               \
         if (_st != HM_OK) return _st;              \
     } while (0)
+
+/* Wait for the stream.  HM_SYNC_SPIN_US > 0 (environment, read once per
+ * process): poll it for up to that long first, then block.  (Measured with a
+ * HIP API trace: after a polled wait the next few launches took ~60 us each
+ * instead of ~6, so the default is a plain blocking wait.) */
+static int hm_spin_us()
+{
+    static const int us = [] {
+        const char* e = getenv("HM_SYNC_SPIN_US");
+        return e ? atoi(e) : 0;
+    }();
+    return us;
+}
+static hipError_t hm_sync(hipStream_t s)
+{
+    const int spin = hm_spin_us();
+    if (spin > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        for (;;) {
+            const hipError_t e = hipStreamQuery(s);
+            if (e != hipErrorNotReady) return e;
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin)) break;
+        }
+    }
+    return hipStreamSynchronize(s);
+}
 
 /* named arena slots */
 enum {
@@ -336,7 +363,7 @@ static int read_state(hm_ctx* ctx)
 {
     HIPCHK(hipMemcpyAsync(ctx->host_state, ctx->state, ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                           ctx->stream));
-    HIPCHK(hipStreamSynchronize(ctx->stream));
+    HIPCHK(hm_sync(ctx->stream));
     return HM_OK;
 }
 
@@ -395,7 +422,7 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
     ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
     unsigned long long* up = ctx->host_state + ST_COUNT;
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hm_sync(s));
     up[0] = 0;
     up[1] = 0;
     up[2] = ~0ull;
@@ -448,7 +475,7 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
         hm_launch_scan(s, c, m, partial, S, tot + 1);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hm_sync(s));
         const uint64_t u = down[0];
         uint64_t* cout = (cin == cnt0) ? cnt1 : cnt0;
         hm_launch_rle_scatter(s, cur, m, sh, flag, idx, S, c, oth, end);
@@ -579,6 +606,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
      * record is an API call, and small calls (stream batches) are bound by
      * the host's issue rate */
     const bool timing = n >= (1ll << 24);
+    /* keys per aggregation work item: HM_TA, halved (down to 16K) until the
+     * call has >= 512 items' worth of points -- a 1e7-point call otherwise
+     * runs ~40 items on 256 CUs */
+    uint32_t ta = HM_TA;
+    while (ta > 16384 && (uint64_t)n < (uint64_t)ta * 512) ta >>= 1;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
     ctx->last_levels = L;
 
@@ -675,7 +707,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             /* region sizes: a sampled digit histogram with a generous margin */
             /* ~256K samples (1M samples above 2^28 points took 90 us per 1e9-point
              * count; the regions' 8-sigma margins scale with sqrt(stride)) */
-            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> ctx->sample_log2);
+            /* (2^16 samples below 2^24 points, where the sample pass's ~30 us
+             * is a batch's cost; the regions' slack scales with the stride) */
+            const int slog = n < (1ll << 24) ? std::min(ctx->sample_log2, 16) : ctx->sample_log2;
+            const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> slog);
             HIPCHK(hipMemsetAsync(hist, 0, HM_D1 * 4, s));
             uint32_t* hot_counts = nullptr;
             uint32_t* hot_tiles = nullptr;
@@ -765,7 +800,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             ba.fill = fill;
             ba.rbase = rbase;
             ba.smask = smask;
-            ba.item_keys = (L == 1) ? HM_TA : HM_TN;
+            ba.item_keys = (L == 1) ? ta : HM_TN;
             ba.sparse_max = (L == 1) ? HM_SP_MAX : 0u;
             ba.total = tot;
             if (hot_on) {   /* hot parents all zero when no tile turned out hot */
@@ -884,7 +919,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 l1_reruns++;
                 HIPCHK(hipMemcpyAsync(hc, fill, FS * 4, hipMemcpyDeviceToHost, s));
                 if (ctx->debug_l1) HIPCHK(hipMemcpyAsync(hb, rcap, FS * 4, hipMemcpyDeviceToHost, s));
-                HIPCHK(hipStreamSynchronize(s));
+                HIPCHK(hm_sync(s));
                 if (ctx->debug_l1) {
                     /* HM_DEBUG_L1=1: the overflowing regions, and the sample behind them */
                     for (int i = 0; i < FS; i++)
@@ -947,7 +982,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 ENSURE(B_DESC0 + 0, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
                 b.desc = desc;
                 if (L > 1) ENSURE(B_SEG, ((uint64_t)V.items + 1) * 16 * sizeof(uint32_t), seg1);
-                hm_launch_items(s, b, runs_cur, V.items, (L == 1) ? HM_TA : HM_TN, desc, L > 1 ? seg1 : nullptr);
+                hm_launch_items(s, b, runs_cur, V.items, (L == 1) ? ta : HM_TN, desc, L > 1 ? seg1 : nullptr);
                 HIPCHK(hipGetLastError());
             }
             keys_cur = kout;
@@ -1015,7 +1050,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ra.nruns = nruns;
         ra.runs = runs_sh;
         ra.parent_item_begin = parent_item_begin;
-        ra.item_keys = (l == L - 1) ? HM_TA : HM_TN;
+        ra.item_keys = (l == L - 1) ? ta : HM_TN;
         ra.sparse_max = (l == L - 1) ? HM_SP_MAX : 0u;
         uint64_t *partial, *tot;
         ENSURE(B_SHOFF, (V.nchildren << sb) * sizeof(uint32_t), ra.shoff);
@@ -1051,7 +1086,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         HIPCHK(hipGetLastError());
         unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
         HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hm_sync(s));
         const uint64_t nflat = down[0];
         ra.nflat = nflat;
         uint2* flat;
@@ -1147,7 +1182,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             uint4* desc;
             ENSURE(B_DESC0 + l, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
             b.desc = desc;
-            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? HM_TA : HM_TN, desc, nullptr);
+            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? ta : HM_TN, desc, nullptr);
             HIPCHK(hipGetLastError());
         }
 
@@ -1415,7 +1450,7 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     HIPCHK(hipGetLastError());
     std::vector<uint64_t> h(m + 2);
     HIPCHK(hipMemcpyAsync(h.data(), off, (m + 2) * 8, hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hm_sync(s));
     for (int r = 0; r < nranks; r++)
         send_counts[r] = (int64_t)(h[(uint64_t)(r + 1) * blocks] - h[(uint64_t)r * blocks]);
     return (count_bytes == 4 && h[m + 1]) ? HM_E_WIDE : HM_OK;
@@ -1531,7 +1566,7 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in,
         hm_launch_mb_merge(s, a);
         HIPCHK(hipGetLastError());
         HIPCHK(hipMemcpyAsync(down, st, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-        HIPCHK(hipStreamSynchronize(s));
+        HIPCHK(hm_sync(s));
         if (!down[1]) {
             *n_out = (int64_t)down[0];
             return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
@@ -1563,7 +1598,7 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in,
     hm_launch_table_extract(s, t, keys_out, counts_out, (uint64_t)capacity, t.state + HMS_ST_CURSOR);
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(down, t.state, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hm_sync(s));
     if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;   /* cannot happen: load factor <= 1/2 */
     *n_out = (int64_t)down[HMS_ST_CURSOR];
     return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
@@ -1627,6 +1662,7 @@ struct hm_stream {
     HmsBuckets bk{};                      /* (group, period) buckets */
     uint32_t *bflag = nullptr, *blist = nullptr, *bloc = nullptr; /* per bucket: last batch, list, run */
     uint32_t epoch = 0;
+    uint32_t last_nparts = 1;             /* buckets of the previous batch (1: count the next one speculatively) */
     /* the cell log: llen cells of lcap; alt: the compaction target */
     uint64_t *lkeys = nullptr, *lcounts = nullptr, *akeys = nullptr, *acounts = nullptr;
     uint64_t lcap = 0, llen = 0;
@@ -1643,7 +1679,7 @@ static int stream_sync_state(hm_stream* s)
 {
     HIPCHK(hipMemcpyAsync(s->hstate, s->state, HMS_ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost,
                           s->ctx->stream));
-    HIPCHK(hipStreamSynchronize(s->ctx->stream));
+    HIPCHK(hm_sync(s->ctx->stream));
     s->nbuckets = s->hstate[HMS_ST_BUCKETS];
     return HM_OK;
 }
@@ -1714,7 +1750,7 @@ static int stream_room(hm_stream* s, uint64_t need)
         HIPCHK(hipMemcpyAsync(k, s->lkeys, s->llen * 8, hipMemcpyDeviceToDevice, q));
         HIPCHK(hipMemcpyAsync(c, s->lcounts, s->llen * 8, hipMemcpyDeviceToDevice, q));
     }
-    HIPCHK(hipStreamSynchronize(q));
+    HIPCHK(hm_sync(q));
     for (uint64_t* p : {s->lkeys, s->lcounts, s->akeys, s->acounts})
         if (p) (void)hipFree(p);
     s->lkeys = k;
@@ -1731,24 +1767,28 @@ static void stream_appended(hm_stream* s, uint64_t m)
     s->llen += m;
 }
 
-/* a batch of one bucket: hm_count's cells written at the log's tail, keyed
- * under that bucket */
-static int stream_fold_one(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
-                           uint32_t bucket)
+/* a batch of one bucket, part 1: hm_count's cells written at the log's tail
+ * (not yet part of the log) */
+static int stream_count_tail(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
+                             int64_t* m)
 {
-    int64_t m = 0;
     int st;
+    *m = 0;
     if ((st = stream_room(s, 2 * (uint64_t)n + 1024))) return st; /* typical batches: fewer cells than 2 per point */
     for (;;) {
         int64_t nx = 0;
         st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, s->lkeys + s->llen, s->lcounts + s->llen,
-                      (int64_t)(s->lcap - s->llen), &m, nullptr, 0, &nx);
+                      (int64_t)(s->lcap - s->llen), m, nullptr, 0, &nx);
         /* the log's keys hold tiles inside [0, 2^z)^2 only */
         if (nx > 0) return HM_E_EXOTIC;
-        if (st != HM_E_CAPACITY) break;
-        if ((st = stream_room(s, (uint64_t)(m + m / 4 + 1024)))) return st;
+        if (st != HM_E_CAPACITY) return st;
+        if ((st = stream_room(s, (uint64_t)(*m + *m / 4 + 1024)))) return st;
     }
-    if (st) return st;
+}
+
+/* part 2: the tail's m cells keyed under the bucket and appended */
+static int stream_take_tail(hm_stream* s, int64_t m, uint32_t bucket)
+{
     hm_launch_stream_rekey(s->ctx->stream, s->lkeys + s->llen, (uint64_t)m, (uint64_t)bucket << s->cb);
     HIPCHK(hipGetLastError());
     stream_appended(s, (uint64_t)m);
@@ -1817,7 +1857,7 @@ static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon,
     HIPCHK(hipGetLastError());
     HIPCHK(hipMemcpyAsync(hb.data(), s->blist, nparts * 4, hipMemcpyDeviceToHost, q));
     HIPCHK(hipMemcpyAsync(start.data() + nparts + 2, a.cursor, (size_t)(nparts + 1) * 8, hipMemcpyDeviceToHost, q));
-    HIPCHK(hipStreamSynchronize(q));
+    HIPCHK(hm_sync(q));
     uint64_t kept = 0;
     for (uint32_t j = 0; j < nparts; j++) {
         start[j] = kept;
@@ -1963,8 +2003,18 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
     hm_launch_stream_buckets(q, a);
     hm_launch_stream_collect(q, s->bflag, s->bk.mask + 1, s->epoch, s->blist, s->state);
     HIPCHK(hipGetLastError());
-    if ((st = stream_sync_state(s))) return st;
+    HIPCHK(hipMemcpyAsync(s->hstate, s->state, HMS_ST_COUNT * sizeof(unsigned long long), hipMemcpyDeviceToHost, q));
+    /* the usual batch is one bucket: count it right away (into the log's
+     * tail); the bucket pass's state arrives with the count's first
+     * read-back.  Any other outcome drops the tail and takes the paths below
+     * (which count again, so errors and their order are the same). */
+    int64_t m1 = 0;
+    const bool spec = s->last_nparts <= 1;   /* the previous batch was one bucket */
+    const int st1 = spec ? stream_count_tail(s, lat, lon, keep, n, &m1) : HM_OK;
+    HIPCHK(hm_sync(q));
+    s->nbuckets = s->hstate[HMS_ST_BUCKETS];
     const uint32_t nparts = (uint32_t)s->hstate[HMS_ST_NLIST];
+    s->last_nparts = nparts;
     const uint32_t lo = (uint32_t)s->hstate[HMS_ST_BMM];
     const unsigned long long e = s->hstate[HMS_ST_ERR];
     if (e != ~0ull) {
@@ -1973,8 +2023,11 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
         return ctx->last_err_kind;
     }
     if (s->hstate[HMS_ST_BFULL]) return HM_E_CAPACITY;   /* max_buckets (group, hour) pairs */
-    if (nparts <= 1) /* one bucket (the usual time-ordered batch), or nothing kept */
-        return stream_fold_one(s, lat, lon, keep, n, nparts ? lo : 0u);
+    if (nparts <= 1) { /* one bucket (the usual time-ordered batch), or nothing kept */
+        if (!spec && (st = stream_count_tail(s, lat, lon, keep, n, &m1))) return st;
+        if (spec && st1) return st1;
+        return stream_take_tail(s, m1, nparts ? lo : 0u);
+    }
     if (nparts <= HMS_MAX_PARTS) return stream_fold_parts(s, lat, lon, keep, n, nparts);
     return stream_fold_grouped(s, lat, lon, keep, n);
 }

@@ -1739,18 +1739,22 @@ __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_reduce(const uint64_t*
     }
 }
 
-/* single block: exclusive scan of up to 4096 partials; total -> *total */
-__global__ __launch_bounds__(1024) void k_scan_partials(uint64_t* partial, uint32_t nb, uint64_t* total)
+/* single block: exclusive scan of up to 1024 * PER values v -> out (may be
+ * v itself: a thread reads its PER values before writing them); total ->
+ * *total.  PER = 4: the partials of a multi-block scan; PER = 16: a whole
+ * scan of <= 16384 values in one dispatch (small calls are dispatch-bound). */
+template <int PER>
+__global__ __launch_bounds__(1024) void k_scan_one(const uint64_t* v, uint32_t n, uint64_t* out, uint64_t* total)
 {
     __shared__ uint64_t ws[17];
     const int tid = threadIdx.x;
-    uint64_t v[4];
+    uint64_t x[PER];
     uint64_t s = 0;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint32_t i = tid * 4 + q;
-        v[q] = i < nb ? partial[i] : 0;
-        s += v[q];
+    for (int q = 0; q < PER; q++) {
+        const uint32_t i = tid * PER + q;
+        x[q] = i < n ? v[i] : 0;
+        s += x[q];
     }
     const uint64_t inc = hm_wave_incl_scan64(s);
     const int w = tid >> 6;
@@ -1768,10 +1772,10 @@ __global__ __launch_bounds__(1024) void k_scan_partials(uint64_t* partial, uint3
     __syncthreads();
     uint64_t off = ws[w] + inc - s;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const uint32_t i = tid * 4 + q;
-        if (i < nb) partial[i] = off;
-        off += v[q];
+    for (int q = 0; q < PER; q++) {
+        const uint32_t i = tid * PER + q;
+        if (i < n) out[i] = off;
+        off += x[q];
     }
     if (tid == 0) *total = ws[16];
 }
@@ -2713,10 +2717,14 @@ void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* part
 {
     uint64_t chunk = HM_SCAN_ITEMS;
     while ((n + chunk - 1) / chunk > HM_SCAN_MAXB) chunk += HM_SCAN_ITEMS;
+    if (n <= 16 * 1024) {
+        hipLaunchKernelGGL(k_scan_one<16>, dim3(1), dim3(1024), 0, s, v, (uint32_t)n, out, total);
+        return;
+    }
     const uint32_t nb = (uint32_t)((n + chunk - 1) / chunk);
     const uint32_t g = nb ? nb : 1;
     hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial);
-    hipLaunchKernelGGL(k_scan_partials, dim3(1), dim3(1024), 0, s, partial, g, total);
+    hipLaunchKernelGGL(k_scan_one<4>, dim3(1), dim3(1024), 0, s, partial, g, partial, total);
     hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out);
 }
 
