@@ -597,8 +597,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     }
     /* key bits after level l: 2*(Z - zs[l]); must fit u32 (level 1 output) */
     if (2 * (Z - zs[0]) > 32) return HM_E_ARG;
-    int st = reset_state(ctx);
-    if (st) return st;
+    int st = HM_OK;
+    /* the call's state words and level 1's zeroed buffers: one fill dispatch,
+     * launched before level 1's sampling */
+    HmFill f1;
+    memset(&f1, 0, sizeof(f1));
+    hm_fill_add(f1, ctx->state + 1, 0, (ST_COUNT - 1) * sizeof(unsigned long long));
+    hm_fill_add(f1, ctx->state + ST_ERR, 0xFF, sizeof(unsigned long long));
+    static_assert(ST_ERR == 0, "error word first");
 
     hipEvent_t* ev = ctx->ev;
     int nev = 0;
@@ -711,7 +717,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
              * is a batch's cost; the regions' slack scales with the stride) */
             const int slog = n < (1ll << 24) ? std::min(ctx->sample_log2, 16) : ctx->sample_log2;
             const uint64_t stride = std::max<uint64_t>(1, (uint64_t)n >> slog);
-            HIPCHK(hipMemsetAsync(hist, 0, HM_D1 * 4, s));
+            hm_fill_add(f1, hist, 0, HM_D1 * 4);
+            hm_fill_add(f1, fill, 0, FS * 4);
             uint32_t* hot_counts = nullptr;
             uint32_t* hot_tiles = nullptr;
             uint32_t* hot_hash = nullptr;
@@ -722,15 +729,17 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 ENSURE(B_HOT, (HM_MAX_HOT + HM_HOT_SLOTS + 2 * HM_HOT_CAND + 1) * 4, hot_tiles);
                 ENSURE(B_HOT_PARENT, HM_MAX_F1, hot_parent);
                 hot_hash = hot_tiles + HM_MAX_HOT;
-                HIPCHK(hipMemsetAsync(hot_counts, 0, 4ull << (2 * zb), s));
-                HIPCHK(hipMemsetAsync(hot_hash + HM_HOT_SLOTS + 2 * HM_HOT_CAND, 0, 4, s));   /* candidates */
-                HIPCHK(hipMemsetAsync(hot_parent, 0, HM_MAX_F1, s));
+                hm_fill_add(f1, hot_counts, 0, 4ull << (2 * zb));
+                hm_fill_add(f1, hot_hash + HM_HOT_SLOTS + 2 * HM_HOT_CAND, 0, 4);   /* candidates */
+                hm_fill_add(f1, hot_parent, 0, HM_MAX_F1);
                 a.hot_z = zb;
                 a.hot_hash = hot_hash;
                 a.hot_n = hot_n;
             } else {
                 a.hot_z = -1;
             }
+            hm_launch_fill(s, f1);
+            f1.k = 0;
             if (n > 0) hm_launch_sample_digits(s, a, stride, hist, hot_counts);
             HIPCHK(hipGetLastError());
             if (hot_on) {
@@ -843,11 +852,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                     ENSURE(slot_k ? B_KEYS_A : B_KEYS_B, (total_cap + 8) * 2, kh);
                     a.keys_hot = kh;
                 }
-                HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
-                /* ST_XCOUNT .. ST_OVERFLOW (XCOUNT, SLOW, REDO, REDO_OUT, OVERFLOW;
-                 * CURSOR, NSLOTS, XCURSOR are still 0 here) in one memset */
-                static_assert(ST_XCOUNT == 1 && ST_OVERFLOW == 8 && ST_NHOT > ST_OVERFLOW, "level-1 words");
-                HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, 8 * 8, s));
+                if (attempt > 0) {
+                    /* (the first attempt's are zero from the call's fill) */
+                    HIPCHK(hipMemsetAsync(fill, 0, FS * 4, s));
+                    /* ST_XCOUNT .. ST_OVERFLOW (XCOUNT, SLOW, REDO, REDO_OUT, OVERFLOW;
+                     * CURSOR, NSLOTS, XCURSOR are still 0 here) in one memset */
+                    static_assert(ST_XCOUNT == 1 && ST_OVERFLOW == 8 && ST_NHOT > ST_OVERFLOW, "level-1 words");
+                    HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, 8 * 8, s));
+                }
                 if (timing) HIPCHK(hipEventRecord(ev[0], s));
                 hm_launch_part1(s, a, tiles_in, V.out16, from_tiles ? 1 : 0);
                 HIPCHK(hipGetLastError());
@@ -1405,12 +1417,13 @@ extern "C" int64_t hm_dense_grid_size(int dense_zmax)
 }
 
 extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks,
-                              int delta, int dense_zmax, uint64_t* grid, uint64_t* keys_out, void* counts_out,
-                              int count_bytes, int64_t* send_counts)
+                              int delta, int dense_zmax, uint64_t* grid, void* keys_out, void* counts_out,
+                              int layout, int64_t* send_counts)
 {
+    const bool rec = layout == HM_CELLS_REC10;
     if (!ctx || n < 0 || nranks < 1 || nranks > 64 || delta < 0 || delta > 28 || dense_zmax > 14 ||
-        (count_bytes != 4 && count_bytes != 8) || (dense_zmax >= 0 && !grid) || !send_counts ||
-        (n > 0 && (!keys || !counts || !keys_out || !counts_out)))
+        (layout != HM_CELLS_U32 && layout != HM_CELLS_U64 && !rec) || (dense_zmax >= 0 && !grid) ||
+        !send_counts || (n > 0 && (!keys || !counts || !keys_out || (!rec && !counts_out))))
         return HM_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -1436,13 +1449,18 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     a.dense_zmax = dense_zmax;
     a.grid = grid;
     a.block_off = off;
-    a.keys_out = keys_out;
-    if (count_bytes == 4) {
-        a.counts_out32 = (uint32_t*)counts_out;
+    if (layout == HM_CELLS_U64) {
+        a.keys_out = (uint64_t*)keys_out;
+        a.counts_out = (uint64_t*)counts_out;
+    } else {
+        if (rec) {
+            a.rec_out = (uint16_t*)keys_out;
+        } else {
+            a.keys_out = (uint64_t*)keys_out;
+            a.counts_out32 = (uint32_t*)counts_out;
+        }
         a.wide = (unsigned long long*)(off + m + 1);
         HIPCHK(hipMemsetAsync(a.wide, 0, 8, s));
-    } else {
-        a.counts_out = (uint64_t*)counts_out;
     }
     hm_launch_cells_route(s, a, false);
     hm_launch_scan(s, a.block_cnt, m, partial, off, off + m);
@@ -1453,16 +1471,19 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
     HIPCHK(hm_sync(s));
     for (int r = 0; r < nranks; r++)
         send_counts[r] = (int64_t)(h[(uint64_t)(r + 1) * blocks] - h[(uint64_t)r * blocks]);
-    return (count_bytes == 4 && h[m + 1]) ? HM_E_WIDE : HM_OK;
+    return (layout != HM_CELLS_U64 && h[m + 1]) ? HM_E_WIDE : HM_OK;
 }
 
-static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in, int count_bytes, int64_t n,
+static int cells_merge(hm_ctx* ctx, const void* keys_in, const void* counts_in, int layout, int64_t n,
                        const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
                        int64_t* n_out)
 {
-    const uint64_t* counts = count_bytes == 8 ? (const uint64_t*)counts_in : nullptr;
-    const uint32_t* counts32 = count_bytes == 4 ? (const uint32_t*)counts_in : nullptr;
-    if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && !keys) || (n > 0 && !counts && !counts32) ||
+    const uint16_t* recs = layout == HM_CELLS_REC10 ? (const uint16_t*)keys_in : nullptr;
+    const uint64_t* keys = recs ? nullptr : (const uint64_t*)keys_in;
+    const uint64_t* counts = layout == HM_CELLS_U64 ? (const uint64_t*)counts_in : nullptr;
+    const uint32_t* counts32 = layout == HM_CELLS_U32 ? (const uint32_t*)counts_in : nullptr;
+    if (((uintptr_t)recs & 3) != 0) return HM_E_ARG;   /* records: 4-byte aligned (the merge loads words) */
+    if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && !keys_in) || (n > 0 && !recs && !counts && !counts32) ||
         (capacity > 0 && (!keys_out || !counts_out)) || nruns < 0 || (nruns > 0 && !runs))
         return HM_E_ARG;
     int64_t sum = 0;
@@ -1495,6 +1516,7 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in,
         p1.kin = keys;
         p1.cin = counts;
         p1.cin32 = counts32;
+        p1.rin = recs;
         p1.n = (uint64_t)n;
         p1.nseg = 1;
         p1.C = chunks((uint64_t)n, 65536, 512);
@@ -1525,6 +1547,7 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in,
             p2.kin = pk;
             p2.cin = pc;
             p2.cin32 = nullptr;
+            p2.rin = nullptr;
             p2.segoff = off1;
             p2.segstride = p1.C;
             p2.nseg = 1u << b1;
@@ -1582,8 +1605,8 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in,
     t.mask = cap - 1;
     HIPCHK(hipMemsetAsync(t.state, 0, 8 * sizeof(unsigned long long), s));
     hm_launch_stream_init(s, t);
-    if (counts32) {
-        /* u32 input counts: the partition pass's u64 copy, in partition order */
+    if (!counts) {
+        /* u32 counts or records: the partition pass's u64 copy, in partition order */
         hm_launch_cells_merge(s, pk_all, pc_all, (uint64_t)n, t);
     } else if (runs) {
         /* runs of distinct keys: no two threads of a launch insert one key */
@@ -1604,19 +1627,24 @@ static int cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts_in,
     return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
 }
 
-extern "C" int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes, int64_t n,
-                              uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+static bool cells_layout_ok(int layout)
 {
-    if (count_bytes != 4 && count_bytes != 8) return HM_E_ARG;
-    return cells_merge(ctx, keys, counts, count_bytes, n, nullptr, 0, keys_out, counts_out, capacity, n_out);
+    return layout == HM_CELLS_U64 || layout == HM_CELLS_U32 || layout == HM_CELLS_REC10;
 }
 
-extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes,
-                                   int64_t n, const int64_t* runs, int nruns, uint64_t* keys_out,
-                                   uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+extern "C" int hm_cells_merge(hm_ctx* ctx, const void* keys, const void* counts, int layout, int64_t n,
+                              uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
 {
-    if (count_bytes != 4 && count_bytes != 8) return HM_E_ARG;
-    return cells_merge(ctx, keys, counts, count_bytes, n, runs, nruns, keys_out, counts_out, capacity, n_out);
+    if (!cells_layout_ok(layout)) return HM_E_ARG;
+    return cells_merge(ctx, keys, counts, layout, n, nullptr, 0, keys_out, counts_out, capacity, n_out);
+}
+
+extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const void* keys, const void* counts, int layout, int64_t n,
+                                   const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out,
+                                   int64_t capacity, int64_t* n_out)
+{
+    if (!cells_layout_ok(layout)) return HM_E_ARG;
+    return cells_merge(ctx, keys, counts, layout, n, runs, nruns, keys_out, counts_out, capacity, n_out);
 }
 
 extern "C" int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out,
@@ -1724,7 +1752,7 @@ static int stream_compact(hm_stream* s)
     int st;
     if (!s->akeys && (st = stream_alloc2(s->lcap, &s->akeys, &s->acounts))) return st;
     int64_t m = 0;
-    if ((st = cells_merge(s->ctx, s->lkeys, s->lcounts, 8, (int64_t)s->llen, nullptr, 0, s->akeys, s->acounts,
+    if ((st = cells_merge(s->ctx, s->lkeys, s->lcounts, HM_CELLS_U64, (int64_t)s->llen, nullptr, 0, s->akeys, s->acounts,
                           (int64_t)s->lcap, &m)))
         return st;
     std::swap(s->lkeys, s->akeys);
@@ -2091,7 +2119,7 @@ extern "C" int hm_stream_rollup(hm_stream* s, int span, int merge_groups, int64_
     /* equal label cells summed */
     if ((st = stream_buf(s, s->mk, m * 8)) || (st = stream_buf(s, s->mc, m * 8))) return st;
     int64_t nd = 0;
-    if ((st = cells_merge(ctx, (const uint64_t*)s->rk.p, (const uint64_t*)s->rc.p, 8, (int64_t)m, nullptr, 0,
+    if ((st = cells_merge(ctx, (const uint64_t*)s->rk.p, (const uint64_t*)s->rc.p, HM_CELLS_U64, (int64_t)m, nullptr, 0,
                           (uint64_t*)s->mk.p, (uint64_t*)s->mc.p, (int64_t)m, &nd)))
         return st;
     *n_out = nd;

@@ -2491,6 +2491,46 @@ __global__ __launch_bounds__(64 * HM_POOLW_WAVES) void k_pool_waves(HmPoolArgs a
 /* host launchers                                                            */
 /* ------------------------------------------------------------------------ */
 
+__global__ __launch_bounds__(256) void k_fill(HmFill f)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256, t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    for (int e = 0; e < f.k; e++) {
+        const uint32_t w = f.word[e];
+        if (f.unit[e] == 16) {
+            uint4* p = (uint4*)f.p[e];
+            const uint4 v = make_uint4(w, w, w, w);
+            for (uint64_t i = t; i < f.bytes[e] / 16; i += stride) p[i] = v;
+        } else if (f.unit[e] == 4) {
+            uint32_t* p = (uint32_t*)f.p[e];
+            for (uint64_t i = t; i < f.bytes[e] / 4; i += stride) p[i] = w;
+        } else {
+            uint8_t* p = (uint8_t*)f.p[e];
+            for (uint64_t i = t; i < f.bytes[e]; i += stride) p[i] = (uint8_t)w;
+        }
+    }
+}
+
+void hm_fill_add(HmFill& f, void* p, int value, uint64_t bytes)
+{
+    if (!bytes) return;
+    const uint32_t b = (uint32_t)value & 0xFFu;
+    const uintptr_t a = (uintptr_t)p;
+    f.p[f.k] = p;
+    f.bytes[f.k] = bytes;
+    f.word[f.k] = b * 0x01010101u;
+    f.unit[f.k] = (a % 16 == 0 && bytes % 16 == 0) ? 16u : (a % 4 == 0 && bytes % 4 == 0) ? 4u : 1u;
+    f.k++;
+}
+
+void hm_launch_fill(hipStream_t s, const HmFill& f)
+{
+    if (!f.k) return;
+    uint64_t most = 0;
+    for (int e = 0; e < f.k; e++) most = std::max<uint64_t>(most, f.bytes[e] / f.unit[e]);
+    const uint64_t blocks = std::min<uint64_t>(2048, std::max<uint64_t>(1, (most + 255) / 256));
+    hipLaunchKernelGGL(k_fill, dim3((unsigned)blocks), dim3(256), 0, s, f);
+}
+
 void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
                        int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow)
 {

@@ -380,6 +380,19 @@ struct HmPoolArgs {
     HmOut out;
 };
 
+/* several memsets in one dispatch (a small call is launch-bound: each
+ * hipMemsetAsync is a dispatch of its own) */
+#define HM_FILL_MAX 10
+struct HmFill {
+    void* p[HM_FILL_MAX];
+    uint64_t bytes[HM_FILL_MAX];
+    uint32_t word[HM_FILL_MAX];    /* the byte value replicated 4 times */
+    uint32_t unit[HM_FILL_MAX];    /* 16, 4 or 1: store width (alignment of p and bytes) */
+    int k;
+};
+void hm_fill_add(HmFill& f, void* p, int value, uint64_t bytes);
+void hm_launch_fill(hipStream_t s, const HmFill& f);
+
 void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int64_t n, int zoom, int64_t* row,
                        int64_t* col, uint8_t* status, unsigned long long* err_word, unsigned long long* slow);
 /* mode: 0 fast path + redo list, 1 tile input (exact row/col given), 2 fused exact (fallback) */
@@ -585,8 +598,9 @@ struct HmRouteArgs {
     const uint64_t* block_off; /* [nranks * blocks] exclusive scan of block_cnt */
     uint64_t* keys_out;
     uint64_t* counts_out;      /* u64 counts, or */
-    uint32_t* counts_out32;    /* u32 counts (the exchange's 12 B/cell) */
-    unsigned long long* wide;  /* counts_out32: set when a sent count needs 64 bits */
+    uint32_t* counts_out32;    /* u32 counts, or */
+    uint16_t* rec_out;         /* 10-B records (48-bit key, u32 count; hm_rec_put) */
+    unsigned long long* wide;  /* u32 counts: set when a sent count needs 64 bits */
 };
 unsigned hm_route_blocks(uint64_t n);
 /* bucketed merge of (key, count) cells: hash-partition into 2^lb buckets
@@ -619,6 +633,7 @@ struct HmMbPass {
     const uint64_t* kin;
     const uint64_t* cin;
     const uint32_t* cin32;      /* u32 input counts instead of cin (pass 1 of a merge of received cells) */
+    const uint16_t* rin;        /* or 10-B records instead of kin/cin (hm_rec_put) */
     uint64_t n;
     const uint64_t* segoff;
     uint32_t segstride, nseg, C;

@@ -53,37 +53,51 @@ class DeviceOps:
             _lib.raise_for(rc)
 
     def route(self, keys, counts, ws, dense_zmax, narrow=False):
-        """-> (dense grid, keys and counts grouped by owner, group sizes,
-        wide).  narrow: counts travel as int32 (12 B per cell) unless one
-        needs 64 bits -- then wide is True and the counts returned are of no
-        use (route again with narrow=False)."""
+        """-> (dense grid, parts, group sizes, wide).  parts: the cells grouped
+        by owner as [(tensor, elements per cell)]: narrow -> one uint8 tensor
+        of 10-byte records (HM_CELLS_REC10: 48-bit key, u32 count), else int64
+        keys and int64 counts.  wide (narrow only): a count needs 64 bits and
+        the parts are of no use (route again with narrow=False)."""
         from . import _lib
 
         n = keys.numel()
         gsz = int(self.L.hm_dense_grid_size(dense_zmax))
         grid = torch.empty(max(gsz, 1), dtype=torch.int64, device=keys.device)
-        ko = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
-        co = torch.empty(max(n, 1), dtype=torch.int32 if narrow else torch.int64, device=keys.device)
         send = (ctypes.c_int64 * ws)()
-        rc = self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax,
-                                   self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko), self._p(co),
-                                   4 if narrow else 8, send)
+        if narrow:
+            rec = torch.empty(max(n, 1) * 5, dtype=torch.int16, device=keys.device)
+            rc = self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax,
+                                       self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(rec),
+                                       ctypes.c_void_p(0), _lib.HM_CELLS_REC10, send)
+        else:
+            ko = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
+            co = torch.empty_like(ko)
+            rc = self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax,
+                                       self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko), self._p(co),
+                                       _lib.HM_CELLS_U64, send)
         wide = rc == _lib.HM_E_WIDE
         if not wide:
             self._check(rc)
         sent = list(send)
         m = sum(sent)
-        return grid[:gsz], ko[:m], co[:m], sent, wide
+        parts = [(rec[:5 * m].view(torch.uint8), 10)] if narrow else [(ko[:m], 1), (co[:m], 1)]
+        return grid[:gsz], parts, sent, wide
 
-    def merge(self, keys, counts, runs=None, out=None):
-        """Sum equal keys (counts int32 or int64; the sums are int64); runs
-        (list of sizes): consecutive runs of distinct keys (one sending rank's
-        cells each), merged without count atomics.  out: (keys, counts)
-        tensors to write into (their length is the capacity; MemoryError if
-        the merged cells do not fit)."""
+    def merge(self, keys, counts=None, runs=None, out=None):
+        """Sum equal keys.  keys int64 with counts int32 or int64, or (counts
+        None) keys = 10-byte records (HM_CELLS_REC10, uint8); the sums are
+        int64.  runs (list of sizes): consecutive runs of distinct keys (one
+        sending rank's cells each), merged without count atomics.  out: (keys,
+        counts) tensors to write into (their length is the capacity;
+        MemoryError if the merged cells do not fit)."""
         from . import _lib
 
-        n = keys.numel()
+        if counts is None:
+            layout, n = _lib.HM_CELLS_REC10, keys.numel() * keys.element_size() // 10
+        elif counts.element_size() in (4, 8):
+            layout, n = (_lib.HM_CELLS_U32 if counts.element_size() == 4 else _lib.HM_CELLS_U64), keys.numel()
+        else:
+            raise TypeError("merge: counts must be int32 or int64")
         if out is not None:
             ko, co = out
             cap = ko.numel()
@@ -92,15 +106,12 @@ class DeviceOps:
             ko = torch.empty(cap, dtype=torch.int64, device=keys.device)
             co = torch.empty_like(ko)
         nout = ctypes.c_int64(0)
-        cb = counts.element_size()
-        if cb not in (4, 8):
-            raise TypeError("merge: counts must be int32 or int64")
         if runs is not None:
             ra = (ctypes.c_int64 * max(len(runs), 1))(*runs)
-            rc = self.L.hm_cells_merge_runs(self.ctx.ptr, self._p(keys), self._p(counts), cb, n, ra, len(runs),
+            rc = self.L.hm_cells_merge_runs(self.ctx.ptr, self._p(keys), self._p(counts), layout, n, ra, len(runs),
                                             self._p(ko), self._p(co), cap, ctypes.byref(nout))
         else:
-            rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), cb, n, self._p(ko),
+            rc = self.L.hm_cells_merge(self.ctx.ptr, self._p(keys), self._p(counts), layout, n, self._p(ko),
                                        self._p(co), cap, ctypes.byref(nout))
         if rc == _lib.HM_E_CAPACITY and out is not None:
             raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (nout.value, cap))
@@ -126,6 +137,24 @@ class DeviceOps:
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
         return ko[:nout.value], co[:nout.value]
+
+
+def pack_records(keys: torch.Tensor, counts: torch.Tensor) -> torch.Tensor:
+    """HM_CELLS_REC10 records (uint8, 10 per cell: five little-endian u16) of
+    HM_KEY keys (zooms <= 21) and counts < 2^32 -- the device's layout, for
+    the CPU stand-ins and tests."""
+    z, r, c = keys >> 58, (keys >> 29) & 0x1FFFFF, keys & 0x1FFFFF
+    p = (z << 42) | (r << 21) | c
+    w = torch.stack([p & 0xFFFF, (p >> 16) & 0xFFFF, (p >> 32) & 0xFFFF, counts & 0xFFFF, (counts >> 16) & 0xFFFF], 1)
+    return (((w + 32768) % 65536) - 32768).to(torch.int16).reshape(-1).view(torch.uint8)
+
+
+def unpack_records(rec: torch.Tensor):
+    """(int64 keys, int64 counts) of HM_CELLS_REC10 records."""
+    w = rec.contiguous().view(torch.int16).reshape(-1, 5).to(torch.int64) & 0xFFFF
+    p = w[:, 0] | (w[:, 1] << 16) | (w[:, 2] << 32)
+    keys = ((p >> 42) << 58) | (((p >> 21) & 0x1FFFFF) << 29) | (p & 0x1FFFFF)
+    return keys, w[:, 3] | (w[:, 4] << 16)
 
 
 def record_owner(cells: torch.Tensor, ws: int) -> torch.Tensor:
@@ -234,17 +263,18 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         ops = DeviceOps(buffers.keys.device.index or 0)
     keys = buffers.keys[:m]
     counts = buffers.counts[:m]
-    # counts travel as int32 (12 B per cell, not 16) unless some rank holds a
-    # cell count >= 2^32: every rank's flag rides on the group-size exchange,
-    # so all ranks agree before the keys/counts all-to-all
-    grid, sk, sc, sent, wide = ops.route(keys, counts, ws, dense_zmax, narrow=True)
+    # cells travel as 10-byte records (48-bit key, u32 count: one all-to-all,
+    # 10 B per cell, not 16) unless some rank holds a cell count >= 2^32:
+    # every rank's flag rides on the group-size exchange, so all ranks agree
+    # before the cells' all-to-all
+    grid, parts, sent, wide = ops.route(keys, counts, ws, dense_zmax, narrow=True)
     send = torch.tensor([[s, int(wide)] for s in sent], dtype=torch.int64, device=keys.device)
     recv = torch.empty_like(send)
     dist.all_to_all_single(recv, send)
     recv = recv.cpu()
     rl = recv[:, 0].tolist()
     if bool(recv[:, 1].any()):
-        grid, sk, sc, sent, _ = ops.route(keys, counts, ws, dense_zmax, narrow=False)
+        grid, parts, sent, _ = ops.route(keys, counts, ws, dense_zmax, narrow=False)
     if dense_zmax >= 0:
         dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
     # the owned cells are at most the received ones plus (rank 0) the dense
@@ -255,20 +285,21 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         buffers.keys = torch.empty(need, dtype=torch.int64, device=keys.device)
         buffers.counts = torch.empty_like(buffers.keys)
         buffers.capacity = need
-    nk = torch.empty(sum(rl), dtype=torch.int64, device=keys.device)
-    nc = torch.empty(sum(rl), dtype=sc.dtype, device=keys.device)
-    dist.all_to_all_single(nk, sk, rl, sent)
-    dist.all_to_all_single(nc, sc, rl, sent)
+    got = []
+    for t, w in parts:
+        r = torch.empty(sum(rl) * w, dtype=t.dtype, device=keys.device)
+        dist.all_to_all_single(r, t, [x * w for x in rl], [x * w for x in sent])
+        got.append(r)
     if isinstance(ops, DeviceOps):
-        # merged cells straight into the buffers (the sent copies are in nk)
-        uk, _ = ops.merge(nk, nc, rl, out=(buffers.keys, buffers.counts))
+        # merged cells straight into the buffers (the received copies are in got)
+        uk, _ = ops.merge(*got, runs=rl, out=(buffers.keys, buffers.counts))
         n = uk.numel()
         if dense_zmax >= 0 and rank == 0:
             dk, _ = ops.dense_cells(grid, dense_zmax, out=(buffers.keys[n:], buffers.counts[n:]))
             n += dk.numel()
     else:
         parts_k, parts_c = [], []
-        uk, uc = ops.merge(nk, nc, rl)
+        uk, uc = ops.merge(*got, runs=rl)
         parts_k.append(uk)
         parts_c.append(uc)
         if dense_zmax >= 0 and rank == 0:

@@ -81,7 +81,7 @@ extern "C" {
 #define HM_E_CAPACITY 17 /* output arrays too small; *n_out holds the size needed */
 #define HM_E_HIP 18      /* HIP runtime error (no device, launch failure) */
 #define HM_E_NOMEM 19    /* device allocation failed */
-#define HM_E_WIDE 20     /* hm_cells_route with count_bytes = 4: a count >= 2^32 (outputs complete otherwise) */
+#define HM_E_WIDE 20     /* hm_cells_route with u32 counts: a count >= 2^32 (outputs complete otherwise) */
 
 /* Output cell key of hm_count: zoom in bits 58..63, row in 29..57, col in 0..28.
  * Sorting keys sorts by (zoom, row, col). */
@@ -250,25 +250,35 @@ int hm_stream_destroy(hm_stream* s);
  *                    (a hash of the heatmap row key (zoom, row >> delta,
  *                    col >> delta), so each output row has one owner);
  *                    send_counts (host int64[nranks]) receives the group sizes
- *                    for an RCCL all-to-all.  nranks <= 64.  count_bytes 4:
- *                    counts_out is u32[n] (the exchange moves 12 B per cell,
- *                    not 16); a count >= 2^32 returns HM_E_WIDE after filling
- *                    everything else (the caller's ranks then agree to route
- *                    again with count_bytes 8: a rank's cells count fewer
- *                    points than it holds, so only > 2^32-point shards can).
- *   hm_cells_merge   sum the counts of equal keys over n received cells
- *                    (counts u32 or u64 per count_bytes; output u64);
+ *                    for an RCCL all-to-all.  nranks <= 64.  layout (below):
+ *                    HM_CELLS_REC10 packs each cell into keys_out as one
+ *                    10-byte record (counts_out unused), so ONE all-to-all of
+ *                    10 B per cell moves keys and counts (16 B in round 2);
+ *                    with u32 counts (REC10, U32) a count >= 2^32 returns
+ *                    HM_E_WIDE after filling everything else (the caller's
+ *                    ranks then agree to route again as HM_CELLS_U64: a rank's
+ *                    cells count fewer points than it holds, so only shards
+ *                    of >= 2^32 points can).
+ *   hm_cells_merge   sum the counts of equal keys over n received cells in
+ *                    `layout` (outputs: u64 keys, u64 counts);
  *   hm_cells_merge_runs  the same when the n cells are nruns consecutive runs
  *                    (host int64 sizes) each of distinct keys -- one rank's
  *                    cells each -- so only the key claim is atomic.
  *   hm_dense_cells   the non-empty cells of a (reduced) dense grid. */
 int64_t hm_dense_grid_size(int dense_zmax);
+/* exchanged cell layouts: keys u64[n] + counts u64[n]; keys u64[n] + counts
+ * u32[n]; or n records of 10 bytes in `keys` (five u16: the key as zoom << 42
+ * | row << 21 | col in 48 bits -- sparse zooms <= 21 -- and the u32 count;
+ * the array 4-byte aligned) */
+#define HM_CELLS_U64 8
+#define HM_CELLS_U32 4
+#define HM_CELLS_REC10 10
 int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks, int delta,
-                   int dense_zmax, uint64_t* grid, uint64_t* keys_out, void* counts_out, int count_bytes,
+                   int dense_zmax, uint64_t* grid, void* keys_out, void* counts_out, int layout,
                    int64_t* send_counts);
-int hm_cells_merge(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes, int64_t n,
-                   uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out);
-int hm_cells_merge_runs(hm_ctx* ctx, const uint64_t* keys, const void* counts, int count_bytes, int64_t n,
+int hm_cells_merge(hm_ctx* ctx, const void* keys, const void* counts, int layout, int64_t n, uint64_t* keys_out,
+                   uint64_t* counts_out, int64_t capacity, int64_t* n_out);
+int hm_cells_merge_runs(hm_ctx* ctx, const void* keys, const void* counts, int layout, int64_t n,
                         const int64_t* runs, int nruns, uint64_t* keys_out, uint64_t* counts_out, int64_t capacity,
                         int64_t* n_out);
 int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out, uint64_t* counts_out,

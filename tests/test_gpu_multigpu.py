@@ -29,12 +29,17 @@ def _cells(n, seed):
 def test_route_kernel_contract(gpu, ws, dz, narrow):
     keys, counts = _cells(300_000, ws)
     ops = multigpu.DeviceOps(0)
-    g, sk, sc, sent, wide = ops.route(keys.cuda(), counts.cuda(), ws, dz, narrow=narrow)
-    rg, rk, rc, rsent, rwide = TorchOps.route(keys, counts, ws, dz, narrow=narrow)
+    g, parts, sent, wide = ops.route(keys.cuda(), counts.cuda(), ws, dz, narrow=narrow)
+    rg, rparts, rsent, rwide = TorchOps.route(keys, counts, ws, dz, narrow=narrow)
     assert sent == rsent and not wide and not rwide
-    assert sc.dtype == (torch.int32 if narrow else torch.int64)
+    assert [w for _, w in parts] == ([10] if narrow else [1, 1])
     assert torch.equal(g.cpu(), rg)
-    sk, sc = sk.cpu(), sc.cpu()
+    if narrow:   # 10-byte records: the same bytes as the CPU packing, cell by cell
+        sk, sc = multigpu.unpack_records(parts[0][0].cpu())
+        rk, rc = multigpu.unpack_records(rparts[0][0])
+    else:
+        sk, sc = parts[0][0].cpu(), parts[1][0].cpu()
+        rk, rc = rparts[0][0], rparts[1][0]
     at = 0
     for n in sent:                         # same cells per owner (order inside a group is free)
         a = torch.argsort(sk[at:at + n])
@@ -58,11 +63,12 @@ def test_route_narrow_flags_wide_counts(gpu):
     i = int(torch.nonzero(z == 15)[0])
     counts[i] = (1 << 33) + 7
     ops = multigpu.DeviceOps(0)
-    _, _, _, sent, wide = ops.route(keys.cuda(), counts.cuda(), 4, 10, narrow=True)
+    _, _, sent, wide = ops.route(keys.cuda(), counts.cuda(), 4, 10, narrow=True)
     assert wide and sum(sent) == int((z > 10).sum())
-    _, sk, sc, sent2, wide2 = ops.route(keys.cuda(), counts.cuda(), 4, 10, narrow=False)
+    _, parts, sent2, wide2 = ops.route(keys.cuda(), counts.cuda(), 4, 10, narrow=False)
+    sk, sc = parts[0][0].cpu(), parts[1][0].cpu()
     assert not wide2 and sent2 == sent
-    assert int(sc.cpu()[sk.cpu() == keys[i]].item()) == (1 << 33) + 7
+    assert int(sc[sk == keys[i]].item()) == (1 << 33) + 7
 
 
 def test_merge_narrow_counts(gpu):
@@ -80,6 +86,29 @@ def test_merge_narrow_counts(gpu):
         o = torch.argsort(uk.cpu())
         assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
     assert int(ec.max()) >= 1 << 32
+
+
+@pytest.mark.parametrize("n", [1, 100, 5000, 3_000_000])
+def test_merge_records(gpu, n):
+    """hm_cells_merge(_runs) of HM_CELLS_REC10 records (48-bit keys of
+    zooms 11..21, u32 counts), sums past 2^32."""
+    g = torch.Generator().manual_seed(n)
+    z = torch.randint(11, 22, (n,), generator=g, dtype=torch.int64)
+    r = torch.randint(0, 1 << 21, (n,), generator=g, dtype=torch.int64) & ((1 << z) - 1)
+    c = torch.randint(0, 1 << 21, (n,), generator=g, dtype=torch.int64) & ((1 << z) - 1)
+    base = (z << 58) | (r << 29) | c
+    runs = [base, base[::2], base[::3]]
+    k = torch.cat(runs)
+    cnt = torch.randint(1, (1 << 32) - 1, (k.numel(),), generator=g, dtype=torch.int64)
+    rec = multigpu.pack_records(k, cnt)
+    kk, cc = multigpu.unpack_records(rec)
+    assert torch.equal(kk, k) and torch.equal(cc, cnt)
+    ek, ec = TorchOps.merge(k, cnt)
+    ops = multigpu.DeviceOps(0)
+    for rl in (None, [x.numel() for x in runs]):
+        uk, uc = ops.merge(rec.cuda(), None, rl)
+        o = torch.argsort(uk.cpu())
+        assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
 
 
 def test_merge_kernel_sums_duplicates(gpu):

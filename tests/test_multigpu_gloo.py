@@ -67,11 +67,13 @@ class TorchOps:
         own = multigpu.record_owner(rec, ws)
         o = torch.argsort(own, stable=True)
         wide = narrow and bool((sc >> 32).any())
-        sc = sc[o].to(torch.int32) if narrow else sc[o]
-        return grid, sk[o], sc, torch.bincount(own, minlength=ws).tolist(), wide
+        parts = [(multigpu.pack_records(sk[o], sc[o]), 10)] if narrow else [(sk[o], 1), (sc[o], 1)]
+        return grid, parts, torch.bincount(own, minlength=ws).tolist(), wide
 
     @staticmethod
-    def merge(keys, counts, runs=None):
+    def merge(keys, counts=None, runs=None):
+        if counts is None:                      # HM_CELLS_REC10 records
+            keys, counts = multigpu.unpack_records(keys)
         u, inv = torch.unique(keys, return_inverse=True)
         t = torch.zeros(u.numel(), dtype=torch.int64)
         t.index_add_(0, inv, counts.to(torch.int64))
@@ -155,3 +157,20 @@ def test_merge_two_ranks(kind, zmax, dense_zmax):
     xo = np.lexsort((xs[:, 2], xs[:, 1], xs[:, 0]))
     rxo = np.lexsort((rx[:, 2], rx[:, 1], rx[:, 0]))
     assert np.array_equal(xs[xo], rx[rxo])
+
+
+def test_records_round_trip():
+    """HM_CELLS_REC10 packing (the exchange's 10-byte cells): keys of zooms
+    0..21 at their extreme rows/columns and counts up to 2^32 - 1."""
+    g = torch.Generator().manual_seed(7)
+    z = torch.arange(22, dtype=torch.int64).repeat(50)
+    lim = (1 << z) - 1
+    r = torch.where(torch.arange(z.numel()) % 2 == 0, lim, torch.randint(0, 1 << 21, z.shape, generator=g) & lim)
+    c = torch.where(torch.arange(z.numel()) % 3 == 0, lim, torch.randint(0, 1 << 21, z.shape, generator=g) & lim)
+    keys = (z << 58) | (r << 29) | c
+    counts = torch.randint(1, 1 << 32, z.shape, generator=g, dtype=torch.int64)
+    counts[:3] = torch.tensor([1, (1 << 32) - 1, 1 << 31])
+    rec = multigpu.pack_records(keys, counts)
+    assert rec.dtype == torch.uint8 and rec.numel() == 10 * keys.numel()
+    k2, c2 = multigpu.unpack_records(rec)
+    assert torch.equal(k2, keys) and torch.equal(c2, counts)

@@ -1,0 +1,18 @@
+#!/bin/bash
+# multi-GPU exchange: device tests, merge phases, 1-rank RCCL rehearsal vs plain at 1.25e9
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+O="$R/gpurun_out/${1:-r03aa}"
+mkdir -p "$O"
+timeout -k 10 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_gpu_multigpu.py tests/test_gpu_chunked.py > "$O/pytest.log" 2>&1
+rc=$?; tail -3 "$O/pytest.log"; [ $rc -eq 0 ] || exit $rc
+echo "== merge phases"
+timeout -k 10 300 python -u tools/merge_profile.py > "$O/merge.log" 2>&1 || { tail -20 "$O/merge.log"; exit 1; }
+grep '^{' "$O/merge.log" | cut -c1-600
+echo "== plain / dist rehearsal"
+timeout -k 10 300 python -u bench.py --steps 5 --warmup 1 --points 1.25e9 --cpu-sample 0 > "$O/plain.log" 2>&1 || { tail -20 "$O/plain.log"; exit 1; }
+{ grep -h '^{"metric"' "$O/plain.log" || true; } | cut -c1-330
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 1 --steps 5 --warmup 1 --points 1.25e9 --cpu-sample 0 --force-dist > "$O/dist1.log" 2>&1 || { tail -30 "$O/dist1.log"; exit 1; }
+{ grep -h '^{"metric"' "$O/dist1.log" || true; } | cut -c1-330
+echo "== done"

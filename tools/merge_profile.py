@@ -46,8 +46,9 @@ def main():
         m, bufs = device.count_device(lat, lon, None, 0, 18, 0, buffers=bufs)
         t0 = mark("count", t0)
         keys, counts = bufs.keys[:m], bufs.counts[:m]
-        grid, sk, sc, sent, wide = ops.route(keys, counts, 1, 10, narrow=True)
+        grid, parts, sent, wide = ops.route(keys, counts, 1, 10, narrow=True)
         assert not wide
+        rec = parts[0][0]
         t0 = mark("route", t0)
         dist.reduce(grid, dst=0)
         t0 = mark("reduce", t0)
@@ -55,12 +56,10 @@ def main():
         recv = torch.empty_like(send)
         dist.all_to_all_single(recv, send)
         rl = recv.tolist()
-        nk = torch.empty(sum(rl), dtype=torch.int64, device="cuda")
-        nc = torch.empty(sum(rl), dtype=sc.dtype, device="cuda")
-        dist.all_to_all_single(nk, sk, rl, sent)
-        dist.all_to_all_single(nc, sc, rl, sent)
+        nrec = torch.empty(sum(rl) * 10, dtype=torch.uint8, device="cuda")
+        dist.all_to_all_single(nrec, rec, [x * 10 for x in rl], [x * 10 for x in sent])
         t0 = mark("all_to_all", t0)
-        uk, uc = ops.merge(nk, nc, rl)
+        uk, uc = ops.merge(nrec, None, rl)
         t0 = mark("merge", t0)
         dk, dc = ops.dense_cells(grid, 10)
         t0 = mark("dense_cells", t0)
