@@ -1482,7 +1482,7 @@ static int cells_merge(hm_ctx* ctx, const void* keys_in, const void* counts_in, 
     const uint64_t* keys = recs ? nullptr : (const uint64_t*)keys_in;
     const uint64_t* counts = layout == HM_CELLS_U64 ? (const uint64_t*)counts_in : nullptr;
     const uint32_t* counts32 = layout == HM_CELLS_U32 ? (const uint32_t*)counts_in : nullptr;
-    if (((uintptr_t)recs & 3) != 0) return HM_E_ARG;   /* records: 4-byte aligned (the merge loads words) */
+    if (((uintptr_t)recs & 1) != 0) return HM_E_ARG;   /* records: u16 words */
     if (!ctx || !n_out || n < 0 || capacity < 0 || (n > 0 && !keys_in) || (n > 0 && !recs && !counts && !counts32) ||
         (capacity > 0 && (!keys_out || !counts_out)) || nruns < 0 || (nruns > 0 && !runs))
         return HM_E_ARG;

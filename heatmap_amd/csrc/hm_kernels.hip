@@ -2296,10 +2296,27 @@ __device__ __forceinline__ void hm_small_dispatch(uint32_t nk, F&& f)
     if constexpr (HI >= 4096) f(std::integral_constant<int, 64>{});
 }
 
-/* Persistent: wave w takes the 64-bucket batches w, w + waves, ...; a bucket
- * is this instantiation's when LO < nkeys <= HI (larger ones are
- * k_aggregate's). The LO == 0 instantiation runs first and zeroes the cell
- * count of every bucket that is not its own. */
+/* Which buckets a wave looks at.  LO == 0 (the narrow instantiation, most
+ * buckets): wave w takes the batches of spbatch consecutive buckets w, w +
+ * waves, ...  LO > 0 (the wide one: buckets of > HM_SPW_SPLIT keys, few and
+ * clustered in space, i.e. in bucket order): lane j of wave w at step s looks
+ * at bucket (64 s + j) waves + w, so neighbouring big buckets go to different
+ * waves (consecutive batches left one wave sorting several of them while the
+ * others idled: the tail of a stream batch's 513-2048-key pass). */
+template <uint32_t LO>
+struct HmSmallMap {
+    static __device__ __forceinline__ uint32_t first(uint32_t wid, uint32_t spb) { return LO ? 0u : wid * spb; }
+    static __device__ __forceinline__ uint32_t step(uint32_t nw, uint32_t spb) { return LO ? 64u : nw * spb; }
+    static __device__ __forceinline__ uint64_t bucket(uint32_t s0, uint32_t lane, uint32_t wid, uint32_t nw)
+    {
+        return LO ? (uint64_t)(s0 + lane) * nw + wid : (uint64_t)s0 + lane;
+    }
+    static __device__ __forceinline__ bool lane_in(uint32_t lane, uint32_t spb) { return LO ? true : lane < spb; }
+};
+
+/* Persistent: a bucket is this instantiation's when LO < nkeys <= HI (larger
+ * ones are k_aggregate's). The LO == 0 instantiation runs first and zeroes the
+ * cell count of every bucket that is not its own. */
 template <uint32_t LO, uint32_t HI>
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
 {
@@ -2308,10 +2325,13 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
     uint16_t* ks = kss[threadIdx.x >> 6];
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
     const uint32_t zmask = hm_small_zmask(a);
-    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * a.spbatch; b0 < a.B.count;
-         b0 += nw * a.spbatch) {
-        const uint32_t bl = b0 + lane;
-        const bool in = (lane < a.spbatch) & (bl < a.B.count);
+    const uint32_t wid = blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6);
+    const uint32_t step = HmSmallMap<LO>::step(nw, a.spbatch);
+    for (uint32_t s0 = HmSmallMap<LO>::first(wid, a.spbatch); HmSmallMap<LO>::bucket(s0, 0, wid, nw) < a.B.count;
+         s0 += step) {
+        const uint64_t bl64 = HmSmallMap<LO>::bucket(s0, lane, wid, nw);
+        const bool in = HmSmallMap<LO>::lane_in(lane, a.spbatch) & (bl64 < a.B.count);
+        const uint32_t bl = in ? (uint32_t)bl64 : 0u;
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
         const bool small = in & (LO == 0 || nkl > LO) & (nkl <= HI);
         const uint32_t rbl = small ? a.B.rbase[bl] : 0u, nrl = small ? a.B.nruns[bl] : 0u;
@@ -2322,7 +2342,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
         while (m) {
             const int i = __builtin_ctzll(m);
             m &= m - 1;
-            const uint32_t b = b0 + i;
+            const uint32_t b = __shfl(bl, i, 64);
             const uint32_t nk = __shfl(nkl, i, 64), r0 = __shfl(rbl, i, 64), nr = __shfl(nrl, i, 64);
             const uint32_t kb = __shfl(kbl, i, 64);
             /* gather: runs 64 at a time, consecutive keys to consecutive lanes */
@@ -2366,10 +2386,13 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
     const uint32_t zmask = hm_small_zmask(a);
     const uint64_t base = *a.spbase;
-    for (uint32_t b0 = (blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6)) * a.spbatch; b0 < a.B.count;
-         b0 += nw * a.spbatch) {
-        const uint32_t bl = b0 + lane;
-        const bool in = (lane < a.spbatch) & (bl < a.B.count);
+    const uint32_t wid = blockIdx.x * (HM_SPW_THREADS / 64) + (threadIdx.x >> 6);
+    const uint32_t step = HmSmallMap<LO>::step(nw, a.spbatch);
+    for (uint32_t s0 = HmSmallMap<LO>::first(wid, a.spbatch); HmSmallMap<LO>::bucket(s0, 0, wid, nw) < a.B.count;
+         s0 += step) {
+        const uint64_t bl64 = HmSmallMap<LO>::bucket(s0, lane, wid, nw);
+        const bool in = HmSmallMap<LO>::lane_in(lane, a.spbatch) & (bl64 < a.B.count);
+        const uint32_t bl = in ? (uint32_t)bl64 : 0u;
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
         const bool small = in & (LO == 0 || nkl > LO) & (nkl <= HI);
         const uint32_t kbl = small ? a.B.keybase[bl] : 0u;

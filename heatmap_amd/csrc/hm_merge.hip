@@ -78,21 +78,6 @@ __device__ __forceinline__ uint64_t hm_rec_key(const uint16_t* r)
 }
 __device__ __forceinline__ uint32_t hm_rec_count(const uint16_t* r) { return (uint32_t)r[3] | ((uint32_t)r[4] << 16); }
 
-/* records [t0, t0 + tn) of rin (4-B aligned) into LDS st with coalesced u32
- * loads (a lane's five u16 loads of its own record touched five lines per
- * wave-load); returns record t0's address in LDS.  Block-wide, ends with a
- * barrier.  A trailing half word is read as u16 (no read past the records). */
-__device__ __forceinline__ const uint16_t* hm_rec_stage(const uint16_t* rin, uint64_t t0, uint32_t tn, uint32_t* st)
-{
-    const uint64_t h0 = 5 * t0, h1 = 5 * (t0 + tn);   /* u16 units */
-    const uint64_t w0 = h0 >> 1, w1 = h1 >> 1;
-    const uint32_t* r32 = (const uint32_t*)rin;
-    for (uint64_t w = w0 + threadIdx.x; w < w1; w += blockDim.x) st[w - w0] = r32[w];
-    if ((h1 & 1) && threadIdx.x == 0) ((uint16_t*)st)[h1 - 1 - 2 * w0] = rin[h1 - 1];
-    __syncthreads();
-    return (const uint16_t*)st + (h0 - 2 * w0);
-}
-
 /* pass 1 (count) / pass 2 (scatter) over the same block-contiguous cells:
  * both passes see identical per-block owner counts, so pass 1's block totals,
  * scanned owner-major, are pass 2's reservations (slots inside a block's
@@ -285,7 +270,6 @@ __device__ __forceinline__ uint32_t hm_mb_bucket(uint64_t k, int lb)
  * cell and took 1.2 ms for 28M cells). */
 #define HM_MB_PPT 16
 #define HM_MB_TILE (256 * HM_MB_PPT)
-#define HM_MB_CHUNK 1024                      /* count pass: records staged at a time */
 #define HM_MB_MAXD 128
 template <bool SCATTER>
 __global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
@@ -294,11 +278,7 @@ __global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
     __shared__ uint32_t toff[HM_MB_MAXD];
     __shared__ unsigned long long gb[HM_MB_MAXD];
     __shared__ uint32_t scr[256 / 64 + 1];
-    /* scatter: keys | counts of a tile (the staged records of a tile before
-     * them); count: staged records of HM_MB_CHUNK cells */
-    __shared__ unsigned long long skc[SCATTER ? 2 * HM_MB_TILE : HM_MB_CHUNK * 10 / 8 + 2];
-    unsigned long long* const sk = skc;
-    unsigned long long* const sc = skc + (SCATTER ? HM_MB_TILE : 0);
+    __shared__ unsigned long long sk[SCATTER ? HM_MB_TILE : 1], sc[SCATTER ? HM_MB_TILE : 1];
     __shared__ uint8_t sd[SCATTER ? HM_MB_TILE : 1];
     const int tid = threadIdx.x;
     const uint32_t s = blockIdx.x / a.C, c = blockIdx.x % a.C;
@@ -314,17 +294,9 @@ __global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
     }
     __syncthreads();
     if (!SCATTER) {
-        if (a.rin) {
-            for (uint64_t t0 = c0; t0 < c1; t0 += HM_MB_CHUNK) {
-                const uint32_t tn = (uint32_t)min((uint64_t)HM_MB_CHUNK, c1 - t0);
-                const uint16_t* r = hm_rec_stage(a.rin, t0, tn, (uint32_t*)skc);
-                for (uint32_t i = tid; i < tn; i += 256)
-                    atomicAdd(&hist[(uint32_t)(hms_hash(hm_rec_key(r + 5 * i)) >> a.shift) & dm], 1u);
-                __syncthreads();
-            }
-        } else {
-            for (uint64_t i = c0 + tid; i < c1; i += 256)
-                atomicAdd(&hist[(uint32_t)(hms_hash(a.kin[i]) >> a.shift) & dm], 1u);
+        for (uint64_t i = c0 + tid; i < c1; i += 256) {
+            const uint64_t k = a.rin ? hm_rec_key(a.rin + 5 * i) : a.kin[i];
+            atomicAdd(&hist[(uint32_t)(hms_hash(k) >> a.shift) & dm], 1u);
         }
         __syncthreads();
         for (uint32_t d = tid; d < nd; d += 256) a.cnt[cbase + (uint64_t)d * a.C] = hist[d];
@@ -332,7 +304,6 @@ __global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
     }
     for (uint64_t t0 = c0; t0 < c1; t0 += HM_MB_TILE) {
         const uint32_t tn = (uint32_t)min((uint64_t)HM_MB_TILE, c1 - t0);
-        const uint16_t* rs = a.rin ? hm_rec_stage(a.rin, t0, tn, (uint32_t*)skc) : nullptr;
         uint64_t k[HM_MB_PPT], cc[HM_MB_PPT];
         uint32_t d[HM_MB_PPT], r[HM_MB_PPT];
 #pragma unroll
@@ -340,8 +311,8 @@ __global__ __launch_bounds__(256) void k_mb_pass(HmMbPass a)
             const uint32_t i = j * 256 + tid;
             const bool v = i < tn;
             if (a.rin) {
-                k[j] = v ? hm_rec_key(rs + 5 * i) : 0ull;
-                cc[j] = v ? (uint64_t)hm_rec_count(rs + 5 * i) : 0ull;
+                k[j] = v ? hm_rec_key(a.rin + 5 * (t0 + i)) : 0ull;
+                cc[j] = v ? (uint64_t)hm_rec_count(a.rin + 5 * (t0 + i)) : 0ull;
             } else {
                 k[j] = v ? a.kin[t0 + i] : 0ull;
                 cc[j] = v ? (a.cin32 ? (uint64_t)a.cin32[t0 + i] : a.cin[t0 + i]) : 0ull;

@@ -269,7 +269,7 @@ int64_t hm_dense_grid_size(int dense_zmax);
 /* exchanged cell layouts: keys u64[n] + counts u64[n]; keys u64[n] + counts
  * u32[n]; or n records of 10 bytes in `keys` (five u16: the key as zoom << 42
  * | row << 21 | col in 48 bits -- sparse zooms <= 21 -- and the u32 count;
- * the array 4-byte aligned) */
+ * the array 2-byte aligned) */
 #define HM_CELLS_U64 8
 #define HM_CELLS_U32 4
 #define HM_CELLS_REC10 10
