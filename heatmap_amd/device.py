@@ -18,6 +18,16 @@ _CTX = {}
 _CTX_LOCK = threading.Lock()
 
 
+def gpu_available() -> bool:
+    """A GPU torch can use (the host-side row assembly then sorts on it)."""
+    try:
+        import torch
+
+        return torch.cuda.is_available()
+    except Exception:   # pragma: no cover
+        return False
+
+
 def _torch():
     import torch
 

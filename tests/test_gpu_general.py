@@ -120,3 +120,42 @@ def test_huge_latitudes(gpu):
     keep = (oracle.project(lat, lon, 18)[2] == 0).astype(np.uint8)
     lat2, lon2 = np.where(keep == 1, lat, 10.0), lon
     _same(device.count(lat2, lon2, None, 0, 18).sorted(), oracle.count(lat2, lon2, None, 0, 18))
+
+
+def test_sum_by_cell_device_matches_host(gpu):
+    """heatmap._sum_by_cell on the GPU (row assembly of large row sets) equals
+    the numpy lexsort path: unique (zoom, row, col) in order, summed columns."""
+    from heatmap_amd import heatmap as hm
+
+    g = np.random.default_rng(3)
+    parts = []
+    for m in (700_000, 500_000):
+        z = g.integers(7, 22, m)
+        r = g.integers(0, 1 << 12, m) & ((1 << z) - 1)
+        c = g.integers(0, 1 << 12, m) & ((1 << z) - 1)
+        v = g.integers(0, 1 << 40, (m, 3))
+        parts.append((z, r, c, v))
+    dev = hm._sum_by_cell(parts, device_min=1)
+    host = hm._sum_by_cell(parts, device_min=1 << 62)
+    for a, b in zip(dev, host):
+        assert np.array_equal(np.asarray(a), np.asarray(b))
+
+
+def test_row_order_device_matches_host(gpu):
+    """heatmap._row_order's GPU sorts give np.lexsort's permutation on
+    distinct bins."""
+    from heatmap_amd import heatmap as hm
+
+    g = np.random.default_rng(4)
+    m = 1_500_000
+    zoom = g.integers(7, 22, m)
+    row = g.integers(0, 1 << 21, m) & ((1 << zoom) - 1)
+    col = g.integers(0, 1 << 21, m) & ((1 << zoom) - 1)
+    label = g.integers(0, 3000, m)
+    span = g.integers(0, 3, m)
+    key = (label << 40) | (span << 36) | (zoom << 30) | (row << 15) | col
+    keep = np.unique(key, return_index=True)[1]       # distinct bins
+    zoom, row, col, label, span = zoom[keep], row[keep], col[keep], label[keep], span[keep]
+    d = 5
+    args = (label, span, zoom - d, row >> d, col >> d, zoom, row, col)
+    assert np.array_equal(hm._row_order(*args, device_min=1), hm._row_order(*args, device_min=1 << 62))
