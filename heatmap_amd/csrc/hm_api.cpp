@@ -1666,6 +1666,20 @@ extern "C" int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax,
     return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
 }
 
+extern "C" int hm_format_bins(hm_ctx* ctx, const int64_t* zoom, const int64_t* row, const int64_t* col,
+                              const int64_t* value, const uint8_t* head, const uint8_t* last, const int64_t* offset,
+                              int64_t n, uint8_t* text)
+{
+    if (!ctx || n < 0 || (n > 0 && (!zoom || !row || !col || !value || !head || !last || !offset || !text)))
+        return HM_E_ARG;
+    if (n == 0) return HM_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HmFormatArgs a{zoom, row, col, value, head, last, offset, n, text};
+    hm_launch_format_bins(ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    return HM_OK;
+}
+
 extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
                         const double* table, int k)
 {

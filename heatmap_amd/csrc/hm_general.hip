@@ -372,3 +372,53 @@ void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* col
     hipLaunchKernelGGL(k_tiles_list, dim3(hm_ggrid((uint64_t)n, 256 * HM_TL_PPT, 4096)), dim3(256), 0, s, rows, cols, keep, group,
                        n, row, col, grp, idx, count);
 }
+
+/* ------------------------------------------------------------------------ */
+/* row JSON text: one thread per bin writes  ["{"] "z_r_c": V.0 ("}" | ", ")  */
+/* ------------------------------------------------------------------------ */
+
+__device__ __forceinline__ uint8_t* hm_put_u64(uint8_t* p, uint64_t x)
+{
+    char d[20];
+    int k = 0;
+    do {
+        d[k++] = (char)('0' + x % 10);
+        x /= 10;
+    } while (x);
+    while (k) *p++ = (uint8_t)d[--k];
+    return p;
+}
+
+__global__ __launch_bounds__(256) void k_format_bins(HmFormatArgs a)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < (uint64_t)a.n; i += stride) {
+        uint8_t* p = a.text + a.offset[i];
+        if (a.head[i]) *p++ = '{';
+        *p++ = '"';
+        p = hm_put_u64(p, (uint64_t)a.zoom[i]);
+        *p++ = '_';
+        p = hm_put_u64(p, (uint64_t)a.row[i]);
+        *p++ = '_';
+        p = hm_put_u64(p, (uint64_t)a.col[i]);
+        *p++ = '"';
+        *p++ = ':';
+        *p++ = ' ';
+        p = hm_put_u64(p, (uint64_t)a.value[i]);
+        *p++ = '.';
+        *p++ = '0';
+        if (a.last[i]) {
+            *p++ = '}';
+        } else {
+            *p++ = ',';
+            *p++ = ' ';
+        }
+    }
+}
+
+void hm_launch_format_bins(hipStream_t s, const HmFormatArgs& a)
+{
+    if (a.n <= 0) return;
+    const uint64_t blocks = std::min<uint64_t>(8192, ((uint64_t)a.n + 255) / 256);
+    hipLaunchKernelGGL(k_format_bins, dim3((unsigned)blocks), dim3(256), 0, s, a);
+}

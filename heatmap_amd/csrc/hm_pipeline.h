@@ -380,6 +380,16 @@ struct HmPoolArgs {
     HmOut out;
 };
 
+/* row JSON text of bins (k_format_bins, hm_general.hip) */
+struct HmFormatArgs {
+    const int64_t *zoom, *row, *col, *value;
+    const uint8_t *head, *last;
+    const int64_t* offset;
+    int64_t n;
+    uint8_t* text;
+};
+void hm_launch_format_bins(hipStream_t s, const HmFormatArgs& a);
+
 /* several memsets in one dispatch (a small call is launch-bound: each
  * hipMemsetAsync is a dispatch of its own) */
 #define HM_FILL_MAX 10

@@ -375,6 +375,50 @@ def _row_order(label, span, tz, tr, tc, zoom, row, col, device_min=None):
     return np.lexsort((col, row, zoom, tc, tr, tz, span, label))
 
 
+def _heat_text_device(z, r, c, v, starts, device_min=None):
+    """The rows' heatmap JSON (bins in row order, non-negative integer
+    counts below 1e16) written on the GPU by hm_format_bins: one thread per
+    bin, byte offsets from an exclusive scan of the bin lengths.  Returns a
+    pyarrow LargeStringArray, or None (small sets, no GPU: the host path)."""
+    lim = SUM_BY_CELL_DEVICE_MIN if device_min is None else device_min
+    n = int(np.asarray(z).size)
+    if n < lim or not device.gpu_available() or min(int(np.min(z)), int(np.min(r)), int(np.min(c))) < 0:
+        return None
+    import ctypes
+
+    import pyarrow as pa
+    import torch
+
+    dz, dr, dc, dv = (torch.from_numpy(np.ascontiguousarray(x, np.int64)).cuda() for x in (z, r, c, v))
+    st = torch.from_numpy(np.asarray(starts, np.int64)).cuda()
+    head = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    head[st] = 1
+    last = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    last[st[1:] - 1] = 1
+    last[n - 1] = 1
+
+    def digits(x):
+        d = torch.ones_like(x)
+        p = 10
+        for _ in range(18):
+            d += (x >= p).to(torch.int64)
+            p *= 10
+        return d
+
+    ln = digits(dz) + digits(dr) + digits(dc) + digits(dv) + 8 + head.to(torch.int64) + 2 - last.to(torch.int64)
+    off = torch.cumsum(ln, 0) - ln
+    total = int((off[-1] + ln[-1]).item())
+    text = torch.empty(max(total, 1), dtype=torch.uint8, device="cuda")
+    ctx = device.context(torch.cuda.current_device())
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    rc = ctx.L.hm_format_bins(ctx.ptr, p(dz), p(dr), p(dc), p(dv), p(head), p(last), p(off), n, p(text))
+    if rc != _lib.HM_OK:
+        _lib.raise_for(rc)
+    offsets = np.append(off[st].cpu().numpy(), total).astype(np.int64)
+    data = text[:total].cpu().numpy()
+    return pa.LargeStringArray.from_buffers(len(starts), pa.py_buffer(offsets), pa.py_buffer(data))
+
+
 def cells_to_table(cells: Cells):
     """pyarrow Table(id: string, heatmap: string) of the rows, the heatmap
     JSON-encoded as heatmap_to_json would (json.dumps of the bin dict, floats
@@ -398,19 +442,21 @@ def cells_to_table(cells: Cells):
     # float repr of integer-valued counts below 1e16 is "<int>.0"; others via repr
     vi = v.astype(np.int64)
     small = (v == vi) & (np.abs(v) < 1e16)
-    vs = pc.binary_join_element_wise(s(vi), t(".0"), t(""))
-    if not small.all():
-        vs = vs.to_pylist()
-        for i in np.flatnonzero(~small).tolist():
-            vs[i] = repr(float(v[i]))
-        vs = pa.array(vs, pa.large_string())
-    bins = pc.binary_join_element_wise(s(z), s(r), s(c), t("_"))
-    pieces = pc.binary_join_element_wise(t('"'), bins, t('": '), vs, t(""))
-    # 64-bit offsets throughout: a batch can hold more than 2^31 bins or 2 GiB
-    # of JSON text (int32 offsets would wrap silently)
-    offsets = np.append(starts, lab.size).astype(np.int64)
-    joined = pc.binary_join(pa.LargeListArray.from_arrays(pa.array(offsets, pa.int64()), pieces), t(", "))
-    heat = pc.binary_join_element_wise(t("{"), joined, t("}"), t(""))
+    heat = _heat_text_device(z, r, c, vi, starts) if small.all() and vi.min() >= 0 else None
+    if heat is None:
+        vs = pc.binary_join_element_wise(s(vi), t(".0"), t(""))
+        if not small.all():
+            vs = vs.to_pylist()
+            for i in np.flatnonzero(~small).tolist():
+                vs[i] = repr(float(v[i]))
+            vs = pa.array(vs, pa.large_string())
+        bins = pc.binary_join_element_wise(s(z), s(r), s(c), t("_"))
+        pieces = pc.binary_join_element_wise(t('"'), bins, t('": '), vs, t(""))
+        # 64-bit offsets throughout: a batch can hold more than 2^31 bins or 2 GiB
+        # of JSON text (int32 offsets would wrap silently)
+        offsets = np.append(starts, lab.size).astype(np.int64)
+        joined = pc.binary_join(pa.LargeListArray.from_arrays(pa.array(offsets, pa.int64()), pieces), t(", "))
+        heat = pc.binary_join_element_wise(t("{"), joined, t("}"), t(""))
     names = pa.array(cells.labels, pa.large_string()).take(pa.array(lab[starts]))
     spans = pa.array(cells.spans, pa.large_string()).take(pa.array(sp[starts]))
     ids = pc.binary_join_element_wise(names, spans,

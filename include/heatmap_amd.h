@@ -284,6 +284,18 @@ int hm_cells_merge_runs(hm_ctx* ctx, const void* keys, const void* counts, int l
 int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out, uint64_t* counts_out,
                    int64_t capacity, int64_t* n_out);
 
+/* Row JSON text (heatmap_to_json, heatmap.py:92-95 via list_to_dict :120-126):
+ * the bins of the rows, in row order (device arrays, n of them), are written
+ * as  {"z_r_c": V.0, ...}  per row -- json.dumps of the bin dict with Python's
+ * float repr of integer-valued counts below 1e16 (callers format others on
+ * the host).  head/last: 1 on a row's first/last bin; offset: each bin's
+ * first byte (an exclusive scan of the bin lengths the caller computed:
+ * 1 + digits(z) + 1 + digits(r) + 1 + digits(c) + 3 + digits(v) + 2, plus
+ * 1 for a first bin's "{" and 1 for a last bin's "}" or 2 for ", ").  z, r,
+ * c >= 0; v >= 0 integers.  Asynchronous. */
+int hm_format_bins(hm_ctx* ctx, const int64_t* zoom, const int64_t* row, const int64_t* col, const int64_t* value,
+                   const uint8_t* head, const uint8_t* last, const int64_t* offset, int64_t n, uint8_t* text);
+
 /* Benchmark/test utility, not part of the reference boundary: fill lat/lon
  * (device) with points start..start+n-1 of a synthetic cloud, bit-identical
  * to heatmap_amd/synth.py.  kind: 0 uniform, 1 hotspots (table = device

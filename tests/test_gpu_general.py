@@ -159,3 +159,31 @@ def test_row_order_device_matches_host(gpu):
     d = 5
     args = (label, span, zoom - d, row >> d, col >> d, zoom, row, col)
     assert np.array_equal(hm._row_order(*args, device_min=1), hm._row_order(*args, device_min=1 << 62))
+
+
+def test_heat_text_device_matches_host(gpu):
+    """Row JSON written on the GPU (hm_format_bins) is byte-identical to the
+    pyarrow host assembly: rows of 1..40 bins, counts 0 .. 1e16 - 1."""
+    import pyarrow as pa
+
+    from heatmap_amd import heatmap as hm
+
+    g = np.random.default_rng(5)
+    sizes = g.integers(1, 41, 60_000)
+    n = int(sizes.sum())
+    starts = np.concatenate([[0], np.cumsum(sizes)[:-1]]).astype(np.int64)
+    z = g.integers(0, 22, n)
+    r = g.integers(0, 1 << 21, n) & ((1 << z) - 1)
+    c = g.integers(0, 1 << 21, n) & ((1 << z) - 1)
+    v = np.where(g.random(n) < 0.5, g.integers(0, 1000, n), g.integers(0, 10 ** 16, n))
+    v[:3] = [0, 10 ** 16 - 2, 9]
+    v = v.astype(np.float64).astype(np.int64)   # the product's counts are float64 values (Cells.value)
+    dev = hm._heat_text_device(z, r, c, v, starts, device_min=1)
+    assert dev is not None and len(dev) == starts.size
+    host = []
+    ends = np.append(starts[1:], n)
+    for a, b in zip(starts[:2000].tolist(), ends[:2000].tolist()):
+        host.append("{" + ", ".join('"%d_%d_%d": %s' % (z[i], r[i], c[i], repr(float(v[i])))
+                                    for i in range(a, b)) + "}")
+    assert isinstance(dev, pa.LargeStringArray)
+    assert dev.slice(0, 2000).to_pylist() == host
