@@ -375,25 +375,20 @@ def _row_order(label, span, tz, tr, tc, zoom, row, col, device_min=None):
     return np.lexsort((col, row, zoom, tc, tr, tz, span, label))
 
 
-def _heat_text_device(z, r, c, v, starts, device_min=None):
-    """The rows' heatmap JSON (bins in row order, non-negative integer
-    counts below 1e16) written on the GPU by hm_format_bins: one thread per
-    bin, byte offsets from an exclusive scan of the bin lengths.  Returns a
-    pyarrow LargeStringArray, or None (small sets, no GPU: the host path)."""
-    lim = SUM_BY_CELL_DEVICE_MIN if device_min is None else device_min
-    n = int(np.asarray(z).size)
-    if n < lim or not device.gpu_available() or min(int(np.min(z)), int(np.min(r)), int(np.min(c))) < 0:
-        return None
+def _heat_text_gpu(dz, dr, dc, dv, st):
+    """The rows' heatmap JSON from bins in row order (int64 CUDA tensors;
+    non-negative, counts below 1e16) and the rows' first bins st: written by
+    hm_format_bins, one thread per bin at an exclusive scan of the bins' text
+    lengths.  A pyarrow LargeStringArray."""
     import ctypes
 
     import pyarrow as pa
     import torch
 
-    dz, dr, dc, dv = (torch.from_numpy(np.ascontiguousarray(x, np.int64)).cuda() for x in (z, r, c, v))
-    st = torch.from_numpy(np.asarray(starts, np.int64)).cuda()
-    head = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    n = dz.numel()
+    head = torch.zeros(n, dtype=torch.uint8, device=dz.device)
     head[st] = 1
-    last = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    last = torch.zeros(n, dtype=torch.uint8, device=dz.device)
     last[st[1:] - 1] = 1
     last[n - 1] = 1
 
@@ -408,15 +403,71 @@ def _heat_text_device(z, r, c, v, starts, device_min=None):
     ln = digits(dz) + digits(dr) + digits(dc) + digits(dv) + 8 + head.to(torch.int64) + 2 - last.to(torch.int64)
     off = torch.cumsum(ln, 0) - ln
     total = int((off[-1] + ln[-1]).item())
-    text = torch.empty(max(total, 1), dtype=torch.uint8, device="cuda")
-    ctx = device.context(torch.cuda.current_device())
+    text = torch.empty(max(total, 1), dtype=torch.uint8, device=dz.device)
+    ctx = device.context(dz.device.index or 0)
     p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    dz, dr, dc, dv = (x.contiguous() for x in (dz, dr, dc, dv))
     rc = ctx.L.hm_format_bins(ctx.ptr, p(dz), p(dr), p(dc), p(dv), p(head), p(last), p(off), n, p(text))
     if rc != _lib.HM_OK:
         _lib.raise_for(rc)
     offsets = np.append(off[st].cpu().numpy(), total).astype(np.int64)
     data = text[:total].cpu().numpy()
-    return pa.LargeStringArray.from_buffers(len(starts), pa.py_buffer(offsets), pa.py_buffer(data))
+    return pa.LargeStringArray.from_buffers(int(st.numel()), pa.py_buffer(offsets), pa.py_buffer(data))
+
+
+def _heat_text_device(z, r, c, v, starts, device_min=None):
+    """_heat_text_gpu of host arrays, or None (small sets, no GPU, negative
+    values: the host path)."""
+    lim = SUM_BY_CELL_DEVICE_MIN if device_min is None else device_min
+    n = int(np.asarray(z).size)
+    if n < lim or not device.gpu_available() or min(int(np.min(z)), int(np.min(r)), int(np.min(c))) < 0:
+        return None
+    import torch
+
+    dz, dr, dc, dv = (torch.from_numpy(np.ascontiguousarray(x, np.int64)).cuda() for x in (z, r, c, v))
+    return _heat_text_gpu(dz, dr, dc, dv, torch.from_numpy(np.asarray(starts, np.int64)).cuda())
+
+
+def _cells_to_table_device(cells: Cells):
+    """cells_to_table with the bins kept on the GPU from the row sort to the
+    JSON text: one upload, the order and every per-bin gather on the device;
+    only per-row fields come back for the ids.  None when a value is not a
+    non-negative integer below 1e16 or a coordinate is out of packing range
+    (the host path then)."""
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import torch
+
+    d = cells.delta
+    v = np.asarray(cells.value, np.float64)
+    vi = v.astype(np.int64)
+    if not (np.array_equal(v, vi) and vi.min() >= 0 and vi.max() < 10 ** 16):
+        return None
+    cu = lambda x: torch.from_numpy(np.ascontiguousarray(x, np.int64)).cuda()  # noqa: E731
+    lab, sp, z, r, c = (cu(x) for x in (cells.label, cells.span, cells.zoom, cells.row, cells.col))
+    if (min(int(r.min()), int(c.min()), int(lab.min()), int(sp.min()), int(z.min()) - d) < 0 or
+            max(int(r.max()), int(c.max())) >= (1 << 29) or int(z.max()) >= 64 or int(lab.max()) >= (1 << 40) or
+            int(sp.max()) >= (1 << 20)):
+        return None
+    dv = cu(vi)
+    tz, tr, tc = z - d, r >> d, c >> d
+    perm = torch.arange(z.numel(), device=z.device)
+    for key in ((z << 58) | (r << 29) | c, (tz << 58) | (tr << 29) | tc, (lab << 20) | sp):
+        perm = perm[torch.sort(key[perm], stable=True).indices]
+    lab, sp, z, r, c, dv, tz, tr, tc = (x[perm] for x in (lab, sp, z, r, c, dv, tz, tr, tc))
+    hi, lo = (lab << 20) | sp, (tz << 58) | (tr << 29) | tc
+    head = torch.ones_like(hi, dtype=torch.bool)
+    head[1:] = (hi[1:] != hi[:-1]) | (lo[1:] != lo[:-1])
+    st = torch.nonzero(head).flatten()
+    heat = _heat_text_gpu(z, r, c, dv, st)
+    rl, rs, rz, rr, rc_ = (x[st].cpu().numpy() for x in (lab, sp, tz, tr, tc))
+    s = lambda a: pc.cast(pa.array(a), pa.large_string())  # noqa: E731
+    t = lambda x: pa.scalar(x, pa.large_string())  # noqa: E731
+    names = pa.array(cells.labels, pa.large_string()).take(pa.array(rl))
+    spans = pa.array(cells.spans, pa.large_string()).take(pa.array(rs))
+    ids = pc.binary_join_element_wise(names, spans, pc.binary_join_element_wise(s(rz), s(rr), s(rc_), t("_")),
+                                      t(KEY_SEPERATOR))
+    return pa.table({"id": ids, "heatmap": heat})
 
 
 def cells_to_table(cells: Cells):
@@ -429,6 +480,10 @@ def cells_to_table(cells: Cells):
     d = cells.delta
     if len(cells) == 0:
         return pa.table({"id": pa.array([], pa.large_string()), "heatmap": pa.array([], pa.large_string())})
+    if len(cells) >= SUM_BY_CELL_DEVICE_MIN and device.gpu_available():
+        tab = _cells_to_table_device(cells)
+        if tab is not None:
+            return tab
     tz, tr, tc = cells.zoom - d, cells.row >> d, cells.col >> d
     o = _row_order(cells.label, cells.span, tz, tr, tc, cells.zoom, cells.row, cells.col)
     lab, sp, z, r, c, v = cells.label[o], cells.span[o], cells.zoom[o], cells.row[o], cells.col[o], cells.value[o]

@@ -187,3 +187,32 @@ def test_heat_text_device_matches_host(gpu):
                                     for i in range(a, b)) + "}")
     assert isinstance(dev, pa.LargeStringArray)
     assert dev.slice(0, 2000).to_pylist() == host
+
+
+def test_cells_to_table_device_matches_host(gpu):
+    """cells_to_table's device path (order, gathers and JSON on the GPU) gives
+    the host path's table exactly: ids and heatmap strings, row by row."""
+    from heatmap_amd import heatmap as hm
+
+    g = np.random.default_rng(6)
+    m = 400_000
+    zoom = g.integers(6, 22, m)
+    row = g.integers(0, 1 << 21, m) & ((1 << zoom) - 1)
+    col = g.integers(0, 1 << 21, m) & ((1 << zoom) - 1)
+    label = g.integers(0, 50, m)
+    span = g.integers(0, 2, m)
+    key = (label << 44) | (span << 43) | (zoom << 38) | (row << 19) | col
+    keep = np.unique(key, return_index=True)[1]
+    val = g.integers(1, 10 ** 9, keep.size).astype(np.float64)
+    cells = hm.Cells(["u%d" % i for i in range(50)], label[keep], zoom[keep], row[keep], col[keep], val, 5,
+                     ["alltime", "2024"], span[keep])
+    dev = hm._cells_to_table_device(cells)
+    old = hm.SUM_BY_CELL_DEVICE_MIN
+    hm.SUM_BY_CELL_DEVICE_MIN = 1 << 62
+    try:
+        host = hm.cells_to_table(cells)
+    finally:
+        hm.SUM_BY_CELL_DEVICE_MIN = old
+    assert dev is not None
+    assert dev.column("id").to_pylist() == host.column("id").to_pylist()
+    assert dev.column("heatmap").to_pylist() == host.column("heatmap").to_pylist()
