@@ -2241,13 +2241,13 @@ __device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, u
             run = ((e == 0) | ((prev >> (2 * l)) != (v[u] >> (2 * l)))) ? e : run;
             hs[u] = run;
         }
-        uint32_t x = run;   /* inclusive max-scan over lanes */
-#pragma unroll
-        for (int d = 1; d < 64; d <<= 1) {
-            const uint32_t y = __shfl_up(x, d, 64);
-            if (lane >= (uint32_t)d) x = max(x, y);
-        }
-        uint32_t ex = __shfl_up(x, 1, 64);
+        /* the last head before this lane's elements: heads' positions grow
+         * with the lane, so it is the run of the highest lower lane holding a
+         * head (lane 0 always does: element 0) -- one ballot and one
+         * cross-lane read instead of a 6-step max-scan */
+        const uint64_t hmask = __ballot((run != 0u) | (lane == 0u));
+        const uint64_t below = hmask & ((1ull << lane) - 1ull);
+        uint32_t ex = __shfl(run, below ? 63 - __clzll((long long)below) : 0, 64);
         ex = lane ? ex : 0u;
         const int zl = a.Z - l;
         const int s = lg - l;
