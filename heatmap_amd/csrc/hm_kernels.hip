@@ -2175,12 +2175,12 @@ __device__ __forceinline__ void hm_small_load(const uint16_t* src, uint32_t nk, 
     }
 }
 
-/* last element of its level-l cell (valid elements only) */
+/* last element of its level-l cell (valid elements only); nx = the next
+ * lane's v[0] */
 template <int K>
-__device__ __forceinline__ void hm_small_ends(const uint32_t (&v)[K], uint32_t nk, int l, bool (&end)[K])
+__device__ __forceinline__ void hm_small_ends(const uint32_t (&v)[K], uint32_t nk, int l, bool (&end)[K], uint32_t nx)
 {
     const uint32_t lane = hm_lane();
-    const uint32_t nx = __shfl_down(v[0], 1, 64);
 #pragma unroll
     for (int u = 0; u < K; u++) {
         const uint32_t e = lane * K + u;
@@ -2208,10 +2208,11 @@ __device__ __forceinline__ void hm_small_sort(const HmAggArgs& a, const uint16_t
         if (e < nk) a.codes[kb + e] = (uint16_t)v[u];
     }
     uint32_t total = 0;
+    const uint32_t nx = __shfl_down(v[0], 1, 64);   /* level-independent: once per bucket */
     for (int l = 0; l < lg; l++) {
         if (!((zmask >> l) & 1u)) continue;
         bool end[K];
-        hm_small_ends<K>(v, nk, l, end);
+        hm_small_ends<K>(v, nk, l, end, nx);
 #pragma unroll
         for (int u = 0; u < K; u++) total += __popcll(__ballot(end[u]));
     }
@@ -2226,12 +2227,14 @@ __device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, u
     const int lg = a.lg;
     uint32_t v[K];
     hm_small_load<K>(a.codes + kb, nk, v);
+    /* the neighbours' codes are level-independent: read once per bucket */
+    const uint32_t nx = __shfl_down(v[0], 1, 64);
+    const uint32_t pv = __shfl_up(v[K - 1], 1, 64);
     for (int l = 0; l < lg; l++) {
         if (!((zmask >> l) & 1u)) continue;
         bool end[K];
-        hm_small_ends<K>(v, nk, l, end);
+        hm_small_ends<K>(v, nk, l, end, nx);
         /* segment start of every element: running max of head positions */
-        const uint32_t pv = __shfl_up(v[K - 1], 1, 64);
         uint32_t hs[K];
         uint32_t run = 0;
 #pragma unroll
