@@ -2119,38 +2119,61 @@ __device__ __forceinline__ uint32_t hm_compact7(uint32_t x)
     return (x | (x >> 4)) & 0x00FFu;
 }
 
-/* Ascending bitonic sort of the wave's 64*K values, element e = lane*K + u in
- * v[u]: distances < K swap registers, larger ones exchange across lanes. */
-template <int K>
-__device__ __forceinline__ void hm_wave_bitonic(uint32_t (&v)[K])
+/* the value of lane (lane ^ M): DPP quad permutes for M = 1, 2 (no LDS
+ * instruction), ds_swizzle's xor mode below 32 (no address), a bpermute for
+ * 32 (HIP's __shfl_xor is a bpermute with a computed address for every M) */
+template <int M>
+__device__ __forceinline__ uint32_t hm_xor_lane(uint32_t v)
 {
-    const uint32_t lane = hm_lane();
+    if constexpr (M == 1)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   /* quad_perm [1,0,3,2] */
+    else if constexpr (M == 2)
+        return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x4E, 0xF, 0xF, false);   /* quad_perm [2,3,0,1] */
+    else if constexpr (M < 32)
+        return (uint32_t)__builtin_amdgcn_ds_swizzle((int)v, (M << 10) | 0x1F);           /* xor within 32 lanes */
+    else
+        return __shfl_xor(v, M, 64);
+}
+
+/* Ascending bitonic sort of the wave's 64*K values, element e = lane*K + u in
+ * v[u]: distances < K swap registers, larger ones exchange across lanes.
+ * Compile-time recursion over (size, stride), so every lane exchange has a
+ * constant distance (hm_xor_lane). */
+template <int K, int SIZE, int STRIDE>
+__device__ __forceinline__ void hm_bitonic_step(uint32_t (&v)[K], uint32_t lane)
+{
+    if constexpr (STRIDE >= K) {
 #pragma unroll
-    for (uint32_t size = 2; size <= 64u * K; size <<= 1) {
+        for (int u = 0; u < K; u++) {
+            const uint32_t e = lane * K + u;
+            const uint32_t o = hm_xor_lane<STRIDE / K>(v[u]);
+            const bool take_min = ((e & STRIDE) == 0) == ((e & SIZE) == 0);
+            v[u] = take_min ? min(v[u], o) : max(v[u], o);
+        }
+    } else {
 #pragma unroll
-        for (uint32_t stride = size >> 1; stride > 0; stride >>= 1) {
-            if (stride >= (uint32_t)K) {
-#pragma unroll
-                for (int u = 0; u < K; u++) {
-                    const uint32_t e = lane * K + u;
-                    const uint32_t o = __shfl_xor(v[u], (int)(stride / K), 64);
-                    const bool take_min = ((e & stride) == 0) == ((e & size) == 0);
-                    v[u] = take_min ? min(v[u], o) : max(v[u], o);
-                }
-            } else {
-#pragma unroll
-                for (int u = 0; u < K; u++) {
-                    if ((u & stride) == 0) {
-                        const int w = u | (int)stride;
-                        const bool up = ((lane * K + u) & size) == 0;
-                        const uint32_t lo = min(v[u], v[w]), hi = max(v[u], v[w]);
-                        v[u] = up ? lo : hi;
-                        v[w] = up ? hi : lo;
-                    }
-                }
+        for (int u = 0; u < K; u++) {
+            if ((u & STRIDE) == 0) {
+                const int w = u | STRIDE;
+                const bool up = ((lane * K + u) & SIZE) == 0;
+                const uint32_t lo = min(v[u], v[w]), hi = max(v[u], v[w]);
+                v[u] = up ? lo : hi;
+                v[w] = up ? hi : lo;
             }
         }
     }
+    if constexpr (STRIDE > 1) hm_bitonic_step<K, SIZE, STRIDE / 2>(v, lane);
+}
+template <int K, int SIZE>
+__device__ __forceinline__ void hm_bitonic_size(uint32_t (&v)[K], uint32_t lane)
+{
+    hm_bitonic_step<K, SIZE, SIZE / 2>(v, lane);
+    if constexpr (SIZE < 64 * K) hm_bitonic_size<K, SIZE * 2>(v, lane);
+}
+template <int K>
+__device__ __forceinline__ void hm_wave_bitonic(uint32_t (&v)[K])
+{
+    hm_bitonic_size<K, 2>(v, hm_lane());
 }
 
 /* Small buckets run in two passes so that the output needs no per-bucket
