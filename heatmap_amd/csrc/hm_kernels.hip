@@ -2373,6 +2373,22 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
             const uint32_t kb = __shfl(kbl, i, 64);
             /* gather: runs 64 at a time, consecutive keys to consecutive lanes */
             uint32_t fill = 0;
+            if (nr <= 4) {
+                /* few runs (the common case: one per parent item): their
+                 * bounds in scalar registers, a key's run by three compares
+                 * instead of a 6-step shuffle search */
+                const uint2 run = lane < nr ? a.in.run[r0 + lane] : make_uint2(0, 0);
+                const uint32_t x0 = __builtin_amdgcn_readlane(run.x, 0), x1 = __builtin_amdgcn_readlane(run.x, 1);
+                const uint32_t x2 = __builtin_amdgcn_readlane(run.x, 2), x3 = __builtin_amdgcn_readlane(run.x, 3);
+                const uint32_t p1 = __builtin_amdgcn_readlane(run.y, 0);
+                const uint32_t p2 = p1 + __builtin_amdgcn_readlane(run.y, 1);
+                const uint32_t p3 = p2 + __builtin_amdgcn_readlane(run.y, 2);
+                const uint32_t tot = p3 + __builtin_amdgcn_readlane(run.y, 3);
+                for (uint32_t j = lane; j < tot; j += 64) {
+                    const uint32_t src = j < p1 ? x0 + j : j < p2 ? x1 + (j - p1) : j < p3 ? x2 + (j - p2) : x3 + (j - p3);
+                    ks[j] = a.keys[src];
+                }
+            } else
             for (uint32_t c0 = 0; c0 < nr; c0 += 64) {
                 const uint32_t q = c0 + lane;
                 const uint2 run = q < nr ? a.in.run[r0 + q] : make_uint2(0, 0);
