@@ -35,7 +35,7 @@ EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_st
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
            "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_cells_merge_runs",
-           "hm_dense_cells", "hm_format_bins"]
+           "hm_dense_cells", "hm_format_bins", "hm_bench_read"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -97,6 +97,7 @@ def load() -> ctypes.CDLL:
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
         L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]
+        L.hm_bench_read.argtypes = [vp, vp, vp, c.c_int64, vp]
         L.hm_stream_create.argtypes = [vp, c.c_int, c.c_int, c.c_uint32, c.c_int64, c.c_int64, P(vp)]
         L.hm_stream_add.argtypes = [vp, vp, vp, vp, vp, vp, c.c_int64]
         L.hm_stream_cells.argtypes = [vp, P(c.c_int64), P(c.c_int64), P(c.c_int64)]

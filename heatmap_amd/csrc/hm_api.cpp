@@ -1691,6 +1691,15 @@ extern "C" int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int
     return HM_OK;
 }
 
+extern "C" int hm_bench_read(hm_ctx* ctx, const void* a, const void* b, int64_t bytes_each, uint64_t* sink)
+{
+    if (!ctx || bytes_each < 0 || (bytes_each & 15) || (bytes_each > 0 && (!a || !b || !sink))) return HM_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    if (bytes_each > 0) hm_launch_read_stream(ctx->stream, a, b, (uint64_t)bytes_each, sink);
+    HIPCHK(hipGetLastError());
+    return HM_OK;
+}
+
 /* ------------------------------------------------------------------------ */
 /* streaming: resident multi-zoom heatmap (kernels in hm_stream.hip)          */
 /* ------------------------------------------------------------------------ */

@@ -37,7 +37,7 @@
 #ifdef HM_STAMPS
 /* phase timing (profiling builds only, tools/stamps.py): thread 0 of the first
  * HM_STAMP_BLOCKS blocks of one kernel records s_memtime at up to 12 points.
- * HM_STAMPS = 1: k_partition, 2: k_project_partition, 3: k_partition_fr */
+ * HM_STAMPS = 1: k_partition, 2: k_project_partition, 3: k_partition_fr, 4: k_l1_fast */
 #define HM_STAMP_BLOCKS 65536
 __device__ unsigned long long g_stamps[HM_STAMP_BLOCKS * 12];
 #define HM_STAMP_M(m, k)                                                                       \
@@ -114,6 +114,15 @@ __device__ __forceinline__ void hm_exotic_append(const HmExotic& x, bool p, int6
     }
 }
 
+
+/* hot-tile lookup of zoom-zb tile (rs, cs) in the LDS table image: h when the
+ * tile is hot, >= 2^16 otherwise (hm_pipeline.h) */
+__device__ __forceinline__ uint32_t hm_hot_find(const uint2* tab, uint32_t rs, uint32_t cs)
+{
+    const uint2 e = tab[hm_hot_bucket(rs, cs)];
+    const uint32_t tk = rs << HM_HOT_TAG;
+    return min(e.x ^ tk, e.y ^ tk);
+}
 
 /* ------------------------------------------------------------------------ */
 /* level 1: projection fused with the first partition                        */
@@ -301,16 +310,8 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         uint32_t dg = (rd << wd) | (HM_SKEW_CUR ? ((cd + (rd << 3)) & wm) : cd);
         key = ((r & lowm) << hb) | (c & lowm);
         if (H) {   /* block-uniform */
-            const uint32_t t = ((r >> hs) << a.hot_z) | (c >> hs);
-            const uint32_t tk = t << HM_HOT_HBITS;
-#if HM_HOT_WAYS == 4
-            const uint4 e = hsh4[hm_hot_bucket(t)];
-            const uint32_t x = min(min(e.x ^ tk, e.y ^ tk), min(e.z ^ tk, e.w ^ tk));
-#else
-            const uint2 e = ((const uint2*)hsh4)[hm_hot_bucket(t)];
-            const uint32_t x = min(e.x ^ tk, e.y ^ tk);
-#endif
-            const bool hot = x < (uint32_t)HM_HOT_LIMIT;   /* an empty way leaves x >= HM_HOT_LIMIT */
+            const uint32_t x = hm_hot_find((const uint2*)hsh4, r >> hs, c >> hs);
+            const bool hot = x < (uint32_t)HM_HOT_LIMIT;   /* a miss leaves x >= 2^16 */
             dg = hot ? HM_MAX_F1 + x : dg;
             key = hot ? (((r & hm) << hs) | (c & hm)) : key;
         }
@@ -514,6 +515,344 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     if (MODE == 0) HM_STAMP_M(2, 7);
 }
 
+/* ------------------------------------------------------------------------ */
+/* level 1, whole lat/lon tiles (the hot launch of every hm_count call)      */
+/* ------------------------------------------------------------------------ */
+/* k_l1_fast: the same level-1 pass as k_project_partition<OutT, 0, true> --
+ * the same regions, reservations, keys and deferred points -- with the
+ * per-point instruction budget cut (round 4):
+ *
+ *  projection  v_fract_f64 gives each coordinate's fraction in one op and the
+ *              floor is a truncating convert (both coordinates are positive on
+ *              the accepted range); the column is one fma (lon * kz + 180 kz,
+ *              inside the same 2^-49 guard); the column range test is
+ *              |lon| < 180 on the input (an accepted y lies in [0, 2^z));
+ *  hot lookup  row-tagged 2-way buckets (hm_hot_find): the tile's row and
+ *              column are shifts of the point's, no tile id is built, and the
+ *              digit is ONE min3 over (way 0, way 1, cold slot) because hot
+ *              tiles take the LOW slots [0, HM_MAX_HOT) of this kernel's
+ *              numbering and cold digits the slots above;
+ *  count+rank  one plain returning LDS atomic per point; lanes are grouped on
+ *              lane 0's slot only when a wave-uniform test finds >=
+ *              HM_L1_MERGE_MIN of them (skewed clouds), so a hotspot wave pays
+ *              two VALU ops per point for the test;
+ *  staging     each staged entry is (key, destination position): the copy-out
+ *              reads one 8-B LDS word per key and needs no per-digit lookup;
+ *              the stage holds the cold keys first and the hot keys after them
+ *              (one packed 16|16-bit block scan), so the copy-out's two store
+ *              kinds are wave-uniform; hot keys are staged in the cold layout
+ *              and narrowed to their zb-relative u16 form in the copy-out.
+ *
+ * Internal slot s: hot tile h -> s = h; cold z1 digit d -> s = HM_MAX_HOT +
+ * hm_dslot(d) (the bank-skewed slot).  Thread t owns slots q * T + t. */
+#ifndef HM_L1_MERGE_MIN
+#define HM_L1_MERGE_MIN 6
+#endif
+#define HM_L1_SLOTS (HM_MAX_HOT + HM_MAX_F1)
+#define HM_L1_CW 1600                       /* slot words (>= HM_L1_SLOTS + 64 dummies), a multiple of 64 */
+static_assert(HM_L1_CW >= HM_L1_SLOTS + 64 && HM_L1_CW % 64 == 0, "count and delta words pair as read2st64");
+static_assert(HM_L1_SLOTS % HM_P1_THREADS == 0, "slots per thread");
+
+#ifndef HM_L1_FAST
+#define HM_L1_FAST 1
+#endif
+template <typename OutT>
+__global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
+{
+    /* staged (key, destination), + one pad entry per lane for points that
+     * stage nothing; during the projection its first 32 KB hold the
+     * polynomial table and the hot-tile table */
+    __shared__ __attribute__((aligned(16))) uint2 ent[HM_T1 + 64];
+    /* per slot: count (atomics) then stage offset in [0, CW); destination minus
+     * stage position in [CW, 2 CW) -- one ds_read2st64_b32 reads both */
+    __shared__ uint32_t cw[2 * HM_L1_CW];
+    __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
+    __shared__ uint32_t s_over;
+    /* the polynomial table plus one poison row (HM_YTAB_ROWS): NaN
+     * coefficients.  Rows 0-15 (polar distance d in [4, 5): |lat| in [85, 86))
+     * are poisoned too, so the table itself rejects every point with |lat| >
+     * 85, |lat| > 90, NaN or inf (the clamped index lands on a poison row, the
+     * NaN fails the guard test): no latitude range test per point.  An
+     * accepted point has |lat| <= 85, Y in (0, 1), 0 < R < 2^Z. */
+    constexpr int YROWS = HM_YTAB_ROWS + 1, YPOISON = 16;
+    constexpr int YN = YROWS * HM_YTAB_STRIDE;
+    static_assert(sizeof(double) * YN <= 16384 && HM_HOT_SLOTS * 4 <= 16384, "tables fit the stage");
+    static_assert(HM_YTAB_K == 6 && HM_YTAB_E0 == 2, "rows 0-15 are d in [4, 5)");
+    double* const tab = (double*)ent;
+    uint2* const hot2 = (uint2*)((char*)ent + 16384);
+    const int tid = threadIdx.x;
+    const int F = 1 << a.dbits;
+    const uint32_t H = a.hot_z >= 0 ? *a.hot_n : 0u;
+    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);
+    const double scale = hm_exp2i(a.Z);
+    const double nscale = -scale, hscale = 0.5 * scale;
+    const double kz = HM_INV360 * scale;
+    const double c180 = 180.0 * kz;
+    const double ghalf = 0.5 - HM_Y_EPS * scale;       /* row: |frac - 1/2| < ghalf */
+    const double ghalf2 = 0.5 - scale * 0x1p-49;       /* column */
+    constexpr int PERD = HM_L1_SLOTS / HM_P1_THREADS;
+    const int wd = a.dbits >> 1;
+    /* slot -> digit (hot slot h: digit HM_MAX_F1 + h; cold slot: unskewed) */
+    auto digit_of = [&](uint32_t sl) -> uint32_t {
+        if (sl < HM_MAX_HOT) return HM_MAX_F1 + sl;
+        const uint32_t u = sl - HM_MAX_HOT, m = (1u << wd) - 1u;
+        return HM_SKEW_CUR ? ((u & ~m) | ((u - ((u >> wd) << 3)) & m)) : u;
+    };
+    auto live = [&](uint32_t sl) {
+        return sl < HM_MAX_HOT ? sl < H : (sl - HM_MAX_HOT) < (uint32_t)F;
+    };
+    /* keep bytes, then the tables, then the points (vmcnt retires in order) */
+    uint32_t kp[HM_P1_PPT / 2];
+    if (a.keep) {
+        const uint16_t* kp2 = (const uint16_t*)(a.keep + base);
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = kp2[k * HM_P1_THREADS + tid];
+    } else {
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = 0x0101;
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    constexpr int TPT = (YN + HM_P1_THREADS - 1) / HM_P1_THREADS;
+    double tv[TPT];
+#pragma unroll
+    for (int q = 0; q < TPT; q++) {
+        const int i = q * HM_P1_THREADS + tid;
+        tv[q] = i < YPOISON * HM_YTAB_STRIDE || i >= HM_YTAB_N ? __builtin_nan("") : c_ytab[i];
+    }
+    uint32_t smk[PERD], rcap2[PERD][2], rbase2[PERD][2];
+#pragma unroll
+    for (int q = 0; q < PERD; q++) {
+        const uint32_t sl = q * HM_P1_THREADS + tid;
+        const uint32_t d = digit_of(sl);
+        const uint32_t s0 = hm_l1i(d, 0), s1 = hm_l1i(d, blockIdx.x & (HM_L1_SHARDS - 1));
+        const bool lv = live(sl);
+        smk[q] = lv ? a.smask[d] : 0u;
+        rcap2[q][0] = lv ? a.rcap[s0] : 0u;
+        rcap2[q][1] = lv ? a.rcap[s1] : 0u;
+        rbase2[q][0] = lv ? a.rbase[s0] : 0u;
+        rbase2[q][1] = lv ? a.rbase[s1] : 0u;
+    }
+    uint4 hv0 = make_uint4(0u, 0u, 0u, 0u), hv1 = hv0;
+    if (H) {
+        hv0 = ((const uint4*)a.hot_hash)[tid];
+        hv1 = ((const uint4*)a.hot_hash)[HM_P1_THREADS + tid];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    double2 la[HM_P1_PPT / 2], lo[HM_P1_PPT / 2];
+    {
+        const double2* lat2 = (const double2*)(a.lat + base);
+        const double2* lon2 = (const double2*)(a.lon + base);
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT / 2; k++) {
+            la[k] = lat2[k * HM_P1_THREADS + tid];
+            lo[k] = lon2[k * HM_P1_THREADS + tid];
+        }
+    }
+    for (int i = tid; i < HM_L1_CW; i += HM_P1_THREADS) cw[i] = 0;
+    if (tid == 0) s_over = 0;
+    if (H) {
+        ((uint4*)hot2)[tid] = hv0;
+        ((uint4*)hot2)[HM_P1_THREADS + tid] = hv1;
+    }
+#pragma unroll
+    for (int q = 0; q < TPT; q++) {
+        const int i = q * HM_P1_THREADS + tid;
+        if (i < YN) tab[i] = tv[q];
+    }
+    __syncthreads();
+    HM_STAMP_M(4, 1);
+    const int hb = a.restbits >> 1;
+    const uint32_t lowm = (1u << hb) - 1u;
+    const uint32_t keym = (uint32_t)((1ull << (2 * hb)) - 1ull);
+    const uint32_t wm = (1u << wd) - 1u;
+    const int hs = a.hot_z >= 0 ? a.Z - a.hot_z : 0;
+    const uint32_t dummy = HM_L1_SLOTS + (uint32_t)hm_lane();
+    uint32_t slot[HM_P1_PPT], key[HM_P1_PPT];
+    uint32_t redo = 0;
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT; k++) {
+        const double pa = (k & 1) ? la[k >> 1].y : la[k >> 1].x;
+        const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
+        /* row: Y = 1/2 - sign(lat) g(90 - |lat|) (hm_fast_g), R = Y 2^Z */
+        const double dd = 90.0 - fabs(pa);
+        const uint32_t dh = (uint32_t)(hm_d2u(dd) >> 32);
+        constexpr uint32_t I0 = (1023u + HM_YTAB_E0) << HM_YTAB_K;
+        const uint32_t ii = min((dh >> (20 - HM_YTAB_K)) - I0, (uint32_t)HM_YTAB_ROWS);   /* wraps below d = 4 */
+        const double dlo = hm_u2d((uint64_t)(dh & ~((1u << (20 - HM_YTAB_K)) - 1u)) << 32);
+        const double t = dd - dlo;
+        const double* cf = tab + ii * HM_YTAB_STRIDE;
+        double p = cf[5];
+        p = fma(p, t, cf[4]);
+        p = fma(p, t, cf[3]);
+        p = fma(p, t, cf[2]);
+        p = fma(p, t, cf[1]);
+        p = fma(p, t, cf[0]);
+        const double R = fma(copysign(p, pa), nscale, hscale);
+        const double fr = __builtin_amdgcn_fract(R);
+        /* column: y = (lon + 180) / 360 * 2^z within 2^(z-51.3); guard 2^(z-49) */
+        const double y = fma(po, kz, c180);
+        const double fc = __builtin_amdgcn_fract(y);
+        const bool ok = (int)(fabs(fr - 0.5) < ghalf) & (int)(fabs(po) < 180.0) & (int)(fabs(fc - 0.5) < ghalf2);
+        const uint32_t r = (uint32_t)(int32_t)R;   /* truncation = floor: R, y > 0 when ok */
+        const uint32_t c = (uint32_t)(int32_t)y;
+        const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFFu) != 0;
+        redo |= (uint32_t)!ok << k;
+        /* cold slot: bank-skewed z1 digit above the hot slots */
+        const uint32_t rd = r >> hb, cd = c >> hb;
+        const uint32_t rdw = (rd << wd) + HM_MAX_HOT;
+        uint32_t sl = HM_SKEW_CUR ? (((cd + (rd << 3)) & wm) | rdw) : (cd | rdw);
+        if (H) sl = min(hm_hot_find(hot2, r >> hs, c >> hs), sl);   /* block-uniform */
+        key[k] = ((r << hb) | (c & lowm)) & keym;
+        slot[k] = (ok & kept) ? sl : dummy;
+        asm volatile("" : "+v"(slot[k]), "+v"(key[k]));
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    HM_STAMP_M(4, 2);
+    /* deferred points: k_redo resolves them exactly */
+    if (__builtin_amdgcn_ballot_w64(redo != 0)) {
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT; k++) {
+            const bool rd = (redo >> k) & 1u;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(rd);
+            if (m) {
+                uint64_t b = 0;
+                if (hm_lane() == __ffsll((unsigned long long)m) - 1) b = atomicAdd(a.redo_count, (unsigned long long)__popcll(m));
+                b = __shfl(b, __ffsll((unsigned long long)m) - 1, 64);
+                const uint64_t q = b + hm_mbcnt(m);
+                if (rd && q < a.redo_cap)
+                    a.redo_idx[q] = (uint32_t)(base + 2 * ((int64_t)(k >> 1) * HM_P1_THREADS + tid) + (k & 1));
+            }
+        }
+        const uint32_t ws = hm_wave_sum((uint32_t)__popc(redo));
+        if (hm_lane() == 0 && ws) atomicAdd(a.slow_count, (unsigned long long)ws);
+    }
+    /* count + rank: one returning atomic per point; a wave whose lanes mostly
+     * share lane 0's slot adds for them once (lane 0 adds the group size, the
+     * rest of the group hits private dummy words) */
+    uint32_t rank[HM_P1_PPT];
+    uint32_t merged = 0;   /* wave-uniform: points whose atomic was grouped */
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT; k++) {
+        const uint32_t k0 = __builtin_amdgcn_readfirstlane(slot[k]);
+        const uint64_t m = __builtin_amdgcn_ballot_w64(slot[k] == k0);
+        const uint32_t pm = (uint32_t)__builtin_popcountll(m);
+        uint32_t idx = slot[k], inc = 1u;
+        if (pm >= HM_L1_MERGE_MIN) {
+            merged |= 1u << k;
+            const bool in = (m >> hm_lane()) & 1ull;
+            idx = (in && hm_lane() != 0) ? dummy : idx;
+            inc = hm_lane() == 0 ? pm : inc;
+        }
+        rank[k] = atomicAdd(&cw[idx], inc);
+    }
+    if (merged) {
+#pragma unroll
+        for (int k = 0; k < HM_P1_PPT; k++)
+            if ((merged >> k) & 1u) {
+                const uint32_t k0 = __builtin_amdgcn_readfirstlane(slot[k]);
+                const uint64_t m = __builtin_amdgcn_ballot_w64(slot[k] == k0);
+                const uint32_t r0 = __builtin_amdgcn_readfirstlane(rank[k]);
+                if ((m >> hm_lane()) & 1ull) rank[k] = r0 + hm_mbcnt(m);
+            }
+    }
+    __syncthreads();
+    HM_STAMP_M(4, 3);
+    /* reservations: one returning global atomic per non-empty (digit, shard) */
+    uint32_t cnt[PERD], gpos[PERD];
+#pragma unroll
+    for (int q = 0; q < PERD; q++) {
+        const uint32_t sl = q * HM_P1_THREADS + tid;
+        const uint32_t d = digit_of(sl);
+        const uint32_t sh = smk[q] != 0 ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u;
+        cnt[q] = live(sl) ? cw[sl] : 0u;
+        gpos[q] = 0;
+        if (cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1i(d, sh)], cnt[q]);
+    }
+    /* stage offsets: cold slots (q >= 1) first, hot slots (q = 0) after them,
+     * from one scan of (cold count | hot count << 16) */
+    static_assert(HM_MAX_HOT == HM_P1_THREADS && PERD == 3, "slot q = 0 is the hot tiles");
+    uint32_t tot2;
+    const uint32_t pre = hm_block_excl_scan<HM_P1_THREADS>((cnt[1] + cnt[2]) | (cnt[0] << 16), scr, &tot2);
+    const uint32_t C = tot2 & 0xFFFFu, total = C + (tot2 >> 16);
+    uint32_t offq[PERD];
+    offq[1] = pre & 0xFFFFu;
+    offq[2] = offq[1] + cnt[1];
+    offq[0] = C + (pre >> 16);
+    bool over = false;
+#pragma unroll
+    for (int q = 0; q < PERD; q++) {
+        const uint32_t sl = q * HM_P1_THREADS + tid;
+        if (live(sl)) {
+            const uint32_t rc = smk[q] != 0 ? rcap2[q][1] : rcap2[q][0];
+            const uint32_t rb = smk[q] != 0 ? rbase2[q][1] : rbase2[q][0];
+            const bool fits = (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rc;
+            over |= cnt[q] && !fits;
+            cw[sl] = offq[q];
+            /* a region that overflowed: destinations >= 0xFFF00000 (no key
+             * position reaches it), dropped by the copy-out */
+            cw[HM_L1_CW + sl] = (fits ? rb + gpos[q] : 0xFFF00000u) - offq[q];
+        }
+    }
+    if (over) {
+        atomicOr(a.overflow, 1ull);
+        s_over = 1;
+    }
+    __syncthreads();
+    HM_STAMP_M(4, 4);
+    /* staging, branch-free: a point that stages nothing writes its lane's pad entry */
+#pragma unroll
+    for (int k = 0; k < HM_P1_PPT; k++) {
+        const uint32_t o = cw[slot[k]], dl = cw[HM_L1_CW + slot[k]];   /* (dummies: in range, unused) */
+        const uint32_t pos = slot[k] < HM_L1_SLOTS ? o + rank[k] : HM_T1 + (uint32_t)hm_lane();
+        ent[pos] = make_uint2(key[k], dl + pos);
+    }
+    __syncthreads();
+    HM_STAMP_M(4, 5);
+    /* copy-out: a wave stores 64 consecutive staged keys -- cold keys in [0, C)
+     * as OutT, hot keys in [C, total) as u16 (zb-relative); the kind tests
+     * are wave-uniform except in the one wave straddling C or total */
+    char* const outb = (char*)a.keys_out;
+    char* const houtb = (char*)a.keys_hot;
+    const uint32_t hm = (1u << hs) - 1u;
+    auto put_cold = [&](uint2 e) { *(OutT*)(outb + (uint64_t)e.y * sizeof(OutT)) = (OutT)e.x; };
+    auto put_hot = [&](uint2 e) {
+        /* (row offset, col offset) in the zoom-zb tile, from the cold key */
+        const uint32_t hk = (((e.x >> hb) & hm) << hs) | (e.x & hm);
+        *(uint16_t*)(houtb + (uint64_t)e.y * 2u) = (uint16_t)hk;
+    };
+    uint2 e[HM_P1_PPT];
+#pragma unroll
+    for (int j = 0; j < HM_P1_PPT; j++) e[j] = ent[j * HM_P1_THREADS + tid];   /* past total: unused */
+    const uint32_t wofs = (uint32_t)tid & ~63u;
+    if (!s_over) {
+#pragma unroll
+        for (int j = 0; j < HM_P1_PPT; j++) {
+            const uint32_t wb = __builtin_amdgcn_readfirstlane(j * HM_P1_THREADS + wofs);
+            const uint32_t i = j * HM_P1_THREADS + tid;
+            if (wb + 64 <= C) {
+                put_cold(e[j]);
+            } else if (wb >= C && wb + 64 <= total) {
+                put_hot(e[j]);
+            } else if (wb < total) {
+                if (i < C) put_cold(e[j]);
+                else if (i < total) put_hot(e[j]);
+            }
+        }
+    } else {
+        /* a region overflowed (the host re-runs the level with exact sizes) */
+#pragma unroll
+        for (int j = 0; j < HM_P1_PPT; j++) {
+            const uint32_t i = j * HM_P1_THREADS + tid;
+            if (i < total && e[j].y < 0xFFF00000u) {
+                if (i < C) put_cold(e[j]);
+                else put_hot(e[j]);
+            }
+        }
+    }
+    HM_STAMP_M(4, 6);
+}
+
 /* Sampled digit histogram of level 1 (every stride-th point, fast projection
  * only): sizes the per-digit key regions k_project_partition fills. */
 #define HM_SAMPLE_HSLOTS 4096   /* per-block hash of sampled hot-zoom tiles */
@@ -657,21 +996,24 @@ __global__ __launch_bounds__(1024) void k_hot_hash(HmHotArgs a)
         }
     }
     __syncthreads();
-    for (int pass = 0; pass < 2; pass++) {
+    /* pass 0: above the cutoff bin; 1: at it; 2: below it (only while hot
+     * digits are left: candidates whose bucket was full leave room) */
+    for (int pass = 0; pass < 3; pass++) {
+        if (pass == 2 && nh >= HM_HOT_LIMIT) break;   /* (block-uniform: read after the barrier) */
         for (uint32_t j = tid; j < nc; j += 1024) {
             const uint32_t t = a.cand[2 * j], c = a.cand[2 * j + 1];
             const uint32_t bn = hm_hot_bin(c);
-            if (pass == 0 ? bn <= cut : bn != cut) continue;   /* pass 0: above the cutoff; 1: at it */
-            const uint32_t b = hm_hot_bucket(t);
+            if (pass == 0 ? bn <= cut : pass == 1 ? bn != cut : bn >= cut) continue;
+            const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
+            const uint32_t b = hm_hot_bucket(tr, tc);
             const uint32_t w = atomicAdd(&fill[b], 1u);
             if (w >= HM_HOT_WAYS) continue;
             const uint32_t h = atomicAdd(&nh, 1u);
             if (h >= HM_HOT_LIMIT) continue;   /* its way stays empty */
-            tab[b * HM_HOT_WAYS + w] = (t << HM_HOT_HBITS) | h;
+            tab[b * HM_HOT_WAYS + w] = (tr << HM_HOT_TAG) | h;
             a.tiles[h] = t;
             a.hist[HM_MAX_F1 + h] = c;
             const int s = a.zb - a.z1;
-            const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
             const uint32_t d = ((tr >> s) << a.z1) | (tc >> s);
             a.hotparent[d] = 1;
             atomicSub(&a.hist[d], c);   /* those samples' keys leave the cold digit */
@@ -2623,7 +2965,10 @@ void hm_launch_part1(hipStream_t s, const HmPart1Args& a0, uint32_t grid, bool o
         else HM_P1_CASE(T, 2, FL, G);              \
     } while (0)
     if (full) {
-        if (out16) HM_P1_MODES(uint16_t, true, full);
+        if (mode == 0 && HM_L1_FAST) {
+            if (out16) hipLaunchKernelGGL(k_l1_fast<uint16_t>, dim3(full), b, 0, s, a);
+            else hipLaunchKernelGGL(k_l1_fast<uint32_t>, dim3(full), b, 0, s, a);
+        } else if (out16) HM_P1_MODES(uint16_t, true, full);
         else HM_P1_MODES(uint32_t, true, full);
     }
     if (grid > full) {
@@ -2941,4 +3286,52 @@ void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int6
     if (blocks > 256 * 32) blocks = 256 * 32;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_synth, dim3((unsigned)blocks), dim3(256), 0, s, kind, seed, start, n, lat, lon, tab, k);
+}
+
+/* ------------------------------------------------------------------------ */
+/* HBM read-stream peak (bench.py's measured_peak): K1's access shape without  */
+/* its arithmetic -- two fp64 arrays read once, 16 B per lane per load (the   */
+/* double2 loads of k_project_partition), HM_RS_INFLIGHT loads in flight per */
+/* lane, one XOR per block written so nothing is dead.                       */
+/* ------------------------------------------------------------------------ */
+#define HM_RS_THREADS 512
+#define HM_RS_V 4   /* 16-B loads in flight per lane and array (8 in all, K1 has 16) */
+__global__ __launch_bounds__(HM_RS_THREADS) void k_read_stream(const uint4* __restrict__ a, const uint4* __restrict__ b,
+                                                            uint64_t n16, uint64_t* __restrict__ sink)
+{
+    constexpr uint64_t TILE = (uint64_t)HM_RS_THREADS * HM_RS_V;   /* vectors of each array per tile */
+    uint32_t acc = 0;
+    for (uint64_t t0 = (uint64_t)blockIdx.x * TILE; t0 < n16; t0 += (uint64_t)gridDim.x * TILE) {
+        uint4 va[HM_RS_V], vb[HM_RS_V];
+        if (t0 + TILE <= n16) {
+#pragma unroll
+            for (int k = 0; k < HM_RS_V; k++) {
+                va[k] = a[t0 + (uint64_t)k * HM_RS_THREADS + threadIdx.x];
+                vb[k] = b[t0 + (uint64_t)k * HM_RS_THREADS + threadIdx.x];
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < HM_RS_V; k++) {
+                const uint64_t i = t0 + (uint64_t)k * HM_RS_THREADS + threadIdx.x;
+                va[k] = i < n16 ? a[i] : make_uint4(0u, 0u, 0u, 0u);
+                vb[k] = i < n16 ? b[i] : make_uint4(0u, 0u, 0u, 0u);
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < HM_RS_V; k++)
+            acc ^= va[k].x ^ va[k].y ^ va[k].z ^ va[k].w ^ vb[k].x ^ vb[k].y ^ vb[k].z ^ vb[k].w;
+    }
+    acc = hm_wave_sum(acc);
+    if (hm_lane() == 0 && acc == 0x9E3779B9u) sink[blockIdx.x] = acc;   /* data-dependent: the loads stay live */
+}
+
+void hm_launch_read_stream(hipStream_t s, const void* a, const void* b, uint64_t bytes_each, uint64_t* sink)
+{
+    const uint64_t n16 = bytes_each / 16;
+    const uint64_t tile = (uint64_t)HM_RS_THREADS * HM_RS_V;
+    uint64_t blocks = (n16 + tile - 1) / tile;
+    if (blocks > 256ull * 16) blocks = 256ull * 16;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_read_stream, dim3((unsigned)blocks), dim3(HM_RS_THREADS), 0, s, (const uint4*)a,
+                       (const uint4*)b, n16, sink);
 }

@@ -31,29 +31,30 @@
 #ifndef HM_MAX_HOT
 #define HM_MAX_HOT 512
 #endif
-#define HM_HOT_HBITS (HM_MAX_HOT > 512 ? 10 : 9)   /* h's bits in a table entry */
-/* hot tiles a call may use: with 10-bit h, h = 1023 is left out so that no
- * entry equals HM_HOT_EMPTY (tile 2^22 - 1 would) */
-#define HM_HOT_LIMIT (HM_HOT_HBITS == 10 ? 1023 : HM_MAX_HOT)
+/* hot-tile table: HM_HOT_BUCKETS buckets of 2 entries (one 8-B LDS read per
+ * lookup, no probe loop).  Zoom-zb tile (rs, cs) (zb <= 11: both < 2^11) sits
+ * in bucket (rs * K + cs) mod HM_HOT_BUCKETS, a bijection of cs for a given
+ * rs, so an entry needs only the row as its tag: entry = rs << 16 | h,
+ * HM_HOT_EMPTY.  XOR with the looked-up tile's rs << 16 leaves exactly h for
+ * the matching way and >= 2^16 for any other (or an empty one).  A candidate
+ * whose bucket is full stays cold (k_hot_hash). */
+#define HM_HOT_LIMIT HM_MAX_HOT
 #define HM_D1 (HM_MAX_F1 + HM_MAX_HOT)      /* level-1 digit slots: cold z1 digits, then hot tiles */
-/* hot-tile table: HM_HOT_BUCKETS buckets of HM_HOT_WAYS entries (one 16-B LDS
- * read per lookup, no probe loop); entry = tile << HM_HOT_HBITS | h, HM_HOT_EMPTY.  A
- * candidate whose bucket is full stays cold (k_hot_hash). */
-#ifndef HM_HOT_WAYS
-#define HM_HOT_WAYS 2                       /* 2 or 4 (one 8- or 16-B read): 2 measured 0.13 ms faster */
-#endif
+#define HM_HOT_WAYS 2
 #define HM_HOT_SLOTS 4096
 #define HM_HOT_BUCKETS (HM_HOT_SLOTS / HM_HOT_WAYS)
-#define HM_HOT_BBITS (HM_HOT_WAYS == 4 ? 10 : 11)
+#define HM_HOT_BBITS 11
+#define HM_HOT_TAG 16                       /* entry = rs << HM_HOT_TAG | h */
+#define HM_HOT_MULT 0x9E3779u               /* low 11 bits 1913: rows 1..7 apart never share a column's bucket */
 #define HM_HOT_CAND 4096                    /* candidates k_hot_select may list */
 #define HM_HOT_EMPTY 0xFFFFFFFFu
-static_assert(HM_MAX_HOT <= 1024 && (HM_MAX_HOT & 255) == 0, "h takes the low 9 or 10 bits of a table entry");
-/* bucket of zoom-zb tile t (t < 2^22: zb <= 11) */
-__host__ __device__ inline uint32_t hm_hot_bucket(uint32_t t)
+static_assert(HM_MAX_HOT <= 1024 && (HM_MAX_HOT & 255) == 0, "hot tiles");
+/* bucket of zoom-zb tile (rs, cs), zb <= HM_HOT_BBITS */
+__host__ __device__ inline uint32_t hm_hot_bucket(uint32_t rs, uint32_t cs)
 {
-    return ((t & 0xFFFFFFu) * 0x9E3779u) >> (32 - HM_HOT_BBITS);   /* 24-bit product: v_mul_u32_u24, full rate */
+    return (rs * HM_HOT_MULT + cs) & (HM_HOT_BUCKETS - 1u);   /* v_mad_u32_u24 */
 }
-static_assert(HM_HOT_BUCKETS == 1 << HM_HOT_BBITS && (HM_HOT_WAYS == 2 || HM_HOT_WAYS == 4), "hot-tile table");
+static_assert(HM_HOT_BUCKETS == 1 << HM_HOT_BBITS, "hot-tile table");
 /* level-1 (digit, shard) arrays (fill, rbase, rcap) are shard-major: the
  * digits one wave reserves for sit in consecutive words, so its returning
  * atomics coalesce into a few 64-B requests instead of one per digit */
@@ -459,6 +460,7 @@ void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint
 /* small buckets: sort pass, scan, one reservation, emit pass (partial: 4096 u64) */
 void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial);
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents);
+void hm_launch_read_stream(hipStream_t s, const void* a, const void* b, uint64_t bytes_each, uint64_t* sink);
 void hm_launch_synth(hipStream_t s, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
                      const double* tab, int k);
 

@@ -173,5 +173,5 @@ class Tile:
         out = []
         for z in range(Tile.MAX_ZOOM, Tile.MIN_ZOOM, -1):
             p = device.project(lat, lon, z, raise_errors=True)
-            out.append(Tile.tile_id_from_row_column(int(p.row[0]), int(p.col[0]), z))
+            out.append(Tile.tile_id_from_row_column(int(p.row[0]), int(_cols(p)[0]), z))
         return out

@@ -306,6 +306,13 @@ int hm_format_bins(hm_ctx* ctx, const int64_t* zoom, const int64_t* row, const i
 int hm_synth(hm_ctx* ctx, int kind, uint64_t seed, int64_t start, int64_t n, double* lat, double* lon,
              const double* table, int k);
 
+/* Benchmark utility, not part of the reference boundary: read two device
+ * arrays of bytes_each bytes (a multiple of 16) once with 16-B loads -- the
+ * access shape of hm_count's level-1 kernel over lat/lon, with none of its
+ * arithmetic -- as bench.py's measured HBM read peak.  sink: device uint64_t
+ * array of 4096 words (written only on an improbable checksum).  Asynchronous. */
+int hm_bench_read(hm_ctx* ctx, const void* a, const void* b, int64_t bytes_each, uint64_t* sink);
+
 #ifdef __cplusplus
 }
 #endif

@@ -28,6 +28,7 @@ NAMES = {
                 "dbase", "copy"],
     "stamps2": ["start", "item+loads_issue+init", "count_rank(loads)", "barrier", "scan+run_atomics", "scatter",
                 "copy+runs"],
+    "stamps4": ["start", "issue+lds_setup", "project(loads)", "redo+count_rank", "reserve+scan", "stage", "copy"],
 }[VAR]
 K = len(NAMES)
 n = int(float(os.environ.get("HM_POINTS", "2.5e8")))

@@ -22,6 +22,11 @@ VARIANTS = {
     "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py (k_partition)
     "stamps1": ["HM_STAMPS=2"],              # k_project_partition
     "stamps2": ["HM_STAMPS=3"],              # k_partition_fr
+    "stamps4": ["HM_STAMPS=4"],              # k_l1_fast
+    "l1old": ["HM_L1_FAST=0"],               # level 1 through k_project_partition (round 3)
+    "l1m3": ["HM_L1_MERGE_MIN=3"],
+    "l1m12": ["HM_L1_MERGE_MIN=12"],
+    "l1nomerge": ["HM_L1_MERGE_MIN=65"],
     # tuning knobs (compile-time macros of the shipped sources)
     "noskew": ["HM_SKEW_CUR=0"],
     "p1_512x8": ["HM_P1_PPT=8"],
