@@ -823,7 +823,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 ENSURE(B_SLOTS, cap * 4, slots);
                 ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
                 ba.slots = slots;
-                ba.nslots = (uint32_t*)(ctx->state + ST_NSLOTS);
+                ba.nslots = ctx->state + ST_NSLOTS;
                 ba.slot_bucket = slot_bucket;
             }
             unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
@@ -1165,7 +1165,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             ENSURE(B_SLOTS, cap * 4, slots);
             ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
             ca.slots = slots;
-            ca.nslots = (uint32_t*)(ctx->state + ST_NSLOTS);
+            ca.nslots = ctx->state + ST_NSLOTS;
             ca.slot_bucket = slot_bucket;
         }
         hm_launch_compact(s, ca);

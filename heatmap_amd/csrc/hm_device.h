@@ -83,9 +83,21 @@ __device__ __forceinline__ uint32_t hm_wave_sum(uint32_t v)
     return v;
 }
 
+/* Workgroup barrier that orders LDS only: __syncthreads() also releases
+ * global memory, i.e. waits (vmcnt(0)) for every global load and store the
+ * wave has in flight -- prefetched points included.  For kernels whose waves
+ * share data through LDS alone. */
+__device__ __forceinline__ void hm_lds_barrier()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 /* Block-wide exclusive scan of one value per thread; returns the block total
- * in *total.  `scratch` needs (blockDim/64 + 1) u32 of LDS. */
-template <int THREADS>
+ * in *total.  `scratch` needs (blockDim/64 + 1) u32 of LDS.  LDS_ONLY: the
+ * barriers are hm_lds_barrier(). */
+template <int THREADS, bool LDS_ONLY = false>
 __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scratch, uint32_t* total)
 {
     constexpr int NW = THREADS / 64;
@@ -93,17 +105,17 @@ __device__ __forceinline__ uint32_t hm_block_excl_scan(uint32_t v, uint32_t* scr
     const int w = threadIdx.x >> 6;
     uint32_t inc = hm_wave_incl_scan(v);
     if (lane == 63) scratch[w] = inc;
-    __syncthreads();
+    if (LDS_ONLY) hm_lds_barrier(); else __syncthreads();
     if (w == 0) {
         uint32_t s = lane < NW ? scratch[lane] : 0u;
         uint32_t si = hm_wave_incl_scan(s);
         if (lane < NW) scratch[lane] = si - s;
         if (lane == NW - 1) scratch[NW] = si;
     }
-    __syncthreads();
+    if (LDS_ONLY) hm_lds_barrier(); else __syncthreads();
     uint32_t r = scratch[w] + inc - v;
     *total = scratch[NW];
-    __syncthreads();
+    if (LDS_ONLY) hm_lds_barrier(); else __syncthreads();
     return r;
 }
 
@@ -203,8 +215,11 @@ __device__ __forceinline__ uint32_t hm_lds_claim(uint32_t* cur, uint32_t dummy, 
 __device__ __forceinline__ void hm_lds_count_fast(uint32_t* hist, uint32_t dummy_lane, uint32_t key, bool valid)
 {
     const uint32_t k0 = __builtin_amdgcn_readfirstlane(key);
-    const uint64_t m = __ballot(valid & (key == k0));
-    if (__popcll(m) > HM_MERGE_MIN) {
+    /* (the raw ballot: __ballot materialises the predicate in a VGPR first;
+     * a 32-bit popcount compare stays on the scalar unit) */
+    const uint64_t m = __builtin_amdgcn_ballot_w64(key == k0) & __builtin_amdgcn_ballot_w64(valid);
+    if ((uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32)) >
+        HM_MERGE_MIN) {
         const int l = __ffsll((unsigned long long)m) - 1;
         const bool same = (m >> hm_lane()) & 1ull;
         const bool lead = hm_lane() == l;

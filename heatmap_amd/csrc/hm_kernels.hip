@@ -115,6 +115,14 @@ __device__ __forceinline__ void hm_exotic_append(const HmExotic& x, bool p, int6
 }
 
 
+/* a value the compiler must recompute where it is used (keeps per-lane
+ * 64-bit addresses from being hoisted out of a loop and spilled) */
+__device__ __forceinline__ uint32_t hm_opaque(uint32_t x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
+
 /* hot-tile lookup of zoom-zb tile (rs, cs) in the LDS table image: h when the
  * tile is hot, >= 2^16 otherwise (hm_pipeline.h) */
 __device__ __forceinline__ uint32_t hm_hot_find(const uint2* tab, uint32_t rs, uint32_t cs)
@@ -141,12 +149,16 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
     /* the projection's polynomial table; after the projection it holds, per
      * digit, (region position - stage offset) */
     __shared__ double tab[HM_YTAB_N];
-    static_assert(sizeof(OutT) * HM_T1 >= HM_HOT_SLOTS * 4, "the hot-tile table lives in the stage");
+    /* the hot-tile table lives in the stage and the region info in sdig when
+     * they fit (8192-point tiles), else in arrays of their own */
+    constexpr bool HSEP = sizeof(OutT) * HM_T1 < HM_HOT_SLOTS * 4;
+    constexpr bool RSEP = sizeof(uint16_t) * HM_T1 < HM_D1 * sizeof(uint2);
+    __shared__ __attribute__((aligned(16))) uint32_t hsep[HSEP ? HM_HOT_SLOTS : 4];
+    __shared__ __attribute__((aligned(8))) uint2 rsep[RSEP ? HM_D1 : 1];
     static_assert(sizeof(double) * HM_YTAB_N >= HM_D1 * 4, "dbase lives in the polynomial table");
-    uint4* const hsh4 = (uint4*)stage;
+    uint4* const hsh4 = HSEP ? (uint4*)hsep : (uint4*)stage;
     uint32_t* const dbase = (uint32_t*)tab;
-    uint2* const rinfo = (uint2*)sdig;
-    static_assert(sizeof(uint16_t) * HM_T1 >= HM_D1 * sizeof(uint2), "region info lives in sdig");
+    uint2* const rinfo = RSEP ? rsep : (uint2*)sdig;
     constexpr bool FROM_TILES = MODE == 1;
     const int tid = threadIdx.x;
     const int F = 1 << a.dbits;
@@ -215,12 +227,11 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         rbase2[q][1] = lv ? a.rbase[s1] : 0u;
     }
     /* the hot-tile table, also ahead of the points (stored to LDS below) */
-    static_assert(HM_HOT_SLOTS == 8 * HM_P1_THREADS, "the table is two uint4 per thread");
-    uint4 hv0 = make_uint4(0u, 0u, 0u, 0u), hv1 = hv0;   /* (no array: it would live in scratch) */
-    if (H) {
-        hv0 = ((const uint4*)a.hot_hash)[tid];
-        hv1 = ((const uint4*)a.hot_hash)[HM_P1_THREADS + tid];
-    }
+    constexpr int HV = HM_HOT_SLOTS / 4 / HM_P1_THREADS;
+    static_assert(HM_HOT_SLOTS == 4 * HV * HM_P1_THREADS, "the table is HV uint4 per thread");
+    uint4 hv[HV];
+#pragma unroll
+    for (int j = 0; j < HV; j++) hv[j] = H ? ((const uint4*)a.hot_hash)[j * HM_P1_THREADS + tid] : make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_sched_barrier(0);
     /* issue every load of the tile before any arithmetic: 16 points x 16 B per
      * lane in flight (double2 = two consecutive points of one array).  Full
@@ -278,8 +289,8 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
         rinfo[d] = make_uint2(sh ? rbase2[q][1] : rbase2[q][0], ((sh ? rcap2[q][1] : rcap2[q][0]) << 1) | sh);
     }
     if (H) {
-        hsh4[tid] = hv0;
-        hsh4[HM_P1_THREADS + tid] = hv1;
+#pragma unroll
+        for (int j = 0; j < HV; j++) hsh4[j * HM_P1_THREADS + tid] = hv[j];
     }
     if (!FROM_TILES) {
 #pragma unroll
@@ -554,10 +565,14 @@ static_assert(HM_L1_CW >= HM_L1_SLOTS + 64 && HM_L1_CW % 64 == 0, "count and del
 static_assert(HM_L1_SLOTS % HM_P1_THREADS == 0, "slots per thread");
 
 #ifndef HM_L1_FAST
-#define HM_L1_FAST 1
+#define HM_L1_FAST 1                        /* 0: k_project_partition, 1: k_l1_fast */
+#endif
+#ifndef HM_L1_WAVES
+#define HM_L1_WAVES 4                       /* k_l1_fast: waves per SIMD its registers allow (4: 2 blocks of 8 waves per CU) */
 #endif
 template <typename OutT>
-__global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
+__global__ __launch_bounds__(HM_P1_THREADS) __attribute__((amdgpu_waves_per_eu(HM_L1_WAVES, HM_L1_WAVES))) void
+k_l1_fast(HmPart1Args a)
 {
     /* staged (key, destination), + one pad entry per lane for points that
      * stage nothing; during the projection its first 32 KB hold the
@@ -568,16 +583,15 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
     __shared__ uint32_t cw[2 * HM_L1_CW];
     __shared__ uint32_t scr[HM_P1_THREADS / 64 + 1];
     __shared__ uint32_t s_over;
-    /* the polynomial table plus one poison row (HM_YTAB_ROWS): NaN
-     * coefficients.  Rows 0-15 (polar distance d in [4, 5): |lat| in [85, 86))
-     * are poisoned too, so the table itself rejects every point with |lat| >
-     * 85, |lat| > 90, NaN or inf (the clamped index lands on a poison row, the
-     * NaN fails the guard test): no latitude range test per point.  An
-     * accepted point has |lat| <= 85, Y in (0, 1), 0 < R < 2^Z. */
-    constexpr int YROWS = HM_YTAB_ROWS + 1, YPOISON = 16;
+    /* the polynomial table plus one poison row (HM_YTAB_ROWS, NaN
+     * coefficients) that the clamped index of |lat| > 90, NaN and inf lands
+     * on.  Points with 85.05 < |lat| <= 90 are rejected by the latitude test
+     * (an accepted point has Y in (0, 1), 0 < R < 2^Z).  (Poisoning the table
+     * down to |lat| > 85 instead saves that test but sends 0.06% of a uniform
+     * cloud to the exact path: 46x the deferred points, on one counter.) */
+    constexpr int YROWS = HM_YTAB_ROWS + 1;
     constexpr int YN = YROWS * HM_YTAB_STRIDE;
     static_assert(sizeof(double) * YN <= 16384 && HM_HOT_SLOTS * 4 <= 16384, "tables fit the stage");
-    static_assert(HM_YTAB_K == 6 && HM_YTAB_E0 == 2, "rows 0-15 are d in [4, 5)");
     double* const tab = (double*)ent;
     uint2* const hot2 = (uint2*)((char*)ent + 16384);
     const int tid = threadIdx.x;
@@ -618,7 +632,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
 #pragma unroll
     for (int q = 0; q < TPT; q++) {
         const int i = q * HM_P1_THREADS + tid;
-        tv[q] = i < YPOISON * HM_YTAB_STRIDE || i >= HM_YTAB_N ? __builtin_nan("") : c_ytab[i];
+        tv[q] = i >= HM_YTAB_N ? __builtin_nan("") : c_ytab[i];
     }
     uint32_t smk[PERD], rcap2[PERD][2], rbase2[PERD][2];
 #pragma unroll
@@ -633,11 +647,10 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
         rbase2[q][0] = lv ? a.rbase[s0] : 0u;
         rbase2[q][1] = lv ? a.rbase[s1] : 0u;
     }
-    uint4 hv0 = make_uint4(0u, 0u, 0u, 0u), hv1 = hv0;
-    if (H) {
-        hv0 = ((const uint4*)a.hot_hash)[tid];
-        hv1 = ((const uint4*)a.hot_hash)[HM_P1_THREADS + tid];
-    }
+    constexpr int HV = HM_HOT_SLOTS / 4 / HM_P1_THREADS;
+    uint4 hv[HV];
+#pragma unroll
+    for (int j = 0; j < HV; j++) hv[j] = H ? ((const uint4*)a.hot_hash)[j * HM_P1_THREADS + tid] : make_uint4(0u, 0u, 0u, 0u);
     __builtin_amdgcn_sched_barrier(0);
     double2 la[HM_P1_PPT / 2], lo[HM_P1_PPT / 2];
     {
@@ -652,15 +665,15 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
     for (int i = tid; i < HM_L1_CW; i += HM_P1_THREADS) cw[i] = 0;
     if (tid == 0) s_over = 0;
     if (H) {
-        ((uint4*)hot2)[tid] = hv0;
-        ((uint4*)hot2)[HM_P1_THREADS + tid] = hv1;
+#pragma unroll
+        for (int j = 0; j < HV; j++) ((uint4*)hot2)[j * HM_P1_THREADS + tid] = hv[j];
     }
 #pragma unroll
     for (int q = 0; q < TPT; q++) {
         const int i = q * HM_P1_THREADS + tid;
         if (i < YN) tab[i] = tv[q];
     }
-    __syncthreads();
+    hm_lds_barrier();
     HM_STAMP_M(4, 1);
     const int hb = a.restbits >> 1;
     const uint32_t lowm = (1u << hb) - 1u;
@@ -693,7 +706,8 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
         /* column: y = (lon + 180) / 360 * 2^z within 2^(z-51.3); guard 2^(z-49) */
         const double y = fma(po, kz, c180);
         const double fc = __builtin_amdgcn_fract(y);
-        const bool ok = (int)(fabs(fr - 0.5) < ghalf) & (int)(fabs(po) < 180.0) & (int)(fabs(fc - 0.5) < ghalf2);
+        const bool ok = (int)(fabs(pa) <= HM_LAT_SQ) & (int)(fabs(fr - 0.5) < ghalf) & (int)(fabs(po) < 180.0) &
+                        (int)(fabs(fc - 0.5) < ghalf2);
         const uint32_t r = (uint32_t)(int32_t)R;   /* truncation = floor: R, y > 0 when ok */
         const uint32_t c = (uint32_t)(int32_t)y;
         const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFFu) != 0;
@@ -736,7 +750,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
     for (int k = 0; k < HM_P1_PPT; k++) {
         const uint32_t k0 = __builtin_amdgcn_readfirstlane(slot[k]);
         const uint64_t m = __builtin_amdgcn_ballot_w64(slot[k] == k0);
-        const uint32_t pm = (uint32_t)__builtin_popcountll(m);
+        const uint32_t pm = (uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32));
         uint32_t idx = slot[k], inc = 1u;
         if (pm >= HM_L1_MERGE_MIN) {
             merged |= 1u << k;
@@ -756,7 +770,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
                 if ((m >> hm_lane()) & 1ull) rank[k] = r0 + hm_mbcnt(m);
             }
     }
-    __syncthreads();
+    hm_lds_barrier();
     HM_STAMP_M(4, 3);
     /* reservations: one returning global atomic per non-empty (digit, shard) */
     uint32_t cnt[PERD], gpos[PERD];
@@ -769,16 +783,25 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
         gpos[q] = 0;
         if (cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1i(d, sh)], cnt[q]);
     }
-    /* stage offsets: cold slots (q >= 1) first, hot slots (q = 0) after them,
-     * from one scan of (cold count | hot count << 16) */
-    static_assert(HM_MAX_HOT == HM_P1_THREADS && PERD == 3, "slot q = 0 is the hot tiles");
+    /* stage offsets: cold slots (q >= QH) first, hot slots (q < QH) after
+     * them, from one scan of (cold count | hot count << 16) */
+    constexpr int QH = HM_MAX_HOT / HM_P1_THREADS;
+    static_assert(HM_MAX_HOT % HM_P1_THREADS == 0 && QH >= 1 && QH < PERD, "slots q < QH are the hot tiles");
+    uint32_t csum = 0, hsum = 0;
+#pragma unroll
+    for (int q = 0; q < PERD; q++) (q < QH ? hsum : csum) += cnt[q];
     uint32_t tot2;
-    const uint32_t pre = hm_block_excl_scan<HM_P1_THREADS>((cnt[1] + cnt[2]) | (cnt[0] << 16), scr, &tot2);
+    const uint32_t pre = hm_block_excl_scan<HM_P1_THREADS, true>(csum | (hsum << 16), scr, &tot2);
     const uint32_t C = tot2 & 0xFFFFu, total = C + (tot2 >> 16);
     uint32_t offq[PERD];
-    offq[1] = pre & 0xFFFFu;
-    offq[2] = offq[1] + cnt[1];
-    offq[0] = C + (pre >> 16);
+    {
+        uint32_t oc = pre & 0xFFFFu, oh = C + (pre >> 16);
+#pragma unroll
+        for (int q = 0; q < PERD; q++) {
+            offq[q] = q < QH ? oh : oc;
+            (q < QH ? oh : oc) += cnt[q];
+        }
+    }
     bool over = false;
 #pragma unroll
     for (int q = 0; q < PERD; q++) {
@@ -798,7 +821,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
         atomicOr(a.overflow, 1ull);
         s_over = 1;
     }
-    __syncthreads();
+    hm_lds_barrier();
     HM_STAMP_M(4, 4);
     /* staging, branch-free: a point that stages nothing writes its lane's pad entry */
 #pragma unroll
@@ -807,7 +830,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, 2) void k_l1_fast(HmPart1Args a)
         const uint32_t pos = slot[k] < HM_L1_SLOTS ? o + rank[k] : HM_T1 + (uint32_t)hm_lane();
         ent[pos] = make_uint2(key[k], dl + pos);
     }
-    __syncthreads();
+    hm_lds_barrier();
     HM_STAMP_M(4, 5);
     /* copy-out: a wave stores 64 consecutive staged keys -- cold keys in [0, C)
      * as OutT, hot keys in [C, total) as u16 (zb-relative); the kind tests
@@ -1178,7 +1201,7 @@ __global__ __launch_bounds__(1024) void k_level1_buckets(HmL1Args a)
         if (a.slots) {
             int32_t sl = -1;
             if (nit > 1) {
-                sl = (int32_t)atomicAdd(a.nslots, 1u);
+                sl = (int32_t)atomicAdd(a.nslots, 1ull);
                 a.slot_bucket[sl] = idx;
             }
             a.slots[idx] = sl;
@@ -2196,7 +2219,7 @@ __global__ __launch_bounds__(256) void k_compact(HmCompactArgs a)
                 const uint32_t nit = (uint32_t)(a.vals[c] & 0xFFFFFFFFull);
                 int32_t sl = -1;
                 if (nit > 1) {
-                    sl = (int32_t)atomicAdd(a.nslots, 1u);
+                    sl = (int32_t)atomicAdd(a.nslots, 1ull);
                     a.slot_bucket[sl] = idx;
                 }
                 a.slots[idx] = sl;
@@ -2273,6 +2296,59 @@ __device__ void hm_pyramid(T* v, int lg, int z_top, uint64_t prefix, const HmOut
     }
 }
 
+/* Emit the non-empty cells i in [0, n) of v (cells with zoom outside [zmin,
+ * zmax] skipped) with ONE output reservation per block, coalesced: wave w
+ * takes the 64-cell chunks w, w + NW, ...; a chunk's non-empty cells go to
+ * consecutive output positions (ballot + mbcnt), so one store instruction
+ * writes one contiguous run of keys and one of counts.  cell(i) -> (zoom,
+ * key) of cell i; the cells may be written in any order.  Every thread of
+ * the block must call. */
+template <int THREADS, typename CellF>
+__device__ void hm_emit_cells(const uint32_t* v, uint32_t n, CellF cell, const HmOut& o, uint32_t* scr,
+                              unsigned long long* sbase)
+{
+    constexpr int NW = THREADS / 64;
+    const int lane = hm_lane(), w = threadIdx.x >> 6;
+    uint32_t c = 0;
+    for (uint32_t i0 = (uint32_t)w * 64; i0 < n; i0 += NW * 64) {
+        const uint32_t i = i0 + lane;
+        int z = 0;
+        uint64_t k = 0;
+        if (i < n) cell(i, z, k);
+        const bool nz = i < n && v[i] != 0 && z >= o.zmin && z <= o.zmax;
+        c += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(nz));
+    }
+    if (lane == 0) scr[w] = c;
+    __syncthreads();
+    if (w == 0) {
+        const uint32_t x = lane < NW ? scr[lane] : 0u;
+        const uint32_t incl = hm_wave_incl_scan(x);
+        if (lane < NW) scr[lane] = incl - x;
+        if (lane == NW - 1) *sbase = incl ? atomicAdd(o.cursor, (unsigned long long)incl) : 0ull;
+    }
+    __syncthreads();
+    uint64_t base = *sbase + scr[w];
+    __syncthreads();
+    for (uint32_t i0 = (uint32_t)w * 64; i0 < n; i0 += NW * 64) {
+        const uint32_t i = i0 + lane;
+        int z = 0;
+        uint64_t k = 0;
+        uint32_t x = 0;
+        if (i < n) {
+            cell(i, z, k);
+            x = v[i];
+        }
+        const bool nz = x != 0 && z >= o.zmin && z <= o.zmax;
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+        const uint64_t pos = base + hm_mbcnt(m);
+        if (nz && pos < o.capacity) {
+            o.keys[pos] = k;
+            o.counts[pos] = x;
+        }
+        base += (uint32_t)__builtin_popcountll(m);
+    }
+}
+
 /* Bucket pyramid with two output reservations per block: level z_top (4^lg
  * cells in v) is emitted first; then levels z_top-1 .. z_top-lg+1 are built as
  * consecutive regions of v (the first in place), counted together, reserved
@@ -2284,7 +2360,10 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
 {
     const uint32_t n0 = 1u << (2 * lg);
     if (lg == 0) return v[0];   /* the bucket is the zoom-z_top cell; k_pool emits it */
-    if (z_top >= o.zmin && z_top <= o.zmax) hm_emit_level<uint32_t, THREADS>(v, n0, z_top, prefix, lg, o, scr, sbase);
+    hm_emit_cells<THREADS>(v, n0, [&](uint32_t i, int& z, uint64_t& k) {
+        z = z_top;
+        k = hm_cell_key(z_top, prefix, lg, i);
+    }, o, scr, sbase);
     __syncthreads();
     /* level z_top-1 in place into v[0 .. n0/4) */
     uint32_t n = n0 >> 2;
@@ -2318,65 +2397,45 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
         end += m;
         n = m;
     }
-    /* v[off[lg]] is the bucket total (zoom z_top - lg); count levels 1..lg-1 */
+    /* v[off[lg]] is the bucket total (zoom z_top - lg); emit levels 1..lg-1 */
     const uint64_t total = v[off[lg]];
-    const uint32_t per = (end + THREADS - 1) / THREADS;
-    const uint32_t i0 = threadIdx.x * per, i1 = min(i0 + per, off[lg]);
-    uint32_t c = 0;
-    for (uint32_t i = i0; i < i1; i++) {
+    hm_emit_cells<THREADS>(v, off[lg], [&](uint32_t i, int& z, uint64_t& key) {
         int k = 1;
         while (k < lg - 1 && i >= off[k + 1]) k++;
-        const int z = z_top - k;
-        c += (v[i] != 0 && z >= o.zmin && z <= o.zmax);
-    }
-    uint32_t tot;
-    uint32_t pos = hm_block_excl_scan<THREADS>(c, scr, &tot);
-    if (tot) {
-        if (threadIdx.x == 0) *sbase = atomicAdd(o.cursor, (unsigned long long)tot);
-        __syncthreads();
-        const uint64_t base = *sbase;
-        for (uint32_t i = i0; i < i1; i++) {
-            int k = 1;
-            while (k < lg - 1 && i >= off[k + 1]) k++;
-            const int z = z_top - k;
-            const uint32_t x = v[i];
-            if (x != 0 && z >= o.zmin && z <= o.zmax) {
-                const uint64_t q = base + pos;
-                if (q < o.capacity) {
-                    o.keys[q] = hm_cell_key(z, prefix, lg - k, i - off[k]);
-                    o.counts[q] = x;
-                }
-                pos++;
-            }
-        }
-    }
+        z = z_top - k;
+        key = hm_cell_key(z, prefix, lg - k, i - off[k]);
+    }, o, scr, sbase);
     __syncthreads();
     return total;
 }
 
-/* ------------------------------------------------------------------------ */
-/* final level: dense 128x128 LDS histogram per zoom-zb bucket               */
-/* ------------------------------------------------------------------------ */
-
+/* Final level, dense buckets: one block per <= HM_TA-key work item counts the
+ * item's u16 keys in an LDS 2^lg x 2^lg histogram.  The rows are padded to
+ * 2^lg + 8 words (cell (r, c) at r (2^lg + 8) + c: a cluster's cells in one
+ * column fall in different banks, the row stride no longer being a multiple
+ * of the 64 banks); the padding is squeezed out before the pyramid.  A
+ * single-item bucket emits its pyramid; an item of a multi-item bucket adds
+ * its histogram into the bucket's slot and k_aggregate_merged emits it. */
+#define HM_AG_ROW(lg) ((1u << (lg)) + 8u)
+#define HM_AG_PADDED (128u * (128u + 8u))
+static_assert(HM_AG_LG == 7 && HM_AG_CELLS == 128 * 128, "padded histogram");
 __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
 {
-    __shared__ uint32_t grid[HM_AG_CELLS + 64];   /* + 64 dummy words (hm_lds_count) */
+    __shared__ uint32_t grid[HM_AG_PADDED + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
     __shared__ HmRunLds<256> L;
     const int tid = threadIdx.x;
-    const uint32_t ncell = 1u << (2 * a.lg);
-    for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) grid[i] = 0;
+    const uint32_t side = 1u << a.lg, ncell = side * side, npad = side * HM_AG_ROW(a.lg);
+    for (uint32_t i = tid; i < npad; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
     if (hm_block_id() >= a.items) return;   /* block-uniform */
     const HmItem it = hm_item(a.B, hm_block_id());
-    /* HM_AG_SKEW: counted at skewed slots (hm_skew), un-skewed before the
-     * pyramid (for column-clustered keys) */
     struct {
         uint32_t* grid;
         uint32_t dummy;
         int lg;
-        __device__ __forceinline__ uint32_t sl(uint32_t k) { return HM_AG_SKEW ? hm_skew(k, lg) : k; }
+        __device__ __forceinline__ uint32_t sl(uint32_t k) { return k + ((k >> lg) << 3); }   /* padded row */
         __device__ __forceinline__ void cnt(uint32_t k, bool v)
         {
             if (HM_AG_FAST)
@@ -2396,39 +2455,44 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
             cnt(x.w & 0xFFFFu, v);
             cnt(x.w >> 16, v);
         }
-    } f{grid, HM_AG_CELLS, a.lg};
+    } f{grid, HM_AG_PADDED, a.lg};
     hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);
-    if (HM_AG_SKEW) {
-        constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;
-        uint32_t x[CPT];
+    /* squeeze the padding out: cell i back at i */
+    constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;
+    uint32_t x[CPT];
 #pragma unroll
-        for (int k = 0; k < CPT; k++) {
-            const uint32_t i = k * HM_AG_THREADS + tid;
-            x[k] = i < ncell ? grid[hm_skew(i, a.lg)] : 0u;
-        }
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < CPT; k++) {
-            const uint32_t i = k * HM_AG_THREADS + tid;
-            if (i < ncell) grid[i] = x[k];
-        }
+    for (int k = 0; k < CPT; k++) {
+        const uint32_t i = k * HM_AG_THREADS + tid;
+        x[k] = i < ncell ? grid[i + ((i >> a.lg) << 3)] : 0u;
     }
-    __syncthreads();
-    if (it.nitems == 1) {
-        const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[it.bucket], a.out, scr, &sbase);
-        if (tid == 0) a.totals[it.bucket] = t;
-    } else {
+    if (it.nitems > 1) {
+        /* added into the bucket's slot (coalesced: consecutive threads,
+         * consecutive words).  Measured against a slot per item summed by
+         * k_aggregate_merged: the same on hotspots, and the skew cloud's one
+         * 3400-item bucket made that sum a 3.7 ms single-block tail */
         uint32_t* g = a.gslots + (uint64_t)a.B.slots[it.bucket] * HM_AG_CELLS;
         uint32_t s = 0;
-        for (uint32_t i = tid; i < ncell; i += HM_AG_THREADS) {
-            const uint32_t x = grid[i];
-            if (x) atomicAdd(&g[i], x);
-            s += x;
+#pragma unroll
+        for (int k = 0; k < CPT; k++) {
+            const uint32_t i = k * HM_AG_THREADS + tid;
+            if (i < ncell && x[k]) atomicAdd(&g[i], x[k]);
+            s += x[k];
         }
         s = hm_wave_sum(s);
         if (hm_lane() == 0 && s) atomicAdd(&a.totals[it.bucket], (unsigned long long)s);
+        return;
     }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < CPT; k++) {
+        const uint32_t i = k * HM_AG_THREADS + tid;
+        if (i < ncell) grid[i] = x[k];
+    }
+    __syncthreads();
+    const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[it.bucket], a.out, scr, &sbase);
+    if (tid == 0) a.totals[it.bucket] = t;
 }
+/* one block per multi-item bucket: its summed histogram, then its pyramid */
 __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
 {
     __shared__ uint32_t grid[HM_AG_CELLS];
@@ -2437,8 +2501,8 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
     const uint32_t ncell = 1u << (2 * a.lg);
     if (hm_block_id() >= a.nslots) return;
     const uint32_t b = a.slot_bucket[hm_block_id()];
-    const uint32_t* g = a.gslots + (uint64_t)hm_block_id() * HM_AG_CELLS;
-    for (uint32_t i = threadIdx.x; i < ncell; i += HM_AG_THREADS) grid[i] = g[i];
+    const uint4* g = (const uint4*)(a.gslots + (uint64_t)hm_block_id() * HM_AG_CELLS);
+    for (uint32_t v = threadIdx.x; v < ncell / 4; v += HM_AG_THREADS) ((uint4*)grid)[v] = g[v];
     __syncthreads();
     hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[b], a.out, scr, &sbase);
 }

@@ -121,7 +121,11 @@ __global__ __launch_bounds__(HM_ROUTE_THREADS) void k_cells_route(HmRouteArgs a)
             }
         } else {
             hm_lds_count(hist, HM_MAX_RANKS, o, sp);
-            if (a.wide && __any(sp && (a.counts[i] >> 32) != 0ull) && (tid & 63) == 0)
+            /* wide: a count needs 64 bits, or (10-byte records) a key does not
+             * fit 48 bits (zoom > 21, row or column >= 2^21) */
+            const bool kw = a.rec_out && (z > 21 || ((k >> 29) & 0x1FFFFFFFull) >= (1ull << 21) ||
+                                          (k & 0x1FFFFFFFull) >= (1ull << 21));
+            if (a.wide && __any(sp && ((a.counts[i] >> 32) != 0ull || kw)) && (tid & 63) == 0)
                 atomicOr(a.wide, 1ull);
         }
     }

@@ -91,9 +91,6 @@ __host__ __device__ inline uint32_t hm_l1i(uint32_t d, uint32_t sh) { return sh 
 #ifndef HM_AG_FAST
 #define HM_AG_FAST 1                        /* k_aggregate: hm_lds_count_fast (merge only wave-heavy keys) */
 #endif
-#ifndef HM_AG_SKEW
-#define HM_AG_SKEW 0                        /* 1: k_aggregate counts at hm_skew slots (0 measured 0.09 ms faster on hotspots, neutral on skew) */
-#endif
 #ifndef HM_TA
 #define HM_TA (1u << 18)                    /* keys per aggregation work item */
 #endif
@@ -284,7 +281,7 @@ struct HmL1Args {
     uint32_t* child_begin;
     uint64_t* total;           /* count << 32 | items */
     int32_t* slots;            /* last level only */
-    uint32_t* nslots;
+    unsigned long long* nslots;   /* multi-item buckets (their merge slots) */
     uint32_t* slot_bucket;
     const uint8_t* hotparent;  /* digits that are buckets for their hot children alone (or null) */
     uint32_t* d2b;             /* digit -> bucket index (or null) */
@@ -347,7 +344,7 @@ struct HmCompactArgs {
     uint32_t* child_begin;
     uint32_t* c2b;          /* [nchildren] or NULL: bucket index of each kept child */
     int32_t* slots;         /* last level only */
-    uint32_t* nslots;
+    unsigned long long* nslots;   /* multi-item buckets (their merge slots) */
     uint32_t* slot_bucket;
 };
 
@@ -365,7 +362,7 @@ struct HmAggArgs {
     unsigned long long* spbase; /* output position of the small buckets' region */
     uint32_t spbatch;           /* consecutive buckets per wave step (power of 2, <= 64) */
     unsigned long long* totals;
-    uint32_t* gslots;
+    uint32_t* gslots;           /* [nslots][HM_AG_CELLS]: a multi-item bucket's summed histogram */
     const uint32_t* slot_bucket;
     HmOut out;
 };

@@ -240,6 +240,15 @@ def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, de
             b = free.get()
             if b is None:
                 break
+            # buffers the merge grew were allocated on its side stream: tell the
+            # caching allocator the count's stream uses them too, so a later
+            # growth does not hand their memory to the side stream while this
+            # stream's count may still write it
+            cur = torch.cuda.current_stream()
+            for name in ("keys", "counts", "xcells"):
+                t = getattr(b, name, None)
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(cur)
             m, b = count(b)
             if ctx is not None:
                 stages.append(ctx.last_stats()[1][:5])

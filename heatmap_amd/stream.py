@@ -255,7 +255,12 @@ class StreamingHeatmap:
         torch = self._torch
         self.ctx.bind_stream()
         span = SPANS[timespan]
-        cap = max(1024, self._log_capacity())   # >= the log's cells >= the rollup's
+        # start from the last rollup of this kind (the log's capacity doubles as
+        # batches arrive and can far exceed the distinct cells): a short
+        # estimate costs one HM_E_CAPACITY retry with the exact size
+        memo = self.__dict__.setdefault("_rollup_n", {})
+        mk = (span, bool(merge_groups), int(select))
+        cap = min(max(1024, self._log_capacity()), max(1024, int(memo.get(mk, 1 << 20) * 1.25) + 1024))
         dev = "cuda:%d" % self.device_index
         while True:
             keys = torch.empty(cap, dtype=torch.int64, device=dev)
@@ -271,6 +276,7 @@ class StreamingHeatmap:
                 continue
             if rc != _lib.HM_OK:
                 _lib.raise_for(rc)
+            memo[mk] = n.value
             return n.value, keys, counts, groups, periods
 
     def rollup(self, timespan: str = "alltime", merge_groups: bool = True, select: int = -1):

@@ -254,7 +254,9 @@ int hm_stream_destroy(hm_stream* s);
  *                    HM_CELLS_REC10 packs each cell into keys_out as one
  *                    10-byte record (counts_out unused), so ONE all-to-all of
  *                    10 B per cell moves keys and counts (16 B in round 2);
- *                    with u32 counts (REC10, U32) a count >= 2^32 returns
+ *                    with u32 counts (REC10, U32) a count >= 2^32 -- or,
+ *                    for REC10, a sparse key beyond 48 bits (zoom > 21, row
+ *                    or column >= 2^21) -- returns
  *                    HM_E_WIDE after filling everything else (the caller's
  *                    ranks then agree to route again as HM_CELLS_U64: a rank's
  *                    cells count fewer points than it holds, so only shards

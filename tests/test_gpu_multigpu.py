@@ -71,6 +71,22 @@ def test_route_narrow_flags_wide_counts(gpu):
     assert int(sc[sk == keys[i]].item()) == (1 << 33) + 7
 
 
+def test_route_narrow_flags_wide_keys(gpu):
+    """narrow routing of sparse keys beyond the 10-byte record's 48 bits (a
+    zoom-22 cell; a row of 2^21): HM_E_WIDE, as the CPU stand-in flags; routed
+    again wide, the keys arrive intact."""
+    keys, counts = _cells(50_000, 4)
+    for bad in ((22 << 58) | (5 << 29) | 7, (20 << 58) | ((1 << 21) << 29) | 3):
+        k2 = torch.cat([keys, torch.tensor([bad], dtype=torch.int64)])
+        c2 = torch.cat([counts, torch.tensor([3], dtype=torch.int64)])
+        ops = multigpu.DeviceOps(0)
+        _, _, sent, wide = ops.route(k2.cuda(), c2.cuda(), 4, 10, narrow=True)
+        _, _, rsent, rwide = TorchOps.route(k2, c2, 4, 10, narrow=True)
+        assert wide and rwide and sent == rsent
+        _, parts, _, wide2 = ops.route(k2.cuda(), c2.cuda(), 4, 10, narrow=False)
+        assert not wide2 and int((parts[0][0].cpu() == bad).sum()) == 1
+
+
 def test_merge_narrow_counts(gpu):
     """hm_cells_merge(_runs) of int32 counts (the exchange's width) sums into
     int64, past 2^32 where many ranks' counts of one cell add up."""

@@ -66,7 +66,9 @@ class TorchOps:
         rec = torch.stack([sk >> 58, (sk >> 29) & M29, sk & M29], 1)
         own = multigpu.record_owner(rec, ws)
         o = torch.argsort(own, stable=True)
-        wide = narrow and bool((sc >> 32).any())
+        # a count past 32 bits, or a key past the record's 48 (zoom > 21, row or col >= 2^21)
+        zk, rk, ck = sk >> 58, (sk >> 29) & M29, sk & M29
+        wide = narrow and bool((sc >> 32).any() or (zk > 21).any() or (rk >= 1 << 21).any() or (ck >= 1 << 21).any())
         parts = [(multigpu.pack_records(sk[o], sc[o]), 10)] if narrow else [(sk[o], 1), (sc[o], 1)]
         return grid, parts, torch.bincount(own, minlength=ws).tolist(), wide
 

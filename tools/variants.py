@@ -27,6 +27,9 @@ VARIANTS = {
     "l1m3": ["HM_L1_MERGE_MIN=3"],
     "l1m12": ["HM_L1_MERGE_MIN=12"],
     "l1nomerge": ["HM_L1_MERGE_MIN=65"],
+    "t4k512": ["HM_P1_PPT=8", "HM_L1_WAVES=6"],            # 4096-point tiles, 3 blocks of 8 waves per CU
+    "t4k256": ["HM_P1_THREADS=256", "HM_L1_WAVES=3"],      # 4096-point tiles, 3 blocks of 4 waves per CU
+    "m16": ["HM_L1_MERGE_MIN=16"],
     # tuning knobs (compile-time macros of the shipped sources)
     "noskew": ["HM_SKEW_CUR=0"],
     "p1_512x8": ["HM_P1_PPT=8"],
@@ -51,9 +54,6 @@ VARIANTS = {
     "lz3": ["HM_LEVEL_ZOOMS=3"],            # levels z5, z8, z11 (zmax 18)
     "split256": ["HM_SPW_SPLIT=256"],       # narrow small-bucket instantiation up to 256 keys
     "sp1024": ["HM_SP_MAX=1024"],           # buckets of 1025-2048 keys to k_aggregate
-    "hot2": ["HM_HOT_WAYS=2"],              # 2-way hot-tile buckets (8-B read)
-    "agns": ["HM_AG_SKEW=0"],               # k_aggregate without the skewed slots
-    "hot2agns": ["HM_HOT_WAYS=2", "HM_AG_SKEW=0"],
     "agslow": ["HM_AG_FAST=0"],             # k_aggregate with the lane-0 merge on every key
     "agm4": ["HM_MERGE_MIN=4"],
     "agm16": ["HM_MERGE_MIN=16"],
@@ -74,6 +74,18 @@ PATCHES = {
     "noatom1": [("hm_kernels.hip", "if (d < F && cnt[q]) gpos[q] = atomicAdd(&a.fill[slot[q]], cnt[q]);",
                  "if (d < F && cnt[q]) gpos[q] = 0;")],
 }
+# k_l1_fast (level 1, whole tiles): compute without the point loads, loads
+# without the key stores, and no region reservation atomics
+PATCHES["l1noload"] = [("hm_kernels.hip", """            la[k] = lat2[k * HM_P1_THREADS + tid];
+            lo[k] = lon2[k * HM_P1_THREADS + tid];""", """            la[k] = make_double2(40.0 + 1e-7 * (double)(tid + 1024 * k), 40.0 + 1.3e-7 * (double)(tid + 1024 * k));
+            lo[k] = make_double2(-122.0 + 1e-7 * (double)(tid + 1024 * k), -122.0 + 1.7e-7 * (double)(tid + 1024 * k));""")]
+PATCHES["l1nostore"] = [
+    ("hm_kernels.hip", "auto put_cold = [&](uint2 e) { *(OutT*)(outb + (uint64_t)e.y * sizeof(OutT)) = (OutT)e.x; };",
+     "auto put_cold = [&](uint2 e) { if (e.x == 0xFFFFFFFFu && e.y == 0x1234567u) *(OutT*)outb = (OutT)e.x; };"),
+    ("hm_kernels.hip", "        *(uint16_t*)(houtb + (uint64_t)e.y * 2u) = (uint16_t)hk;",
+     "        if (hk == 0xFFFFFFFFu && e.y == 0x1234567u) *(uint16_t*)houtb = (uint16_t)hk;")]
+PATCHES["l1noatom"] = [("hm_kernels.hip", "        if (cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1i(d, sh)], cnt[q]);",
+                        "        if (cnt[q]) gpos[q] = 0;")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
