@@ -325,9 +325,11 @@ def main():
         step_ms_ev = dt / args.steps * 1e3     # host clock, max over ranks: the steps overlap on two streams
         cells_rank = int(t[4]) // ws           # cells one rank's count emits (before the exchange)
         dist_info = {"points_per_gpu": per, "local_ms_per_step": float(tmax[2]),
+                     "n1_rate_at_this_size": per / (float(tmax[2]) * 1e-3),
                      "merge_ms_per_step": float(tmax[3]), "merge_ms_mean_over_ranks": float(t[3]) / ws,
                      "efficiency_vs_local": float(tmax[2]) / step_ms_ev,
-                     "note": "local = the same count on this rank's shard with no exchange (max over ranks); "
+                     "note": "local = the same count on this rank's shard with no exchange (max over ranks): "
+                             "n1_rate_at_this_size is the one-GPU rate at this per-GPU size (points/s); "
                              "merge = route + RCCL reduce/all-to-all + owner merge of one step, host clock on the "
                              "merge thread, overlapped with the next step's count"}
     else:

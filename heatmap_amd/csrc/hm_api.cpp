@@ -148,7 +148,7 @@ enum {
     B_SLOTBKT, B_GSLOTS, B_SPCODES, B_DESC0,
     /* exotic list and the general path (hm_general.hip) */
     B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
-    B_GEN_S, B_GEN_END, B_GEN_CNT0, B_GEN_CNT1, B_GEN_HIST, B_GEN_OFF, B_GEN_ORAND, B_GL_GRP,
+    B_GEN_HIST, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
     B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS, B_MB_CNT2, B_MB_OFF2,
@@ -407,20 +407,18 @@ extern "C" int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int
 /* capacity).  Errors (tiles beyond the key's range) go to the error word.      */
 /* ------------------------------------------------------------------------ */
 static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint32_t* group, const int64_t* index,
-                     uint64_t n, int Z, int zmin, const HmGenEmit& e, uint64_t* total)
+                     uint64_t n, int Z, int zmin, const HmGenEmit& e, uint64_t* total, const double* lat = nullptr,
+                     const double* lon = nullptr, const uint8_t* keep = nullptr)
 {
     *total = 0;
     if (n == 0) return HM_OK;
     if (n >= (1ull << 32)) return HM_E_ARG;   /* radix ranks are u32 */
     hipStream_t s = ctx->stream;
     ulonglong2 *ka, *kb;
-    uint64_t *flag, *idx, *c, *S, *end, *cnt0, *cnt1, *partial, *tot, *hist, *off;
     unsigned long long* orand;
     ENSURE(B_GEN_KA, n * 16, ka);
     ENSURE(B_GEN_KB, n * 16, kb);
     ENSURE(B_GEN_ORAND, 4 * 8, orand);
-    ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
-    ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
     unsigned long long* up = ctx->host_state + ST_COUNT;
     HIPCHK(hm_sync(s));
     up[0] = 0;
@@ -428,65 +426,87 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     up[2] = ~0ull;
     up[3] = ~0ull;
     HIPCHK(hipMemcpyAsync(orand, up, 4 * 8, hipMemcpyHostToDevice, s));
-    HmGenArgs ga;
-    ga.row = row;
-    ga.col = col;
-    ga.group = group;
-    ga.index = index;
-    ga.n = n;
-    ga.Z = Z;
-    ga.keys = ka;
-    ga.orand = orand;
-    ga.err_word = ctx->state + ST_ERR;
-    hm_launch_gen_keys(s, ga);
+    if (lat) {
+        /* points: projected straight into keys (the kept ones, compacted) */
+        ctx->host_state[ST_XCOUNT] = 0;
+        HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, sizeof(unsigned long long), s));
+        hm_launch_project_keys(s, lat, lon, keep, group, (int64_t)n, Z, ka, ctx->state + ST_XCOUNT,
+                               ctx->state + ST_ERR, orand);
+    } else {
+        HmGenArgs ga;
+        ga.row = row;
+        ga.col = col;
+        ga.group = group;
+        ga.index = index;
+        ga.n = n;
+        ga.Z = Z;
+        ga.keys = ka;
+        ga.orand = orand;
+        ga.err_word = ctx->state + ST_ERR;
+        hm_launch_gen_keys(s, ga);
+    }
     HIPCHK(hipGetLastError());
     unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
     HIPCHK(hipMemcpyAsync(down, orand, 4 * 8, hipMemcpyDeviceToHost, s));
     int st;
     if ((st = read_state(ctx))) return st;
     if ((st = take_error(ctx))) return st;
+    if (lat) {
+        n = ctx->host_state[ST_XCOUNT];
+        if (n == 0) return HM_OK;
+    }
     /* LSD passes over the digits that differ between keys */
     const unsigned __int128 var = ((((unsigned __int128)down[1]) << 64) | down[0]) ^
                                   ((((unsigned __int128)down[3]) << 64) | down[2]);
-    const uint64_t nt = hm_rx_tiles(n);
-    ENSURE(B_GEN_HIST, nt * 256 * 8, hist);
-    ENSURE(B_GEN_OFF, nt * 256 * 8, off);
-    ulonglong2 *cur = ka, *oth = kb;
-    for (int sh = 0; sh < 128; sh += 8) {
-        if (!(uint64_t)((var >> sh) & 0xFF)) continue;
-        hm_launch_rx_pass(s, cur, oth, n, sh, hist, off, partial, tot);
+    int shs[16], np = 0;
+    for (int sh = 0; sh < 128; sh += 8)
+        if ((uint64_t)((var >> sh) & 0xFF)) shs[np++] = sh;
+    uint8_t* rxs;
+    ENSURE(B_GEN_HIST, 256 + 16 * 2048 + hm_rx_os_tiles(n) * 2048, rxs);
+    ulonglong2* cur = hm_launch_rx_sort(s, ka, kb, n, shs, np, rxs);
+    ulonglong2* oth = cur == ka ? kb : ka;
+    HIPCHK(hipGetLastError());
+    /* zoom cascade (k_cascade): step k makes the zoom-(Z-k) cells and writes
+     * the records of zoom Z-k+1; a last launch writes the zmin records.  Item
+     * counts and record offsets stay on the device (one read-back at the end) */
+    const int K = Z - zmin + 1;
+    const uint64_t ntc = hm_cascade_tiles(n);
+    uint8_t* cs;
+    uint32_t *e0, *e1;
+    ENSURE(B_GEN_FLAG, 512 + ntc * 8, cs);
+    ENSURE(B_GEN_IDX, n * 4, e0);
+    ENSURE(B_GEN_C, n * 4, e1);
+    unsigned* tick = (unsigned*)cs;
+    uint32_t* mdev = (uint32_t*)(cs + 128);
+    unsigned long long* rbase = (unsigned long long*)(cs + 256);
+    static_assert(HM_MAX_ZOOM + 3 <= 32, "cascade state slots");
+    HIPCHK(hipMemsetAsync(cs, 0, 512 + ntc * 8, s));
+    HmCascArgs ca;
+    memset(&ca, 0, sizeof(ca));
+    ca.tstat = (uint64_t*)(cs + 512);
+    ca.e = e;
+    for (int k = 0; k <= K; k++) {
+        ca.kin = k ? oth : cur;
+        ca.ein = k ? (k & 1 ? e0 : e1) : nullptr;
+        ca.m_in = k ? mdev + (k - 1) : nullptr;
+        ca.m_host = n;
+        ca.shift = k ? 2 : 0;
+        ca.zin = Z - k + 1;
+        ca.emit = k > 0;
+        ca.kout = k ? cur : oth;
+        ca.eout = k & 1 ? e1 : e0;
+        ca.m_out = mdev + k;
+        ca.epoch = (uint64_t)k + 1;
+        ca.ticket = tick + k;
+        ca.rbase_in = k ? rbase + k : nullptr;
+        ca.rbase_out = k ? rbase + k + 1 : nullptr;
+        hm_launch_cascade(s, ca, n, k == K);
         HIPCHK(hipGetLastError());
-        std::swap(cur, oth);
+        if (k) std::swap(cur, oth);
     }
-    /* zoom cascade: level z = Z, Z-1, ..., zmin; cur holds the sorted keys */
-    ENSURE(B_GEN_FLAG, n * 8, flag);
-    ENSURE(B_GEN_IDX, n * 8, idx);
-    ENSURE(B_GEN_C, n * 8, c);
-    ENSURE(B_GEN_S, n * 8, S);
-    ENSURE(B_GEN_END, n * 8, end);
-    ENSURE(B_GEN_CNT0, n * 8, cnt0);
-    ENSURE(B_GEN_CNT1, n * 8, cnt1);
-    const uint64_t* cin = nullptr;
-    uint64_t m = n, emitted = 0;
-    for (int z = Z; z >= zmin; z--) {
-        const int sh = z == Z ? 0 : 2;
-        hm_launch_rle_prep(s, cur, cin, m, sh, flag, c);
-        hm_launch_scan(s, flag, m, partial, idx, tot + 0);
-        hm_launch_scan(s, c, m, partial, S, tot + 1);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hm_sync(s));
-        const uint64_t u = down[0];
-        uint64_t* cout = (cin == cnt0) ? cnt1 : cnt0;
-        hm_launch_rle_scatter(s, cur, m, sh, flag, idx, S, c, oth, end);
-        hm_launch_rle_emit(s, e, oth, end, u, z, cout, emitted, 1);
-        HIPCHK(hipGetLastError());
-        emitted += u;
-        std::swap(cur, oth);
-        cin = cout;
-        m = u;
-    }
-    *total = emitted;
+    HIPCHK(hipMemcpyAsync(down, rbase + K + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hm_sync(s));
+    *total = down[0];
     return HM_OK;
 }
 
@@ -502,20 +522,18 @@ static int count_fallback(hm_ctx* ctx, const double* lat, const double* lon, con
 {
     int st = reset_state(ctx);
     if (st) return st;
-    int64_t *row, *col, *idx;
-    ENSURE(B_X_ROW, (uint64_t)n * 8 + 8, row);
-    ENSURE(B_X_COL, (uint64_t)n * 8 + 8, col);
-    ENSURE(B_X_IDX, (uint64_t)n * 8 + 8, idx);
-    uint32_t* grp;
-    ENSURE(B_GL_GRP, (uint64_t)n * 4 + 4, grp);
-    if (rows)
+    int64_t *row = nullptr, *col = nullptr, *idx = nullptr;
+    if (rows) {
+        uint32_t* grp;
+        ENSURE(B_X_ROW, (uint64_t)n * 8 + 8, row);
+        ENSURE(B_X_COL, (uint64_t)n * 8 + 8, col);
+        ENSURE(B_X_IDX, (uint64_t)n * 8 + 8, idx);
+        ENSURE(B_GL_GRP, (uint64_t)n * 4 + 4, grp);
         hm_launch_tiles_list(ctx->stream, rows, cols, keep, nullptr, n, row, col, grp, idx, ctx->state + ST_XCOUNT);
-    else
-        hm_launch_project_list(ctx->stream, lat, lon, keep, nullptr, n, zmax, row, col, grp, idx,
-                               ctx->state + ST_XCOUNT, ctx->state + ST_ERR);
-    HIPCHK(hipGetLastError());
-    if ((st = read_state(ctx))) return st;
-    if ((st = take_error(ctx))) return st;
+        HIPCHK(hipGetLastError());
+        if ((st = read_state(ctx))) return st;
+        if ((st = take_error(ctx))) return st;
+    }
     HmGenEmit e;
     memset(&e, 0, sizeof(e));
     e.cells = xcells_out;
@@ -528,7 +546,11 @@ static int count_fallback(hm_ctx* ctx, const double* lat, const double* lon, con
     e.kcursor = ctx->state + ST_CURSOR;
     e.xcursor = ctx->state + ST_XCURSOR;
     uint64_t total = 0;
-    if ((st = gen_count(ctx, row, col, nullptr, idx, ctx->host_state[ST_XCOUNT], zmax, zmin, e, &total))) return st;
+    if (rows)
+        st = gen_count(ctx, row, col, nullptr, idx, ctx->host_state[ST_XCOUNT], zmax, zmin, e, &total);
+    else   /* points projected straight into keys */
+        st = gen_count(ctx, nullptr, nullptr, nullptr, nullptr, (uint64_t)n, zmax, zmin, e, &total, lat, lon, keep);
+    if (st) return st;
     if ((st = read_state(ctx))) return st;
     *n_out = (int64_t)ctx->host_state[ST_CURSOR];
     *nx_out = (int64_t)ctx->host_state[ST_XCURSOR];
@@ -1352,29 +1374,28 @@ static int grouped_impl(hm_ctx* ctx, const double* lat, const double* lon, const
     int st = reset_state(ctx);
     if (st) return st;
     if (n == 0) return HM_OK;
-    int64_t *row, *col, *idx;
-    uint32_t* grp;
-    ENSURE(B_X_ROW, (uint64_t)n * 8, row);
-    ENSURE(B_X_COL, (uint64_t)n * 8, col);
-    ENSURE(B_X_IDX, (uint64_t)n * 8, idx);
-    ENSURE(B_GL_GRP, (uint64_t)n * 4, grp);
-    if (rows)
-        hm_launch_tiles_list(ctx->stream, rows, cols, keep, group, n, row, col, grp, idx, ctx->state + ST_XCOUNT);
-    else
-        hm_launch_project_list(ctx->stream, lat, lon, keep, group, n, zmax, row, col, grp, idx,
-                               ctx->state + ST_XCOUNT, ctx->state + ST_ERR);
-    HIPCHK(hipGetLastError());
-    if ((st = read_state(ctx))) return st;
-    if ((st = take_error(ctx))) return st;
-    const uint64_t m = ctx->host_state[ST_XCOUNT];
     uint64_t total = 0;
     HmGenEmit e;
     memset(&e, 0, sizeof(e));
     e.cells = cells_out;
     e.capacity = (uint64_t)capacity;
     e.width = 5;
-    if ((st = gen_count(ctx, row, col, grp, idx, m, zmax, zmin, e, &total))) return st;
-    if ((st = read_state(ctx))) return st;
+    if (rows) {
+        int64_t *row, *col, *idx;
+        uint32_t* grp;
+        ENSURE(B_X_ROW, (uint64_t)n * 8, row);
+        ENSURE(B_X_COL, (uint64_t)n * 8, col);
+        ENSURE(B_X_IDX, (uint64_t)n * 8, idx);
+        ENSURE(B_GL_GRP, (uint64_t)n * 4, grp);
+        hm_launch_tiles_list(ctx->stream, rows, cols, keep, group, n, row, col, grp, idx, ctx->state + ST_XCOUNT);
+        HIPCHK(hipGetLastError());
+        if ((st = read_state(ctx))) return st;
+        if ((st = take_error(ctx))) return st;
+        st = gen_count(ctx, row, col, grp, idx, ctx->host_state[ST_XCOUNT], zmax, zmin, e, &total);
+    } else {   /* points projected straight into keys */
+        st = gen_count(ctx, nullptr, nullptr, group, nullptr, (uint64_t)n, zmax, zmin, e, &total, lat, lon, keep);
+    }
+    if (st) return st;
     *n_out = (int64_t)total;
     return total > (uint64_t)capacity ? HM_E_CAPACITY : HM_OK;
 }

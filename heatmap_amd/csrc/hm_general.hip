@@ -19,53 +19,17 @@
  * and the zoom cascade is a run-length reduction of the previous zoom's sorted
  * unique cells: zoom Z-k+1's cells shifted by 2 are non-decreasing.
  *
- * Radix sort: keys only, 8-bit digits, LSD, stable; digits that are the same
- * in every key (an OR/AND reduction taken while the keys are built) are
- * skipped.  A wave owns a tile of 1024 consecutive keys; its per-digit ranks
- * come from an 8-ballot match in tile order, so the scatter is stable.
+ * Radix sort: keys only, 8-bit digits, LSD, stable, one sweep per digit
+ * (k_rx_onesweep); digits that are the same in every key (an OR/AND
+ * reduction taken while the keys are built) are skipped.
  */
 #include <hip/hip_runtime.h>
+#include <utility>
 #include "hm_device.h"
 #include "hm_pipeline.h"
 #include "../../include/heatmap_amd.h"
 
-typedef unsigned __int128 hm_u128;
-
-__device__ __forceinline__ hm_u128 hm_ld128(const ulonglong2* p, uint64_t i)
-{
-    const ulonglong2 v = p[i];
-    return ((hm_u128)v.y << 64) | (hm_u128)v.x;
-}
-
-__device__ __forceinline__ void hm_st128(ulonglong2* p, uint64_t i, hm_u128 k)
-{
-    p[i] = make_ulonglong2((unsigned long long)k, (unsigned long long)(k >> 64));
-}
-
-/* 21 -> 42 bit spread / compact (Morton halves) */
-__device__ __forceinline__ uint64_t hm_spread21(uint64_t x)
-{
-    x &= 0x1FFFFFull;
-    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
-    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x << 2)) & 0x3333333333333333ull;
-    return (x | (x << 1)) & 0x5555555555555555ull;
-}
-
-__device__ __forceinline__ uint64_t hm_compact21(uint64_t x)
-{
-    x &= 0x5555555555555555ull;
-    x = (x | (x >> 1)) & 0x3333333333333333ull;
-    x = (x | (x >> 2)) & 0x0F0F0F0F0F0F0F0Full;
-    x = (x | (x >> 4)) & 0x00FF00FF00FF00FFull;
-    x = (x | (x >> 8)) & 0x0000FFFF0000FFFFull;
-    return (x | (x >> 16)) & 0x00000000FFFFFFFFull;
-}
-
-#define HM_GEN_SR_BIAS 16
-#define HM_GEN_SC_BITS 48
-#define HM_GEN_SC_BIAS (1ll << 47)
+#include "hm_genkey.h"
 
 /* ------------------------------------------------------------------------ */
 /* keys                                                                      */
@@ -79,16 +43,9 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
     const int Z = a.Z;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
         const int64_t r = a.row[i], c = a.col[i];
-        const int64_t sr = r >> Z, sc = c >> Z;
-        const uint64_t m = (hm_spread21((uint64_t)r & ((1ull << Z) - 1)) << 1) |
-                           hm_spread21((uint64_t)c & ((1ull << Z) - 1));
-        hm_u128 k = 0;
-        if (sr >= -HM_GEN_SR_BIAS && sr < HM_GEN_SR_BIAS && sc >= -HM_GEN_SC_BIAS && sc < HM_GEN_SC_BIAS) {
-            const uint64_t g = a.group ? (uint64_t)a.group[i] : 0ull;
-            const hm_u128 root = ((hm_u128)g << 53) | ((hm_u128)(uint64_t)(sr + HM_GEN_SR_BIAS) << 48) |
-                                 (hm_u128)(uint64_t)(sc + HM_GEN_SC_BIAS);
-            k = (root << (2 * Z)) | (hm_u128)m;
-        } else {
+        bool ok;
+        const hm_u128 k = hm_gen_key(r, c, a.group ? a.group[i] : 0u, Z, &ok);
+        if (!ok) {
             /* representable by the reference, beyond this path's key */
             const uint64_t src = a.index ? (uint64_t)a.index[i] : i;
             atomicMin(a.err_word, ((unsigned long long)src << 8) | (unsigned long long)HM_E_RANGE);
@@ -115,166 +72,396 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 }
 
 /* ------------------------------------------------------------------------ */
-/* LSD radix sort pass (keys only, stable)                                   */
-/* ------------------------------------------------------------------------ */
-
-#define HM_RX_WT 1024                 /* keys per wave tile */
-#define HM_RX_J (HM_RX_WT / 64)
-
-__device__ __forceinline__ uint32_t hm_rx_digit(hm_u128 k, int sh) { return (uint32_t)(k >> sh) & 0xFFu; }
-
-/* per wave tile: digit histogram, digit-major into hist[d * ntiles + t] */
-__global__ __launch_bounds__(256) void k_rx_hist(const ulonglong2* __restrict__ keys, uint64_t n, int sh,
-                                                 uint64_t ntiles, uint64_t* __restrict__ hist)
-{
-    __shared__ uint32_t h[4][256];
-    const int w = threadIdx.x >> 6, lane = hm_lane();
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + w;
-#pragma unroll
-    for (int q = 0; q < 4; q++) h[w][lane * 4 + q] = 0;
-    __syncthreads();
-    if (t < ntiles) {
-        for (int j = 0; j < HM_RX_J; j++) {
-            const uint64_t i = t * HM_RX_WT + (uint64_t)j * 64 + lane;
-            if (i < n) atomicAdd(&h[w][hm_rx_digit(hm_ld128(keys, i), sh)], 1u);
-        }
-    }
-    __syncthreads();
-    if (t < ntiles) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t d = lane * 4 + q;
-            hist[(uint64_t)d * ntiles + t] = h[w][d];
-        }
-    }
-}
-
-/* stable scatter: keys of a wave tile in index order; the lanes of one
- * 64-key step holding digit d are matched with 8 ballots, ranked by lane */
-__global__ __launch_bounds__(256) void k_rx_scatter(const ulonglong2* __restrict__ in, ulonglong2* __restrict__ out,
-                                                    uint64_t n, int sh, uint64_t ntiles, const uint64_t* __restrict__ off)
-{
-    __shared__ uint32_t base[4][256];
-    const int w = threadIdx.x >> 6, lane = hm_lane();
-    const uint64_t t = (uint64_t)blockIdx.x * 4 + w;
-    if (t < ntiles) {
-#pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const uint32_t d = lane * 4 + q;
-            base[w][d] = (uint32_t)off[(uint64_t)d * ntiles + t];
-        }
-    }
-    __syncthreads();
-    if (t >= ntiles) return;   /* wave-uniform */
-    for (int j = 0; j < HM_RX_J; j++) {
-        const uint64_t i = t * HM_RX_WT + (uint64_t)j * 64 + lane;
-        const bool v = i < n;
-        const hm_u128 k = v ? hm_ld128(in, i) : (hm_u128)0;
-        const uint32_t d = hm_rx_digit(k, sh);
-        uint64_t m = __ballot(v);
-#pragma unroll
-        for (int b = 0; b < 8; b++) {
-            const uint64_t bb = __ballot((d >> b) & 1u);
-            m &= ((d >> b) & 1u) ? bb : ~bb;
-        }
-        const uint32_t rank = hm_mbcnt(m);
-        const uint32_t p = base[w][d] + rank;
-        __builtin_amdgcn_wave_barrier();
-        if (v && rank == 0) base[w][d] = p + (uint32_t)__popcll(m);
-        __builtin_amdgcn_wave_barrier();
-        if (v) hm_st128(out, p, k);
-    }
-}
-
-/* ------------------------------------------------------------------------ */
 /* zoom cascade: run-length reduction of sorted cells                        */
 /* ------------------------------------------------------------------------ */
 
-/* head flags and counts of (key >> s) over a sorted list */
-__global__ __launch_bounds__(256) void k_rle_prep(const ulonglong2* __restrict__ keys, const uint64_t* __restrict__ cnt,
-                                                  uint64_t n, int s, uint64_t* __restrict__ flag, uint64_t* __restrict__ c)
-{
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        const hm_u128 k = hm_ld128(keys, i) >> s;
-        const bool head = i == 0 || (hm_ld128(keys, i - 1) >> s) != k;
-        flag[i] = head;
-        c[i] = cnt ? cnt[i] : 1ull;
-    }
-}
+/* One zoom step per launch.  The input is a sorted list of level-(z+1) cells
+ * (or, at the first step, the sorted raw keys, every one a point), each with
+ * its END: the inclusive prefix of the counts, so a cell's count is END[i] -
+ * END[i-1].  A zoom-z cell is key >> 2; its END is the END of the last fine
+ * cell of its run -- prefixes survive coarsening, so no count is ever summed.
+ * The step writes the unique zoom-z keys and their ENDs, compacted: a head's
+ * slot is the number of heads before it, from a block scan of head ballots
+ * and a decoupled look-back over the tiles (tiles taken in order from a
+ * ticket, so every predecessor is held by a running block).  In the same
+ * pass it writes the records of its input level (level z+1, at the running
+ * record offset + i).  Sizes stay on the device: the step reads its item
+ * count from the previous step's m_out, so the zoom cascade runs without a
+ * host round trip.  Traffic per step: 20 B read per input cell, 20 B written
+ * per output cell, one record per input cell. */
+#define HM_CS_THREADS 256
+#define HM_CS_IT 8
+#define HM_CS_TILE (HM_CS_THREADS * HM_CS_IT)
+#define HM_CS_FLAG_AGG 1ull
+#define HM_CS_FLAG_INC 2ull
+#define HM_CS_VBITS 38
 
-/* unique keys at their index; segment end (inclusive count prefix) per cell */
-__global__ __launch_bounds__(256) void k_rle_scatter(const ulonglong2* __restrict__ keys, uint64_t n, int s,
-                                                     const uint64_t* __restrict__ flag, const uint64_t* __restrict__ idx,
-                                                     const uint64_t* __restrict__ S, const uint64_t* __restrict__ c,
-                                                     ulonglong2* __restrict__ okey, uint64_t* __restrict__ oend)
+/* one record of cell key k at zoom z (all lanes of the wave call it: the
+ * split mode appends per wave) */
+__device__ __forceinline__ void hm_gen_record(const HmGenEmit& e, hm_u128 k, int z, uint64_t cnt, bool in, uint64_t q)
 {
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += stride) {
-        const uint64_t j = idx[i] + flag[i] - 1;   /* segment of i (idx: exclusive head count) */
-        if (flag[i]) hm_st128(okey, j, hm_ld128(keys, i) >> s);
-        if (i + 1 == n || flag[i + 1]) oend[j] = S[i] + c[i];
+    int64_t row = 0, col = 0;
+    hm_u128 root = 0;
+    if (in) {
+        root = k >> (2 * z);
+        const uint64_t m = (uint64_t)(k & ((((hm_u128)1) << (2 * z)) - 1));
+        const int64_t sr = (int64_t)(uint64_t)((root >> 48) & 31) - HM_GEN_SR_BIAS;
+        const int64_t sc = (int64_t)(uint64_t)(root & ((((hm_u128)1) << HM_GEN_SC_BITS) - 1)) - HM_GEN_SC_BIAS;
+        /* sr * 2^z, sc * 2^z as unsigned shifts (two's complement) */
+        row = (int64_t)(((uint64_t)sr << z) + hm_compact21(m >> 1));
+        col = (int64_t)(((uint64_t)sc << z) + hm_compact21(m));
     }
-}
-
-/* counts of zoom z's cells (next level's input) and their records */
-__global__ __launch_bounds__(256) void k_rle_emit(HmGenEmit e, const ulonglong2* __restrict__ okey,
-                                                  const uint64_t* __restrict__ oend, uint64_t u, int z,
-                                                  uint64_t* __restrict__ ocnt, uint64_t base, int emit)
-{
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    const hm_u128 mm = ((hm_u128)1 << (2 * z)) - 1;
-    const uint64_t u_up = (u + 63) & ~63ull;   /* split mode appends per wave */
-    for (uint64_t j = (uint64_t)blockIdx.x * 256 + threadIdx.x; j < u_up; j += stride) {
-        const bool in = j < u;
-        uint64_t cnt = 0;
-        int64_t row = 0, col = 0;
-        hm_u128 root = 0;
-        if (in) {
-            cnt = oend[j] - (j ? oend[j - 1] : 0ull);
-            ocnt[j] = cnt;
-            const hm_u128 k = hm_ld128(okey, j);
-            root = k >> (2 * z);
-            const uint64_t m = (uint64_t)(k & mm);
-            const int64_t sr = (int64_t)(uint64_t)((root >> 48) & 31) - HM_GEN_SR_BIAS;
-            const int64_t sc = (int64_t)(uint64_t)(root & ((((hm_u128)1) << HM_GEN_SC_BITS) - 1)) - HM_GEN_SC_BIAS;
-            /* sr * 2^z, sc * 2^z as unsigned shifts (two's complement) */
-            row = (int64_t)(((uint64_t)sr << z) + hm_compact21(m >> 1));
-            col = (int64_t)(((uint64_t)sc << z) + hm_compact21(m));
-        }
-        if (!emit) continue;
-        uint64_t q = base + j;
-        bool rec = in;
-        if (e.split) {
-            /* hm_count fallback: cells inside [0, 2^z)^2 as (HM_KEY, count),
-             * the others as records; one append per wave and kind */
-            const bool sq = in && (uint64_t)row < (1ull << z) && (uint64_t)col < (1ull << z);
-            rec = in && !sq;
-            const uint64_t ms = __ballot(sq), mx = __ballot(rec);
-            const int ls = ms ? __ffsll((unsigned long long)ms) - 1 : 0;
-            const int lx = mx ? __ffsll((unsigned long long)mx) - 1 : 0;
-            unsigned long long bs = 0, bx = 0;
-            if (ms && hm_lane() == ls) bs = atomicAdd(e.kcursor, (unsigned long long)__popcll(ms));
-            if (mx && hm_lane() == lx) bx = atomicAdd(e.xcursor, (unsigned long long)__popcll(mx));
-            bs = __shfl(bs, ls, 64);
-            bx = __shfl(bx, lx, 64);
-            if (sq) {
-                const uint64_t p = bs + hm_mbcnt(ms);
-                if (p < e.kcapacity) {
-                    e.keys[p] = ((uint64_t)z << 58) | ((uint64_t)row << 29) | (uint64_t)col;
-                    e.counts[p] = cnt;
-                }
+    bool rec = in;
+    if (e.split) {
+        /* hm_count fallback: cells inside [0, 2^z)^2 as (HM_KEY, count), the
+         * others as records; one append per wave and kind */
+        const bool sq = in && (uint64_t)row < (1ull << z) && (uint64_t)col < (1ull << z);
+        rec = in && !sq;
+        const uint64_t ms = __builtin_amdgcn_ballot_w64(sq), mx = __builtin_amdgcn_ballot_w64(rec);
+        const int ls = ms ? __ffsll((unsigned long long)ms) - 1 : 0;
+        const int lx = mx ? __ffsll((unsigned long long)mx) - 1 : 0;
+        unsigned long long bs = 0, bx = 0;
+        if (ms && hm_lane() == ls) bs = atomicAdd(e.kcursor, (unsigned long long)__popcll(ms));
+        if (mx && hm_lane() == lx) bx = atomicAdd(e.xcursor, (unsigned long long)__popcll(mx));
+        bs = __shfl(bs, ls, 64);
+        bx = __shfl(bx, lx, 64);
+        if (sq) {
+            const uint64_t p = bs + hm_mbcnt(ms);
+            if (p < e.kcapacity) {
+                e.keys[p] = ((uint64_t)z << 58) | ((uint64_t)row << 29) | (uint64_t)col;
+                e.counts[p] = cnt;
             }
-            q = bx + hm_mbcnt(mx);
         }
-        if (!rec || q >= e.capacity) continue;
-        int64_t* r = e.cells + q * e.width;
-        int f = 0;
-        if (e.width == 5) r[f++] = (int64_t)(uint64_t)(root >> 53);
-        r[f++] = z;
-        r[f++] = row;
-        r[f++] = col;
-        r[f] = (int64_t)cnt;
+        q = bx + hm_mbcnt(mx);
+    }
+    if (!rec || q >= e.capacity) return;
+    int64_t* r = e.cells + q * e.width;
+    int f = 0;
+    if (e.width == 5) r[f++] = (int64_t)(uint64_t)(root >> 53);
+    r[f++] = z;
+    r[f++] = row;
+    r[f++] = col;
+    r[f] = (int64_t)cnt;
+}
+
+__device__ __forceinline__ uint64_t hm_cs_word(uint64_t epoch, uint64_t flag, uint64_t v)
+{
+    return (epoch << 40) | (flag << HM_CS_VBITS) | v;
+}
+
+/* exclusive prefix of the tiles before `tile` (wave-parallel look-back over
+ * 64 predecessors at a time; a tile < 0 reads as an inclusive 0) */
+__device__ uint64_t hm_cs_lookback(uint64_t* st, int64_t tile, uint64_t epoch)
+{
+    const int lane = hm_lane();
+    uint64_t excl = 0;
+    int64_t p = tile - 1;
+    while (p >= 0) {
+        const int64_t q = p - lane;
+        const uint64_t wv = q >= 0 ? __hip_atomic_load(st + q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                   : hm_cs_word(epoch, HM_CS_FLAG_INC, 0);
+        const uint64_t fl = (wv >> 40) == epoch ? (wv >> HM_CS_VBITS) & 3ull : 0ull;
+        const uint64_t mi = __builtin_amdgcn_ballot_w64(fl == HM_CS_FLAG_INC);
+        const uint64_t mr = __builtin_amdgcn_ballot_w64(fl != 0);
+        const uint64_t upto = mi ? ((mi & (0ull - mi)) << 1) - 1 : ~0ull;   /* lanes up to the first inclusive */
+        if ((mr & upto) != upto) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint64_t v = ((upto >> lane) & 1ull) ? (wv & ((1ull << HM_CS_VBITS) - 1)) : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+        excl += v;
+        if (mi) break;
+        p -= 64;
+    }
+    return excl;
+}
+
+__global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
+{
+    __shared__ uint32_t wtot[HM_CS_IT * 4];
+    __shared__ uint32_t tile_s;
+    __shared__ uint64_t excl_s;
+    const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
+    const uint64_t ntiles = (m + HM_CS_TILE - 1) / HM_CS_TILE;
+    const int lane = hm_lane(), w = threadIdx.x >> 6;
+    const int s = a.shift;
+    const unsigned long long rb = a.rbase_in ? *a.rbase_in : 0ull;
+    if (blockIdx.x == 0 && threadIdx.x == 0 && a.rbase_out) *a.rbase_out = rb + m;
+    if (m == 0 && blockIdx.x == 0 && threadIdx.x == 0) *a.m_out = 0u;
+    for (;;) {
+        if (threadIdx.x == 0) tile_s = atomicAdd(a.ticket, 1u);
+        __syncthreads();
+        const uint64_t tile = tile_s;
+        if (tile >= ntiles) break;
+        const uint64_t t0 = tile * HM_CS_TILE;
+        hm_u128 ks[HM_CS_IT];
+        uint32_t ee[HM_CS_IT], fl[HM_CS_IT];
+#pragma unroll
+        for (int r = 0; r < HM_CS_IT; r++) {
+            const uint64_t i = t0 + (uint64_t)r * HM_CS_THREADS + threadIdx.x;
+            const bool v = i < m;
+            const hm_u128 k = v ? hm_ld128(a.kin, i) : (hm_u128)0;
+            const uint32_t e = a.ein ? (v ? a.ein[i] : 0u) : (uint32_t)(i + 1);
+            /* neighbours: lanes of the wave, the wave's edges from memory */
+            hm_u128 kp = ((hm_u128)__shfl_up((unsigned long long)(k >> 64), 1, 64) << 64) |
+                         (hm_u128)__shfl_up((unsigned long long)k, 1, 64);
+            uint32_t ep = __shfl_up(e, 1, 64);
+            hm_u128 kn = ((hm_u128)__shfl_down((unsigned long long)(k >> 64), 1, 64) << 64) |
+                         (hm_u128)__shfl_down((unsigned long long)k, 1, 64);
+            if (lane == 0 && v && i > 0) {
+                kp = hm_ld128(a.kin, i - 1);
+                ep = a.ein ? a.ein[i - 1] : (uint32_t)i;
+            }
+            if (i == 0) ep = 0;
+            if (lane == 63 && i + 1 < m) kn = hm_ld128(a.kin, i + 1);
+            const hm_u128 kz = k >> s;
+            const bool head = v && (i == 0 || (kp >> s) != kz);
+            const bool tail = v && (i + 1 == m || (kn >> s) != kz);
+            if (a.emit) hm_gen_record(a.e, k, a.zin, (uint64_t)(e - ep), v, rb + i);
+            const uint64_t hb = __builtin_amdgcn_ballot_w64(head);
+            if (lane == 0) wtot[r * 4 + w] = (uint32_t)__popcll(hb);
+            ks[r] = kz;
+            ee[r] = e;
+            fl[r] = (uint32_t)head | ((uint32_t)tail << 1) | (hm_mbcnt(hb) << 2);
+        }
+        __syncthreads();
+        if (w == 0) {
+            const uint32_t x = lane < HM_CS_IT * 4 ? wtot[lane] : 0u;
+            uint32_t inc = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += y;
+            }
+            const uint64_t agg = __shfl(inc, 63, 64);
+            if (lane < HM_CS_IT * 4) wtot[lane] = inc - x;
+            if (lane == 0)
+                __hip_atomic_store(a.tstat + tile, hm_cs_word(a.epoch, tile ? HM_CS_FLAG_AGG : HM_CS_FLAG_INC, agg),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t excl = tile ? hm_cs_lookback(a.tstat, (int64_t)tile, a.epoch) : 0ull;
+            if (lane == 0) {
+                if (tile)
+                    __hip_atomic_store(a.tstat + tile, hm_cs_word(a.epoch, HM_CS_FLAG_INC, excl + agg),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (tile + 1 == ntiles) *a.m_out = (uint32_t)(excl + agg);
+                excl_s = excl;
+            }
+        }
+        __syncthreads();
+        const uint64_t excl = excl_s;
+#pragma unroll
+        for (int r = 0; r < HM_CS_IT; r++) {
+            const uint64_t j = excl + wtot[r * 4 + w] + (fl[r] >> 2);
+            if (fl[r] & 1u) hm_st128(a.kout, j, ks[r]);
+            if (fl[r] & 2u) a.eout[j + (fl[r] & 1u) - 1] = ee[r];
+        }
+        __syncthreads();
+    }
+}
+
+/* the records of the last level (nothing below it to fold into) */
+__global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
+{
+    const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
+    const unsigned long long rb = *a.rbase_in;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *a.rbase_out = rb + m;
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    const uint64_t m_up = (m + 63) & ~63ull;   /* whole waves: split mode appends per wave */
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m_up; i += stride) {
+        const bool v = i < m;
+        const hm_u128 k = v ? hm_ld128(a.kin, i) : (hm_u128)0;
+        const uint32_t e = v ? a.ein[i] : 0u, ep = (v && i) ? a.ein[i - 1] : 0u;
+        hm_gen_record(a.e, k, a.zin, (uint64_t)(e - ep), v, rb + i);
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* one-sweep LSD radix sort (keys only, stable)                              */
+/* ------------------------------------------------------------------------ */
+/* The digit histograms of every pass come from ONE read of the keys
+ * (k_rx_hist_all); a pass is then one kernel: a block takes the next tile of
+ * HM_OS_TILE keys from a ticket, ranks them (per wave: 8-ballot digit match
+ * in key order; waves in order), publishes its per-digit counts and resolves
+ * its per-digit global offsets with a decoupled look-back over the earlier
+ * tiles (one thread per digit), then writes the tile through LDS in digit
+ * order, so a digit's keys leave as one contiguous run.  Per pass: 16 B read
+ * and 16 B written per key, plus 2 KB of look-back words per tile. */
+#define HM_OS_THREADS 256
+#define HM_OS_IT 16
+#define HM_OS_TILE (HM_OS_THREADS * HM_OS_IT)
+#define HM_OS_MAXP 16
+
+struct HmRxAll {
+    const ulonglong2* keys;
+    uint64_t n;
+    int np;
+    int sh[HM_OS_MAXP];
+    unsigned long long* hist;   /* [np][256] */
+};
+
+__global__ __launch_bounds__(256) void k_rx_hist_all(HmRxAll a)
+{
+    __shared__ uint32_t h[HM_OS_MAXP * 256];
+    for (int i = threadIdx.x; i < a.np * 256; i += 256) h[i] = 0;
+    __syncthreads();
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
+        const hm_u128 k = hm_ld128(a.keys, i);
+        for (int p = 0; p < a.np; p++) atomicAdd(&h[p * 256 + ((uint32_t)(k >> a.sh[p]) & 0xFFu)], 1u);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.np * 256; i += 256)
+        if (h[i]) atomicAdd(&a.hist[i], (unsigned long long)h[i]);
+}
+
+/* exclusive digit offsets of every pass, in place (one wave per pass) */
+__global__ __launch_bounds__(64) void k_rx_digit_offsets(unsigned long long* hist)
+{
+    unsigned long long* hp = hist + blockIdx.x * 256;
+    const int lane = hm_lane();
+    unsigned long long v[4], t = 0;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        v[q] = hp[lane * 4 + q];
+        t += v[q];
+    }
+    unsigned long long inc = t;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned long long y = __shfl_up(inc, o, 64);
+        if (lane >= o) inc += y;
+    }
+    unsigned long long b = inc - t;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+        hp[lane * 4 + q] = b;
+        b += v[q];
+    }
+}
+
+struct HmRxPass {
+    const ulonglong2* in;
+    ulonglong2* out;
+    uint64_t n;
+    int sh;
+    const unsigned long long* goff;   /* 256 exclusive digit offsets of this pass */
+    uint64_t* tstat;                  /* [tiles][256] look-back words */
+    uint64_t epoch;
+    unsigned* ticket;
+};
+
+__global__ __launch_bounds__(HM_OS_THREADS) void k_rx_onesweep(HmRxPass a)
+{
+    __shared__ ulonglong2 stage[HM_OS_TILE];
+    __shared__ uint32_t wcnt[4][256];
+    __shared__ uint32_t dbase[256];      /* tile-local start of each digit */
+    __shared__ uint64_t gbase[256];      /* global start of each digit's run of this tile */
+    __shared__ uint32_t wtot[4];
+    __shared__ uint32_t tile_s;
+    const int w = threadIdx.x >> 6, lane = hm_lane();
+    const int sh = a.sh;
+    const uint64_t ntiles = (a.n + HM_OS_TILE - 1) / HM_OS_TILE;
+    for (;;) {
+        if (threadIdx.x == 0) tile_s = atomicAdd(a.ticket, 1u);
+        wcnt[0][threadIdx.x] = 0;
+        wcnt[1][threadIdx.x] = 0;
+        wcnt[2][threadIdx.x] = 0;
+        wcnt[3][threadIdx.x] = 0;
+        __syncthreads();
+        const uint64_t tile = tile_s;
+        if (tile >= ntiles) break;
+        const uint64_t t0 = tile * HM_OS_TILE + (uint64_t)w * (HM_OS_TILE / 4);
+        hm_u128 k[HM_OS_IT];
+        uint32_t rk[HM_OS_IT / 2];
+#pragma unroll
+        for (int r = 0; r < HM_OS_IT; r++) {
+            const uint64_t i = t0 + (uint64_t)r * 64 + lane;
+            const bool v = i < a.n;
+            k[r] = v ? hm_ld128(a.in, i) : ~(hm_u128)0;
+        }
+#pragma unroll
+        for (int r = 0; r < HM_OS_IT; r++) {
+            const uint64_t i = t0 + (uint64_t)r * 64 + lane;
+            const bool v = i < a.n;
+            const uint32_t d = (uint32_t)(k[r] >> sh) & 0xFFu;
+            uint64_t m = __builtin_amdgcn_ballot_w64(v);
+#pragma unroll
+            for (int b = 0; b < 8; b++) {
+                const uint64_t bb = __builtin_amdgcn_ballot_w64((d >> b) & 1u);
+                m &= ((d >> b) & 1u) ? bb : ~bb;
+            }
+            const uint32_t below = hm_mbcnt(m);
+            const uint32_t prev = wcnt[w][d];
+            __builtin_amdgcn_wave_barrier();
+            if (v && below == 0) wcnt[w][d] = prev + (uint32_t)__popcll(m);
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t rank = v ? prev + below : 0xFFFFu;
+            if (r & 1) rk[r >> 1] |= rank << 16;
+            else rk[r >> 1] = rank;
+        }
+        __syncthreads();
+        /* thread t owns digit t: wave prefixes, tile count, look-back */
+        const uint32_t d = threadIdx.x;
+        const uint32_t c0 = wcnt[0][d], c1 = wcnt[1][d], c2 = wcnt[2][d], c3 = wcnt[3][d];
+        const uint32_t cnt = c0 + c1 + c2 + c3;
+        uint64_t* st = a.tstat + tile * 256 + d;
+        __hip_atomic_store(st, hm_cs_word(a.epoch, tile ? HM_CS_FLAG_AGG : HM_CS_FLAG_INC, cnt), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t excl = 0;
+        for (int64_t p = (int64_t)tile - 1; p >= 0;) {
+            const uint64_t wv = __hip_atomic_load(a.tstat + (uint64_t)p * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t f = (wv >> 40) == a.epoch ? (wv >> HM_CS_VBITS) & 3ull : 0ull;
+            if (!f) {
+                __builtin_amdgcn_s_sleep(1);
+                continue;
+            }
+            excl += wv & ((1ull << HM_CS_VBITS) - 1);
+            if (f == HM_CS_FLAG_INC) break;
+            p--;
+        }
+        if (tile)
+            __hip_atomic_store(st, hm_cs_word(a.epoch, HM_CS_FLAG_INC, excl + cnt), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        /* tile-local digit starts: exclusive scan of cnt over the 256 digits */
+        uint32_t inc = cnt;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o, 64);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) wtot[w] = inc;
+        __syncthreads();
+        uint32_t wo = 0;
+        for (int q = 0; q < w; q++) wo += wtot[q];
+        const uint32_t db = wo + inc - cnt;
+        dbase[d] = db;
+        gbase[d] = a.goff[d] + excl;
+        __syncthreads();
+        /* wave prefixes per digit into wcnt (read back per key) */
+        wcnt[0][d] = db;
+        wcnt[1][d] = db + c0;
+        wcnt[2][d] = db + c0 + c1;
+        wcnt[3][d] = db + c0 + c1 + c2;
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < HM_OS_IT; r++) {
+            const uint32_t rank = (rk[r >> 1] >> ((r & 1) * 16)) & 0xFFFFu;
+            if (rank != 0xFFFFu) {
+                const uint32_t dd = (uint32_t)(k[r] >> sh) & 0xFFu;
+                stage[wcnt[w][dd] + rank] = make_ulonglong2((unsigned long long)k[r], (unsigned long long)(k[r] >> 64));
+            }
+        }
+        __syncthreads();
+        const uint32_t valid = (uint32_t)min<uint64_t>(HM_OS_TILE, a.n - tile * HM_OS_TILE);
+        for (uint32_t j = threadIdx.x; j < valid; j += HM_OS_THREADS) {
+            const ulonglong2 v = stage[j];
+            const hm_u128 kk = ((hm_u128)v.y << 64) | (hm_u128)v.x;
+            const uint32_t dg = (uint32_t)(kk >> sh) & 0xFFu;
+            a.out[gbase[dg] + (j - dbase[dg])] = v;
+        }
+        __syncthreads();
     }
 }
 
@@ -333,37 +520,51 @@ void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a)
     hipLaunchKernelGGL(k_gen_keys, dim3(hm_ggrid(a.n, 256, 8192)), dim3(256), 0, s, a);
 }
 
-uint64_t hm_rx_tiles(uint64_t n) { return (n + HM_RX_WT - 1) / HM_RX_WT; }
+uint64_t hm_rx_os_tiles(uint64_t n) { return (n + HM_OS_TILE - 1) / HM_OS_TILE; }
 
-void hm_launch_rx_pass(hipStream_t s, const ulonglong2* in, ulonglong2* out, uint64_t n, int sh, uint64_t* hist,
-                       uint64_t* off, uint64_t* partial, uint64_t* total)
+/* LSD sort of n keys over the digits at shifts sh[0..np) (ascending), state =
+ * 256 B tickets + np x 2 KB histograms + tiles x 2 KB look-back words, zeroed
+ * here.  Returns the buffer that holds the sorted keys. */
+ulonglong2* hm_launch_rx_sort(hipStream_t s, ulonglong2* a, ulonglong2* b, uint64_t n, const int* sh, int np,
+                              uint8_t* state)
 {
-    const uint64_t nt = hm_rx_tiles(n);
-    const unsigned blocks = (unsigned)((nt + 3) / 4);
-    hipLaunchKernelGGL(k_rx_hist, dim3(blocks), dim3(256), 0, s, in, n, sh, nt, hist);
-    hm_launch_scan(s, hist, nt * 256, partial, off, total);
-    hipLaunchKernelGGL(k_rx_scatter, dim3(blocks), dim3(256), 0, s, in, out, n, sh, nt, off);
+    if (np == 0) return a;
+    const uint64_t nt = hm_rx_os_tiles(n);
+    (void)hipMemsetAsync(state, 0, 256 + HM_OS_MAXP * 2048 + nt * 2048, s);
+    HmRxAll h;
+    h.keys = a;
+    h.n = n;
+    h.np = np;
+    for (int p = 0; p < np; p++) h.sh[p] = sh[p];
+    h.hist = (unsigned long long*)(state + 256);
+    hipLaunchKernelGGL(k_rx_hist_all, dim3(hm_ggrid(n, 256 * 16, 2048)), dim3(256), 0, s, h);
+    hipLaunchKernelGGL(k_rx_digit_offsets, dim3(np), dim3(64), 0, s, h.hist);
+    ulonglong2 *in = a, *out = b;
+    for (int p = 0; p < np; p++) {
+        HmRxPass x;
+        x.in = in;
+        x.out = out;
+        x.n = n;
+        x.sh = sh[p];
+        x.goff = h.hist + p * 256;
+        x.tstat = (uint64_t*)(state + 256 + HM_OS_MAXP * 2048);
+        x.epoch = (uint64_t)p + 1;
+        x.ticket = (unsigned*)state + p;
+        hipLaunchKernelGGL(k_rx_onesweep, dim3(hm_ggrid(nt, 1, 512)), dim3(HM_OS_THREADS), 0, s, x);
+        std::swap(in, out);
+    }
+    return in;
 }
 
-void hm_launch_rle_prep(hipStream_t s, const ulonglong2* keys, const uint64_t* cnt, uint64_t n, int sh, uint64_t* flag,
-                        uint64_t* c)
+void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only)
 {
-    hipLaunchKernelGGL(k_rle_prep, dim3(hm_ggrid(n, 256, 16384)), dim3(256), 0, s, keys, cnt, n, sh, flag, c);
+    if (emit_only)
+        hipLaunchKernelGGL(k_cascade_emit, dim3(hm_ggrid(bound, 256, 4096)), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_cascade, dim3(hm_ggrid(bound, HM_CS_TILE, 2048)), dim3(HM_CS_THREADS), 0, s, a);
 }
 
-void hm_launch_rle_scatter(hipStream_t s, const ulonglong2* keys, uint64_t n, int sh, const uint64_t* flag,
-                           const uint64_t* idx, const uint64_t* S, const uint64_t* c, ulonglong2* okey, uint64_t* oend)
-{
-    hipLaunchKernelGGL(k_rle_scatter, dim3(hm_ggrid(n, 256, 16384)), dim3(256), 0, s, keys, n, sh, flag, idx, S, c,
-                       okey, oend);
-}
-
-void hm_launch_rle_emit(hipStream_t s, const HmGenEmit& e, const ulonglong2* okey, const uint64_t* oend, uint64_t u,
-                        int z, uint64_t* ocnt, uint64_t base, int emit)
-{
-    hipLaunchKernelGGL(k_rle_emit, dim3(hm_ggrid(u, 256, 16384)), dim3(256), 0, s, e, okey, oend, u, z, ocnt, base,
-                       emit);
-}
+uint64_t hm_cascade_tiles(uint64_t n) { return (n + HM_CS_TILE - 1) / HM_CS_TILE; }
 
 void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
                           const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,

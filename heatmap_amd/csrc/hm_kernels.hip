@@ -30,6 +30,7 @@
  * per call, u64 out): the reference's float sums of 1.0 are exact below 2^53.
  */
 #include <hip/hip_runtime.h>
+#include "hm_genkey.h"
 #include "hm_device.h"
 #include "hm_project.h"
 #include "hm_pipeline.h"
@@ -3184,6 +3185,85 @@ void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon,
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_project_list, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, row, col,
                        grp, idx, count, err_word);
+}
+
+/* The same list as general-path keys (hm_genkey.h), built while projecting:
+ * the kept points' 128-bit (group, super tile, Morton) keys, compacted, and
+ * the OR / AND of all keys (the radix sort skips digits they agree on).
+ * Errors (projection, or a tile beyond the key's fields) by input index. */
+__global__ __launch_bounds__(256) void k_project_keys(const double* lat, const double* lon, const uint8_t* keep,
+                                                      const uint32_t* group, int64_t n, int Z, ulonglong2* keys,
+                                                      unsigned long long* count, unsigned long long* err_word,
+                                                      unsigned long long* orand)
+{
+    __shared__ double tab[HM_YTAB_N];
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long base_s;
+    hm_load_ytab(tab);
+    __syncthreads();
+    unsigned long long o_lo = 0, o_hi = 0, n_lo = ~0ull, n_hi = ~0ull;
+    constexpr int64_t TILE = 256 * HM_PL_PPT;
+    for (int64_t t0 = (int64_t)blockIdx.x * TILE; t0 < n; t0 += (int64_t)gridDim.x * TILE) {
+        hm_u128 k[HM_PL_PPT];
+        uint32_t pm = 0;
+#pragma unroll
+        for (int j = 0; j < HM_PL_PPT; j++) {
+            const int64_t i = t0 + (int64_t)j * 256 + threadIdx.x;
+            k[j] = 0;
+            bool ok = false;
+            if (i < n) {
+                /* every point projects (and raises) first, kept or not */
+                int64_t r = 0, c = 0;
+                int slow = 0;
+                int st = hm_project_point(lat[i], lon[i], Z, &r, &c, &slow, tab);
+                if (st == HM_OK && (!keep || keep[i])) {
+                    k[j] = hm_gen_key(r, c, group ? group[i] : 0u, Z, &ok);
+                    if (!ok) st = HM_E_RANGE;   /* representable by the reference, beyond this path's key */
+                }
+                if (st != HM_OK) atomicMin(err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+            }
+            pm |= (uint32_t)ok << j;
+            if (ok) {
+                o_lo |= (unsigned long long)k[j];
+                o_hi |= (unsigned long long)(k[j] >> 64);
+                n_lo &= (unsigned long long)k[j];
+                n_hi &= (unsigned long long)(k[j] >> 64);
+            }
+        }
+        uint32_t tot;
+        uint32_t pos = hm_block_excl_scan<256>((uint32_t)__popc(pm), scr, &tot);
+        if (threadIdx.x == 0) base_s = tot ? atomicAdd(count, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        const unsigned long long b = base_s;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < HM_PL_PPT; j++)
+            if ((pm >> j) & 1u) hm_st128(keys, b + pos++, k[j]);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        o_lo |= __shfl_xor(o_lo, o, 64);
+        o_hi |= __shfl_xor(o_hi, o, 64);
+        n_lo &= __shfl_xor(n_lo, o, 64);
+        n_hi &= __shfl_xor(n_hi, o, 64);
+    }
+    if (hm_lane() == 0) {
+        atomicOr(&orand[0], o_lo);
+        atomicOr(&orand[1], o_hi);
+        atomicAnd(&orand[2], n_lo);
+        atomicAnd(&orand[3], n_hi);
+    }
+}
+
+void hm_launch_project_keys(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
+                            const uint32_t* group, int64_t n, int Z, ulonglong2* keys, unsigned long long* count,
+                            unsigned long long* err_word, unsigned long long* orand)
+{
+    int64_t blocks = (n + 256 * HM_PL_PPT - 1) / (256 * HM_PL_PPT);
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_project_keys, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, keys,
+                       count, err_word, orand);
 }
 
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16, bool few_runs)

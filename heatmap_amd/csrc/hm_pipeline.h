@@ -583,18 +583,35 @@ struct HmGenEmit {
     unsigned long long* xcursor;
 };
 void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a);
+void hm_launch_project_keys(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
+                            const uint32_t* group, int64_t n, int Z, ulonglong2* keys, unsigned long long* count,
+                            unsigned long long* err_word, unsigned long long* orand);
 void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
                           const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
                           unsigned long long* count);
-uint64_t hm_rx_tiles(uint64_t n);
-void hm_launch_rx_pass(hipStream_t s, const ulonglong2* in, ulonglong2* out, uint64_t n, int sh, uint64_t* hist,
-                       uint64_t* off, uint64_t* partial, uint64_t* total);
-void hm_launch_rle_prep(hipStream_t s, const ulonglong2* keys, const uint64_t* cnt, uint64_t n, int sh, uint64_t* flag,
-                        uint64_t* c);
-void hm_launch_rle_scatter(hipStream_t s, const ulonglong2* keys, uint64_t n, int sh, const uint64_t* flag,
-                           const uint64_t* idx, const uint64_t* S, const uint64_t* c, ulonglong2* okey, uint64_t* oend);
-void hm_launch_rle_emit(hipStream_t s, const HmGenEmit& e, const ulonglong2* okey, const uint64_t* oend, uint64_t u,
-                        int z, uint64_t* ocnt, uint64_t base, int emit);
+uint64_t hm_rx_os_tiles(uint64_t n);
+ulonglong2* hm_launch_rx_sort(hipStream_t s, ulonglong2* a, ulonglong2* b, uint64_t n, const int* sh, int np,
+                              uint8_t* state);
+struct HmCascArgs {
+    const ulonglong2* kin;      /* sorted level-(z+1) cells (or raw keys) */
+    const uint32_t* ein;        /* their END prefixes; null: raw keys, END = i + 1 */
+    const uint32_t* m_in;       /* item count on the device (null: m_host) */
+    uint64_t m_host;
+    int shift;                  /* 0 at the first step (unique raw keys), 2 after */
+    int zin;                    /* zoom of the input cells (their records) */
+    int emit;                   /* write the input level's records */
+    ulonglong2* kout;
+    uint32_t* eout;
+    uint32_t* m_out;
+    uint64_t* tstat;            /* look-back words, one per tile */
+    uint64_t epoch;             /* distinct per step of a call (tstat zeroed per call) */
+    unsigned* ticket;
+    const unsigned long long* rbase_in;   /* record offset of the input level */
+    unsigned long long* rbase_out;        /* = rbase_in + m (offset of the next level) */
+    HmGenEmit e;
+};
+void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only);
+uint64_t hm_cascade_tiles(uint64_t n);
 
 /* multi-GPU cell exchange (hm_merge.hip) */
 struct HmRouteArgs {

@@ -26,9 +26,10 @@ Every coarser tile is the arithmetic shift of the detail-zoom tile.  The
 reference re-projects tile centres instead (heatmap.py:60-61,89); the two
 agree on the windows heatmap_amd/chain_window.py lists (generated and checked
 tile by tile by tools/chain_window.c; they contain [0, 2^z)^2 at every zoom).
-Points whose tiles leave those windows (within ~1e-6 deg of a pole, or
-|lon| > 11520) raise DevicePathUnsupported instead of returning rows that
-could differ from the reference's.
+Detail tiles outside them (within ~1e-6 deg of a pole, or |lon| > 11520) take
+the reference's literal chain instead (ChainFix: centres by the reference's
+inverse projection, re-projected on the device), and their counts move from
+the shift's cells to the tiles that chain reaches.
 
 build_heatmaps(locations) keeps the reference's RDD-shaped interface for
 locations produced by dataframe_loader (all with count 1.0 and tileId at the
@@ -187,11 +188,27 @@ class Cells:
     The batch pipeline's only timespan label is 'alltime' (heatmap.py:62-63);
     the streaming heatmap's rollups carry year / month / day labels too."""
 
-    def __init__(self, labels, label, zoom, row, col, value, delta, spans=("alltime",), span=None):
+    def __init__(self, labels, label, zoom, row, col, value, delta, spans=("alltime",), span=None, tile_override=None):
         self.labels, self.label, self.zoom, self.row, self.col, self.value = labels, label, zoom, row, col, value
         self.delta = delta
         self.spans = list(spans)
         self.span = np.zeros(np.asarray(zoom).size, np.int64) if span is None else np.asarray(span, np.int64)
+        # {(zoom, row, col): row tile} for bins outside the chain windows whose
+        # row tile is not the shift (ChainFix); None: every row tile is the shift
+        self.tile_override = tile_override or None
+
+    def row_tiles(self):
+        """(zoom - delta, row tile row, row tile col) of every bin"""
+        d = self.delta
+        z, r, c = (np.asarray(x, np.int64) for x in (self.zoom, self.row, self.col))
+        tz, tr, tc = z - d, r >> d, c >> d
+        if self.tile_override:
+            tr, tc = tr.copy(), tc.copy()
+            for i in range(z.size):
+                o = self.tile_override.get((int(z[i]), int(r[i]), int(c[i])))
+                if o is not None:
+                    tr[i], tc[i] = o
+        return tz, tr, tc
 
     def __len__(self):
         return int(self.zoom.size)
@@ -212,9 +229,12 @@ def concat_cells(parts, labels, delta) -> Cells:
     def cat(name, dtype):
         return np.concatenate([np.asarray(getattr(c, name), dtype) for c in parts]) if parts else np.zeros(0, dtype)
 
+    over = {}
+    for c in parts:
+        over.update(c.tile_override or {})
     return Cells(labels, cat("label", np.int64), cat("zoom", np.int64), cat("row", np.int64), cat("col", np.int64),
                  cat("value", np.float64), delta, spans or ["alltime"],
-                 np.concatenate(span) if span else np.zeros(0, np.int64))
+                 np.concatenate(span) if span else np.zeros(0, np.int64), tile_override=over)
 
 
 # cells above which _sum_by_cell sorts on the GPU (a 3-key numpy lexsort of
@@ -245,7 +265,7 @@ def _sum_by_cell(parts, device_min=None):
     if z.size == 0:
         return z, r, c, v
     lim = SUM_BY_CELL_DEVICE_MIN if device_min is None else device_min
-    if z.size >= lim and device.gpu_available() and r.min() >= 0 and c.min() >= 0 and \
+    if z.size >= lim and v.dtype.kind in "iu" and device.gpu_available() and r.min() >= 0 and c.min() >= 0 and \
             max(int(r.max()), int(c.max())) < (1 << 29) and int(z.max()) < 64:
         return _sum_by_cell_device(z, r, c, v)
     o = np.lexsort((c, r, z))
@@ -256,32 +276,122 @@ def _sum_by_cell(parts, device_min=None):
     return z[starts], r[starts], c[starts], np.add.reduceat(v, starts, axis=0)
 
 
-def _check_chain_window(zoom, row, col, zmax, d):
-    """Raise DevicePathUnsupported when a detail-zoom tile leaves the windows
-    on which the reference's centre re-projection equals the shift."""
-    m = zoom == zmax
-    if not m.any():
-        return
-    rlo, rhi, clo, chi = int(row[m].min()), int(row[m].max()), int(col[m].min()), int(col[m].max())
-
-    def inside(win, lo, hi):
-        return win[0] <= lo and hi < win[1]
-
+def _in_chain_window(row, col, zmax, d):
+    """Mask of detail-zoom tiles (row, col) whose every level lies inside the
+    windows on which the reference's centre re-projection (heatmap.py:60-61,
+    89) equals the shift (heatmap_amd/chain_window.py)."""
+    row, col = np.asarray(row, np.int64), np.asarray(col, np.int64)
+    ok = np.ones(row.size, dtype=bool)
     for z in range(zmax, d, -1):
         # row tile at z - d (heatmap.py:89); level z re-projected from z+1,
         # the first level at its own zoom (heatmap.py:60-61)
-        checks = [(z, d), (z, 0) if z == zmax else (z + 1, 1)]
-        for zz, j in checks:
+        for zz, j in [(z, d), (z, 0) if z == zmax else (z + 1, 1)]:
             kk = zmax - zz
-            if not (inside(chain_window.ROWS[zz][j], rlo >> kk, rhi >> kk) and
-                    inside(chain_window.COLS[zz][j], clo >> kk, chi >> kk)):
-                raise _lib.DevicePathUnsupported(
-                    "tiles at zoom %d span rows [%d, %d], cols [%d, %d]: outside the window where the "
-                    "reference's tile-centre re-projection (heatmap.py:60-61,89) equals the shift"
-                    % (zz, rlo >> kk, rhi >> kk, clo >> kk, chi >> kk))
+            (rlo, rhi), (clo, chi) = chain_window.ROWS[zz][j], chain_window.COLS[zz][j]
+            r, c = row >> kk, col >> kk
+            ok &= (r >= rlo) & (r < rhi) & (c >= clo) & (c < chi)
+    return ok
 
 
-def combine_cells(labels, all_cells, grouped_cells, zmax, d, span_label="alltime") -> Cells:
+def _device_project(lat, lon, z):
+    p = device.project(lat, lon, z, raise_errors=True)
+    return np.asarray(p.row, np.int64), np.asarray(p.col, np.int64)
+
+
+def _recentre(z, rows, cols, z_to, project=None):
+    """Tiles at zoom z_to holding the centres of tiles (z, rows, cols), as
+    reference tile.py:33-54 then tile.py:9-21 compute them: the centre on the
+    host with the reference's inverse projection and operation order
+    (Tile.latitude_from_row: exp/atan, raising what the reference raises), its
+    forward projection on the device (hm_project, bit-exact)."""
+    if len(rows) == 0:
+        return np.zeros(0, np.int64), np.zeros(0, np.int64)
+    lat = np.array([(Tile.latitude_from_row(int(r), z) + Tile.latitude_from_row(int(r) + 1, z)) / 2.0
+                    for r in rows], np.float64)
+    lon = np.array([(Tile.longitude_from_column(int(c) + 1, z) + Tile.longitude_from_column(int(c), z)) / 2.0
+                    for c in cols], np.float64)
+    return (project or _device_project)(lat, lon, z_to)
+
+
+class ChainFix:
+    """The reference's literal re-projection chain for the detail tiles that
+    leave the shift windows (within ~1e-6 deg of a pole, |lon| > 11520): per
+    level z, the tile each such detail tile's points reach (t_z) and the row
+    tile of that level's bins (heatmap.py:89).  first_applied: the detail tiles
+    are already the first level's (t_zmax given).  project(lat, lon, z) ->
+    (rows, cols): the forward projection (the device's hm_project; the CPU
+    tests pass the oracle's)."""
+
+    def __init__(self, rows, cols, zmax, d, first_applied=False, project=None):
+        self.rows, self.cols, self.zmax, self.d = np.asarray(rows, np.int64), np.asarray(cols, np.int64), zmax, d
+        self.level, self.rowtile = {}, {}
+        r, c = (self.rows, self.cols) if first_applied else _recentre(zmax, self.rows, self.cols, zmax, project)
+        for z in range(zmax, d, -1):
+            if z < zmax:
+                r, c = _recentre(z + 1, r, c, z, project)
+            self.level[z] = (r, c)
+            self.rowtile[z] = _recentre(z, r, c, z - d, project)
+
+    def shift_and_chain(self, z):
+        """(shift rows, shift cols, chain rows, chain cols) of the detail tiles at zoom z"""
+        k = self.zmax - z
+        r, c = self.level[z]
+        return self.rows >> k, self.cols >> k, r, c
+
+    def overrides(self):
+        """{(z, row, col): (row tile row, row tile col)} where the row tile is
+        not the shift (heatmap.py:89 re-projects the bin's centre)"""
+        out = {}
+        for z, (tr, tc) in self.rowtile.items():
+            r, c = self.level[z]
+            for i in np.flatnonzero((tr != (r >> self.d)) | (tc != (c >> self.d))).tolist():
+                out[(z, int(r[i]), int(c[i]))] = (int(tr[i]), int(tc[i]))
+        return out
+
+
+def _apply_chain(all_cells, grouped_cells, zmax, d, first_applied=False, project=None):
+    """Device cells (the shift pyramid) corrected for detail tiles outside the
+    chain windows: each such tile's counts move, level by level, from the
+    shift's cell to the reference's re-projected tile.  Returns (all_cells,
+    grouped_cells, row-tile overrides or None)."""
+    nz, nr, nc = (np.asarray(x, np.int64) for x in all_cells[:3])
+    gg, gz, gr, gc = (np.asarray(x, np.int64) for x in grouped_cells[:4])
+    nn, gn = np.asarray(all_cells[3]), np.asarray(grouped_cells[4])
+    det = nz == zmax
+    bad = det & ~_in_chain_window(nr, nc, zmax, d)
+    if not bad.any():
+        return all_cells, grouped_cells, None
+    fix = ChainFix(nr[bad], nc[bad], zmax, d, first_applied, project)
+    index = {(int(r), int(c)): i for i, (r, c) in enumerate(zip(fix.rows.tolist(), fix.cols.tolist()))}
+    # all points: n per detail tile, moved at every level
+    nb = nn[bad]
+    parts = [(nz, nr, nc, nn[:, None])]
+    for z in range(zmax, d, -1):
+        sr, sc, cr, cc = fix.shift_and_chain(z)
+        zz = np.full(sr.size, z, np.int64)
+        parts += [(zz, sr, sc, -nb[:, None]), (zz, cr, cc, nb[:, None])]
+    az, ar, ac, av = _sum_by_cell(parts, device_min=1 << 62)
+    keepc = av[:, 0] != 0
+    all_out = (az[keepc], ar[keepc], ac[keepc], av[keepc, 0])
+    # grouped points: the same move per (group, detail tile); the group rides
+    # in the zoom field (zoom < 64) of the cell key
+    gdet = (gz == zmax) & ~_in_chain_window(gr, gc, zmax, d)
+    if gdet.any():
+        ti = np.array([index[(int(r), int(c))] for r, c in zip(gr[gdet].tolist(), gc[gdet].tolist())], np.int64)
+        gb, gnb = gg[gdet], gn[gdet]
+        parts = [(gg * 64 + gz, gr, gc, gn[:, None])]
+        for z in range(zmax, d, -1):
+            sr, sc, cr, cc = fix.shift_and_chain(z)
+            zz = gb * 64 + z
+            parts += [(zz, sr[ti], sc[ti], -gnb[:, None]), (zz, cr[ti], cc[ti], gnb[:, None])]
+        kz, kr, kc, kv = _sum_by_cell(parts, device_min=1 << 62)
+        keepg = kv[:, 0] != 0
+        grouped_cells = (kz[keepg] // 64, kz[keepg] % 64, kr[keepg], kc[keepg], kv[keepg, 0])
+    return all_out, grouped_cells, fix.overrides()
+
+
+def combine_cells(labels, all_cells, grouped_cells, zmax, d, span_label="alltime", first_applied=False,
+                  project=None, exact_levels=None) -> Cells:
     """The bins of one timespan's rows from its per-cell counts.
 
     all_cells = (zoom, row, col, n): every kept point; grouped_cells =
@@ -289,35 +399,44 @@ def combine_cells(labels, all_cells, grouped_cells, zmax, d, span_label="alltime
     'all', merged into the 'all' rows).  Row layout: heatmap.py:55,85-90,
     120-126; 'all' weighting: heatmap.py:64-70 applied level by level (module
     docstring)."""
-    nz, nr, nc, nn = (np.asarray(x, np.int64) for x in all_cells)
-    gg, gz, gr, gc, gn = (np.asarray(x, np.int64) for x in grouped_cells)
-    _check_chain_window(nz, nr, nc, zmax, d)
+    if exact_levels is None:
+        all_cells, grouped_cells, over = _apply_chain(all_cells, grouped_cells, zmax, d, first_applied, project)
+    else:   # the cells already follow the reference's chain; exact_levels: its row-tile overrides
+        over = exact_levels
+    nz, nr, nc = (np.asarray(x, np.int64) for x in all_cells[:3])
+    gg, gz, gr, gc = (np.asarray(x, np.int64) for x in grouped_cells[:4])
+    # counts (int64), or float weights (build_heatmaps of weighted locations)
+    vt = np.float64 if (np.asarray(all_cells[3]).dtype.kind == "f" or
+                        np.asarray(grouped_cells[4]).dtype.kind == "f") else np.int64
+    nn, gn = np.asarray(all_cells[3], vt), np.asarray(grouped_cells[4], vt)
     # 'all' rows: per cell n, a (literal 'all'), U (other groups)
-    nv = np.stack([nn, np.zeros(nz.size, np.int64), np.zeros(nz.size, np.int64)], 1)
+    nv = np.stack([nn, np.zeros(nz.size, vt), np.zeros(nz.size, vt)], 1)
     lit = gg == 0
-    gv = np.stack([np.zeros(gz.size, np.int64), np.where(lit, gn, 0), np.where(lit, 0, gn)], 1)
+    gv = np.stack([np.zeros(gz.size, vt), np.where(lit, gn, 0), np.where(lit, 0, gn)], 1)
     az, ar, ac, av = _sum_by_cell([(nz, nr, nc, nv), (gz, gr, gc, gv)])
     sel = az > d
     az, ar, ac, av = az[sel], ar[sel], ac[sel], av[sel]
     k = zmax - az
-    w = np.left_shift(np.int64(1), k)
+    w = np.left_shift(np.int64(1), k).astype(vt)
     value_all = ((av[:, 0] + av[:, 1]) * w + (w - 1) * av[:, 2]).astype(np.float64)
     # user-group rows (the literal 'all' group is not a row of its own)
     us = (~lit) & (gz > d)
     label = np.concatenate([np.zeros(az.size, np.int64), gg[us]])
     return Cells(labels, label, np.concatenate([az, gz[us]]), np.concatenate([ar, gr[us]]),
                  np.concatenate([ac, gc[us]]), np.concatenate([value_all, gn[us].astype(np.float64)]), d,
-                 [span_label])
+                 [span_label], tile_override=over)
 
 
-def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None) -> Cells:
+def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None,
+                   project=None) -> Cells:
     """The bins of build_heatmaps' rows from per-cell counts.
 
     count_all(keep) -> (zoom, row, col, count) arrays of the kept points;
     count_grouped(keep, gid) -> (group, zoom, row, col, count) per group id.
     Both cover zooms delta+1 .. max_zoom_level+delta and are the only places
     points are touched (the device in the product, the oracle in the CPU
-    tests)."""
+    tests); project: the forward projection of re-projected tile centres
+    (ChainFix; the device by default)."""
     mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
     d = DETAIL_ZOOM_DELTA if delta is None else delta
     zmax = mz + d
@@ -327,23 +446,22 @@ def assemble_cells(count_all, count_grouped, user_id, keep=None, max_zoom_level=
     # every point is projected (and may raise) even when not kept, as
     # dataframe_loader does (heatmap.py:27-29): count_all sees all points
     allc = count_all(keep)
-    _check_chain_window(np.asarray(allc[0], np.int64), np.asarray(allc[1], np.int64),
-                        np.asarray(allc[2], np.int64), zmax, d)
     if plan.grouped.any():
         grp = count_grouped(plan.grouped, plan.gid)
     else:
         grp = tuple(np.zeros(0, np.int64) for _ in range(5))
-    return combine_cells(plan.labels, allc, grp, zmax, d)
+    return combine_cells(plan.labels, allc, grp, zmax, d, project=project)
 
 
 def cells_to_rows(cells: Cells) -> dict:
     """{row_id: {bin_id: float}} (heatmap.py:85-90,120-126)."""
     rows = {}
-    d = cells.delta
     labels, spans = cells.labels, cells.spans
-    for g, t, z, r, c, v in zip(cells.label.tolist(), cells.span.tolist(), cells.zoom.tolist(), cells.row.tolist(),
-                                cells.col.tolist(), cells.value.tolist()):
-        rid = "%s|%s|%d_%d_%d" % (labels[g], spans[t], z - d, r >> d, c >> d)
+    tz, tr, tc = cells.row_tiles()
+    for g, t, z, r, c, v, a, b, e in zip(cells.label.tolist(), cells.span.tolist(), cells.zoom.tolist(),
+                                         cells.row.tolist(), cells.col.tolist(), cells.value.tolist(), tz.tolist(),
+                                         tr.tolist(), tc.tolist()):
+        rid = "%s|%s|%d_%d_%d" % (labels[g], spans[t], a, b, e)
         rows.setdefault(rid, {})["%d_%d_%d" % (z, r, c)] = v
     return rows
 
@@ -480,11 +598,11 @@ def cells_to_table(cells: Cells):
     d = cells.delta
     if len(cells) == 0:
         return pa.table({"id": pa.array([], pa.large_string()), "heatmap": pa.array([], pa.large_string())})
-    if len(cells) >= SUM_BY_CELL_DEVICE_MIN and device.gpu_available():
+    if len(cells) >= SUM_BY_CELL_DEVICE_MIN and device.gpu_available() and not cells.tile_override:
         tab = _cells_to_table_device(cells)
         if tab is not None:
             return tab
-    tz, tr, tc = cells.zoom - d, cells.row >> d, cells.col >> d
+    tz, tr, tc = cells.row_tiles()
     o = _row_order(cells.label, cells.span, tz, tr, tc, cells.zoom, cells.row, cells.col)
     lab, sp, z, r, c, v = cells.label[o], cells.span[o], cells.zoom[o], cells.row[o], cells.col[o], cells.value[o]
     tz, tr, tc = tz[o], tr[o], tc[o]
@@ -520,9 +638,10 @@ def cells_to_table(cells: Cells):
     return pa.table({"id": ids, "heatmap": heat})
 
 
-def assemble_rows(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None) -> dict:
+def assemble_rows(count_all, count_grouped, user_id, keep=None, max_zoom_level=None, delta=None,
+                  project=None) -> dict:
     """assemble_cells -> {row_id: heatmap dict}."""
-    return cells_to_rows(assemble_cells(count_all, count_grouped, user_id, keep, max_zoom_level, delta))
+    return cells_to_rows(assemble_cells(count_all, count_grouped, user_id, keep, max_zoom_level, delta, project))
 
 
 # --------------------------------------------------------------------------
@@ -565,21 +684,86 @@ def heatmap_table(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None,
 
 def build_heatmaps(locations):
     """heatmap.py:107-118 on an iterable (or RDD-like .collect()) of locations
-    produced by dataframe_loader.  Returns [(row_id, heatmap_dict)]."""
+    {"userId", "tileId", "count"}: dataframe_loader output (zoom-21 tiles,
+    count 1.0: the device counts the tiles), or any zoom and any float count
+    -- heatmap_to_locations output fed back in, say.  Returns [(row_id,
+    heatmap_dict)]."""
     if hasattr(locations, "collect"):
         locations = locations.collect()
-    zmax = MAX_ZOOM_LEVEL + DETAIL_ZOOM_DELTA
-    rows, cols, users = [], [], []
+    d = DETAIL_ZOOM_DELTA
+    zmax = MAX_ZOOM_LEVEL + d
+    zs, rows, cols, users, w = [], [], [], [], []
     for loc in locations:
-        if loc["count"] != 1.0:
-            raise NotImplementedError("device build_heatmaps counts locations of weight 1.0 "
-                                      "(dataframe_loader output); got %r" % (loc["count"],))
         z, r, c = (int(x) for x in loc["tileId"].split("_"))
-        if z != zmax:
-            raise NotImplementedError("locations must carry zoom-%d tile ids (dataframe_loader output)" % zmax)
+        zs.append(z)
         rows.append(r)
         cols.append(c)
         users.append(loc["userId"])
-    out = build_heatmaps_columnar(np.array(rows, dtype=np.int64), np.array(cols, dtype=np.int64), users,
-                                  tiles=True)
-    return list(out.items())
+        w.append(float(loc["count"]))
+    if all(z == zmax for z in zs) and all(x == 1.0 for x in w):
+        out = build_heatmaps_columnar(np.array(rows, dtype=np.int64), np.array(cols, dtype=np.int64), users,
+                                      tiles=True)
+        return list(out.items())
+    return list(cells_to_rows(weighted_location_cells(zs, rows, cols, users, w, zmax, d)).items())
+
+
+def weighted_location_cells(zs, rows, cols, users, weights, zmax, d, project=None) -> Cells:
+    """Bins of build_heatmaps' rows for locations at any zoom with any float
+    count.  The first level takes the tile holding each location tile's centre
+    at the detail zoom (heatmap.py:60-61: tile_from_tile_id, then
+    tile_id_from_lat_long); the levels below follow the shift, or the literal
+    chain outside its windows (ChainFix); weights are summed per (group, cell)
+    in float64 (the reference's reduceByKey sums; exact for integer-valued
+    counts below 2^53)."""
+    zs = np.asarray(zs, np.int64)
+    n = zs.size
+    T_r = np.zeros(n, np.int64)
+    T_c = np.zeros(n, np.int64)
+    for z0 in np.unique(zs).tolist():
+        m = np.flatnonzero(zs == z0)
+        keys = sorted({(rows[i], cols[i]) for i in m.tolist()})
+        tr, tc = _recentre(z0, [k[0] for k in keys], [k[1] for k in keys], zmax, project)
+        at = {k: j for j, k in enumerate(keys)}
+        for i in m.tolist():
+            j = at[(rows[i], cols[i])]
+            T_r[i], T_c[i] = tr[j], tc[j]
+    wv = np.asarray(weights, np.float64)
+    plan = group_plan(users)
+    # every level's tile of each distinct first-level tile: the shift inside
+    # the windows, the literal chain outside (ChainFix)
+    U, inv = np.unique(np.stack([T_r, T_c], 1), axis=0, return_inverse=True)
+    inv = inv.reshape(-1)
+    ur, uc = U[:, 0].copy(), U[:, 1].copy()
+    lev = {z: (ur >> (zmax - z), uc >> (zmax - z)) for z in range(zmax, d, -1)}
+    bad = ~_in_chain_window(ur, uc, zmax, d)
+    over = {}
+    if bad.any():
+        fix = ChainFix(ur[bad], uc[bad], zmax, d, first_applied=True, project=project)
+        for z in range(zmax, d, -1):
+            r, c = lev[z][0].copy(), lev[z][1].copy()
+            r[bad], c[bad] = fix.level[z]
+            lev[z] = (r, c)
+        over = fix.overrides()
+    gsel = plan.grouped
+    az, ar, ac, av, gg, gz, gr, gc, gv = [], [], [], [], [], [], [], [], []
+    for z in range(zmax, d, -1):
+        lr, lc = lev[z][0][inv], lev[z][1][inv]
+        az.append(np.full(n, z, np.int64))
+        ar.append(lr)
+        ac.append(lc)
+        av.append(wv)
+        gg.append(plan.gid[gsel].astype(np.int64))
+        gz.append(np.full(int(gsel.sum()), z, np.int64))
+        gr.append(lr[gsel])
+        gc.append(lc[gsel])
+        gv.append(wv[gsel])
+    cz, cr, cc, cv = _sum_by_cell([(np.concatenate(az), np.concatenate(ar), np.concatenate(ac),
+                                    np.concatenate(av)[:, None])])
+    allc = (cz, cr, cc, cv[:, 0])
+    if gsel.any():
+        kz, kr, kc, kv = _sum_by_cell([(np.concatenate(gg) * 64 + np.concatenate(gz), np.concatenate(gr),
+                                        np.concatenate(gc), np.concatenate(gv)[:, None])])
+        grp = (kz // 64, kz % 64, kr, kc, kv[:, 0])
+    else:
+        grp = (np.zeros(0, np.int64),) * 4 + (np.zeros(0, np.float64),)
+    return combine_cells(plan.labels, allc, grp, zmax, d, exact_levels=over)

@@ -211,7 +211,10 @@ def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, de
     for b in bufsets:
         free.put(b)
     owned, err, last = [], [], [None]
-    side = torch.cuda.Stream()
+    # the merge stream takes the highest priority: its kernels (and the RCCL
+    # calls' copies) are dispatched ahead of the next count's, which fill the CUs
+    lo, hi = torch.cuda.Stream.priority_range()
+    side = torch.cuda.Stream(priority=min(lo, hi))
 
     def merger():
         try:

@@ -13,9 +13,11 @@ def _s64(v):
 def device_digest(torch, keys, counts):
     """tests/conftest.py cells_digest of HM_KEY cells, on the device (int64
     arithmetic wraps like the uint64 original; right shifts made logical)."""
-    z = keys >> 58
-    r = (keys >> 29) & M29
-    c = keys & M29
+    return device_cells_digest(torch, keys >> 58, (keys >> 29) & M29, keys & M29, counts)
+
+
+def device_cells_digest(torch, z, r, c, counts):
+    """cells_digest of (zoom, row, col, count) int64 CUDA tensors."""
 
     def lsr(x, k):
         return (x >> k) & ((1 << (64 - k)) - 1)
@@ -32,4 +34,4 @@ def device_digest(torch, keys, counts):
         y = x[:h] ^ x[h:2 * h]
         x = torch.cat([y, x[2 * h:]]) if x.numel() & 1 else y
     xr = (int(x[0].item()) & _U) if x.numel() else 0
-    return [int(keys.numel()), int(counts.sum().item()), s, xr]
+    return [int(z.numel()), int(counts.sum().item()), s, xr]

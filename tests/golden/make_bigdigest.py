@@ -51,7 +51,47 @@ CASES = {
     "hotspots_1e7_start0_z0-18": ("hotspots", 0, 0, 10_000_000, 0, 18),
     "hotspots_1e7_start70M_z0-18": ("hotspots", 0, 70_000_000, 10_000_000, 0, 18),
     "hotspots_1e7_start190M_z0-18": ("hotspots", 0, 190_000_000, 10_000_000, 0, 18),
+    # the reference's production zooms: detail zooms 21..6 (heatmap.py:16-17,109)
+    "hotspots_1e9_z6-21": ("hotspots", 0, 0, 1_000_000_000, 6, 21),
 }
+
+# grouped: name: (kind, seed, n, users, zmin, zmax); point i's group is
+# ((i * 2654435761) >> 7) % users (tools/bench_grouped.py).  The digest is over
+# records (zoom, (group << (zoom + 1)) | row, col, count): a group-tagged row
+# that every coarser zoom's shift keeps separable (rows < 2^zoom here)
+GROUPED = {
+    "grouped_hotspots_1e8_u10000_z6-21": ("hotspots", 0, 100_000_000, 10_000, 6, 21),
+}
+
+
+def run_grouped(kind, seed, n, users, zmin, zmax):
+    """The C oracle's projection of every point at zmax, the group folded into
+    the row's high bits, and its tile-input count (every coarser zoom the
+    shift): exactly the per-(group, zoom, row, col) counts of hm_count_grouped
+    for in-square points."""
+    t0 = time.time()
+    lat, lon = synth.generate(kind, n, seed=seed)
+    r, c, st, _ = oracle.project(lat, lon, zmax)
+    del lat, lon
+    assert int(st.max()) == 0
+    assert r.min() >= 0 and r.max() < (1 << zmax) and c.min() >= 0 and c.max() < (1 << zmax)
+    g = ((np.arange(n, dtype=np.int64) * 2654435761) >> 7) % users
+    rt = (g << (zmax + 1)) | r
+    del g, r
+    parts = []
+    for z in range(zmax, zmin - 1, -1):   # one zoom at a time (its tiles the shift of the zmax ones)
+        k = zmax - z
+        out = oracle.count_tiles(rt >> k, c >> k, z, z)
+        parts.append(cells_digest(out["zoom"], out["row"], out["col"], out["count"]))
+        print("  zoom %d: %d records (%.0f s)" % (z, parts[-1][0], time.time() - t0), flush=True)
+        del out
+    x = 0
+    for p in parts:
+        x ^= p[3]
+    dg = [sum(p[0] for p in parts), sum(p[1] for p in parts), sum(p[2] for p in parts) % (1 << 64), x]
+    return {"kind": kind, "seed": seed, "n": n, "users": users, "zmin": zmin, "zmax": zmax,
+            "group_of_point": "((i * 2654435761) >> 7) % users", "row_tag": "(group << (zoom + 1)) | row",
+            "digest": list(dg), "seconds": round(time.time() - t0, 1)}
 
 
 def _merge(keys, counts, k2, c2):
@@ -110,6 +150,13 @@ def main():
             continue
         print(name, flush=True)
         d[name] = run_case(*case)
+        json.dump(d, open(OUT, "w"), indent=1)
+        print("  ->", d[name]["digest"], flush=True)
+    for name, case in GROUPED.items():
+        if a.only and name != a.only:
+            continue
+        print(name, flush=True)
+        d[name] = run_grouped(*case)
         json.dump(d, open(OUT, "w"), indent=1)
         print("  ->", d[name]["digest"], flush=True)
 

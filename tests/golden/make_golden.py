@@ -279,6 +279,96 @@ def heatmap_goldens(hm, rng):
     print("heatmap goldens:", meta)
 
 
+def chain_goldens(hm, rng):
+    """Rows of points whose tiles leave the shift windows (heatmap_amd/chain_window.py):
+    within ~1e-6 deg of the poles and |lon| > 11520, where the reference's
+    tile-centre re-projection (heatmap.py:60-61,89) is not the shift.  Points
+    whose chain raises in the reference (row21 >= 7,295,112) are left out."""
+    users = ["x1", "u1", "u2", "rt-9", "route"]
+    cases = []
+    for name, mz, d, seed in (("chain_poles_farlon_z21", 16, 5, 31), ("chain_poles_farlon_z14", 9, 5, 32)):
+        r = np.random.default_rng(seed)
+        la = list(47.6 + r.normal(0, 0.01, 120))
+        lo = list(-122.3 + r.normal(0, 0.01, 120))
+        # north pole: 90 - 10^U(-9.5, -5) (rows far below the window at zoom 21)
+        for e in r.uniform(-9.5, -5.0, 40):
+            la.append(90.0 - 10.0 ** e)
+            lo.append(float(r.uniform(-180, 180)))
+        # south pole: the chain still returns (rows up to ~7.29e6 at zoom 21)
+        for e in r.uniform(-5.5, -3.5, 25):
+            la.append(-90.0 + 10.0 ** e)
+            lo.append(float(r.uniform(-180, 180)))
+        # far longitudes: |lon| in (11520, 3e5), and a few beyond
+        for v in r.uniform(11520.0, 3e5, 30):
+            la.append(float(r.uniform(-60, 60)))
+            lo.append(float(v) * (1 if r.random() < 0.5 else -1))
+        for v in (1e6, -2.5e6, 7.77e7):
+            la.append(10.0)
+            lo.append(v)
+        rows = mixed_rows(np.array(la), np.array(lo), rng, users, 0.15)
+        # drop the points whose chain raises in the reference
+        ok = []
+        for row in rows:
+            try:
+                run_build_heatmaps(hm, [row], mz, d)
+                ok.append(row)
+            except (ValueError, OverflowError):
+                pass
+        cases.append((name, ok, mz, d))
+    meta = []
+    for name, rows, mz, d in cases:
+        res = run_build_heatmaps(hm, rows, mz, d)
+        with gzip.open(os.path.join(HERE, "heatmap_rows_%s.json.gz" % name), "wt") as f:
+            json.dump({"max_zoom_level": mz, "detail_zoom_delta": d, "input": rows, "rows": res}, f)
+        meta.append((name, len(rows), len(res)))
+    print("chain goldens:", meta)
+
+
+def weighted_locations_golden(hm, rng):
+    """build_heatmaps on locations other than dataframe_loader's: tiles at other
+    zooms (coarser and finer than the detail zoom), dyadic float counts (exact
+    in any summation order), and one level's heatmap_to_locations output fed
+    back in; with default constants and MAX_ZOOM_LEVEL = 9.  Some tiles lie
+    outside the shift windows (poles, far columns)."""
+    users = ["x1", "u1", "u2", "rt-9", "route", "all"]
+    out = {}
+    for mz in (16, 9):
+        hm.MAX_ZOOM_LEVEL = mz
+        try:
+            zmax = mz + 5
+            locs = []
+            r = np.random.default_rng(40 + mz)
+            for i in range(300):
+                z = int(r.choice([zmax, zmax, zmax - 3, zmax + 2, 12, 7]))
+                la = float(47.6 + r.normal(0, 0.05)) if i % 10 else float(r.uniform(-85, 85))
+                lo = float(-122.3 + r.normal(0, 0.05)) if i % 10 else float(r.uniform(-180, 180))
+                if i % 37 == 0:
+                    la = 90.0 - 10.0 ** float(r.uniform(-9, -6))
+                if i % 41 == 0:
+                    lo = float(r.uniform(12000, 90000))
+                tid = hm.Tile.tile_id_from_lat_long(la, lo, z)
+                locs.append({"userId": users[int(r.integers(0, len(users)))], "tileId": tid,
+                             "count": float(r.choice([1.0, 2.0, 0.5, 3.25, 7.0])), "timespan": "alltime"})
+            # one level of the reference's own output, fed back in as locations
+            rows = [{"latitude": float(47.6 + r.normal(0, 0.02)), "longitude": float(-122.3 + r.normal(0, 0.02)),
+                     "source": "gps", "user_id": users[int(r.integers(0, len(users)))], "timestamp": 0}
+                    for _ in range(200)]
+            lvl = list(hm.build_heatmaps(RDD(rows).flatMap(hm.dataframe_loader)))
+            lvl = [b for b in lvl if b[0].split("|")[2].startswith("%d_" % (zmax - 1 - 5))]
+            for b in lvl[:40]:
+                locs.extend(hm.heatmap_to_locations(b))
+            res = {}
+            for k, v in hm.build_heatmaps(RDD(locs)):
+                assert k not in res
+                res[k] = v
+            out[str(mz)] = {"locations": locs, "rows": res}
+        finally:
+            hm.MAX_ZOOM_LEVEL = 16
+    with gzip.open(os.path.join(HERE, "weighted_locations.json.gz"), "wt") as f:
+        json.dump(out, f)
+    print("weighted locations:", {k: (len(v["locations"]), len(v["rows"])) for k, v in out.items()})
+
+
 def canonical_digest(items):
     h = hashlib.sha256()
     for it in items:
@@ -383,6 +473,10 @@ def main():
         hotspot_zoom_digest(Tile)
     if "utils" in todo or not a.only:
         tile_utils_golden(Tile, np.random.default_rng(20261016))
+    if "chain" in todo or not a.only:
+        chain_goldens(hm, np.random.default_rng(20261017))
+    if "weighted" in todo or not a.only:
+        weighted_locations_golden(hm, np.random.default_rng(20261018))
     if "c1" in todo and not a.quick:
         config1_digest(Tile, hm)
 

@@ -20,7 +20,7 @@ from heatmap_amd import device
 
 pytestmark = pytest.mark.gpu
 
-from digest import device_digest  # noqa: E402
+from digest import device_cells_digest, device_digest  # noqa: E402
 
 
 def _golden(name):
@@ -32,7 +32,8 @@ def _golden(name):
 
 
 @pytest.mark.parametrize("name,hot", [("hotspots_1e9_z0-18", 1), ("hotspots_1e9_z0-18", 0),
-                                      ("skew_1e9_z0-18", 1), ("skew_1e9_z0-18", 0), ("uniform_6e8_z0-18", 1)])
+                                      ("skew_1e9_z0-18", 1), ("skew_1e9_z0-18", 0), ("uniform_6e8_z0-18", 1),
+                                      ("hotspots_1e9_z6-21", 1)])
 def test_fullsize_cloud(gpu, name, hot):
     torch = gpu
     g = _golden(name)
@@ -77,3 +78,33 @@ def test_fullsize_stream(gpu):
         n, keys, counts = s.extract_device(base + k)[:3]
         assert device_digest(torch, keys[:n], counts[:n]) == _golden(name)["digest"], name
     s.close()
+
+
+def test_fullsize_grouped(gpu):
+    """hm_count_grouped at the reference's production zooms (detail zooms 21..6,
+    heatmap.py:16-17,109): 1e8 hotspot points x 10,000 user groups, every
+    (group, zoom, row, col, count) record against the C oracle's digest
+    (tests/golden/make_bigdigest.py: group-tagged rows, every zoom the shift)."""
+    torch = gpu
+    import ctypes
+
+    from heatmap_amd import _lib
+
+    g = _golden("grouped_hotspots_1e8_u10000_z6-21")
+    n, users, zmin, zmax = g["n"], g["users"], g["zmin"], g["zmax"]
+    lat = torch.empty(n, dtype=torch.float64, device="cuda")
+    lon = torch.empty(n, dtype=torch.float64, device="cuda")
+    device.synth(g["kind"], lat, lon, seed=g["seed"])
+    grp = (((torch.arange(n, device="cuda", dtype=torch.int64) * 2654435761) >> 7) % users).to(torch.int32)
+    ctx = device.context(0)
+    cap = 10 * n
+    cells = torch.empty(5 * cap, dtype=torch.int64, device="cuda")
+    nout = ctypes.c_int64(0)
+    p = device._ptr
+    rc = ctx.L.hm_count_grouped(ctx.ptr, p(lat), p(lon), ctypes.c_void_p(0), p(grp), n, zmin, zmax, p(cells), cap,
+                                ctypes.byref(nout))
+    assert rc == _lib.HM_OK, rc
+    del lat, lon, grp
+    rec = cells[:5 * nout.value].reshape(-1, 5)
+    gr, z, r, c, cnt = (rec[:, i] for i in range(5))
+    assert device_cells_digest(torch, z, (gr << (z + 1)) | r, c, cnt) == g["digest"]

@@ -12,7 +12,7 @@ import pyarrow.parquet as pq
 import pytest
 
 from heatmap_amd import heatmap, io
-from test_oracle import _oracle_counters
+from test_oracle import _oracle_counters, _oracle_project
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
 NAMES = sorted(f for f in os.listdir(GOLDEN) if f.startswith("heatmap_rows_"))
@@ -58,7 +58,8 @@ def test_table_matches_reference_rows(tmp_path, name):
     g = _golden(name)
     lat, lon, keep, users = io.load_locations(g["input"])
     mz, d = g["max_zoom_level"], g["detail_zoom_delta"]
-    rows = heatmap.assemble_rows(*_oracle_counters(lat, lon, d + 1, mz + d), users, keep, mz, d)
+    rows = heatmap.assemble_rows(*_oracle_counters(lat, lon, d + 1, mz + d), users, keep, mz, d,
+                                 project=_oracle_project)
     t = io.rows_to_table(rows)
     assert t.column_names == ["id", "heatmap"]
     p = str(tmp_path / "heatmaps.parquet")
@@ -69,9 +70,11 @@ def test_table_matches_reference_rows(tmp_path, name):
 @pytest.mark.gpu
 @pytest.mark.parametrize("name", NAMES)
 def test_batch_main_on_device(gpu, tmp_path, name):
-    """All five reference row goldens (incl. edges_z14: kept points outside
-    [0, 2^z)^2, and seattle_mixed_z21: the reference's own constants), end to
-    end on the device: columnar load, two device passes, vectorised rows."""
+    """Every reference row golden (incl. edges_z14: kept points outside
+    [0, 2^z)^2; seattle_mixed_z21: the reference's own constants; chain_*:
+    tiles near the poles and at |lon| > 11520, outside the shift windows),
+    end to end on the device: columnar load, two device passes, vectorised
+    rows."""
     g = _golden(name)
     p = str(tmp_path / "out.parquet")
     t = io.batch_main(g["input"], sink=p, max_zoom_level=g["max_zoom_level"], delta=g["detail_zoom_delta"])
@@ -126,3 +129,17 @@ def test_chain_window_table_matches_reference_chain():
             clo, chi = cw.COLS[z][j]
             for c in (clo, chi - 1, -1, 1 << z):
                 assert oracle._recentre(z, 0, c, z - j)[1] == c >> j, (z, j, c)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mz", ["16", "9"])
+def test_build_heatmaps_weighted_locations_on_device(gpu, mz, monkeypatch):
+    """build_heatmaps(locations) with tiles at other zooms and float counts
+    (the reference accepts its own heatmap_to_locations output fed back in):
+    rows equal to the reference's (tests/golden/weighted_locations.json.gz)."""
+    import gzip
+    import json
+
+    g = json.load(gzip.open(os.path.join(GOLDEN, "weighted_locations.json.gz"), "rt"))[mz]
+    monkeypatch.setattr(heatmap, "MAX_ZOOM_LEVEL", int(mz))
+    assert dict(heatmap.build_heatmaps(g["locations"])) == g["rows"]

@@ -116,14 +116,14 @@ def _cloud(kind, n, start):
     return lat, lon
 
 
-def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out):
+def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out, wide_rank=1):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=ws)
     per = n // ws
     lat, lon = _cloud(kind, per, rank * per)
     k, c, x = _split(oracle.count(lat, lon, None, zmin, zmax))
-    if kind == "skew" and rank == 1:
+    if kind == "skew" and rank == wide_rank:
         # one rank's count of one sparse cell past 2^32: every rank routes its
         # counts as int64 (the flag rides on the group-size exchange)
         j = int(np.nonzero((k >> 58) > dense_zmax)[0][0])
@@ -135,22 +135,31 @@ def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("kind,zmax,dense_zmax", [("hotspots", 18, 8), ("uniform", 12, -1), ("skew", 18, 10)])
-def test_merge_two_ranks(kind, zmax, dense_zmax):
-    ws, n, zmin = 2, 60000, 0
+@pytest.mark.parametrize("ws,kind,zmax,dense_zmax", [(2, "hotspots", 18, 8), (2, "uniform", 12, -1),
+                                                      (2, "skew", 18, 10), (4, "hotspots", 16, 10),
+                                                      (4, "skew", 18, 8)])
+def test_merge_ranks(ws, kind, zmax, dense_zmax):
+    """ws gloo ranks (CPU stand-ins of the device operations): the union of
+    the owned cells equals one count; with ws = 4 the owner hash spreads over
+    four ranks and (skew) rank ws - 1 forces every rank onto the int64 route
+    (HM_E_WIDE agreement)."""
+    n, zmin = 60000, 0
+    wide_rank = ws - 1
     mgr = mp.Manager()
     out = mgr.dict()
-    mp.start_processes(_worker, args=(ws, _port(), kind, n, zmin, zmax, dense_zmax, out), nprocs=ws,
+    mp.start_processes(_worker, args=(ws, _port(), kind, n, zmin, zmax, dense_zmax, out, wide_rank), nprocs=ws,
                        join=True, start_method="spawn")
     keys = np.concatenate([out[r][0] for r in range(ws)])
     counts = np.concatenate([out[r][1] for r in range(ws)])
     xs = np.concatenate([out[r][2].reshape(-1, 4) for r in range(ws)])
     assert len(np.unique(keys)) == len(keys)            # every cell has exactly one owner
+    if ws > 2:
+        assert all(len(out[r][0]) > 0 for r in range(ws))   # the owner hash reaches every rank
     lat = np.concatenate([_cloud(kind, n // ws, r * (n // ws))[0] for r in range(ws)])
     lon = np.concatenate([_cloud(kind, n // ws, r * (n // ws))[1] for r in range(ws)])
     rk, rc, rx = _split(oracle.count(lat, lon, None, zmin, zmax))
-    if kind == "skew":                                  # the count rank 1 raised past 2^32
-        k1, _, _ = _split(oracle.count(*_cloud(kind, n // ws, n // ws), None, zmin, zmax))
+    if kind == "skew":                                  # the count rank wide_rank raised past 2^32
+        k1, _, _ = _split(oracle.count(*_cloud(kind, n // ws, wide_rank * (n // ws)), None, zmin, zmax))
         rc[np.searchsorted(rk, k1[(k1 >> 58) > dense_zmax][0])] += 1 << 32
     o, ro = np.argsort(keys), np.argsort(rk)
     assert np.array_equal(keys[o], rk[ro])

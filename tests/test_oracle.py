@@ -127,6 +127,12 @@ def _load_rows(name):
         return json.load(f)
 
 
+def _oracle_project(lat, lon, z):
+    """ChainFix's forward projection through the oracle (CPU tests)."""
+    return (np.array([oracle._row_of(a, z) for a in lat], np.int64),
+            np.array([oracle._col_of(b, z) for b in lon], np.int64))
+
+
 @pytest.mark.parametrize("name", ROW_GOLDENS)
 def test_assemble_rows_vs_reference(name):
     """heatmap_amd's row layout + 'all' weighting on oracle counts == build_heatmaps rows."""
@@ -137,7 +143,8 @@ def test_assemble_rows_vs_reference(name):
     keep = np.array([r["source"] != "background" for r in rows])
     users = [r["user_id"] for r in rows]
     mz, d = g["max_zoom_level"], g["detail_zoom_delta"]
-    cells = heatmap.assemble_cells(*_oracle_counters(lat, lon, d + 1, mz + d), users, keep, mz, d)
+    cells = heatmap.assemble_cells(*_oracle_counters(lat, lon, d + 1, mz + d), users, keep, mz, d,
+                                   project=_oracle_project)
     assert heatmap.cells_to_rows(cells) == g["rows"]
     # the vectorised (id, JSON) table holds the same rows
     t = heatmap.cells_to_table(cells).to_pydict()
@@ -145,7 +152,7 @@ def test_assemble_rows_vs_reference(name):
     assert len(t["id"]) == len(g["rows"])
 
 
-@pytest.mark.parametrize("name", ROW_GOLDENS[:3])
+@pytest.mark.parametrize("name", ROW_GOLDENS[:3] + [n for n in ROW_GOLDENS if "chain" in n])
 def test_python_row_restatement_vs_reference(name):
     """oracle.build_heatmap_rows (literal re-projection chain) == build_heatmaps rows."""
     g = _load_rows(name)
@@ -184,3 +191,16 @@ def test_count_tiles_matches_count():
     b = oracle.count(lat, lon, None, 0, 14)
     for k in ("zoom", "row", "col", "count"):
         assert np.array_equal(a[k], b[k]), k
+
+
+@pytest.mark.parametrize("mz", ["16", "9"])
+def test_weighted_locations_vs_reference(mz):
+    """build_heatmaps on locations at other zooms with float counts (and one
+    level's heatmap_to_locations output) -- the product's host assembly with
+    the oracle's projection == the reference's rows."""
+    g = json.load(gzip.open(os.path.join(GOLDEN, "weighted_locations.json.gz"), "rt"))[mz]
+    locs = g["locations"]
+    zs, rows, cols = zip(*[(int(a), int(b), int(c)) for a, b, c in (l["tileId"].split("_") for l in locs)])
+    cells = heatmap.weighted_location_cells(zs, rows, cols, [l["userId"] for l in locs],
+                                            [l["count"] for l in locs], int(mz) + 5, 5, project=_oracle_project)
+    assert heatmap.cells_to_rows(cells) == g["rows"]
