@@ -35,7 +35,7 @@ EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_st
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
            "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_cells_merge_runs",
-           "hm_dense_cells", "hm_format_bins", "hm_bench_read"]
+           "hm_dense_cells", "hm_format_bins", "hm_format_ids", "hm_bench_read"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -113,6 +113,7 @@ def load() -> ctypes.CDLL:
                                           P(c.c_int64)]
         L.hm_dense_cells.argtypes = [vp, vp, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_format_bins.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, c.c_int64, vp]
+        L.hm_format_ids.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, c.c_int64, vp]
         for name in EXPORTS:
             getattr(L, name).restype = getattr(L, name).restype or c.c_int
         L.hm_status_string.restype = c.c_char_p

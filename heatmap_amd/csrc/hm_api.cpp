@@ -148,7 +148,7 @@ enum {
     B_SLOTBKT, B_GSLOTS, B_SPCODES, B_DESC0,
     /* exotic list and the general path (hm_general.hip) */
     B_X_ROW = B_DESC0 + HM_MAX_LEVELS, B_X_COL, B_X_IDX, B_GEN_KA, B_GEN_KB, B_GEN_FLAG, B_GEN_IDX, B_GEN_C,
-    B_GEN_HIST, B_GEN_ORAND, B_GL_GRP,
+    B_GEN_KHA, B_GEN_KHB, B_GEN_HIST, B_GEN_ORAND, B_GL_GRP,
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
     B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS, B_MB_CNT2, B_MB_OFF2,
@@ -414,10 +414,12 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     if (n == 0) return HM_OK;
     if (n >= (1ull << 32)) return HM_E_ARG;   /* radix ranks are u32 */
     hipStream_t s = ctx->stream;
-    ulonglong2 *ka, *kb;
+    uint64_t *klo[2], *khi[2];
     unsigned long long* orand;
-    ENSURE(B_GEN_KA, n * 16, ka);
-    ENSURE(B_GEN_KB, n * 16, kb);
+    ENSURE(B_GEN_KA, n * 8, klo[0]);
+    ENSURE(B_GEN_KB, n * 8, klo[1]);
+    ENSURE(B_GEN_KHA, n * 8, khi[0]);
+    ENSURE(B_GEN_KHB, n * 8, khi[1]);
     ENSURE(B_GEN_ORAND, 4 * 8, orand);
     unsigned long long* up = ctx->host_state + ST_COUNT;
     HIPCHK(hm_sync(s));
@@ -428,9 +430,8 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     HIPCHK(hipMemcpyAsync(orand, up, 4 * 8, hipMemcpyHostToDevice, s));
     if (lat) {
         /* points: projected straight into keys (the kept ones, compacted) */
-        ctx->host_state[ST_XCOUNT] = 0;
         HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, sizeof(unsigned long long), s));
-        hm_launch_project_keys(s, lat, lon, keep, group, (int64_t)n, Z, ka, ctx->state + ST_XCOUNT,
+        hm_launch_project_keys(s, lat, lon, keep, group, (int64_t)n, Z, klo[0], khi[0], ctx->state + ST_XCOUNT,
                                ctx->state + ST_ERR, orand);
     } else {
         HmGenArgs ga;
@@ -440,7 +441,8 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
         ga.index = index;
         ga.n = n;
         ga.Z = Z;
-        ga.keys = ka;
+        ga.klo = klo[0];
+        ga.khi = khi[0];
         ga.orand = orand;
         ga.err_word = ctx->state + ST_ERR;
         hm_launch_gen_keys(s, ga);
@@ -455,7 +457,9 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
         n = ctx->host_state[ST_XCOUNT];
         if (n == 0) return HM_OK;
     }
-    /* LSD passes over the digits that differ between keys */
+    /* LSD passes over the digits that differ between keys; the high halves
+     * move only when they differ */
+    const bool wide = down[1] != down[3];
     const unsigned __int128 var = ((((unsigned __int128)down[1]) << 64) | down[0]) ^
                                   ((((unsigned __int128)down[3]) << 64) | down[2]);
     int shs[16], np = 0;
@@ -463,8 +467,7 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
         if ((uint64_t)((var >> sh) & 0xFF)) shs[np++] = sh;
     uint8_t* rxs;
     ENSURE(B_GEN_HIST, 256 + 16 * 2048 + hm_rx_os_tiles(n) * 2048, rxs);
-    ulonglong2* cur = hm_launch_rx_sort(s, ka, kb, n, shs, np, rxs);
-    ulonglong2* oth = cur == ka ? kb : ka;
+    const int cur = hm_launch_rx_sort(s, wide, klo, khi, n, shs, np, rxs);
     HIPCHK(hipGetLastError());
     /* zoom cascade (k_cascade): step k makes the zoom-(Z-k) cells and writes
      * the records of zoom Z-k+1; a last launch writes the zmin records.  Item
@@ -485,24 +488,29 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     memset(&ca, 0, sizeof(ca));
     ca.tstat = (uint64_t*)(cs + 512);
     ca.e = e;
+    ca.hic = down[1];
+    int in = cur;   /* buffer of the step's input keys */
     for (int k = 0; k <= K; k++) {
-        ca.kin = k ? oth : cur;
+        ca.kin_lo = klo[in];
+        ca.kin_hi = khi[in];
         ca.ein = k ? (k & 1 ? e0 : e1) : nullptr;
         ca.m_in = k ? mdev + (k - 1) : nullptr;
         ca.m_host = n;
-        ca.shift = k ? 2 : 0;
+        ca.clr = 2 * k;
+        ca.Z = Z;
         ca.zin = Z - k + 1;
         ca.emit = k > 0;
-        ca.kout = k ? cur : oth;
+        ca.kout_lo = klo[1 - in];
+        ca.kout_hi = khi[1 - in];
         ca.eout = k & 1 ? e1 : e0;
         ca.m_out = mdev + k;
         ca.epoch = (uint64_t)k + 1;
         ca.ticket = tick + k;
         ca.rbase_in = k ? rbase + k : nullptr;
         ca.rbase_out = k ? rbase + k + 1 : nullptr;
-        hm_launch_cascade(s, ca, n, k == K);
+        hm_launch_cascade(s, ca, n, k == K, wide);
         HIPCHK(hipGetLastError());
-        if (k) std::swap(cur, oth);
+        in = 1 - in;
     }
     HIPCHK(hipMemcpyAsync(down, rbase + K + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hm_sync(s));
@@ -1697,6 +1705,22 @@ extern "C" int hm_format_bins(hm_ctx* ctx, const int64_t* zoom, const int64_t* r
     HIPCHK(hipSetDevice(ctx->device));
     HmFormatArgs a{zoom, row, col, value, head, last, offset, n, text};
     hm_launch_format_bins(ctx->stream, a);
+    HIPCHK(hipGetLastError());
+    return HM_OK;
+}
+
+extern "C" int hm_format_ids(hm_ctx* ctx, const uint8_t* names, const int64_t* name_off, const int64_t* label,
+                             const uint8_t* spans, const int64_t* span_off, const int64_t* span, const int64_t* tz,
+                             const int64_t* tr, const int64_t* tc, const int64_t* offset, int64_t n, uint8_t* text)
+{
+    if (!ctx || n < 0 ||
+        (n > 0 && (!names || !name_off || !label || !spans || !span_off || !span || !tz || !tr || !tc || !offset ||
+                   !text)))
+        return HM_E_ARG;
+    if (n == 0) return HM_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    HmIdArgs a{names, name_off, label, spans, span_off, span, tz, tr, tc, offset, n, text};
+    hm_launch_format_ids(ctx->stream, a);
     HIPCHK(hipGetLastError());
     return HM_OK;
 }

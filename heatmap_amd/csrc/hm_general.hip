@@ -9,15 +9,15 @@
  *     in one pass, the per-user keys of heatmap.py:64-75.
  *
  * Input: exact zoom-Z tiles (int64 row, col) and an optional u32 group.  A
- * point's key is 128 bits,
- *     group (32) | sr + 16 (5) | sc + 2^47 (48) | morton(ro, co) (2Z)
+ * point's key is 128 bits (hm_genkey.h),
+ *     sr + 16 (5) | sc + 2^47 (48) | group (32) | morton(ro, co) (2Z)
  * where sr = row >> Z and sc = col >> Z (arithmetic shifts) name the point's
  * zoom-0 tile ("super tile", any integers) and ro, co its tile's offsets inside
- * it.  The zoom-(Z-k) cell of the point is key >> 2k: the shift of a tile
- * (exact for negative rows and huge columns too) only drops
- * Morton bits.  So one LSD radix sort of the keys orders every zoom at once,
- * and the zoom cascade is a run-length reduction of the previous zoom's sorted
- * unique cells: zoom Z-k+1's cells shifted by 2 are non-decreasing.
+ * it.  The zoom-(Z-k) cell of the point is the key with its low 2k bits
+ * cleared: the shift of a tile (exact for negative rows and
+ * huge columns too) only drops Morton bits.  So one LSD radix sort of the keys
+ * orders every zoom at once, and the zoom cascade is a run-length reduction of
+ * the previous zoom's sorted unique cells.
  *
  * Radix sort: keys only, 8-bit digits, LSD, stable, one sweep per digit
  * (k_rx_onesweep); digits that are the same in every key (an OR/AND
@@ -34,6 +34,61 @@
 /* ------------------------------------------------------------------------ */
 /* keys                                                                      */
 /* ------------------------------------------------------------------------ */
+/* Keys live as two u64 arrays (low and high halves).  When the high halves
+ * are all equal (one super tile and groups < 2^(64 - 2Z): the usual case)
+ * the sort and the cascade move only the low halves ("narrow", KT =
+ * uint64_t) and the high half is a constant of the call; otherwise both
+ * (KT = hm_u128). */
+
+template <typename KT> __device__ __forceinline__ KT hm_kld(const uint64_t* lo, const uint64_t* hi, uint64_t i);
+template <> __device__ __forceinline__ uint64_t hm_kld<uint64_t>(const uint64_t* lo, const uint64_t*, uint64_t i)
+{
+    return lo[i];
+}
+template <> __device__ __forceinline__ hm_u128 hm_kld<hm_u128>(const uint64_t* lo, const uint64_t* hi, uint64_t i)
+{
+    return ((hm_u128)hi[i] << 64) | (hm_u128)lo[i];
+}
+__device__ __forceinline__ void hm_kst(uint64_t* lo, uint64_t*, uint64_t i, uint64_t k) { lo[i] = k; }
+__device__ __forceinline__ void hm_kst(uint64_t* lo, uint64_t* hi, uint64_t i, hm_u128 k)
+{
+    lo[i] = (uint64_t)k;
+    hi[i] = (uint64_t)(k >> 64);
+}
+__device__ __forceinline__ hm_u128 hm_k128(uint64_t k, uint64_t hic) { return ((hm_u128)hic << 64) | (hm_u128)k; }
+__device__ __forceinline__ hm_u128 hm_k128(hm_u128 k, uint64_t) { return k; }
+__device__ __forceinline__ uint64_t hm_kshfl_up(uint64_t k) { return __shfl_up((unsigned long long)k, 1, 64); }
+__device__ __forceinline__ hm_u128 hm_kshfl_up(hm_u128 k)
+{
+    return ((hm_u128)__shfl_up((unsigned long long)(k >> 64), 1, 64) << 64) |
+           (hm_u128)__shfl_up((unsigned long long)k, 1, 64);
+}
+__device__ __forceinline__ uint64_t hm_kshfl_down(uint64_t k) { return __shfl_down((unsigned long long)k, 1, 64); }
+__device__ __forceinline__ hm_u128 hm_kshfl_down(hm_u128 k)
+{
+    return ((hm_u128)__shfl_down((unsigned long long)(k >> 64), 1, 64) << 64) |
+           (hm_u128)__shfl_down((unsigned long long)k, 1, 64);
+}
+
+/* OR / AND of the keys into orand[0..3] (lo, hi | lo, hi) */
+__device__ __forceinline__ void hm_orand_flush(unsigned long long* orand, unsigned long long o_lo,
+                                               unsigned long long o_hi, unsigned long long n_lo,
+                                               unsigned long long n_hi)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        o_lo |= __shfl_xor(o_lo, o, 64);
+        o_hi |= __shfl_xor(o_hi, o, 64);
+        n_lo &= __shfl_xor(n_lo, o, 64);
+        n_hi &= __shfl_xor(n_hi, o, 64);
+    }
+    if (hm_lane() == 0) {
+        atomicOr(&orand[0], o_lo);
+        atomicOr(&orand[1], o_hi);
+        atomicAnd(&orand[2], n_lo);
+        atomicAnd(&orand[3], n_hi);
+    }
+}
 
 __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 {
@@ -50,25 +105,13 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
             const uint64_t src = a.index ? (uint64_t)a.index[i] : i;
             atomicMin(a.err_word, ((unsigned long long)src << 8) | (unsigned long long)HM_E_RANGE);
         }
-        hm_st128(a.keys, i, k);
+        hm_kst(a.klo, a.khi, i, k);
         o_lo |= (unsigned long long)k;
         o_hi |= (unsigned long long)(k >> 64);
         n_lo &= (unsigned long long)k;
         n_hi &= (unsigned long long)(k >> 64);
     }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        o_lo |= __shfl_xor(o_lo, o, 64);
-        o_hi |= __shfl_xor(o_hi, o, 64);
-        n_lo &= __shfl_xor(n_lo, o, 64);
-        n_hi &= __shfl_xor(n_hi, o, 64);
-    }
-    if (hm_lane() == 0) {
-        atomicOr(&a.orand[0], o_lo);
-        atomicOr(&a.orand[1], o_hi);
-        atomicAnd(&a.orand[2], n_lo);
-        atomicAnd(&a.orand[3], n_hi);
-    }
+    hm_orand_flush(a.orand, o_lo, o_hi, n_lo, n_hi);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -78,7 +121,7 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 /* One zoom step per launch.  The input is a sorted list of level-(z+1) cells
  * (or, at the first step, the sorted raw keys, every one a point), each with
  * its END: the inclusive prefix of the counts, so a cell's count is END[i] -
- * END[i-1].  A zoom-z cell is key >> 2; its END is the END of the last fine
+ * END[i-1].  A zoom-z cell is the key with two more low bits cleared; its END is the END of the last fine
  * cell of its run -- prefixes survive coarsening, so no count is ever summed.
  * The step writes the unique zoom-z keys and their ENDs, compacted: a head's
  * slot is the number of heads before it, from a block scan of head ballots
@@ -87,8 +130,8 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
  * pass it writes the records of its input level (level z+1, at the running
  * record offset + i).  Sizes stay on the device: the step reads its item
  * count from the previous step's m_out, so the zoom cascade runs without a
- * host round trip.  Traffic per step: 20 B read per input cell, 20 B written
- * per output cell, one record per input cell. */
+ * host round trip.  Traffic per step (narrow keys): 12 B read per input
+ * cell, 12 B written per output cell, one record per input cell. */
 #define HM_CS_THREADS 256
 #define HM_CS_IT 8
 #define HM_CS_TILE (HM_CS_THREADS * HM_CS_IT)
@@ -98,19 +141,12 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 
 /* one record of cell key k at zoom z (all lanes of the wave call it: the
  * split mode appends per wave) */
-__device__ __forceinline__ void hm_gen_record(const HmGenEmit& e, hm_u128 k, int z, uint64_t cnt, bool in, uint64_t q)
+__device__ __forceinline__ void hm_gen_record(const HmGenEmit& e, hm_u128 k, int Z, int z, uint64_t cnt, bool in,
+                                              uint64_t q)
 {
     int64_t row = 0, col = 0;
-    hm_u128 root = 0;
-    if (in) {
-        root = k >> (2 * z);
-        const uint64_t m = (uint64_t)(k & ((((hm_u128)1) << (2 * z)) - 1));
-        const int64_t sr = (int64_t)(uint64_t)((root >> 48) & 31) - HM_GEN_SR_BIAS;
-        const int64_t sc = (int64_t)(uint64_t)(root & ((((hm_u128)1) << HM_GEN_SC_BITS) - 1)) - HM_GEN_SC_BIAS;
-        /* sr * 2^z, sc * 2^z as unsigned shifts (two's complement) */
-        row = (int64_t)(((uint64_t)sr << z) + hm_compact21(m >> 1));
-        col = (int64_t)(((uint64_t)sc << z) + hm_compact21(m));
-    }
+    uint32_t g = 0;
+    if (in) hm_gen_decode(k, Z, z, &g, &row, &col);
     bool rec = in;
     if (e.split) {
         /* hm_count fallback: cells inside [0, 2^z)^2 as (HM_KEY, count), the
@@ -137,7 +173,7 @@ __device__ __forceinline__ void hm_gen_record(const HmGenEmit& e, hm_u128 k, int
     if (!rec || q >= e.capacity) return;
     int64_t* r = e.cells + q * e.width;
     int f = 0;
-    if (e.width == 5) r[f++] = (int64_t)(uint64_t)(root >> 53);
+    if (e.width == 5) r[f++] = (int64_t)g;
     r[f++] = z;
     r[f++] = row;
     r[f++] = col;
@@ -178,16 +214,23 @@ __device__ uint64_t hm_cs_lookback(uint64_t* st, int64_t tile, uint64_t epoch)
     return excl;
 }
 
+template <typename KT>
 __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
 {
-    __shared__ uint32_t wtot[HM_CS_IT * 4];
+    constexpr int NW = HM_CS_THREADS / 64, NF = HM_CS_IT * NW;   /* (round, wave) fragments of a tile */
+    __shared__ uint32_t wtot[NF];
+    __shared__ KT kfirst[NF + 1], klast[NF + 1];   /* klast[f + 1]: last key of fragment f; [0]: item t0 - 1 */
+    __shared__ uint32_t elast[NF + 1];
+    __shared__ int64_t stage[NW][64 * 5];               /* a wave's records, written out contiguously */
     __shared__ uint32_t tile_s;
     __shared__ uint64_t excl_s;
     const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
     const uint64_t ntiles = (m + HM_CS_TILE - 1) / HM_CS_TILE;
     const int lane = hm_lane(), w = threadIdx.x >> 6;
-    const int s = a.shift;
+    const KT keep_bits = ~((((KT)1) << a.clr) - 1);
     const unsigned long long rb = a.rbase_in ? *a.rbase_in : 0ull;
+    const int W = a.e.width;
+    const bool staged = a.emit && !a.e.split;
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.rbase_out) *a.rbase_out = rb + m;
     if (m == 0 && blockIdx.x == 0 && threadIdx.x == 0) *a.m_out = 0u;
     for (;;) {
@@ -196,39 +239,85 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
         const uint64_t tile = tile_s;
         if (tile >= ntiles) break;
         const uint64_t t0 = tile * HM_CS_TILE;
-        hm_u128 ks[HM_CS_IT];
-        uint32_t ee[HM_CS_IT], fl[HM_CS_IT];
+        /* every load of the tile first: items, and the items either side */
+        KT k[HM_CS_IT];
+        uint32_t e[HM_CS_IT];
 #pragma unroll
         for (int r = 0; r < HM_CS_IT; r++) {
             const uint64_t i = t0 + (uint64_t)r * HM_CS_THREADS + threadIdx.x;
             const bool v = i < m;
-            const hm_u128 k = v ? hm_ld128(a.kin, i) : (hm_u128)0;
-            const uint32_t e = a.ein ? (v ? a.ein[i] : 0u) : (uint32_t)(i + 1);
-            /* neighbours: lanes of the wave, the wave's edges from memory */
-            hm_u128 kp = ((hm_u128)__shfl_up((unsigned long long)(k >> 64), 1, 64) << 64) |
-                         (hm_u128)__shfl_up((unsigned long long)k, 1, 64);
-            uint32_t ep = __shfl_up(e, 1, 64);
-            hm_u128 kn = ((hm_u128)__shfl_down((unsigned long long)(k >> 64), 1, 64) << 64) |
-                         (hm_u128)__shfl_down((unsigned long long)k, 1, 64);
-            if (lane == 0 && v && i > 0) {
-                kp = hm_ld128(a.kin, i - 1);
-                ep = a.ein ? a.ein[i - 1] : (uint32_t)i;
+            k[r] = v ? hm_kld<KT>(a.kin_lo, a.kin_hi, i) : (KT)0;
+            e[r] = a.ein ? (v ? a.ein[i] : 0u) : (uint32_t)(i + 1);
+        }
+        if (threadIdx.x == 0) {
+            klast[0] = t0 ? hm_kld<KT>(a.kin_lo, a.kin_hi, t0 - 1) : (KT)0;
+            elast[0] = t0 ? (a.ein ? a.ein[t0 - 1] : (uint32_t)t0) : 0u;
+        }
+        if (threadIdx.x == HM_CS_THREADS - 1)
+            kfirst[NF] = t0 + HM_CS_TILE < m ? hm_kld<KT>(a.kin_lo, a.kin_hi, t0 + HM_CS_TILE) : (KT)0;
+#pragma unroll
+        for (int r = 0; r < HM_CS_IT; r++) {
+            const int f = r * NW + w;
+            if (lane == 0) kfirst[f] = k[r];
+            if (lane == 63) {
+                klast[f + 1] = k[r];
+                elast[f + 1] = e[r];
             }
-            if (i == 0) ep = 0;
-            if (lane == 63 && i + 1 < m) kn = hm_ld128(a.kin, i + 1);
-            const hm_u128 kz = k >> s;
-            const bool head = v && (i == 0 || (kp >> s) != kz);
-            const bool tail = v && (i + 1 == m || (kn >> s) != kz);
-            if (a.emit) hm_gen_record(a.e, k, a.zin, (uint64_t)(e - ep), v, rb + i);
+        }
+        __syncthreads();
+        uint32_t fl[HM_CS_IT];
+#pragma unroll
+        for (int r = 0; r < HM_CS_IT; r++) {
+            const int f = r * NW + w;
+            const uint64_t i = t0 + (uint64_t)r * HM_CS_THREADS + threadIdx.x;
+            const bool v = i < m;
+            KT kp = hm_kshfl_up(k[r]), kn = hm_kshfl_down(k[r]);
+            uint32_t ep = __shfl_up(e[r], 1, 64);
+            if (lane == 0) {
+                kp = klast[f];
+                ep = elast[f];
+            }
+            if (lane == 63) kn = kfirst[f + 1];
+            const KT kz = k[r] & keep_bits;
+            const bool head = v && (i == 0 || (kp & keep_bits) != kz);
+            const bool tail = v && (i + 1 == m || (kn & keep_bits) != kz);
+            if (a.emit) {
+                const uint64_t cnt = (uint64_t)(e[r] - ep);
+                if (staged) {
+                    /* the wave's 64 records are consecutive: stage them, then
+                     * store whole 8-B words across the lanes */
+                    const uint64_t i0 = t0 + (uint64_t)r * HM_CS_THREADS + (uint64_t)w * 64;
+                    uint32_t g = 0;
+                    int64_t row = 0, col = 0;
+                    if (v) hm_gen_decode(hm_k128(k[r], a.hic), a.Z, a.zin, &g, &row, &col);
+                    int64_t* sp = &stage[w][lane * W];
+                    int q = 0;
+                    if (W == 5) sp[q++] = (int64_t)g;
+                    sp[q++] = a.zin;
+                    sp[q++] = row;
+                    sp[q++] = col;
+                    sp[q] = (int64_t)cnt;
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    const uint64_t nv = i0 < m ? min<uint64_t>(64, m - i0) : 0;
+                    const uint64_t q0 = rb + i0;
+                    uint64_t nw = q0 < a.e.capacity ? min<uint64_t>(nv, a.e.capacity - q0) * W : 0;
+                    int64_t* dst = a.e.cells + q0 * W;
+                    for (uint32_t x = lane; x < nw; x += 64) dst[x] = stage[w][x];
+                    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                } else {
+                    hm_gen_record(a.e, hm_k128(k[r], a.hic), a.Z, a.zin, cnt, v, rb + i);
+                }
+            }
             const uint64_t hb = __builtin_amdgcn_ballot_w64(head);
-            if (lane == 0) wtot[r * 4 + w] = (uint32_t)__popcll(hb);
-            ks[r] = kz;
-            ee[r] = e;
+            if (lane == 0) wtot[f] = (uint32_t)__popcll(hb);
+            k[r] = kz;
             fl[r] = (uint32_t)head | ((uint32_t)tail << 1) | (hm_mbcnt(hb) << 2);
         }
         __syncthreads();
         if (w == 0) {
-            const uint32_t x = lane < HM_CS_IT * 4 ? wtot[lane] : 0u;
+            const uint32_t x = lane < NF ? wtot[lane] : 0u;
             uint32_t inc = x;
 #pragma unroll
             for (int o = 1; o < 64; o <<= 1) {
@@ -236,7 +325,7 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
                 if (lane >= o) inc += y;
             }
             const uint64_t agg = __shfl(inc, 63, 64);
-            if (lane < HM_CS_IT * 4) wtot[lane] = inc - x;
+            if (lane < NF) wtot[lane] = inc - x;
             if (lane == 0)
                 __hip_atomic_store(a.tstat + tile, hm_cs_word(a.epoch, tile ? HM_CS_FLAG_AGG : HM_CS_FLAG_INC, agg),
                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -253,15 +342,16 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
         const uint64_t excl = excl_s;
 #pragma unroll
         for (int r = 0; r < HM_CS_IT; r++) {
-            const uint64_t j = excl + wtot[r * 4 + w] + (fl[r] >> 2);
-            if (fl[r] & 1u) hm_st128(a.kout, j, ks[r]);
-            if (fl[r] & 2u) a.eout[j + (fl[r] & 1u) - 1] = ee[r];
+            const uint64_t j = excl + wtot[r * NW + w] + (fl[r] >> 2);
+            if (fl[r] & 1u) hm_kst(a.kout_lo, a.kout_hi, j, k[r]);
+            if (fl[r] & 2u) a.eout[j + (fl[r] & 1u) - 1] = e[r];
         }
         __syncthreads();
     }
 }
 
 /* the records of the last level (nothing below it to fold into) */
+template <typename KT>
 __global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
 {
     const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
@@ -271,9 +361,9 @@ __global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
     const uint64_t m_up = (m + 63) & ~63ull;   /* whole waves: split mode appends per wave */
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m_up; i += stride) {
         const bool v = i < m;
-        const hm_u128 k = v ? hm_ld128(a.kin, i) : (hm_u128)0;
+        const KT k = v ? hm_kld<KT>(a.kin_lo, a.kin_hi, i) : (KT)0;
         const uint32_t e = v ? a.ein[i] : 0u, ep = (v && i) ? a.ein[i - 1] : 0u;
-        hm_gen_record(a.e, k, a.zin, (uint64_t)(e - ep), v, rb + i);
+        hm_gen_record(a.e, hm_k128(k, a.hic), a.Z, a.zin, (uint64_t)(e - ep), v, rb + i);
     }
 }
 
@@ -286,21 +376,26 @@ __global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
  * in key order; waves in order), publishes its per-digit counts and resolves
  * its per-digit global offsets with a decoupled look-back over the earlier
  * tiles (one thread per digit), then writes the tile through LDS in digit
- * order, so a digit's keys leave as one contiguous run.  Per pass: 16 B read
- * and 16 B written per key, plus 2 KB of look-back words per tile. */
+ * order, so a digit's keys leave as one contiguous run.  Per pass: 8 B read
+ * and 8 B written per narrow key (16 + 16 wide), plus 2 KB of look-back
+ * words per tile. */
 #define HM_OS_THREADS 256
+#ifndef HM_OS_IT
 #define HM_OS_IT 16
+#endif
 #define HM_OS_TILE (HM_OS_THREADS * HM_OS_IT)
 #define HM_OS_MAXP 16
 
 struct HmRxAll {
-    const ulonglong2* keys;
+    const uint64_t* lo;
+    const uint64_t* hi;
     uint64_t n;
     int np;
     int sh[HM_OS_MAXP];
     unsigned long long* hist;   /* [np][256] */
 };
 
+template <typename KT>
 __global__ __launch_bounds__(256) void k_rx_hist_all(HmRxAll a)
 {
     __shared__ uint32_t h[HM_OS_MAXP * 256];
@@ -308,7 +403,7 @@ __global__ __launch_bounds__(256) void k_rx_hist_all(HmRxAll a)
     __syncthreads();
     const uint64_t stride = (uint64_t)gridDim.x * 256;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < a.n; i += stride) {
-        const hm_u128 k = hm_ld128(a.keys, i);
+        const KT k = hm_kld<KT>(a.lo, a.hi, i);
         for (int p = 0; p < a.np; p++) atomicAdd(&h[p * 256 + ((uint32_t)(k >> a.sh[p]) & 0xFFu)], 1u);
     }
     __syncthreads();
@@ -342,8 +437,10 @@ __global__ __launch_bounds__(64) void k_rx_digit_offsets(unsigned long long* his
 }
 
 struct HmRxPass {
-    const ulonglong2* in;
-    ulonglong2* out;
+    const uint64_t* ilo;
+    const uint64_t* ihi;
+    uint64_t* olo;
+    uint64_t* ohi;
     uint64_t n;
     int sh;
     const unsigned long long* goff;   /* 256 exclusive digit offsets of this pass */
@@ -352,9 +449,10 @@ struct HmRxPass {
     unsigned* ticket;
 };
 
+template <typename KT>
 __global__ __launch_bounds__(HM_OS_THREADS) void k_rx_onesweep(HmRxPass a)
 {
-    __shared__ ulonglong2 stage[HM_OS_TILE];
+    __shared__ KT stage[HM_OS_TILE];
     __shared__ uint32_t wcnt[4][256];
     __shared__ uint32_t dbase[256];      /* tile-local start of each digit */
     __shared__ uint64_t gbase[256];      /* global start of each digit's run of this tile */
@@ -373,13 +471,13 @@ __global__ __launch_bounds__(HM_OS_THREADS) void k_rx_onesweep(HmRxPass a)
         const uint64_t tile = tile_s;
         if (tile >= ntiles) break;
         const uint64_t t0 = tile * HM_OS_TILE + (uint64_t)w * (HM_OS_TILE / 4);
-        hm_u128 k[HM_OS_IT];
+        KT k[HM_OS_IT];
         uint32_t rk[HM_OS_IT / 2];
 #pragma unroll
         for (int r = 0; r < HM_OS_IT; r++) {
             const uint64_t i = t0 + (uint64_t)r * 64 + lane;
             const bool v = i < a.n;
-            k[r] = v ? hm_ld128(a.in, i) : ~(hm_u128)0;
+            k[r] = v ? hm_kld<KT>(a.ilo, a.ihi, i) : ~(KT)0;
         }
 #pragma unroll
         for (int r = 0; r < HM_OS_IT; r++) {
@@ -450,16 +548,15 @@ __global__ __launch_bounds__(HM_OS_THREADS) void k_rx_onesweep(HmRxPass a)
             const uint32_t rank = (rk[r >> 1] >> ((r & 1) * 16)) & 0xFFFFu;
             if (rank != 0xFFFFu) {
                 const uint32_t dd = (uint32_t)(k[r] >> sh) & 0xFFu;
-                stage[wcnt[w][dd] + rank] = make_ulonglong2((unsigned long long)k[r], (unsigned long long)(k[r] >> 64));
+                stage[wcnt[w][dd] + rank] = k[r];
             }
         }
         __syncthreads();
         const uint32_t valid = (uint32_t)min<uint64_t>(HM_OS_TILE, a.n - tile * HM_OS_TILE);
         for (uint32_t j = threadIdx.x; j < valid; j += HM_OS_THREADS) {
-            const ulonglong2 v = stage[j];
-            const hm_u128 kk = ((hm_u128)v.y << 64) | (hm_u128)v.x;
+            const KT kk = stage[j];
             const uint32_t dg = (uint32_t)(kk >> sh) & 0xFFu;
-            a.out[gbase[dg] + (j - dbase[dg])] = v;
+            hm_kst(a.olo, a.ohi, gbase[dg] + (j - dbase[dg]), kk);
         }
         __syncthreads();
     }
@@ -522,46 +619,65 @@ void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a)
 
 uint64_t hm_rx_os_tiles(uint64_t n) { return (n + HM_OS_TILE - 1) / HM_OS_TILE; }
 
-/* LSD sort of n keys over the digits at shifts sh[0..np) (ascending), state =
- * 256 B tickets + np x 2 KB histograms + tiles x 2 KB look-back words, zeroed
- * here.  Returns the buffer that holds the sorted keys. */
-ulonglong2* hm_launch_rx_sort(hipStream_t s, ulonglong2* a, ulonglong2* b, uint64_t n, const int* sh, int np,
-                              uint8_t* state)
+/* LSD sort of n keys (lo[0], hi[0]) over the digits at shifts sh[0..np)
+ * (ascending); (lo[1], hi[1]) is the other buffer.  state = 256 B tickets +
+ * 16 x 2 KB histograms + tiles x 2 KB look-back words, zeroed here.  Returns
+ * the index of the buffer that holds the sorted keys. */
+int hm_launch_rx_sort(hipStream_t s, bool wide, uint64_t* const* lo, uint64_t* const* hi, uint64_t n, const int* sh,
+                      int np, uint8_t* state)
 {
-    if (np == 0) return a;
+    if (np == 0) return 0;
     const uint64_t nt = hm_rx_os_tiles(n);
     (void)hipMemsetAsync(state, 0, 256 + HM_OS_MAXP * 2048 + nt * 2048, s);
     HmRxAll h;
-    h.keys = a;
+    h.lo = lo[0];
+    h.hi = hi[0];
     h.n = n;
     h.np = np;
     for (int p = 0; p < np; p++) h.sh[p] = sh[p];
     h.hist = (unsigned long long*)(state + 256);
-    hipLaunchKernelGGL(k_rx_hist_all, dim3(hm_ggrid(n, 256 * 16, 2048)), dim3(256), 0, s, h);
+    if (wide)
+        hipLaunchKernelGGL(k_rx_hist_all<hm_u128>, dim3(hm_ggrid(n, 256 * 16, 2048)), dim3(256), 0, s, h);
+    else
+        hipLaunchKernelGGL(k_rx_hist_all<uint64_t>, dim3(hm_ggrid(n, 256 * 16, 2048)), dim3(256), 0, s, h);
     hipLaunchKernelGGL(k_rx_digit_offsets, dim3(np), dim3(64), 0, s, h.hist);
-    ulonglong2 *in = a, *out = b;
+    int cur = 0;
     for (int p = 0; p < np; p++) {
         HmRxPass x;
-        x.in = in;
-        x.out = out;
+        x.ilo = lo[cur];
+        x.ihi = hi[cur];
+        x.olo = lo[1 - cur];
+        x.ohi = hi[1 - cur];
         x.n = n;
         x.sh = sh[p];
         x.goff = h.hist + p * 256;
         x.tstat = (uint64_t*)(state + 256 + HM_OS_MAXP * 2048);
         x.epoch = (uint64_t)p + 1;
         x.ticket = (unsigned*)state + p;
-        hipLaunchKernelGGL(k_rx_onesweep, dim3(hm_ggrid(nt, 1, 512)), dim3(HM_OS_THREADS), 0, s, x);
-        std::swap(in, out);
+        if (wide)
+            hipLaunchKernelGGL(k_rx_onesweep<hm_u128>, dim3(hm_ggrid(nt, 1, 512)), dim3(HM_OS_THREADS), 0, s, x);
+        else
+            hipLaunchKernelGGL(k_rx_onesweep<uint64_t>, dim3(hm_ggrid(nt, 1, 1024)), dim3(HM_OS_THREADS), 0, s, x);
+        cur = 1 - cur;
     }
-    return in;
+    return cur;
 }
 
-void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only)
+void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only, bool wide)
 {
-    if (emit_only)
-        hipLaunchKernelGGL(k_cascade_emit, dim3(hm_ggrid(bound, 256, 4096)), dim3(256), 0, s, a);
-    else
-        hipLaunchKernelGGL(k_cascade, dim3(hm_ggrid(bound, HM_CS_TILE, 2048)), dim3(HM_CS_THREADS), 0, s, a);
+    if (emit_only) {
+        if (wide)
+            hipLaunchKernelGGL(k_cascade_emit<hm_u128>, dim3(hm_ggrid(bound, 256, 4096)), dim3(256), 0, s, a);
+        else
+            hipLaunchKernelGGL(k_cascade_emit<uint64_t>, dim3(hm_ggrid(bound, 256, 4096)), dim3(256), 0, s, a);
+    } else {
+        if (wide)
+            hipLaunchKernelGGL(k_cascade<hm_u128>, dim3(hm_ggrid(bound, HM_CS_TILE, 2048)), dim3(HM_CS_THREADS), 0, s,
+                               a);
+        else
+            hipLaunchKernelGGL(k_cascade<uint64_t>, dim3(hm_ggrid(bound, HM_CS_TILE, 2048)), dim3(HM_CS_THREADS), 0,
+                               s, a);
+    }
 }
 
 uint64_t hm_cascade_tiles(uint64_t n) { return (n + HM_CS_TILE - 1) / HM_CS_TILE; }
@@ -622,4 +738,30 @@ void hm_launch_format_bins(hipStream_t s, const HmFormatArgs& a)
     if (a.n <= 0) return;
     const uint64_t blocks = std::min<uint64_t>(8192, ((uint64_t)a.n + 255) / 256);
     hipLaunchKernelGGL(k_format_bins, dim3((unsigned)blocks), dim3(256), 0, s, a);
+}
+
+/* row ids: one thread per row writes  name|span|tz_tr_tc  */
+__global__ __launch_bounds__(256) void k_format_ids(HmIdArgs a)
+{
+    const uint64_t stride = (uint64_t)gridDim.x * 256;
+    for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < (uint64_t)a.n; i += stride) {
+        uint8_t* p = a.text + a.offset[i];
+        const int64_t l = a.label[i], t = a.span[i];
+        for (int64_t q = a.name_off[l]; q < a.name_off[l + 1]; q++) *p++ = a.names[q];
+        *p++ = '|';
+        for (int64_t q = a.span_off[t]; q < a.span_off[t + 1]; q++) *p++ = a.spans[q];
+        *p++ = '|';
+        p = hm_put_u64(p, (uint64_t)a.tz[i]);
+        *p++ = '_';
+        p = hm_put_u64(p, (uint64_t)a.tr[i]);
+        *p++ = '_';
+        p = hm_put_u64(p, (uint64_t)a.tc[i]);
+    }
+}
+
+void hm_launch_format_ids(hipStream_t s, const HmIdArgs& a)
+{
+    if (a.n <= 0) return;
+    const uint64_t blocks = std::min<uint64_t>(8192, ((uint64_t)a.n + 255) / 256);
+    hipLaunchKernelGGL(k_format_ids, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }

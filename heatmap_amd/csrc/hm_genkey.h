@@ -1,24 +1,16 @@
 /* 128-bit cell keys of the general path (hm_general.hip), shared with the
  * list kernels that build them while projecting (hm_kernels.hip):
- *     group (32) | sr + 16 (5) | sc + 2^47 (48) | morton(ro, co) (2Z)
+ *     sr + 16 (5) | sc + 2^47 (48) | group (32) | morton(ro, co) (2Z)
  * sr = row >> Z, sc = col >> Z (arithmetic) name the zoom-0 "super tile";
- * ro, co are the tile's offsets inside it. */
+ * ro, co are the tile's offsets inside it.  The group sits right above the
+ * Morton bits so that a few thousand groups and a single super tile vary in
+ * one contiguous low range of the key (fewest radix digits).  The zoom-(Z-k)
+ * cell of a key is the key with its low 2k bits cleared. */
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 typedef unsigned __int128 hm_u128;
-
-__device__ __forceinline__ hm_u128 hm_ld128(const ulonglong2* p, uint64_t i)
-{
-    const ulonglong2 v = p[i];
-    return ((hm_u128)v.y << 64) | (hm_u128)v.x;
-}
-
-__device__ __forceinline__ void hm_st128(ulonglong2* p, uint64_t i, hm_u128 k)
-{
-    p[i] = make_ulonglong2((unsigned long long)k, (unsigned long long)(k >> 64));
-}
 
 /* 21 -> 42 bit spread / compact (Morton halves) */
 __device__ __forceinline__ uint64_t hm_spread21(uint64_t x)
@@ -53,7 +45,20 @@ __device__ __forceinline__ hm_u128 hm_gen_key(int64_t r, int64_t c, uint32_t g, 
     const uint64_t m = (hm_spread21((uint64_t)r & ((1ull << Z) - 1)) << 1) | hm_spread21((uint64_t)c & ((1ull << Z) - 1));
     *ok = sr >= -HM_GEN_SR_BIAS && sr < HM_GEN_SR_BIAS && sc >= -HM_GEN_SC_BIAS && sc < HM_GEN_SC_BIAS;
     if (!*ok) return 0;
-    const hm_u128 root = ((hm_u128)g << 53) | ((hm_u128)(uint64_t)(sr + HM_GEN_SR_BIAS) << 48) |
-                         (hm_u128)(uint64_t)(sc + HM_GEN_SC_BIAS);
+    const hm_u128 root = ((hm_u128)(uint64_t)(sr + HM_GEN_SR_BIAS) << 80) |
+                         ((hm_u128)(uint64_t)(sc + HM_GEN_SC_BIAS) << 32) | (hm_u128)g;
     return (root << (2 * Z)) | (hm_u128)m;
+}
+
+/* decode of a zoom-z cell key (low 2(Z-z) bits clear) */
+__device__ __forceinline__ void hm_gen_decode(hm_u128 k, int Z, int z, uint32_t* g, int64_t* row, int64_t* col)
+{
+    const hm_u128 root = k >> (2 * Z);
+    const uint64_t m = (uint64_t)(k >> (2 * (Z - z))) & ((1ull << (2 * z)) - 1);
+    const int64_t sr = (int64_t)(uint64_t)((root >> 80) & 31) - HM_GEN_SR_BIAS;
+    const int64_t sc = (int64_t)((uint64_t)(root >> 32) & ((1ull << HM_GEN_SC_BITS) - 1)) - HM_GEN_SC_BIAS;
+    *g = (uint32_t)root;
+    /* sr * 2^z, sc * 2^z as unsigned shifts (two's complement) */
+    *row = (int64_t)(((uint64_t)sr << z) + hm_compact21(m >> 1));
+    *col = (int64_t)(((uint64_t)sc << z) + hm_compact21(m));
 }

@@ -3192,9 +3192,9 @@ void hm_launch_project_list(hipStream_t s, const double* lat, const double* lon,
  * the OR / AND of all keys (the radix sort skips digits they agree on).
  * Errors (projection, or a tile beyond the key's fields) by input index. */
 __global__ __launch_bounds__(256) void k_project_keys(const double* lat, const double* lon, const uint8_t* keep,
-                                                      const uint32_t* group, int64_t n, int Z, ulonglong2* keys,
-                                                      unsigned long long* count, unsigned long long* err_word,
-                                                      unsigned long long* orand)
+                                                      const uint32_t* group, int64_t n, int Z, uint64_t* klo,
+                                                      uint64_t* khi, unsigned long long* count,
+                                                      unsigned long long* err_word, unsigned long long* orand)
 {
     __shared__ double tab[HM_YTAB_N];
     __shared__ uint32_t scr[256 / 64 + 1];
@@ -3238,7 +3238,11 @@ __global__ __launch_bounds__(256) void k_project_keys(const double* lat, const d
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < HM_PL_PPT; j++)
-            if ((pm >> j) & 1u) hm_st128(keys, b + pos++, k[j]);
+            if ((pm >> j) & 1u) {
+                klo[b + pos] = (uint64_t)k[j];
+                khi[b + pos] = (uint64_t)(k[j] >> 64);
+                pos++;
+            }
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
@@ -3256,14 +3260,14 @@ __global__ __launch_bounds__(256) void k_project_keys(const double* lat, const d
 }
 
 void hm_launch_project_keys(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
-                            const uint32_t* group, int64_t n, int Z, ulonglong2* keys, unsigned long long* count,
-                            unsigned long long* err_word, unsigned long long* orand)
+                            const uint32_t* group, int64_t n, int Z, uint64_t* klo, uint64_t* khi,
+                            unsigned long long* count, unsigned long long* err_word, unsigned long long* orand)
 {
     int64_t blocks = (n + 256 * HM_PL_PPT - 1) / (256 * HM_PL_PPT);
     if (blocks > 4096) blocks = 4096;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_project_keys, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, keys,
-                       count, err_word, orand);
+    hipLaunchKernelGGL(k_project_keys, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, klo,
+                       khi, count, err_word, orand);
 }
 
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16, bool few_runs)

@@ -387,6 +387,15 @@ struct HmFormatArgs {
     uint8_t* text;
 };
 void hm_launch_format_bins(hipStream_t s, const HmFormatArgs& a);
+struct HmIdArgs {
+    const uint8_t* names;
+    const int64_t *name_off, *label;
+    const uint8_t* spans;
+    const int64_t *span_off, *span, *tz, *tr, *tc, *offset;
+    int64_t n;
+    uint8_t* text;
+};
+void hm_launch_format_ids(hipStream_t s, const HmIdArgs& a);
 
 /* several memsets in one dispatch (a small call is launch-bound: each
  * hipMemsetAsync is a dispatch of its own) */
@@ -564,7 +573,8 @@ struct HmGenArgs {
     const int64_t* index;       /* input index per entry (error reports), or null */
     uint64_t n;
     int Z;
-    ulonglong2* keys;
+    uint64_t* klo;              /* key halves (hm_genkey.h) */
+    uint64_t* khi;
     unsigned long long* orand;  /* [or_lo, or_hi, and_lo, and_hi] */
     unsigned long long* err_word;
 };
@@ -584,23 +594,27 @@ struct HmGenEmit {
 };
 void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a);
 void hm_launch_project_keys(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
-                            const uint32_t* group, int64_t n, int Z, ulonglong2* keys, unsigned long long* count,
-                            unsigned long long* err_word, unsigned long long* orand);
+                            const uint32_t* group, int64_t n, int Z, uint64_t* klo, uint64_t* khi,
+                            unsigned long long* count, unsigned long long* err_word, unsigned long long* orand);
 void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
                           const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
                           unsigned long long* count);
 uint64_t hm_rx_os_tiles(uint64_t n);
-ulonglong2* hm_launch_rx_sort(hipStream_t s, ulonglong2* a, ulonglong2* b, uint64_t n, const int* sh, int np,
-                              uint8_t* state);
+int hm_launch_rx_sort(hipStream_t s, bool wide, uint64_t* const* lo, uint64_t* const* hi, uint64_t n, const int* sh,
+                      int np, uint8_t* state);
 struct HmCascArgs {
-    const ulonglong2* kin;      /* sorted level-(z+1) cells (or raw keys) */
+    const uint64_t* kin_lo;     /* sorted level-(z+1) cells (or raw keys), low halves */
+    const uint64_t* kin_hi;     /* high halves (wide keys only) */
+    uint64_t hic;               /* narrow keys: the high half of every key */
     const uint32_t* ein;        /* their END prefixes; null: raw keys, END = i + 1 */
     const uint32_t* m_in;       /* item count on the device (null: m_host) */
     uint64_t m_host;
-    int shift;                  /* 0 at the first step (unique raw keys), 2 after */
+    int clr;                    /* low key bits cleared for the output level: 2 (Z - z) */
+    int Z;                      /* zoom of the raw keys */
     int zin;                    /* zoom of the input cells (their records) */
     int emit;                   /* write the input level's records */
-    ulonglong2* kout;
+    uint64_t* kout_lo;
+    uint64_t* kout_hi;
     uint32_t* eout;
     uint32_t* m_out;
     uint64_t* tstat;            /* look-back words, one per tile */
@@ -610,7 +624,7 @@ struct HmCascArgs {
     unsigned long long* rbase_out;        /* = rbase_in + m (offset of the next level) */
     HmGenEmit e;
 };
-void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only);
+void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only, bool wide);
 uint64_t hm_cascade_tiles(uint64_t n);
 
 /* multi-GPU cell exchange (hm_merge.hip) */

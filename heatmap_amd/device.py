@@ -334,11 +334,10 @@ class GroupedCounts:
         return GroupedCounts(self.group[o], self.zoom[o], self.row[o], self.col[o], self.count[o])
 
 
-def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,
-                  tiles: bool = False) -> GroupedCounts:
-    """Per-(group, zoom, row, col) counts in one device pass (hm_count_grouped;
-    tiles=True: lat/lon are int64 zoom-zmax rows/cols, hm_count_grouped_tiles).
-    group: uint32 per point; keep: points to count (all are projected)."""
+def count_grouped_device(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,
+                         tiles: bool = False):
+    """hm_count_grouped with the records left in HBM: an int64 CUDA tensor
+    [m, 5] of (group, zoom, row, col, count), in no particular order."""
     torch = _torch()
     ctx = context(device)
     dt = torch.int64 if tiles else torch.float64
@@ -354,7 +353,10 @@ def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, dev
         kp = _dev(keep, torch.uint8, device)
         if kp.numel() != n:
             raise ValueError("keep must have one entry per point")
-    cap = max(1024, 2 * n + 64)
+    # records <= points x zooms; start there when it is at most 4 GiB of
+    # records (one pass), else at 2 per point and grow on HM_E_CAPACITY
+    nz = int(zmax) - int(zmin) + 1
+    cap = max(1024, n * nz + 64 if n * nz * 40 <= (4 << 30) else 2 * n + 64)
     while True:
         cells = torch.empty(5 * cap, dtype=torch.int64, device=a.device)
         nout = ctypes.c_int64(0)
@@ -368,7 +370,15 @@ def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, dev
             idx, kind = ctx.last_error()
             _lib.raise_for(rc, idx)
         break
-    x = cells[:5 * nout.value].cpu().numpy().reshape(-1, 5)
+    return cells[:5 * nout.value].view(-1, 5)
+
+
+def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,
+                  tiles: bool = False) -> GroupedCounts:
+    """Per-(group, zoom, row, col) counts in one device pass (hm_count_grouped;
+    tiles=True: lat/lon are int64 zoom-zmax rows/cols, hm_count_grouped_tiles).
+    group: uint32 per point; keep: points to count (all are projected)."""
+    x = count_grouped_device(lat, lon, group, keep, zmin, zmax, device, tiles).cpu().numpy()
     return GroupedCounts(x[:, 0].astype(np.uint32), x[:, 1].astype(np.int32), x[:, 2].copy(), x[:, 3].copy(),
                          x[:, 4].copy())
 

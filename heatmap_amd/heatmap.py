@@ -510,15 +510,7 @@ def _heat_text_gpu(dz, dr, dc, dv, st):
     last[st[1:] - 1] = 1
     last[n - 1] = 1
 
-    def digits(x):
-        d = torch.ones_like(x)
-        p = 10
-        for _ in range(18):
-            d += (x >= p).to(torch.int64)
-            p *= 10
-        return d
-
-    ln = digits(dz) + digits(dr) + digits(dc) + digits(dv) + 8 + head.to(torch.int64) + 2 - last.to(torch.int64)
+    ln = _digits(dz) + _digits(dr) + _digits(dc) + _digits(dv) + 8 + head.to(torch.int64) + 2 - last.to(torch.int64)
     off = torch.cumsum(ln, 0) - ln
     total = int((off[-1] + ln[-1]).item())
     text = torch.empty(max(total, 1), dtype=torch.uint8, device=dz.device)
@@ -553,7 +545,6 @@ def _cells_to_table_device(cells: Cells):
     non-negative integer below 1e16 or a coordinate is out of packing range
     (the host path then)."""
     import pyarrow as pa
-    import pyarrow.compute as pc
     import torch
 
     d = cells.delta
@@ -578,13 +569,7 @@ def _cells_to_table_device(cells: Cells):
     head[1:] = (hi[1:] != hi[:-1]) | (lo[1:] != lo[:-1])
     st = torch.nonzero(head).flatten()
     heat = _heat_text_gpu(z, r, c, dv, st)
-    rl, rs, rz, rr, rc_ = (x[st].cpu().numpy() for x in (lab, sp, tz, tr, tc))
-    s = lambda a: pc.cast(pa.array(a), pa.large_string())  # noqa: E731
-    t = lambda x: pa.scalar(x, pa.large_string())  # noqa: E731
-    names = pa.array(cells.labels, pa.large_string()).take(pa.array(rl))
-    spans = pa.array(cells.spans, pa.large_string()).take(pa.array(rs))
-    ids = pc.binary_join_element_wise(names, spans, pc.binary_join_element_wise(s(rz), s(rr), s(rc_), t("_")),
-                                      t(KEY_SEPERATOR))
+    ids = _ids_gpu(cells.labels, cells.spans, lab[st], sp[st], tz[st], tr[st], tc[st])
     return pa.table({"id": ids, "heatmap": heat})
 
 
@@ -676,10 +661,170 @@ def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, d
     return cells_to_rows(heatmap_cells(lat, lon, user_id, keep, max_zoom_level, delta, tiles))
 
 
+# seconds per phase of the last heatmap_table call (device path)
+LAST_TABLE_PHASES = {}
+
+
+def _digits(x):
+    """decimal digits of non-negative int64 CUDA tensors"""
+    import torch
+
+    d = torch.ones_like(x)
+    p = 10
+    for _ in range(18):
+        d += (x >= p).to(torch.int64)
+        p *= 10
+    return d
+
+
+def _ids_gpu(labels, spans, rl, rs, rz, rr, rc):
+    """Row ids "<label>|<span>|<z>_<row>_<col>" of per-row int64 CUDA tensors,
+    written on the GPU (hm_format_ids) at an exclusive scan of their lengths.
+    A pyarrow LargeStringArray."""
+    import ctypes
+
+    import pyarrow as pa
+    import torch
+
+    dev = rl.device
+
+    def blob(texts):
+        b = [t.encode() for t in texts]
+        off = np.zeros(len(b) + 1, np.int64)
+        off[1:] = np.cumsum([len(x) for x in b])
+        data = np.frombuffer(b"".join(b) or b"\0", np.uint8)
+        return torch.from_numpy(data.copy()).to(dev), torch.from_numpy(off).to(dev)
+
+    names, noff = blob(labels)
+    sp, soff = blob(spans)
+    n = rl.numel()
+    ln = (noff[rl + 1] - noff[rl]) + (soff[rs + 1] - soff[rs]) + _digits(rz) + _digits(rr) + _digits(rc) + 4
+    off = torch.cumsum(ln, 0) - ln
+    total = int((off[-1] + ln[-1]).item()) if n else 0
+    text = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    ctx = device.context(dev.index or 0)
+    p = lambda x: ctypes.c_void_p(x.data_ptr())  # noqa: E731
+    rl, rs, rz, rr, rc = (x.contiguous() for x in (rl, rs, rz, rr, rc))
+    if n:
+        rc_ = ctx.L.hm_format_ids(ctx.ptr, p(names), p(noff), p(rl), p(sp), p(soff), p(rs), p(rz), p(rr), p(rc),
+                                  p(off), n, p(text))
+        if rc_ != _lib.HM_OK:
+            _lib.raise_for(rc_)
+    offsets = np.append(off.cpu().numpy(), total).astype(np.int64)
+    data = text[:total].cpu().numpy()
+    return pa.LargeStringArray.from_buffers(int(n), pa.py_buffer(offsets), pa.py_buffer(data))
+
+
+def _device_table(labels, keys, counts, grouped, zmax, d, phases):
+    """heatmap_table's rows from device-resident counts, end to end on the
+    GPU: keys/counts = hm_count's in-square cells (HM_KEY, n) of the kept
+    points; grouped = hm_count_grouped's [m, 5] records.  The 'all' closed
+    form (combine_cells) by a sort of the cell keys and index_adds, the row
+    order by one sort of packed (label, row tile, row, col) keys, the JSON by
+    hm_format_bins; only the per-row id fields come back.  None when the keys
+    do not pack into one int64 (combine_cells + cells_to_table then)."""
+    import time
+
+    import pyarrow as pa
+    import torch
+
+    t0 = time.perf_counter()
+    ks, o = torch.sort(keys)
+    n = counts[o]
+    z = ks >> 58
+    w = torch.ones_like(ks) << (zmax - z)
+    a = torch.zeros_like(n)
+    u = torch.zeros_like(n)
+    if grouped.numel():
+        gg, gz, gr, gc, gn = grouped.unbind(1)
+        gk = (gz << 58) | (gr << 29) | gc
+        pos = torch.searchsorted(ks, gk)
+        lit = gg == 0
+        a.index_add_(0, pos[lit], gn[lit])
+        u.index_add_(0, pos[~lit], gn[~lit])
+        us = ~lit
+        ug, uk, un = gg[us], gk[us], gn[us]
+    else:
+        ug = uk = un = torch.zeros(0, dtype=torch.int64, device=keys.device)
+    value_all = (n + a) * w + (w - 1) * u
+    label = torch.cat([torch.zeros_like(ks), ug])
+    key = torch.cat([ks, uk])
+    val = torch.cat([value_all, un])
+    torch.cuda.synchronize()
+    phases["combine (device)"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    if val.numel() and int(val.max()) >= 10 ** 16:
+        return None
+    lb = max(int(label.max()).bit_length(), 1) if label.numel() else 1
+    if lb + 6 + 2 * zmax > 63:
+        return None
+    z = key >> 58
+    r = (key >> 29) & 0x1FFFFFFF
+    c = key & 0x1FFFFFFF
+    m = (1 << d) - 1
+    tb = zmax - d
+    # (label, row-tile zoom, row-tile row, row-tile col, row, col): within a
+    # row tile (fixed zoom) the bins' (row, col) order is their low bits' order
+    sk = ((label << (6 + 2 * zmax)) | ((z - d) << (2 * zmax)) | ((r >> d) << (tb + 2 * d)) |
+          ((c >> d) << (2 * d)) | ((r & m) << d) | (c & m))
+    sk, o = torch.sort(sk)
+    z, r, c, val = z[o], r[o], c[o], val[o]
+    rk = sk >> (2 * d)
+    head = torch.ones_like(rk, dtype=torch.bool)
+    head[1:] = rk[1:] != rk[:-1]
+    st = torch.nonzero(head).flatten()
+    heat = _heat_text_gpu(z, r, c, val, st)
+    phases["order + JSON (device)"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    rt = rk[st]
+    ids = _ids_gpu(labels, ["alltime"], rt >> (6 + 2 * tb), torch.zeros_like(rt), (rt >> (2 * tb)) & 63,
+                   (rt >> tb) & ((1 << tb) - 1), rt & ((1 << tb) - 1))
+    phases["ids (device)"] = time.perf_counter() - t0
+    return pa.table({"id": ids, "heatmap": heat})
+
+
 def heatmap_table(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None, tiles=False):
     """The same rows as a pyarrow Table(id, heatmap JSON): batchMain's
-    DataFrame (heatmap.py:156-157) without per-cell Python objects."""
-    return cells_to_table(heatmap_cells(lat, lon, user_id, keep, max_zoom_level, delta, tiles))
+    DataFrame (heatmap.py:156-157) without per-cell Python objects.  Cells
+    stay on the device from the two counting passes to the JSON text
+    (_device_table); cells outside [0, 2^z)^2 -- the only ones that can leave
+    the chain windows -- take combine_cells + cells_to_table."""
+    import time
+
+    mz = MAX_ZOOM_LEVEL if max_zoom_level is None else max_zoom_level
+    d = DETAIL_ZOOM_DELTA if delta is None else delta
+    zmax = mz + d
+    n = len(user_id)
+    keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool)
+    ph = LAST_TABLE_PHASES
+    ph.clear()
+    t0 = time.perf_counter()
+    plan = group_plan(user_id, keep)
+    ph["group_plan (host)"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
+    m, buf = device.count_device(lat, lon, keep.astype(np.uint8), d + 1, zmax, tiles=tiles)
+    keys, counts = buf.keys[:m], buf.counts[:m]
+    if plan.grouped.any():
+        grouped = device.count_grouped_device(lat, lon, plan.gid, plan.grouped.astype(np.uint8), d + 1, zmax,
+                                              tiles=tiles)
+    else:
+        grouped = keys.new_zeros((0, 5))
+    ph["counts (device)"] = time.perf_counter() - t0
+    tab = None
+    if buf.nx == 0:
+        tab = _device_table(plan.labels, keys, counts, grouped, zmax, d, ph)
+    if tab is not None:
+        return tab
+    # host assembly from the same counts
+    zk, rk, ck = device.decode_keys(keys.cpu().numpy().view(np.uint64))
+    cnt = counts.cpu().numpy()
+    if buf.nx:
+        x = buf.xcells[:4 * buf.nx].cpu().numpy().reshape(-1, 4)
+        zk, rk, ck, cnt = (np.concatenate([p, q]) for p, q in ((zk, x[:, 0]), (rk, x[:, 1]), (ck, x[:, 2]),
+                                                               (cnt, x[:, 3])))
+    g = grouped.cpu().numpy()
+    cells = combine_cells(plan.labels, (zk, rk, ck, cnt), tuple(g[:, i] for i in range(5)), zmax, d)
+    return cells_to_table(cells)
 
 
 def build_heatmaps(locations):

@@ -298,6 +298,16 @@ int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* 
 int hm_format_bins(hm_ctx* ctx, const int64_t* zoom, const int64_t* row, const int64_t* col, const int64_t* value,
                    const uint8_t* head, const uint8_t* last, const int64_t* offset, int64_t n, uint8_t* text);
 
+/* Row ids (heatmap.py:55,85-90):  <name>|<span>|<tz>_<tr>_<tc>  per row, the
+ * name and span texts taken from byte blobs by index (names + name_off[label],
+ * name_off[label + 1] - name_off[label] bytes; likewise spans).  offset: each
+ * id's first byte (an exclusive scan of the id lengths the caller computed:
+ * name + 1 + span + 1 + digits(tz) + 1 + digits(tr) + 1 + digits(tc)).
+ * tz, tr, tc >= 0.  Asynchronous. */
+int hm_format_ids(hm_ctx* ctx, const uint8_t* names, const int64_t* name_off, const int64_t* label,
+                  const uint8_t* spans, const int64_t* span_off, const int64_t* span, const int64_t* tz,
+                  const int64_t* tr, const int64_t* tc, const int64_t* offset, int64_t n, uint8_t* text);
+
 /* Benchmark/test utility, not part of the reference boundary: fill lat/lon
  * (device) with points start..start+n-1 of a synthetic cloud, bit-identical
  * to heatmap_amd/synth.py.  kind: 0 uniform, 1 hotspots (table = device

@@ -216,3 +216,30 @@ def test_cells_to_table_device_matches_host(gpu):
     assert dev is not None
     assert dev.column("id").to_pylist() == host.column("id").to_pylist()
     assert dev.column("heatmap").to_pylist() == host.column("heatmap").to_pylist()
+
+
+def test_heatmap_table_device_matches_host(gpu):
+    """heatmap_table end to end on the device (counts resident from hm_count /
+    hm_count_grouped through the JSON) == combine_cells + the host
+    cells_to_table on the same counts: 200K hotspot points, 300 users with
+    'x*', 'rt-*' and literal 'all' ids, background rows, zooms 6-21."""
+    from heatmap_amd import heatmap as hm
+    from heatmap_amd import synth
+
+    n = 200_000
+    lat, lon = synth.generate("hotspots", n, seed=11)
+    g = np.random.default_rng(11)
+    names = np.array(["u%d" % i for i in range(300)] + ["x-anon", "rt-7", "rt-9", "all"], dtype=object)
+    user = names[g.integers(0, names.size, n)]
+    keep = g.random(n) > 0.2
+    dev = hm.heatmap_table(lat, lon, user, keep, 16, 5)
+    assert "combine (device)" in hm.LAST_TABLE_PHASES     # the device path ran
+    old = hm.SUM_BY_CELL_DEVICE_MIN
+    hm.SUM_BY_CELL_DEVICE_MIN = 1 << 62
+    try:
+        host = hm.cells_to_table(hm.heatmap_cells(lat, lon, user, keep, 16, 5))
+    finally:
+        hm.SUM_BY_CELL_DEVICE_MIN = old
+    assert dev.num_rows == host.num_rows
+    assert dev.column("id").to_pylist() == host.column("id").to_pylist()
+    assert dev.column("heatmap").to_pylist() == host.column("heatmap").to_pylist()

@@ -94,28 +94,14 @@ def bench_table(a):
     user = names[g]
     user[g % 7 == 3] = "x-anon"          # 'x*' ids: counted in 'all' only (heatmap.py:64-70)
     keep = (np.arange(n) % 5 != 2)       # background rows (heatmap.py:28-29)
-    ph = {}
     hm.heatmap_table(lat[:10000], lon[:10000], user[:10000], keep[:10000], a.zmax - 5, 5)   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    plan = hm.group_plan(user, keep)
-    ph["group_plan"] = time.perf_counter() - t0
-    t1 = time.perf_counter()
-    c = device.count(lat, lon, keep.astype(np.uint8), 6, a.zmax)
-    ph["count_all (device + copy)"] = time.perf_counter() - t1
-    t1 = time.perf_counter()
-    gc = device.count_grouped(lat, lon, plan.gid, plan.grouped.astype(np.uint8), 6, a.zmax)
-    ph["count_grouped (device + copy)"] = time.perf_counter() - t1
-    t1 = time.perf_counter()
-    cells = hm.combine_cells(plan.labels, (c.zoom, c.row, c.col, c.count),
-                             (gc.group, gc.zoom, gc.row, gc.col, gc.count), a.zmax, 5)
-    ph["combine_cells"] = time.perf_counter() - t1
-    t1 = time.perf_counter()
-    tab = hm.cells_to_table(cells)
-    ph["cells_to_table"] = time.perf_counter() - t1
+    tab = hm.heatmap_table(lat, lon, user, keep, a.zmax - 5, 5)
+    ph = dict(hm.LAST_TABLE_PHASES)
     tot = time.perf_counter() - t0
     print(json.dumps({"part": "heatmap_table", "value": n / tot, "unit": "points/s", "seconds": tot,
-                      "points": n, "users": a.users, "rows": tab.num_rows, "bins": len(cells),
+                      "points": n, "users": a.users, "rows": tab.num_rows,
                       "detail_zooms": [6, a.zmax], "phases_s": ph}), flush=True)
 
 
