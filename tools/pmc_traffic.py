@@ -19,7 +19,7 @@ import os
 import sys
 from collections import defaultdict
 
-EXCLUDE = ("k_synth", "at::native", "__amd_rocclr_copyBuffer")   # copies: the bench's measured-peak pass
+EXCLUDE = ("k_synth", "at::native", "__amd_rocclr_copyBuffer", "k_read_stream")   # generator, checks, measured-peak passes
 
 
 def per_kernel(d, counter):
@@ -42,9 +42,12 @@ def main():
     dst = sys.argv[5] if len(sys.argv) > 5 and sys.argv[4] == "--out" else "profiles/pmc_summary.json"
     fetch, fcalls = per_kernel(fd, "FETCH_SIZE")
     write, wcalls = per_kernel(wd, "WRITE_SIZE")
-    # one step = one mode-0 level-1 launch over whole tiles (<OutT, 0, true>; older builds: <OutT, 0>)
-    steps = sum(v for k, v in fcalls.items()
-                if k.startswith("void k_project_partition<") and (k.endswith(", 0>") or k.endswith(", 0, true>")))
+    # one step = one level-1 launch over whole tiles: k_l1_fast (round 4), or the
+    # mode-0 k_project_partition (<OutT, 0, true>; older builds: <OutT, 0>)
+    steps = sum(v for k, v in fcalls.items() if k.startswith("void k_l1_fast<"))
+    if not steps:
+        steps = sum(v for k, v in fcalls.items()
+                    if k.startswith("void k_project_partition<") and (k.endswith(", 0>") or k.endswith(", 0, true>")))
     kernels = {}
     step_bytes = 0.0
     for k in sorted(set(fetch) | set(write)):
@@ -66,7 +69,8 @@ def main():
     json.dump(d, open(dst, "w"), indent=1)
     print("steps %d, HBM bytes per step %.3f GB" % (steps, step_bytes / 1e9))
     for k, v in sorted(kernels.items(), key=lambda kv: -kv[1]["hbm_bytes_per_launch"])[:8]:
-        print("%-60s %10.3f GB x %d" % (k[:60], v["hbm_bytes_per_launch"] / 1e9, v["launches"]))
+        print("%-60s %10.3f GB x %d (fetch %.3f, write %.3f)" % (k[:60], v["hbm_bytes_per_launch"] / 1e9, v["launches"],
+                                                               v["fetch_bytes_corrected"] / 1e9, v["write_bytes"] / 1e9))
 
 
 if __name__ == "__main__":
