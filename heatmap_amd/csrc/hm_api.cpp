@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <unordered_set>
 #include <vector>
 
 #include "../../include/heatmap_amd.h"
@@ -1763,6 +1764,10 @@ struct hm_stream {
     uint64_t *lkeys = nullptr, *lcounts = nullptr, *akeys = nullptr, *acounts = nullptr;
     uint64_t lcap = 0, llen = 0;
     bool compact = true;                  /* the log holds distinct keys */
+    /* while compact: the buckets with cells in the log.  A one-bucket batch
+     * of a bucket not in it keeps the log compact (one count's cells are
+     * distinct), so a stream of new hours never needs a compaction pass */
+    std::unordered_set<uint32_t> log_buckets;
     uint64_t nbuckets = 0;
     unsigned long long* hstate = nullptr; /* pinned mirror of state */
     Buf bids, rec;                        /* per-batch scratch */
@@ -1826,7 +1831,7 @@ static int stream_compact(hm_stream* s)
     std::swap(s->lkeys, s->akeys);
     std::swap(s->lcounts, s->acounts);
     s->llen = (uint64_t)m;
-    s->compact = true;
+    s->compact = true;   /* (compaction adds no bucket: log_buckets stays exact) */
     return HM_OK;
 }
 
@@ -1856,10 +1861,21 @@ static int stream_room(hm_stream* s, uint64_t need)
     return HM_OK;
 }
 
-/* m cells appended at the tail */
-static void stream_appended(hm_stream* s, uint64_t m)
+/* m cells appended at the tail; bucket: the batch's one bucket, or
+ * 0xFFFFFFFF for cells of several buckets (from then on the log's buckets
+ * are not all known, and every append clears the compact flag) */
+static void stream_appended(hm_stream* s, uint64_t m, uint32_t bucket = 0xFFFFFFFFu)
 {
-    if (m) s->compact = s->compact && s->llen == 0;   /* one count's cells are distinct */
+    if (m) {
+        /* one count's cells are distinct: the log stays compact when it was
+         * empty, or when this bucket has no cells in it yet (the log's
+         * buckets all known) */
+        const bool fresh = bucket != 0xFFFFFFFFu && !s->log_buckets.count(0xFFFFFFFFu) &&
+                           !s->log_buckets.count(bucket);
+        s->compact = s->compact && (s->llen == 0 || fresh);
+        if (s->llen == 0) s->log_buckets.clear();
+        s->log_buckets.insert(bucket);
+    }
     s->llen += m;
 }
 
@@ -1887,7 +1903,7 @@ static int stream_take_tail(hm_stream* s, int64_t m, uint32_t bucket)
 {
     hm_launch_stream_rekey(s->ctx->stream, s->lkeys + s->llen, (uint64_t)m, (uint64_t)bucket << s->cb);
     HIPCHK(hipGetLastError());
-    stream_appended(s, (uint64_t)m);
+    stream_appended(s, (uint64_t)m, bucket);
     return HM_OK;
 }
 

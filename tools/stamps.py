@@ -36,7 +36,7 @@ lat = torch.empty(n, dtype=torch.float64, device="cuda")
 lon = torch.empty(n, dtype=torch.float64, device="cuda")
 device.synth("hotspots", lat, lon)
 bufs = device.CountBuffers(64 << 20)
-device.count_device(lat, lon, None, 0, 18, 0, buffers=bufs)
+device.count_device(lat, lon, None, 0, int(os.environ.get("HM_ZMAX", "18")), 0, buffers=bufs)
 torch.cuda.synchronize()
 L = _lib.load()
 L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]

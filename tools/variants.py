@@ -87,6 +87,9 @@ PATCHES["l1nostore"] = [
      "        if (hk == 0xFFFFFFFFu && e.y == 0x1234567u) *(uint16_t*)houtb = (uint16_t)hk;")]
 PATCHES["l1noatom"] = [("hm_kernels.hip", "        if (cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1i(d, sh)], cnt[q]);",
                         "        if (cnt[q]) gpos[q] = 0;")]
+# levels 2.. always on the spread plan (3 zooms per level) when no tile is hot
+PATCHES["spreadall"] = [("hm_api.cpp", "spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, true);",
+                         "spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, false);")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
