@@ -1864,19 +1864,24 @@ static int stream_room(hm_stream* s, uint64_t need)
 /* m cells appended at the tail; bucket: the batch's one bucket, or
  * 0xFFFFFFFF for cells of several buckets (from then on the log's buckets
  * are not all known, and every append clears the compact flag) */
-static void stream_appended(hm_stream* s, uint64_t m, uint32_t bucket = 0xFFFFFFFFu)
+static void stream_appended(hm_stream* s, uint64_t m, const uint32_t* buckets, uint32_t nb)
 {
     if (m) {
-        /* one count's cells are distinct: the log stays compact when it was
-         * empty, or when this bucket has no cells in it yet (the log's
-         * buckets all known) */
-        const bool fresh = bucket != 0xFFFFFFFFu && !s->log_buckets.count(0xFFFFFFFFu) &&
-                           !s->log_buckets.count(bucket);
-        s->compact = s->compact && (s->llen == 0 || fresh);
+        /* each bucket's cells come from one count, so they are distinct: the
+         * log stays compact when it was empty, or when none of the buckets
+         * has cells in it yet (the log's buckets all known) */
         if (s->llen == 0) s->log_buckets.clear();
-        s->log_buckets.insert(bucket);
+        bool fresh = !s->log_buckets.count(0xFFFFFFFFu);
+        for (uint32_t j = 0; j < nb && fresh; j++) fresh = !s->log_buckets.count(buckets[j]);
+        s->compact = s->compact && (s->llen == 0 || fresh);
+        for (uint32_t j = 0; j < nb; j++) s->log_buckets.insert(buckets[j]);
     }
     s->llen += m;
+}
+
+static void stream_appended(hm_stream* s, uint64_t m, uint32_t bucket = 0xFFFFFFFFu)
+{
+    stream_appended(s, m, &bucket, 1);
 }
 
 /* a batch of one bucket, part 1: hm_count's cells written at the log's tail
@@ -2025,8 +2030,8 @@ static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon,
             }
         }
         if (grow) continue;
-        /* several buckets' cells: distinct only across buckets, still a fresh log's */
-        stream_appended(s, off);
+        /* several buckets' cells, each bucket's from one count */
+        stream_appended(s, off, hb.data(), nparts);
         return HM_OK;
     }
 }
