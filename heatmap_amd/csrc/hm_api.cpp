@@ -2110,7 +2110,11 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
     a.n = per_point ? (uint64_t)n : 1;   /* neither: the one (no group, undated) bucket */
     a.base = s->base;
     a.buckets = s->bk;
-    a.out = per_point ? (uint32_t*)s->bids.p : nullptr;
+    /* per-point bucket ids feed only the several-bucket paths: a batch
+     * counted speculatively as one bucket skips writing them (and a batch
+     * that turns out to hold several runs the pass again, below) */
+    const bool spec = s->last_nparts <= 1;   /* the previous batch was one bucket */
+    a.out = per_point && !spec ? (uint32_t*)s->bids.p : nullptr;
     if (++s->epoch == 0) s->epoch = 1;   /* wrapped: stale flags only cost an exchange */
     a.bflag = s->bflag;
     a.epoch = s->epoch;
@@ -2126,7 +2130,6 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
      * read-back.  Any other outcome drops the tail and takes the paths below
      * (which count again, so errors and their order are the same). */
     int64_t m1 = 0;
-    const bool spec = s->last_nparts <= 1;   /* the previous batch was one bucket */
     const int st1 = spec ? stream_count_tail(s, lat, lon, keep, n, &m1) : HM_OK;
     HIPCHK(hm_sync(q));
     s->nbuckets = s->hstate[HMS_ST_BUCKETS];
@@ -2144,6 +2147,13 @@ extern "C" int hm_stream_add(hm_stream* s, const double* lat, const double* lon,
         if (!spec && (st = stream_count_tail(s, lat, lon, keep, n, &m1))) return st;
         if (spec && st1) return st1;
         return stream_take_tail(s, m1, nparts ? lo : 0u);
+    }
+    if (spec && per_point) {
+        /* the ids the speculative pass skipped (the buckets are interned and
+         * listed already: the same epoch, nothing new to flag) */
+        a.out = (uint32_t*)s->bids.p;
+        hm_launch_stream_buckets(q, a);
+        HIPCHK(hipGetLastError());
     }
     if (nparts <= HMS_MAX_PARTS) return stream_fold_parts(s, lat, lon, keep, n, nparts);
     return stream_fold_grouped(s, lat, lon, keep, n);
