@@ -211,10 +211,16 @@ def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, de
     for b in bufsets:
         free.put(b)
     owned, err, last = [], [], [None]
-    # the merge stream takes the highest priority: its kernels (and the RCCL
-    # calls' copies) are dispatched ahead of the next count's, which fill the CUs
-    lo, hi = torch.cuda.Stream.priority_range()
-    side = torch.cuda.Stream(priority=min(lo, hi))
+    # HM_MERGE_PRIORITY=1: the merge stream takes the highest priority, so its
+    # kernels (and the RCCL calls' copies) are dispatched ahead of the next
+    # count's, which fill the CUs
+    import os
+
+    if os.environ.get("HM_MERGE_PRIORITY", "0") == "1":
+        lo, hi = torch.cuda.Stream.priority_range()
+        side = torch.cuda.Stream(priority=min(lo, hi))
+    else:
+        side = torch.cuda.Stream()
 
     def merger():
         try:
