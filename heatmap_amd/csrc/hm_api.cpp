@@ -74,6 +74,8 @@ struct hm_ctx {
     double spread_min_cold = 0;
     int sample_log2 = 18;              /* level-1 region sizing: ~2^sample_log2 sampled points */
     int debug_l1 = 0;                  /* HM_DEBUG_L1: report level-1 region overflows on stderr */
+    int stage_timing = 1;              /* HM_STAGE_TIMING=0: no stage events (hm_last_stats stages read 0) */
+    int contig = 1;                    /* HM_CONTIG=0: 3-level plans keep run-streaming at the last level */
     uint64_t rs_big_min = 0;
     /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
      * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
@@ -153,7 +155,7 @@ enum {
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
     B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS, B_MB_CNT2, B_MB_OFF2,
-    B_MB_KEYS2, B_MB_COUNTS2, B_KEYS_C, B_HOT_FORCE, B_C2B,
+    B_MB_KEYS2, B_MB_COUNTS2, B_KEYS_C, B_HOT_FORCE, B_C2B, B_SEG2, B_CTOT, B_CBASE, B_CCUR,
     B_COUNT
 };
 
@@ -249,6 +251,8 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     if (const char* e = getenv("HM_RUN_SHARD_BITS")) c->run_shard_bits = atoi(e);
     if (const char* e = getenv("HM_SAMPLE_LOG2")) c->sample_log2 = std::min(30, std::max(8, atoi(e)));
     if (const char* e = getenv("HM_DEBUG_L1")) c->debug_l1 = atoi(e);
+    if (const char* e = getenv("HM_STAGE_TIMING")) c->stage_timing = atoi(e);
+    if (const char* e = getenv("HM_CONTIG")) c->contig = atoi(e);
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -291,6 +295,12 @@ int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
     } else if (!strcmp(name, "HM_SPREAD_MIN_COLD")) {
         prev = c->spread_min_cold;
         c->spread_min_cold = value;
+    } else if (!strcmp(name, "HM_CONTIG")) {
+        prev = c->contig;
+        c->contig = value != 0;
+    } else if (!strcmp(name, "HM_STAGE_TIMING")) {
+        prev = c->stage_timing;
+        c->stage_timing = value != 0;
     } else if (!strcmp(name, "HM_SAMPLE_LOG2")) {
         if (!(value >= 8 && value <= 30)) return HM_E_ARG;
         prev = c->sample_log2;
@@ -642,7 +652,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     /* stage timings (hm_last_stats) for calls of >= 2^24 points: each event
      * record is an API call, and small calls (stream batches) are bound by
      * the host's issue rate */
-    const bool timing = n >= (1ll << 24);
+    const bool timing = n >= (1ll << 24) && ctx->stage_timing;
     /* keys per aggregation work item: HM_TA, halved (down to 16K) until the
      * call has >= 512 items' worth of points -- a 1e7-point call otherwise
      * runs ~40 items on 256 CUs */
@@ -682,6 +692,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     int npart = 0;              /* level >= 2 partition launches timed (ev[5..]) */
 
     uint32_t* seg1 = nullptr;   /* level-1 items' run tables (k_partition_fr) */
+    uint32_t* seg2 = nullptr;   /* level-2 items' run tables after a child-contiguous level */
     bool hot_on = false;        /* hot tiles sampled and looked up by level 1 */
     bool spread = false;        /* levels 2.. take fewer zooms (spread_replan) */
     uint32_t nhot = 0;          /* hot tiles found */
@@ -1043,7 +1054,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         /* with hot tiles (their children skip this level) or the spread plan,
          * no child is hot: one counter per child, and the partition kernels'
          * run-slot atomics coalesce (lanes own consecutive digits) */
+        /* a child-contiguous level (HM_PN_CONTIG): the middle level of a
+         * 3-level plan without hot tiles (Z >= 19) writes each child's keys
+         * as ONE run, so the last level reads every item from <= 8 runs
+         * (k_partition_fr) instead of streaming runs of a few keys each */
+        const bool contig = ctx->contig && l == 1 && L == 3 && !nhot && !V.out16 && seg1 != nullptr;
         int sb = ctx->run_shard_bits >= 0 ? ctx->run_shard_bits : ((nhot || spread) ? 0 : HM_RUN_SHARD_BITS);
+        if (contig) sb = 0;
         while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
         const uint64_t run_cap = (ntiles + ((uint64_t)nparents << sb)) << V.dbits;
         if (run_cap >= (1ull << 32)) return HM_E_NOMEM;
@@ -1076,9 +1093,24 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             a.nruns_out = nruns;
             a.runs_out = runs_sh;
             a.items = lv[l - 1].items;
-            a.seg = l == 1 ? seg1 : nullptr;
+            a.seg = l == 1 ? seg1 : seg2;
             if (timing) HIPCHK(hipEventRecord(ev[5 + 2 * (l - 1)], s));
-            hm_launch_partN(s, a, lv[l - 1].items, V.out16, l == 1 && seg1 != nullptr);
+            if (contig) {
+                /* child totals, their scan, then the partition proper */
+                uint64_t *ptl, *ttl;
+                ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), ptl);
+                ENSURE(B_TOTAL, 4 * sizeof(uint64_t), ttl);
+                ENSURE(B_CTOT, V.nchildren * 8, a.ctot);
+                ENSURE(B_CBASE, V.nchildren * 8, a.cbase);
+                ENSURE(B_CCUR, V.nchildren * 4, a.ccur);
+                HIPCHK(hipMemsetAsync(a.ctot, 0, V.nchildren * 8, s));
+                HIPCHK(hipMemsetAsync(a.ccur, 0, V.nchildren * 4, s));
+                a.mode = HM_PN_HIST;
+                hm_launch_partN(s, a, lv[l - 1].items, false, true);
+                hm_launch_scan(s, (const uint64_t*)a.ctot, V.nchildren, ptl, (uint64_t*)a.cbase, ttl + 3);
+                a.mode = HM_PN_CONTIG;
+            }
+            hm_launch_partN(s, a, lv[l - 1].items, V.out16, (l == 1 && seg1 != nullptr) || (l == 2 && seg2 != nullptr));
             HIPCHK(hipGetLastError());
             if (timing) HIPCHK(hipEventRecord(ev[6 + 2 * (l - 1)], s));
             npart = l;
@@ -1225,7 +1257,10 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             uint4* desc;
             ENSURE(B_DESC0 + l, ((uint64_t)V.items + 1) * 2 * sizeof(uint4), desc);
             b.desc = desc;
-            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? ta : HM_TN, desc, nullptr);
+            /* after a child-contiguous level every item of the next spans one run */
+            seg2 = nullptr;
+            if (contig) ENSURE(B_SEG2, ((uint64_t)V.items + 1) * 16 * sizeof(uint32_t), seg2);
+            hm_launch_items(s, b, runs_cur, V.items, (l == L - 1) ? ta : HM_TN, desc, seg2);
             HIPCHK(hipGetLastError());
         }
 

@@ -1712,6 +1712,17 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
         const int d = q * T + tid;
         cnt[q] = d < F ? cur[hm_cur_slot(d, ww)] : 0u;
     }
+    if (a.mode == HM_PN_HIST) {
+        /* the bucket's child totals (a pass before the partition proper) */
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int d = q * T + tid;
+            if (d < F && cnt[q])
+                atomicAdd(&a.ctot[((uint64_t)it.bucket << a.dbits) + d], (unsigned long long)cnt[q]);
+        }
+        return;
+    }
+    const bool contig = a.mode == HM_PN_CONTIG;
     uint32_t offq[PER];
     hm_digit_offsets<T, PER>(cnt, offq, scr);
     const uint32_t tile0 = a.parent.item_begin[it.bucket];
@@ -1724,8 +1735,19 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     for (int q = 0; q < PER; q++) {
         const int d = q * T + tid;
         idx[q] = 0;
-        if (d < F && cnt[q])
-            idx[q] = atomicAdd(&a.nruns_out[((((uint64_t)it.bucket << a.dbits) + d) << a.shard_bits) + sh], 1u);
+        if (d < F && cnt[q]) {
+            const uint64_t child = ((uint64_t)it.bucket << a.dbits) + d;
+            if (contig) {
+                /* idx: the key position of this item's range of the child */
+                idx[q] = (uint32_t)a.cbase[child] + atomicAdd(&a.ccur[child], cnt[q]);
+                if (atomicCAS(&a.nruns_out[child], 0u, 1u) == 0u) {
+                    const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, 0);
+                    a.runs_out[rb] = make_uint2((uint32_t)a.cbase[child], (uint32_t)a.ctot[child]);
+                }
+            } else {
+                idx[q] = atomicAdd(&a.nruns_out[(child << a.shard_bits) + sh], 1u);
+            }
+        }
     }
 #pragma unroll
     for (int q = 0; q < PER; q++) {
@@ -1735,16 +1757,33 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     __syncthreads();
     HM_STAMP_M(3, 4);
     const uint32_t restmask = (a.restbits >= 32) ? 0xFFFFFFFFu : ((1u << a.restbits) - 1u);
-    const uint32_t sh0 = it.a & (V - 1);
+    const uint32_t sh0 = contig ? 0u : it.a & (V - 1);
 #pragma unroll
     for (int k = 0; k < KPT; k++) {
         const bool v = (uint32_t)(k * T + tid) < total;
         const uint32_t ds = kv[k] >> a.restbits;   /* digit slot */
         const uint32_t pos = v ? sh0 + cur[v ? ds : 0u] + rank[k] : (uint32_t)HM_TN + V + (uint32_t)(tid & 63);
-        stage[pos] = (OutT)(kv[k] & restmask);
+        /* (a child-contiguous level stages the digit slot with the key: the
+         * copy-out finds each key's destination from it) */
+        stage[pos] = (OutT)(contig ? kv[k] : kv[k] & restmask);
     }
     __syncthreads();
     HM_STAMP_M(3, 5);
+    if (contig) {
+        /* a digit's keys [offq, offq + cnt) of the stage go to idx.. */
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const int d = q * T + tid;
+            if (d < F) cur[hm_cur_slot(d, ww)] = idx[q] - offq[q];
+        }
+        __syncthreads();
+        OutT* out = (OutT*)a.keys_out;
+        for (uint32_t e = tid; e < total; e += T) {
+            const uint32_t x = (uint32_t)stage[e];
+            out[cur[x >> a.restbits] + e] = (OutT)(x & restmask);
+        }
+        return;
+    }
     {
         /* 16-B vectors [V t, V t + V) of stage map to out[it.a - sh0 + V t ..) */
         OutT* out = (OutT*)a.keys_out + (it.a - sh0);

@@ -297,7 +297,20 @@ struct HmPartNArgs {
     void* keys_out;             /* item g writes its keys at its positions [a, b) */
     uint32_t* nruns_out;
     uint2* runs_out;
+    /* k_partition_fr, child-contiguous levels (HM_PN_HIST / HM_PN_CONTIG):
+     * child = bucket << dbits | digit.  HIST: every item adds its digit
+     * counts into ctot[child] and writes nothing else.  CONTIG: with cbase =
+     * the exclusive scan of ctot, an item reserves its keys of a child at
+     * cbase[child] + atomicAdd(ccur[child]) and the child gets ONE run
+     * (cbase, ctot): the next level reads each child as one contiguous run */
+    int mode;
+    unsigned long long* ctot;
+    const unsigned long long* cbase;
+    uint32_t* ccur;
 };
+#define HM_PN_RUNS 0
+#define HM_PN_HIST 1
+#define HM_PN_CONTIG 2
 
 /* run scan of one level (sharded counters -> flat child-ordered runs) */
 struct HmRsArgs {
