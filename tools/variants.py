@@ -61,7 +61,8 @@ VARIANTS = {
     "ta1m": ["HM_TA=1048576"],
     "hot1k": ["HM_MAX_HOT=1024"],
     "hot1kta1m": ["HM_MAX_HOT=1024", "HM_TA=1048576"],
-    "os8": ["HM_OS_IT=8"],                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
+    "os8": ["HM_OS_IT=8"],
+    "tn16k": ["HM_TN=16384"],               # 16K-key partition items (half the (item, child) pairs)                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
