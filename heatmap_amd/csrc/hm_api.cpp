@@ -18,6 +18,7 @@
 #include <algorithm>
 #include <chrono>
 #include <string>
+#include <thread>
 #include <unordered_set>
 #include <vector>
 
@@ -1785,6 +1786,7 @@ extern "C" int hm_bench_read(hm_ctx* ctx, const void* a, const void* b, int64_t 
 /* streaming: resident multi-zoom heatmap (kernels in hm_stream.hip)          */
 /* ------------------------------------------------------------------------ */
 
+#define HMS_PAR 4
 struct hm_stream {
     hm_ctx* ctx = nullptr;
     int zmin = 0, zmax = 0;
@@ -1799,6 +1801,7 @@ struct hm_stream {
     uint64_t *lkeys = nullptr, *lcounts = nullptr, *akeys = nullptr, *acounts = nullptr;
     uint64_t lcap = 0, llen = 0;
     bool compact = true;                  /* the log holds distinct keys */
+    bool par = true;                      /* several-bucket batches counted concurrently (HM_STREAM_PAR=0: not) */
     /* while compact: the buckets with cells in the log.  A one-bucket batch
      * of a bucket not in it keeps the log compact (one count's cells are
      * distinct), so a stream of new hours never needs a compaction pass */
@@ -1809,6 +1812,11 @@ struct hm_stream {
     Buf plat, plon, pkeep, pstart, pcnt;  /* partition path: bucket-contiguous batch */
     int64_t rcap = 0;                     /* records rec holds */
     Buf rk, rc, mk, mc;                   /* rollup scratch: relabeled and merged cells */
+    /* several-bucket batches: up to HMS_PAR buckets counted at once, each by
+     * its own context, stream and host thread, into its own scratch */
+    hm_ctx* pctx[HMS_PAR] = {};
+    Buf pk[HMS_PAR], pc[HMS_PAR];
+    hipEvent_t pev = nullptr;
 };
 
 static int stream_sync_state(hm_stream* s)
@@ -1978,6 +1986,100 @@ static int stream_fold_grouped(hm_stream* s, const double* lat, const double* lo
     return HM_OK;
 }
 
+/* The several-bucket batch's runs (gathered by stream_fold_parts, the
+ * points not kept last; at most HMS_PAR runs in all) counted at once, each by
+ * its own context, HIP stream and host thread into its own scratch, then
+ * copied to the log's tail in bucket order and keyed -- nothing joins the
+ * log unless every run counted.  HM_FALLBACK: a run failed (the caller's
+ * sequential path re-counts and reports the batch's first failing point). */
+static int stream_fold_parts_par(hm_stream* s, const double* lat, const double* lon, const uint8_t* keep, int64_t n,
+                                 uint32_t nparts, const std::vector<uint64_t>& start, const std::vector<uint32_t>& hb)
+{
+    hm_ctx* ctx = s->ctx;
+    hipStream_t q = ctx->stream;
+    int st;
+    for (int t = 0; t < HMS_PAR; t++) {
+        if (s->pctx[t]) continue;
+        hipStream_t pq = nullptr;
+        HIPCHK(hipStreamCreateWithFlags(&pq, hipStreamNonBlocking));
+        if ((st = hm_ctx_create(&s->pctx[t], ctx->device, pq))) {
+            (void)hipStreamDestroy(pq);
+            return st;
+        }
+    }
+    if (!s->pev) HIPCHK(hipEventCreateWithFlags(&s->pev, hipEventDisableTiming));
+    HIPCHK(hipEventRecord(s->pev, q));   /* the gathered runs are written */
+    const uint32_t nall = nparts + 1;    /* + the points not kept (errors only) */
+    std::vector<int64_t> m(nall, 0);
+    std::vector<int> rc(nall, HM_OK);
+    for (uint32_t j0 = 0; j0 < nall; j0 += HMS_PAR) {
+        const uint32_t j1 = std::min<uint32_t>(nall, j0 + HMS_PAR);
+        std::vector<std::thread> th;
+        for (uint32_t j = j0; j < j1; j++) {
+            const int t = (int)(j - j0);
+            th.emplace_back([&, j, t]() {
+                hm_ctx* c = s->pctx[t];
+                (void)hipSetDevice(c->device);
+                const uint64_t nj = (j < nparts ? start[j + 1] : (uint64_t)n) - start[j];
+                if (!nj) return;
+                if (hipStreamWaitEvent(c->stream, s->pev, 0) != hipSuccess) {
+                    rc[j] = HM_E_HIP;
+                    return;
+                }
+                const double* la = (const double*)s->plat.p + start[j];
+                const double* lo = (const double*)s->plon.p + start[j];
+                const uint8_t* kp = j < nparts ? nullptr : (const uint8_t*)s->pkeep.p;
+                uint64_t cap = j < nparts ? 2 * nj + 1024 : 0;
+                for (;;) {
+                    if (cap && stream_buf(s, s->pk[t], cap * 8) != HM_OK) {
+                        rc[j] = HM_E_NOMEM;
+                        return;
+                    }
+                    if (cap && stream_buf(s, s->pc[t], cap * 8) != HM_OK) {
+                        rc[j] = HM_E_NOMEM;
+                        return;
+                    }
+                    int64_t mj = 0, nx = 0;
+                    const int r = hm_count(c, la, lo, kp, (int64_t)nj, s->zmin, s->zmax,
+                                           cap ? (uint64_t*)s->pk[t].p : nullptr, cap ? (uint64_t*)s->pc[t].p : nullptr,
+                                           (int64_t)cap, &mj, nullptr, 0, &nx);
+                    if (nx > 0) {
+                        rc[j] = HM_E_EXOTIC;
+                        return;
+                    }
+                    if (r == HM_E_CAPACITY && j < nparts) {
+                        cap = (uint64_t)mj + (uint64_t)mj / 4 + 1024;
+                        continue;
+                    }
+                    rc[j] = (r == HM_E_CAPACITY) ? HM_OK : r;   /* the unkept part has no cells */
+                    m[j] = mj;
+                    return;
+                }
+            });
+        }
+        for (auto& x : th) x.join();
+        for (uint32_t j = j0; j < j1; j++)
+            if (rc[j] == HM_E_EXOTIC) return HM_E_EXOTIC;
+        for (uint32_t j = j0; j < j1; j++)
+            if (rc[j] != HM_OK) return HM_FALLBACK;
+        /* this group's cells to the tail, in bucket order */
+        uint64_t need = 0;
+        for (uint32_t j = j0; j < j1 && j < nparts; j++) need += (uint64_t)m[j];
+        if ((st = stream_room(s, need + 1024))) return st;
+        for (uint32_t j = j0; j < j1 && j < nparts; j++) {
+            const int t = (int)(j - j0);
+            if (!m[j]) continue;
+            uint64_t* tk = s->lkeys + s->llen;
+            HIPCHK(hipMemcpyAsync(tk, s->pk[t].p, (size_t)m[j] * 8, hipMemcpyDeviceToDevice, q));
+            HIPCHK(hipMemcpyAsync(s->lcounts + s->llen, s->pc[t].p, (size_t)m[j] * 8, hipMemcpyDeviceToDevice, q));
+            hm_launch_stream_rekey(q, tk, (uint64_t)m[j], (uint64_t)hb[j] << s->cb);
+            HIPCHK(hipGetLastError());
+            stream_appended(s, (uint64_t)m[j], &hb[j], 1);
+        }
+    }
+    return HM_OK;
+}
+
 /* a batch of a few buckets: gathered into one run per bucket (+ one run of
  * the points not kept), one hm_count per run written at the log's tail, all
  * counted before the tail joins the log.  Errors: the batch is re-counted as
@@ -2029,6 +2131,10 @@ static int stream_fold_parts(hm_stream* s, const double* lat, const double* lon,
     if (nun) {
         if ((st = stream_buf(s, s->pkeep, (size_t)nun))) return st;
         HIPCHK(hipMemsetAsync(s->pkeep.p, 0, nun, q));
+    }
+    if (nparts >= 2 && nparts + 1 <= HMS_PAR && s->par) {   /* one group: the batch stays atomic */
+        st = stream_fold_parts_par(s, lat, lon, keep, n, nparts, start, hb);
+        if (st != HM_FALLBACK) return st;
     }
     if ((st = stream_room(s, 2 * kept + 1024))) return st;
     for (;;) {
@@ -2092,6 +2198,7 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
     while (nb < want + want / 4 && nb < (1ull << bb)) nb <<= 1;
     s->bk.mask = nb - 1;
     s->lcap = std::max<uint64_t>(1024, (uint64_t)initial_cells);
+    if (const char* e = getenv("HM_STREAM_PAR")) s->par = atoi(e) != 0;
     int st = HM_OK;
     if (hipMalloc((void**)&s->state, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc((void**)&s->hstate, 2 * HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
@@ -2298,6 +2405,16 @@ extern "C" int hm_stream_destroy(hm_stream* s)
                     s->plat.p, s->plon.p, s->pkeep.p, s->pstart.p, s->pcnt.p, s->rk.p, s->rc.p, s->mk.p, s->mc.p})
         if (p) (void)hipFree(p);
     if (s->hstate) (void)hipHostFree(s->hstate);
+    for (int t = 0; t < HMS_PAR; t++) {
+        for (void* p : {s->pk[t].p, s->pc[t].p})
+            if (p) (void)hipFree(p);
+        if (s->pctx[t]) {
+            hipStream_t q = s->pctx[t]->stream;
+            hm_ctx_destroy(s->pctx[t]);
+            if (q) (void)hipStreamDestroy(q);
+        }
+    }
+    if (s->pev) (void)hipEventDestroy(s->pev);
     delete s;
     return HM_OK;
 }
