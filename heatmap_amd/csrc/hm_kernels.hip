@@ -2622,6 +2622,38 @@ __device__ __forceinline__ void hm_wave_bitonic(uint32_t (&v)[K])
     hm_bitonic_size<K, 2>(v, hm_lane());
 }
 
+/* Two 32-lane ascending bitonic sorts side by side (lanes 0-31 and 32-63,
+ * one value per lane): the 64-lane network's stages up to size 32, with the
+ * direction of size 32 taken inside each half */
+template <int SIZE, int STRIDE>
+__device__ __forceinline__ void hm_seg32_step(uint32_t& v, uint32_t lane)
+{
+    const uint32_t o = hm_xor_lane<STRIDE>(v);
+    const bool take_min = ((lane & STRIDE) == 0) == ((lane & SIZE & 31u) == 0);
+    v = take_min ? min(v, o) : max(v, o);
+    if constexpr (STRIDE > 1) hm_seg32_step<SIZE, STRIDE / 2>(v, lane);
+}
+template <int SIZE>
+__device__ __forceinline__ void hm_seg32_size(uint32_t& v, uint32_t lane)
+{
+    hm_seg32_step<SIZE, SIZE / 2>(v, lane);
+    if constexpr (SIZE < 32) hm_seg32_size<SIZE * 2>(v, lane);
+}
+
+/* Buckets of <= 32 keys (a sparse cloud's common case: the skew background
+ * averages ~24 per zoom-11 bucket) two per wave, one 32-lane segment each:
+ * the bucket of segment g is the g-th of a pair picked from the wave's
+ * ballot.  hm_pair_lane: the wave lane holding this lane's bucket (-1: the
+ * segment has none). */
+__device__ __forceinline__ int hm_pair_lane(uint64_t& mt)
+{
+    const int i0 = __builtin_ctzll(mt);
+    mt &= mt - 1;
+    const int i1 = mt ? __builtin_ctzll(mt) : -1;
+    if (mt) mt &= mt - 1;
+    return (hm_lane() >> 5) ? i1 : i0;
+}
+
 /* Small buckets run in two passes so that the output needs no per-bucket
  * cursor atomic (4M buckets would serialise on it at ~12 ns each):
  *   pass 1 (k_small_sort): a wave gathers a bucket's keys, re-codes them in
@@ -2811,6 +2843,52 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
         if (LO == 0 && in && !small) a.spcnt[bl] = 0;
         if (small) a.totals[bl] = nkl;
         uint64_t m = __ballot(small);
+        if constexpr (LO == 0) {
+            /* buckets of <= 32 keys in <= 4 runs: two per pass of the wave */
+            uint64_t mt = __ballot(small && nkl <= 32 && nrl <= 4);
+            m &= ~mt;
+            const uint32_t j = lane & 31;
+            while (mt) {
+                const int sl = hm_pair_lane(mt);
+                const bool seg = sl >= 0;
+                const int sr = seg ? sl : 0;
+                /* (every shuffle with the whole wave active: a bpermute reads
+                 * garbage from a lane outside the exec mask) */
+                const uint32_t nk0 = __shfl(nkl, sr, 64);
+                const uint32_t b = __shfl(bl, sr, 64), nk = seg ? nk0 : 0u;
+                const uint32_t r0 = __shfl(rbl, sr, 64), nr = __shfl(nrl, sr, 64), kb = __shfl(kbl, sr, 64);
+                /* this lane's key: its run among the bucket's <= 4 */
+                uint32_t src = 0, acc = 0;
+                bool found = false;
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const uint2 run = (seg && (uint32_t)q < nr) ? a.in.run[r0 + q] : make_uint2(0, 0);
+                    if (!found && j < acc + run.y) {
+                        src = run.x + (j - acc);
+                        found = true;
+                    }
+                    acc += run.y;
+                }
+                const bool v_ok = seg && j < nk;
+                uint32_t v = 0xFFFFFFFFu;
+                if (v_ok) {
+                    const uint32_t key = (uint32_t)a.keys[src];
+                    const uint32_t cm = (1u << a.lg) - 1;
+                    v = hm_spread7(key & cm) | (hm_spread7(key >> a.lg) << 1);
+                }
+                hm_seg32_size<2>(v, lane);
+                if (v_ok) a.codes[kb + j] = (uint16_t)v;
+                const uint32_t nx = __shfl_down(v, 1, 64);
+                const uint64_t segm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+                uint32_t total = 0;
+                for (int l = 0; l < a.lg; l++) {
+                    if (!((zmask >> l) & 1u)) continue;
+                    const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
+                    total += (uint32_t)__popcll(__ballot(end) & segm);
+                }
+                if (seg && j == 0) a.spcnt[b] = total;
+            }
+        }
         while (m) {
             const int i = __builtin_ctzll(m);
             m &= m - 1;
@@ -2887,6 +2965,48 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
         const uint64_t cl = small ? a.B.coord[bl] : 0ull;
         const uint64_t ol = small ? a.spoff[bl] : 0ull;
         uint64_t m = __ballot(small);
+        if constexpr (LO == 0) {
+            /* the <= 32-key buckets in pairs, as k_small_sort took them */
+            const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
+            uint64_t mt = __ballot(small && nkl <= 32 && nrl <= 4);
+            m &= ~mt;
+            const uint32_t j = lane & 31;
+            const uint64_t segm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+            while (mt) {
+                const int sl = hm_pair_lane(mt);
+                const bool seg = sl >= 0;
+                const int sr = seg ? sl : 0;
+                const uint32_t nk0 = __shfl(nkl, sr, 64);   /* whole wave active (see k_small_sort) */
+                const uint32_t nk = seg ? nk0 : 0u, kb = __shfl(kbl, sr, 64);
+                const uint64_t coord = __shfl(cl, sr, 64);
+                uint64_t q = base + __shfl(ol, sr, 64);
+                const bool v_ok = seg && j < nk;
+                const uint32_t v = v_ok ? (uint32_t)a.codes[kb + j] : 0xFFFFFFFFu;
+                const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
+                for (int l = 0; l < a.lg; l++) {
+                    if (!((zmask >> l) & 1u)) continue;
+                    const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
+                    const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
+                    /* the segment's last head at or below this lane (its j = 0
+                     * lane is one): the cell's first element */
+                    const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
+                    const uint32_t hl = hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u;
+                    const uint32_t start = (uint32_t)__shfl((int)j, (int)hl, 64);
+                    const uint64_t bal = __ballot(end) & segm;
+                    if (end) {
+                        const uint32_t code = v >> (2 * l);
+                        const int s = a.lg - l;
+                        const uint32_t idx = (hm_compact7(code >> 1) << s) | hm_compact7(code);
+                        const uint64_t p = q + hm_mbcnt(bal);
+                        if (p < a.out.capacity) {
+                            a.out.keys[p] = hm_cell_key(a.Z - l, coord, s, idx);
+                            a.out.counts[p] = (uint64_t)(j - start + 1);
+                        }
+                    }
+                    q += (uint64_t)__popcll(bal);
+                }
+            }
+        }
         while (m) {
             const int i = __builtin_ctzll(m);
             m &= m - 1;
