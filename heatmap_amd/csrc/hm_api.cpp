@@ -1161,9 +1161,19 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         hm_launch_scan(s, ra.nr, V.nchildren, partial, runbase, tot + 0);
         HIPCHK(hipGetLastError());
         unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
-        HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(hm_sync(s));
-        const uint64_t nflat = down[0];
+        /* the flat run list is sized by a bound, its length stays on the
+         * device (tot[0]): at most one run per (parent item, child) and per
+         * key, plus the hot tiles' region shards */
+        uint64_t nflat = std::min<uint64_t>(level_keys, (uint64_t)lv[l - 1].items << V.dbits) +
+                         (uint64_t)HM_MAX_HOT * HM_L1_SHARDS + 1;
+        ra.nflat_dev = tot + 0;
+        if (nflat * 24 > (8ull << 30)) {
+            /* a bound of more than 8 GiB of run buffers: read the count back */
+            HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+            HIPCHK(hm_sync(s));
+            nflat = down[0];
+            ra.nflat_dev = nullptr;
+        }
         ra.nflat = nflat;
         uint2* flat;
         uint64_t* excl;
@@ -1183,7 +1193,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             hr.cnt = ra.cnt;
             hm_launch_hot_runs(s, hr);
         }
-        hm_launch_scan(s, ra.cnt, nflat, partial, excl, tot + 1);
+        hm_launch_scan(s, ra.cnt, nflat, partial, excl, tot + 1, ra.nflat_dev);
         ra.total_keys = tot + 1;
         uint32_t* cnkeys;
         uint32_t* ckeybase;

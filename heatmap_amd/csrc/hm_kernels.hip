@@ -2012,7 +2012,8 @@ __global__ __launch_bounds__(256) void k_rs_keys(HmRsArgs a)
         }
         const uint64_t rb = a.runbase[c];
         const uint64_t kb = a.excl[rb];
-        const uint64_t ke = (rb + nr < a.nflat) ? a.excl[rb + nr] : *a.total_keys;
+        const uint64_t nflat = a.nflat_dev ? *a.nflat_dev : a.nflat;
+        const uint64_t ke = (rb + nr < nflat) ? a.excl[rb + nr] : *a.total_keys;
         const uint32_t nk = (uint32_t)(ke - kb);
         a.nkeys[c] = nk;
         a.keybase[c] = (uint32_t)kb;
@@ -2126,9 +2127,10 @@ void hm_launch_hot_runs(hipStream_t s, const HmHotRunArgs& a)
 #define HM_SCAN_MAXB 4096
 
 __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_reduce(const uint64_t* v, uint64_t n, uint64_t chunk,
-                                                                 uint64_t* partial)
+                                                                 uint64_t* partial, const uint64_t* ndev)
 {
     __shared__ uint64_t red[HM_SCAN_THREADS / 64];
+    if (ndev) n = min(n, *ndev);   /* the live length, read on the device */
     const uint64_t b0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t b1 = min(b0 + chunk, n);
     uint64_t s = 0;
@@ -2149,9 +2151,11 @@ __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_reduce(const uint64_t*
  * *total.  PER = 4: the partials of a multi-block scan; PER = 16: a whole
  * scan of <= 16384 values in one dispatch (small calls are dispatch-bound). */
 template <int PER>
-__global__ __launch_bounds__(1024) void k_scan_one(const uint64_t* v, uint32_t n, uint64_t* out, uint64_t* total)
+__global__ __launch_bounds__(1024) void k_scan_one(const uint64_t* v, uint32_t n, uint64_t* out, uint64_t* total,
+                                                   const uint64_t* ndev)
 {
     __shared__ uint64_t ws[17];
+    if (ndev) n = (uint32_t)min((uint64_t)n, *ndev);
     const int tid = threadIdx.x;
     uint64_t x[PER];
     uint64_t s = 0;
@@ -2187,9 +2191,11 @@ __global__ __launch_bounds__(1024) void k_scan_one(const uint64_t* v, uint32_t n
 
 /* block b: its chunk in sub-chunks of HM_SCAN_ITEMS, carrying the prefix */
 __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v, uint64_t n, uint64_t chunk,
-                                                               const uint64_t* partial, uint64_t* out)
+                                                               const uint64_t* partial, uint64_t* out,
+                                                               const uint64_t* ndev)
 {
     __shared__ uint64_t ws[HM_SCAN_THREADS / 64 + 1];
+    if (ndev) n = min(n, *ndev);
     constexpr int PER = HM_SCAN_ITEMS / HM_SCAN_THREADS;
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = min(c0 + chunk, n);
@@ -3470,19 +3476,23 @@ void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a)
     hipLaunchKernelGGL(k_rs_keys, dim3(hm_grid(a.nchildren, 256, 16384)), dim3(256), 0, s, a);
 }
 
-void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total)
+/* exclusive scan of v[0, n) -> out, total -> *total.  ndev: the length is
+ * min(n, *ndev), read on the device (n: the host's bound, which sizes the
+ * grid) -- no read-back before the scan */
+void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total,
+                    const uint64_t* ndev)
 {
     uint64_t chunk = HM_SCAN_ITEMS;
     while ((n + chunk - 1) / chunk > HM_SCAN_MAXB) chunk += HM_SCAN_ITEMS;
     if (n <= 16 * 1024) {
-        hipLaunchKernelGGL(k_scan_one<16>, dim3(1), dim3(1024), 0, s, v, (uint32_t)n, out, total);
+        hipLaunchKernelGGL(k_scan_one<16>, dim3(1), dim3(1024), 0, s, v, (uint32_t)n, out, total, ndev);
         return;
     }
     const uint32_t nb = (uint32_t)((n + chunk - 1) / chunk);
     const uint32_t g = nb ? nb : 1;
-    hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial);
-    hipLaunchKernelGGL(k_scan_one<4>, dim3(1), dim3(1024), 0, s, partial, g, partial, total);
-    hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, ndev);
+    hipLaunchKernelGGL(k_scan_one<4>, dim3(1), dim3(1024), 0, s, partial, g, partial, total, nullptr);
+    hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out, ndev);
 }
 
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a)

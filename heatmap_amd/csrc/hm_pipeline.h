@@ -325,7 +325,8 @@ struct HmRsArgs {
     uint2* flat;                /* flat runs */
     uint64_t* cnt;              /* flat run key counts (scan input) */
     const uint64_t* excl;       /* exclusive scan of cnt */
-    uint64_t nflat;             /* total runs */
+    uint64_t nflat;             /* total runs (a bound when nflat_dev is set) */
+    const uint64_t* nflat_dev;  /* the total on the device, or null */
     const uint64_t* total_keys;
     uint32_t item_keys;
     uint32_t sparse_max;        /* last level: buckets of <= this many keys get no work items */
@@ -470,7 +471,8 @@ void hm_launch_rs_count(hipStream_t s, const HmRsArgs& a);
 void hm_launch_rs_copy(hipStream_t s, const HmRsArgs& a);
 void hm_launch_rs_keys(hipStream_t s, const HmRsArgs& a);
 /* exclusive scan of v[0..n) into out (any n), total into *total; partial: 4096 u64 */
-void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total);
+void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* partial, uint64_t* out, uint64_t* total,
+                    const uint64_t* ndev = nullptr);
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a);
 /* seg (or null): per item 16 u32, its <= HM_L1_SHARDS runs (k_partition_fr) */
 void hm_launch_items(hipStream_t s, const HmBuckets& B, HmRuns in, uint32_t items, uint32_t T, uint4* desc,
