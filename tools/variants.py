@@ -62,7 +62,9 @@ VARIANTS = {
     "hot1k": ["HM_MAX_HOT=1024"],
     "hot1kta1m": ["HM_MAX_HOT=1024", "HM_TA=1048576"],
     "os8": ["HM_OS_IT=8"],
-    "tn16k": ["HM_TN=16384"],               # 16K-key partition items (half the (item, child) pairs)                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
+    "tn16k": ["HM_TN=16384"],
+    "l1n6": ["HM_L1_NARROW=1", "HM_L1_WAVES=6"],   # k_l1_fast with 4-B staging, 3 blocks per CU (spills)
+    "l1n4": ["HM_L1_NARROW=1", "HM_L1_WAVES=4"],   # 4-B staging at 2 blocks per CU               # 16K-key partition items (half the (item, child) pairs)                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
 }
 
 # Timing-only experiments: text patches applied to a copy of the sources (the
@@ -91,6 +93,12 @@ PATCHES["l1noatom"] = [("hm_kernels.hip", "        if (cnt[q]) gpos[q] = atomicA
 # levels 2.. always on the spread plan (3 zooms per level) when no tile is hot
 PATCHES["spreadall"] = [("hm_api.cpp", "spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, true);",
                          "spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, false);")]
+# k_l1_fast at one block per CU (an 80 KB LDS pad): K1's sensitivity to occupancy
+PATCHES["l1occ1"] = [("hm_kernels.hip", """    __shared__ uint32_t s_over;
+    /* the polynomial table plus one poison row""", """    __shared__ uint32_t s_over;
+    __shared__ uint32_t occpad[20480];
+    if (a.n == -12345) occpad[threadIdx.x] = 1;
+    /* the polynomial table plus one poison row""")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
