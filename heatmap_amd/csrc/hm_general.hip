@@ -133,7 +133,9 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
  * host round trip.  Traffic per step (narrow keys): 12 B read per input
  * cell, 12 B written per output cell, one record per input cell. */
 #define HM_CS_THREADS 256
-#define HM_CS_IT 8
+#ifndef HM_CS_IT
+#define HM_CS_IT 16
+#endif
 #define HM_CS_TILE (HM_CS_THREADS * HM_CS_IT)
 #define HM_CS_FLAG_AGG 1ull
 #define HM_CS_FLAG_INC 2ull
