@@ -382,10 +382,13 @@ __global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
  * and 8 B written per narrow key (16 + 16 wide), plus 2 KB of look-back
  * words per tile. */
 #define HM_OS_THREADS 256
-#ifndef HM_OS_IT
-#define HM_OS_IT 16
-#endif
-#define HM_OS_TILE (HM_OS_THREADS * HM_OS_IT)
+/* keys per thread: 32 narrow keys (211 VGPRs, 72 KB of LDS: 2 blocks per
+ * CU; 16 measured 1.1 ms slower per grouped call), 16 wide ones */
+template <typename KT> struct HmOs {
+    static constexpr int IT = sizeof(KT) == 8 ? 32 : 16;
+    static constexpr int TILE = HM_OS_THREADS * IT;
+};
+#define HM_OS_TILE_MIN (HM_OS_THREADS * 16)   /* look-back words are sized for the smaller tiles */
 #define HM_OS_MAXP 16
 
 struct HmRxAll {
@@ -454,6 +457,7 @@ struct HmRxPass {
 template <typename KT>
 __global__ __launch_bounds__(HM_OS_THREADS) void k_rx_onesweep(HmRxPass a)
 {
+    constexpr int HM_OS_IT = HmOs<KT>::IT, HM_OS_TILE = HmOs<KT>::TILE;
     __shared__ KT stage[HM_OS_TILE];
     __shared__ uint32_t wcnt[4][256];
     __shared__ uint32_t dbase[256];      /* tile-local start of each digit */
@@ -619,7 +623,7 @@ void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a)
     hipLaunchKernelGGL(k_gen_keys, dim3(hm_ggrid(a.n, 256, 8192)), dim3(256), 0, s, a);
 }
 
-uint64_t hm_rx_os_tiles(uint64_t n) { return (n + HM_OS_TILE - 1) / HM_OS_TILE; }
+uint64_t hm_rx_os_tiles(uint64_t n) { return (n + HM_OS_TILE_MIN - 1) / HM_OS_TILE_MIN; }
 
 /* LSD sort of n keys (lo[0], hi[0]) over the digits at shifts sh[0..np)
  * (ascending); (lo[1], hi[1]) is the other buffer.  state = 256 B tickets +
@@ -629,7 +633,8 @@ int hm_launch_rx_sort(hipStream_t s, bool wide, uint64_t* const* lo, uint64_t* c
                       int np, uint8_t* state)
 {
     if (np == 0) return 0;
-    const uint64_t nt = hm_rx_os_tiles(n);
+    const uint64_t nt = wide ? (n + HmOs<hm_u128>::TILE - 1) / HmOs<hm_u128>::TILE
+                             : (n + HmOs<uint64_t>::TILE - 1) / HmOs<uint64_t>::TILE;
     (void)hipMemsetAsync(state, 0, 256 + HM_OS_MAXP * 2048 + nt * 2048, s);
     HmRxAll h;
     h.lo = lo[0];

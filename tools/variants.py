@@ -63,8 +63,8 @@ VARIANTS = {
     "hot1kta1m": ["HM_MAX_HOT=1024", "HM_TA=1048576"],
     "os8": ["HM_OS_IT=8"],
     "tn16k": ["HM_TN=16384"],
-    "cs16": ["HM_CS_IT=16"],                # zoom cascade tiles of 4096 items
-    "cs4": ["HM_CS_IT=4"],                  # zoom cascade tiles of 1024 items
+    "os24": ["HM_OS_IT=24"],                # one-sweep radix tiles of 6144 keys
+    "os32": ["HM_OS_IT=32"],                # one-sweep radix tiles of 8192 keys
     "l1n6": ["HM_L1_NARROW=1", "HM_L1_WAVES=6"],   # k_l1_fast with 4-B staging, 3 blocks per CU (spills)
     "l1n4": ["HM_L1_NARROW=1", "HM_L1_WAVES=4"],   # 4-B staging at 2 blocks per CU               # 16K-key partition items (half the (item, child) pairs)                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
 }
