@@ -1107,7 +1107,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 HIPCHK(hipMemsetAsync(a.ctot, 0, V.nchildren * 8, s));
                 HIPCHK(hipMemsetAsync(a.ccur, 0, V.nchildren * 4, s));
                 a.mode = HM_PN_HIST;
-                hm_launch_partN(s, a, lv[l - 1].items, false, true);
+                hm_launch_partition_hist(s, a);
                 hm_launch_scan(s, (const uint64_t*)a.ctot, V.nchildren, ptl, (uint64_t*)a.cbase, ttl + 3);
                 a.mode = HM_PN_CONTIG;
             }

@@ -1808,6 +1808,78 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
     HM_STAMP_M(3, 6);
 }
 
+/* Child totals of a child-contiguous level (HM_PN_HIST): a block takes
+ * HM_HIST_G consecutive items (items are in bucket order, so they mostly
+ * share a bucket), counts their keys' children in LDS and adds each bucket's
+ * non-zero counts once per block -- HM_HIST_G times fewer global atomics than
+ * one flush per item. */
+#define HM_HIST_G 8
+__global__ __launch_bounds__(HM_FR_THREADS) void k_partition_hist(HmPartNArgs a)
+{
+    constexpr int T = HM_FR_THREADS;
+    constexpr int KPT = HM_TN / T;
+    __shared__ uint32_t cur[HM_MAX_FN];
+    const int tid = threadIdx.x;
+    const int F = 1 << a.dbits;
+    const uint32_t g0 = hm_block_id() * HM_HIST_G;
+    if (g0 >= a.items) return;
+    const uint32_t g1 = min(g0 + HM_HIST_G, a.items);
+    const int sw = a.restbits >> 1, ww = a.dbits >> 1, sp = sw + ww;
+    for (int i = tid; i < F; i += T) cur[i] = 0;
+    __syncthreads();
+    uint32_t bucket = hm_item(a.parent, g0).bucket;
+    for (uint32_t g = g0; g < g1; g++) {
+        const HmItem it = hm_item(a.parent, g);   /* block-uniform */
+        if (it.bucket != bucket) {
+            /* flush the previous bucket's counts */
+            __syncthreads();
+            for (int d = tid; d < F; d += T) {
+                const uint32_t c = cur[hm_cur_slot(d, ww)];
+                if (c) atomicAdd(&a.ctot[((uint64_t)bucket << a.dbits) + d], (unsigned long long)c);
+            }
+            __syncthreads();
+            for (int i = tid; i < F; i += T) cur[i] = 0;
+            __syncthreads();
+            bucket = it.bucket;
+        }
+        const uint4* sg = (const uint4*)(a.seg + 16 * (size_t)g);
+        const uint4 s0 = sg[0], s1 = sg[1], s2 = sg[2], s3 = sg[3];
+        const uint32_t rpos[HM_L1_SHARDS] = {s0.x, s0.z, s1.x, s1.z, s2.x, s2.z, s3.x, s3.z};
+        const uint32_t rsrc[HM_L1_SHARDS] = {s0.y, s0.w, s1.y, s1.w, s2.y, s2.w, s3.y, s3.w};
+        const uint32_t nr = min(it.r1 - it.r0, (uint32_t)HM_L1_SHARDS);
+        const uint32_t total = it.b - it.a;
+        uint32_t kv[KPT];
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            const uint32_t i = (uint32_t)(k * T + tid);
+            const uint32_t p = it.a + i;
+            uint32_t src = rsrc[0] + (p - rpos[0]);
+#pragma unroll
+            for (int j = 1; j < HM_L1_SHARDS; j++)
+                src = ((uint32_t)j < nr && rpos[j] <= p) ? rsrc[j] + (p - rpos[j]) : src;
+            kv[k] = i < total ? a.keys_in[src] : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < KPT; k++) {
+            if ((uint32_t)(k * T + tid) < total) {
+                const uint32_t r = kv[k] >> sp, c = kv[k] & ((1u << sp) - 1u);
+                atomicAdd(&cur[hm_cur_slot(((r >> sw) << ww) | (c >> sw), ww)], 1u);
+            }
+        }
+    }
+    __syncthreads();
+    for (int d = tid; d < F; d += T) {
+        const uint32_t c = cur[hm_cur_slot(d, ww)];
+        if (c) atomicAdd(&a.ctot[((uint64_t)bucket << a.dbits) + d], (unsigned long long)c);
+    }
+}
+
+void hm_launch_partition_hist(hipStream_t s, const HmPartNArgs& a)
+{
+    const uint32_t blocks = (a.items + HM_HIST_G - 1) / HM_HIST_G;
+    if (blocks) hipLaunchKernelGGL(k_partition_hist, hm_grid2(blocks), dim3(HM_FR_THREADS), 0, s, a);
+}
+
 /* ------------------------------------------------------------------------ */
 /* run scan: sharded run counters -> one flat, child-ordered run list        */
 /* ------------------------------------------------------------------------ */

@@ -308,6 +308,7 @@ struct HmPartNArgs {
     const unsigned long long* cbase;
     uint32_t* ccur;
 };
+void hm_launch_partition_hist(hipStream_t s, const HmPartNArgs& a);
 #define HM_PN_RUNS 0
 #define HM_PN_HIST 1
 #define HM_PN_CONTIG 2
