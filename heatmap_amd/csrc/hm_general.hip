@@ -141,38 +141,11 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 #define HM_CS_FLAG_INC 2ull
 #define HM_CS_VBITS 38
 
-/* one record of cell key k at zoom z (all lanes of the wave call it: the
- * split mode appends per wave) */
-__device__ __forceinline__ void hm_gen_record(const HmGenEmit& e, hm_u128 k, int Z, int z, uint64_t cnt, bool in,
-                                              uint64_t q)
+/* one (group,) z, row, col, count record at slot q */
+__device__ __forceinline__ void hm_put_record(const HmGenEmit& e, uint64_t q, uint32_t g, int z, int64_t row,
+                                              int64_t col, uint64_t cnt)
 {
-    int64_t row = 0, col = 0;
-    uint32_t g = 0;
-    if (in) hm_gen_decode(k, Z, z, &g, &row, &col);
-    bool rec = in;
-    if (e.split) {
-        /* hm_count fallback: cells inside [0, 2^z)^2 as (HM_KEY, count), the
-         * others as records; one append per wave and kind */
-        const bool sq = in && (uint64_t)row < (1ull << z) && (uint64_t)col < (1ull << z);
-        rec = in && !sq;
-        const uint64_t ms = __builtin_amdgcn_ballot_w64(sq), mx = __builtin_amdgcn_ballot_w64(rec);
-        const int ls = ms ? __ffsll((unsigned long long)ms) - 1 : 0;
-        const int lx = mx ? __ffsll((unsigned long long)mx) - 1 : 0;
-        unsigned long long bs = 0, bx = 0;
-        if (ms && hm_lane() == ls) bs = atomicAdd(e.kcursor, (unsigned long long)__popcll(ms));
-        if (mx && hm_lane() == lx) bx = atomicAdd(e.xcursor, (unsigned long long)__popcll(mx));
-        bs = __shfl(bs, ls, 64);
-        bx = __shfl(bx, lx, 64);
-        if (sq) {
-            const uint64_t p = bs + hm_mbcnt(ms);
-            if (p < e.kcapacity) {
-                e.keys[p] = ((uint64_t)z << 58) | ((uint64_t)row << 29) | (uint64_t)col;
-                e.counts[p] = cnt;
-            }
-        }
-        q = bx + hm_mbcnt(mx);
-    }
-    if (!rec || q >= e.capacity) return;
+    if (q >= e.capacity) return;
     int64_t* r = e.cells + q * e.width;
     int f = 0;
     if (e.width == 5) r[f++] = (int64_t)g;
@@ -180,6 +153,21 @@ __device__ __forceinline__ void hm_gen_record(const HmGenEmit& e, hm_u128 k, int
     r[f++] = row;
     r[f++] = col;
     r[f] = (int64_t)cnt;
+}
+
+/* split mode (hm_count fallback): cells inside [0, 2^z)^2 go out as
+ * (HM_KEY, count), the others as records */
+__device__ __forceinline__ bool hm_in_square(int64_t row, int64_t col, int z)
+{
+    return (uint64_t)row < (1ull << z) && (uint64_t)col < (1ull << z);
+}
+
+__device__ __forceinline__ void hm_put_key(const HmGenEmit& e, uint64_t p, int z, int64_t row, int64_t col,
+                                           uint64_t cnt)
+{
+    if (p >= e.kcapacity) return;
+    e.keys[p] = ((uint64_t)z << 58) | ((uint64_t)row << 29) | (uint64_t)col;
+    e.counts[p] = cnt;
 }
 
 __device__ __forceinline__ uint64_t hm_cs_word(uint64_t epoch, uint64_t flag, uint64_t v)
@@ -224,15 +212,17 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
     __shared__ KT kfirst[NF + 1], klast[NF + 1];   /* klast[f + 1]: last key of fragment f; [0]: item t0 - 1 */
     __shared__ uint32_t elast[NF + 1];
     __shared__ int64_t stage[NW][64 * 5];               /* a wave's records, written out contiguously */
+    __shared__ uint32_t wsq[NF], wrc[NF];   /* split mode: per-fragment key / record counts, then offsets */
     __shared__ uint32_t tile_s;
     __shared__ uint64_t excl_s;
+    __shared__ unsigned long long bsq_s, brc_s;
     const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
     const uint64_t ntiles = (m + HM_CS_TILE - 1) / HM_CS_TILE;
     const int lane = hm_lane(), w = threadIdx.x >> 6;
     const KT keep_bits = ~((((KT)1) << a.clr) - 1);
     const unsigned long long rb = a.rbase_in ? *a.rbase_in : 0ull;
     const int W = a.e.width;
-    const bool staged = a.emit && !a.e.split;
+    const bool staged = a.emit && !a.e.split, split = a.emit && a.e.split;
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.rbase_out) *a.rbase_out = rb + m;
     if (m == 0 && blockIdx.x == 0 && threadIdx.x == 0) *a.m_out = 0u;
     for (;;) {
@@ -283,6 +273,7 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
             const KT kz = k[r] & keep_bits;
             const bool head = v && (i == 0 || (kp & keep_bits) != kz);
             const bool tail = v && (i + 1 == m || (kn & keep_bits) != kz);
+            uint32_t xs = 0;
             if (a.emit) {
                 const uint64_t cnt = (uint64_t)(e[r] - ep);
                 if (staged) {
@@ -309,13 +300,27 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
                     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
                     __builtin_amdgcn_wave_barrier();
                 } else {
-                    hm_gen_record(a.e, hm_k128(k[r], a.hic), a.Z, a.zin, cnt, v, rb + i);
+                    /* split: classify now, reserve per tile, write after the
+                     * look-back (one cursor atomic per tile and kind) */
+                    bool sq = false;
+                    if (v) {
+                        uint32_t g;
+                        int64_t row, col;
+                        hm_gen_decode(hm_k128(k[r], a.hic), a.Z, a.zin, &g, &row, &col);
+                        sq = hm_in_square(row, col, a.zin);
+                    }
+                    const uint64_t ms = __builtin_amdgcn_ballot_w64(sq), mx = __builtin_amdgcn_ballot_w64(v && !sq);
+                    if (lane == 0) {
+                        wsq[f] = (uint32_t)__popcll(ms);
+                        wrc[f] = (uint32_t)__popcll(mx);
+                    }
+                    xs = (uint32_t)sq << 30 | (uint32_t)(v && !sq) << 31;
                 }
             }
             const uint64_t hb = __builtin_amdgcn_ballot_w64(head);
             if (lane == 0) wtot[f] = (uint32_t)__popcll(hb);
             k[r] = kz;
-            fl[r] = (uint32_t)head | ((uint32_t)tail << 1) | (hm_mbcnt(hb) << 2);
+            fl[r] = (uint32_t)head | ((uint32_t)tail << 1) | (hm_mbcnt(hb) << 2) | xs;
         }
         __syncthreads();
         if (w == 0) {
@@ -339,33 +344,108 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
                 if (tile + 1 == ntiles) *a.m_out = (uint32_t)(excl + agg);
                 excl_s = excl;
             }
+            if (split) {
+                const uint32_t xq = lane < NF ? wsq[lane] : 0u, xr = lane < NF ? wrc[lane] : 0u;
+                uint32_t iq = xq, ir = xr;
+#pragma unroll
+                for (int o = 1; o < 64; o <<= 1) {
+                    const uint32_t yq = __shfl_up(iq, o, 64), yr = __shfl_up(ir, o, 64);
+                    if (lane >= o) {
+                        iq += yq;
+                        ir += yr;
+                    }
+                }
+                const uint32_t tq = __shfl(iq, 63, 64), tr = __shfl(ir, 63, 64);
+                if (lane < NF) {
+                    wsq[lane] = iq - xq;
+                    wrc[lane] = ir - xr;
+                }
+                if (lane == 0) {
+                    bsq_s = tq ? atomicAdd(a.e.kcursor, (unsigned long long)tq) : 0ull;
+                    brc_s = tr ? atomicAdd(a.e.xcursor, (unsigned long long)tr) : 0ull;
+                }
+            }
         }
         __syncthreads();
         const uint64_t excl = excl_s;
 #pragma unroll
         for (int r = 0; r < HM_CS_IT; r++) {
-            const uint64_t j = excl + wtot[r * NW + w] + (fl[r] >> 2);
+            const uint64_t j = excl + wtot[r * NW + w] + ((fl[r] >> 2) & 0x7fu);
             if (fl[r] & 1u) hm_kst(a.kout_lo, a.kout_hi, j, k[r]);
             if (fl[r] & 2u) a.eout[j + (fl[r] & 1u) - 1] = e[r];
+        }
+        if (split) {
+            /* the input cells again (L2-warm), to their reserved slots */
+#pragma unroll 1
+            for (int r = 0; r < HM_CS_IT; r++) {
+                const int f = r * NW + w;
+                const bool sq = (fl[r] >> 30) & 1u, rc = fl[r] >> 31;
+                const uint64_t ms = __builtin_amdgcn_ballot_w64(sq), mx = __builtin_amdgcn_ballot_w64(rc);
+                if (sq || rc) {
+                    const uint64_t i = t0 + (uint64_t)r * HM_CS_THREADS + threadIdx.x;
+                    const KT kk = hm_kld<KT>(a.kin_lo, a.kin_hi, i);
+                    const uint32_t ep = i ? (a.ein ? a.ein[i - 1] : (uint32_t)i) : 0u;
+                    uint32_t g;
+                    int64_t row, col;
+                    hm_gen_decode(hm_k128(kk, a.hic), a.Z, a.zin, &g, &row, &col);
+                    const uint64_t cnt = (uint64_t)(e[r] - ep);
+                    if (sq) hm_put_key(a.e, bsq_s + wsq[f] + hm_mbcnt(ms), a.zin, row, col, cnt);
+                    else hm_put_record(a.e, brc_s + wrc[f] + hm_mbcnt(mx), g, a.zin, row, col, cnt);
+                }
+            }
         }
         __syncthreads();
     }
 }
 
-/* the records of the last level (nothing below it to fold into) */
+/* the records of the last level (nothing below it to fold into); split mode
+ * reserves its slots once per block and kind */
 template <typename KT>
 __global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
 {
+    __shared__ uint32_t wq[4], wr[4];
+    __shared__ unsigned long long bq_s, br_s;
     const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
     const unsigned long long rb = *a.rbase_in;
     if (blockIdx.x == 0 && threadIdx.x == 0) *a.rbase_out = rb + m;
     const uint64_t stride = (uint64_t)gridDim.x * 256;
-    const uint64_t m_up = (m + 63) & ~63ull;   /* whole waves: split mode appends per wave */
+    const uint64_t m_up = (m + 255) & ~255ull;   /* whole blocks: split mode reserves per block */
+    const int lane = hm_lane(), w = threadIdx.x >> 6;
     for (uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x; i < m_up; i += stride) {
         const bool v = i < m;
         const KT k = v ? hm_kld<KT>(a.kin_lo, a.kin_hi, i) : (KT)0;
         const uint32_t e = v ? a.ein[i] : 0u, ep = (v && i) ? a.ein[i - 1] : 0u;
-        hm_gen_record(a.e, hm_k128(k, a.hic), a.Z, a.zin, (uint64_t)(e - ep), v, rb + i);
+        const uint64_t cnt = (uint64_t)(e - ep);
+        uint32_t g = 0;
+        int64_t row = 0, col = 0;
+        if (v) hm_gen_decode(hm_k128(k, a.hic), a.Z, a.zin, &g, &row, &col);
+        if (!a.e.split) {
+            if (v) hm_put_record(a.e, rb + i, g, a.zin, row, col, cnt);
+            continue;
+        }
+        const bool sq = v && hm_in_square(row, col, a.zin), rc = v && !sq;
+        const uint64_t ms = __builtin_amdgcn_ballot_w64(sq), mx = __builtin_amdgcn_ballot_w64(rc);
+        if (lane == 0) {
+            wq[w] = (uint32_t)__popcll(ms);
+            wr[w] = (uint32_t)__popcll(mx);
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t tq = 0, tr = 0;
+            for (int x = 0; x < 4; x++) {
+                const uint32_t q = wq[x], r = wr[x];
+                wq[x] = tq;
+                wr[x] = tr;
+                tq += q;
+                tr += r;
+            }
+            bq_s = tq ? atomicAdd(a.e.kcursor, (unsigned long long)tq) : 0ull;
+            br_s = tr ? atomicAdd(a.e.xcursor, (unsigned long long)tr) : 0ull;
+        }
+        __syncthreads();
+        if (sq) hm_put_key(a.e, bq_s + wq[w] + hm_mbcnt(ms), a.zin, row, col, cnt);
+        if (rc) hm_put_record(a.e, br_s + wr[w] + hm_mbcnt(mx), g, a.zin, row, col, cnt);
+        __syncthreads();
     }
 }
 
