@@ -77,6 +77,14 @@ struct hm_ctx {
     int debug_l1 = 0;                  /* HM_DEBUG_L1: report level-1 region overflows on stderr */
     int stage_timing = 1;              /* HM_STAGE_TIMING=0: no stage events (hm_last_stats stages read 0) */
     int contig = 1;                    /* HM_CONTIG=0: 3-level plans keep run-streaming at the last level */
+    uint32_t ta_min = 16384;           /* HM_TA_MIN: smallest aggregation work item (keys) */
+    uint32_t ta_items = 512;           /* HM_TA_ITEMS: items' worth of points a call must have before ta halves */
+    /* a stream's tail cells: the count re-keys them under the batch's bucket
+     * (read on the device from the stream state) before its last read-back */
+    uint64_t* tail_keys = nullptr;
+    const unsigned long long* tail_state = nullptr;
+    int tail_cb = 0;
+    int tail_done = 0;
     uint64_t rs_big_min = 0;
     /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
      * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
@@ -254,6 +262,8 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     if (const char* e = getenv("HM_DEBUG_L1")) c->debug_l1 = atoi(e);
     if (const char* e = getenv("HM_STAGE_TIMING")) c->stage_timing = atoi(e);
     if (const char* e = getenv("HM_CONTIG")) c->contig = atoi(e);
+    if (const char* e = getenv("HM_TA_MIN")) c->ta_min = (uint32_t)std::max(1024, std::min((int)HM_TA, atoi(e)));
+    if (const char* e = getenv("HM_TA_ITEMS")) c->ta_items = (uint32_t)std::max(1, atoi(e));
     int st = HM_OK;
     if (hipMalloc(&c->state, ST_COUNT * sizeof(unsigned long long)) != hipSuccess) {
         c->state = nullptr;
@@ -658,7 +668,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
      * call has >= 512 items' worth of points -- a 1e7-point call otherwise
      * runs ~40 items on 256 CUs */
     uint32_t ta = HM_TA;
-    while (ta > 16384 && (uint64_t)n < (uint64_t)ta * 512) ta >>= 1;
+    while (ta > ctx->ta_min && (uint64_t)n < (uint64_t)ta * ctx->ta_items) ta >>= 1;
     for (int i = 0; i < 8; i++) ctx->stage_us[i] = 0;
     ctx->last_levels = L;
 
@@ -1079,7 +1089,16 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(kslot, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
         ENSURE(B_RUNS_SH, run_cap * sizeof(uint2), runs_sh);
         ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
-        HIPCHK(hipMemsetAsync(nruns, 0, (V.nchildren << sb) * sizeof(uint32_t), s));
+        uint32_t* rs_big;
+        ENSURE(B_RS_BIG, (HM_RS_BIG_MAX + 1) * sizeof(uint32_t), rs_big);
+        {
+            /* the level's zeroed counters in one launch */
+            HmFill zf;
+            zf.k = 0;
+            hm_fill_add(zf, nruns, 0, (V.nchildren << sb) * sizeof(uint32_t));
+            hm_fill_add(zf, rs_big + HM_RS_BIG_MAX, 0, sizeof(uint32_t));   /* the run scan's big-child count */
+            hm_launch_fill(s, zf);
+        }
 
         {
             HmPartNArgs a;
@@ -1182,10 +1201,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_CNT, (nflat + 1) * sizeof(uint64_t), ra.cnt);
         ra.flat = flat;
         ra.excl = excl;
-        ENSURE(B_RS_BIG, (HM_RS_BIG_MAX + 1) * sizeof(uint32_t), ra.big);
-        ra.nbig = ra.big + HM_RS_BIG_MAX;
+        ra.big = rs_big;
+        ra.nbig = ra.big + HM_RS_BIG_MAX;   /* zeroed with nruns */
         ra.big_min = ctx->rs_big_min;
-        HIPCHK(hipMemsetAsync(ra.nbig, 0, sizeof(uint32_t), s));
         hm_launch_rs_copy(s, ra);
         if (hot_level) {
             hr.runbase = runbase;
@@ -1298,8 +1316,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         const int l = L - 1;
         uint32_t* gslots = nullptr;
         ENSURE(B_GSLOTS, (uint64_t)(nslots ? nslots : 1) * HM_AG_CELLS * 4, gslots);
-        if (nslots) HIPCHK(hipMemsetAsync(gslots, 0, (size_t)nslots * HM_AG_CELLS * 4, s));
-        HIPCHK(hipMemsetAsync(totals[l], 0, ((size_t)lv[l].count + 1) * 8, s));
+        {
+            HmFill zf;
+            zf.k = 0;
+            if (nslots) hm_fill_add(zf, gslots, 0, (size_t)nslots * HM_AG_CELLS * 4);
+            hm_fill_add(zf, totals[l], 0, ((size_t)lv[l].count + 1) * 8);
+            hm_launch_fill(s, zf);
+        }
         HmAggArgs a;
         memset(&a, 0, sizeof(a));
         a.B = B[l];
@@ -1350,6 +1373,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     }
     if (timing) HIPCHK(hipEventRecord(ev[nev], s));
     nev++;
+    if (ctx->tail_keys) {
+        hm_launch_stream_rekey_dev(s, ctx->tail_keys, ctx->state + ST_CURSOR, (uint64_t)capacity, ctx->tail_state,
+                                   ctx->tail_cb);
+        HIPCHK(hipGetLastError());
+        ctx->tail_done = 1;
+    }
     if ((st = read_state(ctx))) return st;
     for (int i = 0; timing && i + 1 < nev; i++) {
         float ms = 0;
@@ -1947,8 +1976,13 @@ static int stream_count_tail(hm_stream* s, const double* lat, const double* lon,
     if ((st = stream_room(s, 2 * (uint64_t)n + 1024))) return st; /* typical batches: fewer cells than 2 per point */
     for (;;) {
         int64_t nx = 0;
+        s->ctx->tail_keys = s->lkeys + s->llen;
+        s->ctx->tail_state = s->state;
+        s->ctx->tail_cb = s->cb;
+        s->ctx->tail_done = 0;
         st = hm_count(s->ctx, lat, lon, keep, n, s->zmin, s->zmax, s->lkeys + s->llen, s->lcounts + s->llen,
                       (int64_t)(s->lcap - s->llen), m, nullptr, 0, &nx);
+        s->ctx->tail_keys = nullptr;
         /* the log's keys hold tiles inside [0, 2^z)^2 only */
         if (nx > 0) return HM_E_EXOTIC;
         if (st != HM_E_CAPACITY) return st;
@@ -1959,7 +1993,9 @@ static int stream_count_tail(hm_stream* s, const double* lat, const double* lon,
 /* part 2: the tail's m cells keyed under the bucket and appended */
 static int stream_take_tail(hm_stream* s, int64_t m, uint32_t bucket)
 {
-    hm_launch_stream_rekey(s->ctx->stream, s->lkeys + s->llen, (uint64_t)m, (uint64_t)bucket << s->cb);
+    /* re-keyed inside the count already unless it took the fallback path */
+    if (!s->ctx->tail_done)
+        hm_launch_stream_rekey(s->ctx->stream, s->lkeys + s->llen, (uint64_t)m, (uint64_t)bucket << s->cb);
     HIPCHK(hipGetLastError());
     stream_appended(s, (uint64_t)m, bucket);
     return HM_OK;

@@ -574,6 +574,11 @@ void hm_launch_stream_collect(hipStream_t s, const uint32_t* bflag, uint64_t nb,
 void hm_launch_stream_part_count(hipStream_t s, const HmsScatterArgs& a);
 void hm_launch_stream_scatter(hipStream_t s, const HmsScatterArgs& a);
 void hm_launch_stream_rekey(hipStream_t s, uint64_t* keys, uint64_t m, uint64_t prefix);
+/* the same with the count m = min(*m_dev, cap) and the bucket (the batch's
+ * only one: state[HMS_ST_BMM] when state[HMS_ST_NLIST] != 0, else 0) read on
+ * the device */
+void hm_launch_stream_rekey_dev(hipStream_t s, uint64_t* keys, const unsigned long long* m_dev, uint64_t cap,
+                                const unsigned long long* state, int cb);
 void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int cb, uint64_t* keys, uint64_t* counts,
                               unsigned long long* state);
 void hm_launch_stream_init(hipStream_t s, const HmsTable& t);

@@ -271,6 +271,17 @@ __global__ __launch_bounds__(256) void k_stream_rekey(uint64_t* __restrict__ key
         keys[i] = prefix | hms_cell(keys[i]);
 }
 
+__global__ __launch_bounds__(256) void k_stream_rekey_dev(uint64_t* __restrict__ keys,
+                                                          const unsigned long long* __restrict__ m_dev, uint64_t cap,
+                                                          const unsigned long long* __restrict__ state, int cb)
+{
+    const uint64_t m = min((uint64_t)*m_dev, cap);
+    const uint64_t prefix = state[HMS_ST_NLIST] ? (uint64_t)(uint32_t)state[HMS_ST_BMM] << cb : 0ull;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < m; i += stride)
+        keys[i] = prefix | hms_cell(keys[i]);
+}
+
 /* grouped-path records (bucket, zoom, row, col, count) -> cell-table keys;
  * records of tiles outside [0, 2^z)^2 are counted, not converted */
 __global__ __launch_bounds__(256) void k_stream_convert(const int64_t* __restrict__ rec, uint64_t m, int cb,
@@ -496,6 +507,12 @@ void hm_launch_stream_scatter(hipStream_t s, const HmsScatterArgs& a)
 void hm_launch_stream_rekey(hipStream_t s, uint64_t* keys, uint64_t m, uint64_t prefix)
 {
     if (m) hipLaunchKernelGGL(k_stream_rekey, hms_grid(m), dim3(256), 0, s, keys, m, prefix);
+}
+
+void hm_launch_stream_rekey_dev(hipStream_t s, uint64_t* keys, const unsigned long long* m_dev, uint64_t cap,
+                                const unsigned long long* state, int cb)
+{
+    if (cap) hipLaunchKernelGGL(k_stream_rekey_dev, dim3(1024), dim3(256), 0, s, keys, m_dev, cap, state, cb);
 }
 
 void hm_launch_stream_convert(hipStream_t s, const int64_t* rec, uint64_t m, int cb, uint64_t* keys, uint64_t* counts,
