@@ -1917,6 +1917,9 @@ __global__ __launch_bounds__(256) void k_rs_count(HmRsArgs a)
  * parent work item: the hot tile of a skewed cloud has 10^5) is listed instead, and k_rs_copy_big
  * spreads its slices over every wave of the grid. */
 #define HM_RS_SLICE 512
+#ifndef HM_RS_LANE_MAX
+#define HM_RS_LANE_MAX 16   /* one-shard children of at most this many runs: one lane each */
+#endif
 
 struct HmRsChild {
     uint32_t n, incl;
@@ -2008,6 +2011,25 @@ __global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
                 if (lane == 0) a.big[slot] = (uint32_t)(c0 + (uint64_t)i);
             } else {
                 m |= 1ull << i;   /* list full: copied here */
+            }
+        }
+        if (a.shard_bits == 0) {
+            /* one shard per child: its runs are one contiguous range, so a
+             * child of few runs is copied by its own lane (64 children in
+             * flight per wave, not one dependent chain after another) */
+            const bool mine = ((m >> lane) & 1ull) && nrl <= HM_RS_LANE_MAX;
+            m &= ~__ballot(mine);
+            if (mine) {
+                const uint32_t n = a.nruns[cl];   /* 0: a hot tile (k_hot_runs lists its runs) */
+                const uint64_t p = cl >> a.dbits, d = cl & ((1ull << a.dbits) - 1);
+                const uint32_t t0 = a.parent_item_begin[p];
+                const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+                const uint64_t src = hm_run_base(t0, tp, p, d, a.dbits, 0);
+                for (uint32_t j = 0; j < n; j++) {
+                    const uint2 r = a.runs[src + j];
+                    a.flat[rbl + j] = r;
+                    a.cnt[rbl + j] = r.y;
+                }
             }
         }
         if (!m) continue;
