@@ -2808,15 +2808,23 @@ __device__ __forceinline__ void hm_small_sort(const HmAggArgs& a, const uint16_t
         const uint32_t e = lane * K + u;
         if (e < nk) a.codes[kb + e] = (uint16_t)v[u];
     }
-    uint32_t total = 0;
-    const uint32_t nx = __shfl_down(v[0], 1, 64);   /* level-independent: once per bucket */
-    for (int l = 0; l < lg; l++) {
-        if (!((zmask >> l) & 1u)) continue;
-        bool end[K];
-        hm_small_ends<K>(v, nk, l, end, nx);
+    /* cells: element e ends a level-l cell iff its code and the next one's
+     * differ above bit 2l, i.e. for the levels below half the bit length of
+     * their xor (the last element ends every level): one count per element,
+     * not a ballot per (level, element) */
+    const uint32_t nx = __shfl_down(v[0], 1, 64);
+    const uint32_t zall = (uint32_t)__popc(zmask);
+    uint32_t cnt = 0;
 #pragma unroll
-        for (int u = 0; u < K; u++) total += __popcll(__ballot(end[u]));
+    for (int u = 0; u < K; u++) {
+        const uint32_t e = lane * K + u;
+        const uint32_t next = (u + 1 < K) ? v[u + 1] : nx;
+        const uint32_t x = v[u] ^ next;
+        const uint32_t hl = (33u - (uint32_t)__clz((int)x)) >> 1;   /* x = 0: 0 */
+        const uint32_t c = e + 1 == nk ? zall : (uint32_t)__popc(zmask & ((1u << hl) - 1u));
+        cnt += e < nk ? c : 0u;
     }
+    const uint32_t total = hm_wave_sum(cnt);
     if (lane == 0) a.spcnt[b] = total;
 }
 
