@@ -2987,13 +2987,14 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
                 hm_seg32_size<2>(v, lane);
                 if (v_ok) a.codes[kb + j] = (uint16_t)v;
                 const uint32_t nx = __shfl_down(v, 1, 64);
-                const uint64_t segm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
-                uint32_t total = 0;
-                for (int l = 0; l < a.lg; l++) {
-                    if (!((zmask >> l) & 1u)) continue;
-                    const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
-                    total += (uint32_t)__popcll(__ballot(end) & segm);
-                }
+                /* cells ended by this element (as in hm_small_sort), summed
+                 * over the 32-lane segment */
+                const uint32_t hl = (33u - (uint32_t)__clz((int)(v ^ nx))) >> 1;
+                uint32_t total = !v_ok ? 0u
+                                       : (j + 1 == nk) ? (uint32_t)__popc(zmask)
+                                                       : (uint32_t)__popc(zmask & ((1u << hl) - 1u));
+#pragma unroll
+                for (int o = 16; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
                 if (seg && j == 0) a.spcnt[b] = total;
             }
         }
