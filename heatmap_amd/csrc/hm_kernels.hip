@@ -2830,16 +2830,56 @@ __device__ __forceinline__ void hm_small_sort(const HmAggArgs& a, const uint16_t
 
 template <int K>
 __device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, uint32_t kb, uint64_t coord,
-                                              uint32_t zmask, uint64_t base)
+                                              uint32_t zmask, uint64_t base, uint32_t* hw)
 {
     const uint32_t lane = hm_lane();
     const int lg = a.lg;
     uint32_t v[K];
     hm_small_load<K>(a.codes + kb, nk, v);
+    /* the three coarsest levels (<= 64 cells each) from a 64-slot LDS
+     * histogram of the codes' top 6 bits, summed by quads: one LDS atomic per
+     * key and one store per level, not a pass over every key per level */
+    const int lc = lg >= 3 ? lg - 3 : 0;
+    if (zmask >> lc) {
+        hw[lane] = 0u;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int u = 0; u < K; u++)
+            if (lane * K + u < nk) atomicAdd(&hw[v[u] >> (2 * lc)], 1u);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t c = hw[lane];   /* prefix = lane (slots past 4^(lg - lc) stay 0) */
+        uint64_t q = base;
+        for (int l = lc; l < lg; l++) {
+            const int g = 2 * (l - lc);   /* this level's prefix: lane >> g on lanes with those bits clear */
+            if (l > lc) {
+                /* sum the 4 finer cells: lanes lane, +2^(g-2), +2·2^(g-2), +3·2^(g-2) */
+                const int st = 1 << (g - 2);
+                c += __shfl_down(c, st, 64);
+                c += __shfl_down(c, 2 * st, 64);
+            }
+            const bool mine = (lane & ((1u << g) - 1u)) == 0u && c != 0u && ((zmask >> l) & 1u);
+            const uint64_t bal = __ballot(mine);
+            if (mine) {
+                const uint32_t code = lane >> g;
+                const int sl = lg - l;
+                const uint32_t idx = (hm_compact7(code >> 1) << sl) | hm_compact7(code);
+                const uint64_t p = q + hm_mbcnt(bal);
+                if (p < a.out.capacity) {
+                    a.out.keys[p] = hm_cell_key(a.Z - l, coord, sl, idx);
+                    a.out.counts[p] = (uint64_t)c;
+                }
+            }
+            q += (uint64_t)__popcll(bal);
+        }
+        base = q;
+        __builtin_amdgcn_wave_barrier();   /* hw is free for the next bucket */
+    }
     /* the neighbours' codes are level-independent: read once per bucket */
     const uint32_t nx = __shfl_down(v[0], 1, 64);
     const uint32_t pv = __shfl_up(v[K - 1], 1, 64);
-    for (int l = 0; l < lg; l++) {
+    for (int l = 0; l < lc; l++) {
         if (!((zmask >> l) & 1u)) continue;
         bool end[K];
         hm_small_ends<K>(v, nk, l, end, nx);
@@ -3057,6 +3097,8 @@ __global__ void k_small_reserve(HmAggArgs a)
 template <uint32_t LO, uint32_t HI>
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
 {
+    __shared__ uint32_t hist[HM_SPW_THREADS / 64][64];
+    uint32_t* hw = hist[threadIdx.x >> 6];
     const uint32_t lane = hm_lane();
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
     const uint32_t zmask = hm_small_zmask(a);
@@ -3121,7 +3163,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
             m &= m - 1;
             const uint32_t nk = __shfl(nkl, i, 64), kb = __shfl(kbl, i, 64);
             const uint64_t coord = __shfl(cl, i, 64), q = base + __shfl(ol, i, 64);
-            hm_small_dispatch<LO, HI>(nk, [&](auto kc) { hm_small_emit<decltype(kc)::value>(a, nk, kb, coord, zmask, q); });
+            hm_small_dispatch<LO, HI>(nk, [&](auto kc) { hm_small_emit<decltype(kc)::value>(a, nk, kb, coord, zmask, q, hw); });
         }
     }
 }

@@ -53,7 +53,10 @@ class Context:
 
     def bind_stream(self):
         torch = _torch()
-        self.L.hm_ctx_set_stream(self.ptr, ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        h = torch.cuda.current_stream(self.device).cuda_stream
+        if h != getattr(self, "_bound", None):   # one C call per change of stream, not per call
+            self.L.hm_ctx_set_stream(self.ptr, ctypes.c_void_p(h))
+            self._bound = h
 
     def last_error(self):
         idx = ctypes.c_int64(-1)
