@@ -2836,12 +2836,19 @@ __device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, u
     const int lg = a.lg;
     uint32_t v[K];
     hm_small_load<K>(a.codes + kb, nk, v);
-    /* the three coarsest levels (<= 64 cells each) from a 64-slot LDS
-     * histogram of the codes' top 6 bits, summed by quads: one LDS atomic per
-     * key and one store per level, not a pass over every key per level */
-    const int lc = lg >= 3 ? lg - 3 : 0;
+    /* the four coarsest levels (<= 256 cells each) from a 256-slot LDS
+     * histogram of the codes' top 8 bits: one LDS atomic per key; the
+     * coarsest-but-three level has 4 slots per lane, the next ones are sums
+     * of 4 (in the lane, then across quads of lanes): one store per level and
+     * slot group instead of a pass over every key per level */
+    /* (buckets of <= 128 keys: the three coarsest levels, 64 slots -- the
+     * fourth costs them more as 256 slots than as a pass over their keys) */
+    constexpr int NC = K >= 4 ? 4 : 3;
+    const int lc = lg >= NC ? lg - NC : 0;
     if (zmask >> lc) {
-        hw[lane] = 0u;
+        uint4* hw4 = (uint4*)hw;
+        if (NC == 4) hw4[lane] = make_uint4(0u, 0u, 0u, 0u);
+        else hw[lane] = 0u;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -2849,20 +2856,9 @@ __device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, u
             if (lane * K + u < nk) atomicAdd(&hw[v[u] >> (2 * lc)], 1u);
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        uint32_t c = hw[lane];   /* prefix = lane (slots past 4^(lg - lc) stay 0) */
         uint64_t q = base;
-        for (int l = lc; l < lg; l++) {
-            const int g = 2 * (l - lc);   /* this level's prefix: lane >> g on lanes with those bits clear */
-            if (l > lc) {
-                /* sum the 4 finer cells: lanes lane, +2^(g-2), +2·2^(g-2), +3·2^(g-2) */
-                const int st = 1 << (g - 2);
-                c += __shfl_down(c, st, 64);
-                c += __shfl_down(c, 2 * st, 64);
-            }
-            const bool mine = (lane & ((1u << g) - 1u)) == 0u && c != 0u && ((zmask >> l) & 1u);
-            const uint64_t bal = __ballot(mine);
+        auto put = [&](bool mine, uint64_t bal, uint32_t code, int l, uint32_t c) {
             if (mine) {
-                const uint32_t code = lane >> g;
                 const int sl = lg - l;
                 const uint32_t idx = (hm_compact7(code >> 1) << sl) | hm_compact7(code);
                 const uint64_t p = q + hm_mbcnt(bal);
@@ -2872,6 +2868,34 @@ __device__ __forceinline__ void hm_small_emit(const HmAggArgs& a, uint32_t nk, u
                 }
             }
             q += (uint64_t)__popcll(bal);
+        };
+        uint32_t c;   /* the count of prefix = lane at level l1 */
+        int l1 = lc;
+        if constexpr (NC == 4) {
+            const uint4 c4 = hw4[lane];   /* prefixes 4 lane + j (slots past 4^(lg - lc) stay 0) */
+            if ((zmask >> lc) & 1u) {
+                const uint32_t cj[4] = {c4.x, c4.y, c4.z, c4.w};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const bool mine = cj[j] != 0u;
+                    put(mine, __ballot(mine), lane * 4u + (uint32_t)j, lc, cj[j]);
+                }
+            }
+            c = c4.x + c4.y + c4.z + c4.w;
+            l1 = lc + 1;
+        } else {
+            c = hw[lane];
+        }
+        for (int l = l1; l < lg; l++) {
+            const int g = 2 * (l - l1);   /* this level's prefix: lane >> g on lanes with those bits clear */
+            if (g) {
+                /* sum the 4 finer cells: lanes lane + {0, 1, 2, 3} 2^(g-2) */
+                const int st = 1 << (g - 2);
+                c += __shfl_down(c, st, 64);
+                c += __shfl_down(c, 2 * st, 64);
+            }
+            const bool mine = (lane & ((1u << g) - 1u)) == 0u && c != 0u && ((zmask >> l) & 1u);
+            put(mine, __ballot(mine), lane >> g, l, c);
         }
         base = q;
         __builtin_amdgcn_wave_barrier();   /* hw is free for the next bucket */
@@ -3097,7 +3121,7 @@ __global__ void k_small_reserve(HmAggArgs a)
 template <uint32_t LO, uint32_t HI>
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
 {
-    __shared__ uint32_t hist[HM_SPW_THREADS / 64][64];
+    __shared__ __attribute__((aligned(16))) uint32_t hist[HM_SPW_THREADS / 64][256];
     uint32_t* hw = hist[threadIdx.x >> 6];
     const uint32_t lane = hm_lane();
     const uint32_t nw = gridDim.x * (HM_SPW_THREADS / 64);
