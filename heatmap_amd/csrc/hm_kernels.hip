@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(256) void k_rs_count(HmRsArgs a)
  * spreads its slices over every wave of the grid. */
 #define HM_RS_SLICE 512
 #ifndef HM_RS_LANE_MAX
-#define HM_RS_LANE_MAX 16   /* one-shard children of at most this many runs: one lane each */
+#define HM_RS_LANE_MAX 256  /* one-shard children of at most this many runs: copied 64 children at a time */
 #endif
 
 struct HmRsChild {
@@ -2014,21 +2014,39 @@ __global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
             }
         }
         if (a.shard_bits == 0) {
-            /* one shard per child: its runs are one contiguous range, so a
-             * child of few runs is copied by its own lane (64 children in
-             * flight per wave, not one dependent chain after another) */
+            /* one shard per child: a child's runs are one contiguous source
+             * range and one contiguous flat range, so the wave copies the runs
+             * of all its (not big, not hot) children of <= HM_RS_LANE_MAX runs
+             * at once: element x of their concatenation finds its child by a
+             * search over the lanes' inclusive run counts (consecutive children
+             * have adjacent flat ranges: the stores coalesce) */
             const bool mine = ((m >> lane) & 1ull) && nrl <= HM_RS_LANE_MAX;
             m &= ~__ballot(mine);
+            uint32_t n = 0;
+            uint64_t src = 0;
             if (mine) {
-                const uint32_t n = a.nruns[cl];   /* 0: a hot tile (k_hot_runs lists its runs) */
+                n = a.nruns[cl];   /* 0: a hot tile (k_hot_runs lists its runs) */
                 const uint64_t p = cl >> a.dbits, d = cl & ((1ull << a.dbits) - 1);
                 const uint32_t t0 = a.parent_item_begin[p];
                 const uint32_t tp = a.parent_item_begin[p + 1] - t0;
-                const uint64_t src = hm_run_base(t0, tp, p, d, a.dbits, 0);
-                for (uint32_t j = 0; j < n; j++) {
-                    const uint2 r = a.runs[src + j];
-                    a.flat[rbl + j] = r;
-                    a.cnt[rbl + j] = r.y;
+                src = hm_run_base(t0, tp, p, d, a.dbits, 0);
+            }
+            const uint32_t incl = hm_wave_incl_scan(n);
+            const uint32_t tot = __shfl(incl, 63, 64);
+            for (uint32_t x0 = 0; x0 < tot; x0 += 64) {
+                const uint32_t x = x0 + lane;
+                const uint32_t xc = min(x, tot - 1u);
+                uint32_t l = 0;
+#pragma unroll
+                for (int st = 32; st > 0; st >>= 1)
+                    if (__shfl(incl, (int)(l + st - 1), 64) <= xc) l += st;
+                l = min(l, 63u);
+                const uint32_t j = xc - (__shfl(incl, (int)l, 64) - __shfl(n, (int)l, 64));
+                const uint64_t sj = __shfl(src, (int)l, 64) + j, dj = __shfl(rbl, (int)l, 64) + j;
+                if (x < tot) {
+                    const uint2 r = a.runs[sj];
+                    a.flat[dj] = r;
+                    a.cnt[dj] = r.y;
                 }
             }
         }
