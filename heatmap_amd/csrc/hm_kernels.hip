@@ -2301,31 +2301,43 @@ __global__ __launch_bounds__(1024) void k_scan_one(const uint64_t* v, uint32_t n
     if (tid == 0) *total = ws[16];
 }
 
-/* block b: its chunk in sub-chunks of HM_SCAN_ITEMS, carrying the prefix */
+/* block b: its chunk in sub-chunks of HM_SCAN_ITEMS, carrying the prefix.
+ * The sub-chunk passes through LDS both ways (padded one word per 16), so
+ * global loads and stores are lane-consecutive while each thread scans 16
+ * consecutive values */
+#define HM_SCAN_PAD(i) ((i) + ((i) >> 4))
 __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v, uint64_t n, uint64_t chunk,
                                                                const uint64_t* partial, uint64_t* out,
                                                                const uint64_t* ndev)
 {
     __shared__ uint64_t ws[HM_SCAN_THREADS / 64 + 1];
+    __shared__ uint64_t buf[HM_SCAN_PAD(HM_SCAN_ITEMS)];
     if (ndev) n = min(n, *ndev);
     constexpr int PER = HM_SCAN_ITEMS / HM_SCAN_THREADS;
+    const uint32_t tid = threadIdx.x;
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = min(c0 + chunk, n);
     uint64_t carry = partial[blockIdx.x];
     for (uint64_t s0 = c0; s0 < c1; s0 += HM_SCAN_ITEMS) {
-        const uint64_t b0 = s0 + (uint64_t)threadIdx.x * PER;
+        const uint64_t m = min<uint64_t>(c1 - s0, HM_SCAN_ITEMS);
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const uint32_t i = (uint32_t)q * HM_SCAN_THREADS + tid;
+            buf[HM_SCAN_PAD(i)] = i < m ? v[s0 + i] : 0ull;
+        }
+        __syncthreads();
         uint64_t x[PER];
         uint64_t s = 0;
 #pragma unroll
         for (int q = 0; q < PER; q++) {
-            x[q] = (b0 + q < c1) ? v[b0 + q] : 0;
+            x[q] = buf[HM_SCAN_PAD(tid * PER + q)];
             s += x[q];
         }
         const uint64_t inc = hm_wave_incl_scan64(s);
-        const int w = threadIdx.x >> 6;
+        const int w = tid >> 6;
         if (hm_lane() == 63) ws[w] = inc;
         __syncthreads();
-        if (threadIdx.x == 0) {
+        if (tid == 0) {
             uint64_t acc = 0;
             for (int k = 0; k < HM_SCAN_THREADS / 64; k++) {
                 const uint64_t t = ws[k];
@@ -2338,10 +2350,16 @@ __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v
         uint64_t off = carry + ws[w] + inc - s;
 #pragma unroll
         for (int q = 0; q < PER; q++) {
-            if (b0 + q < c1) out[b0 + q] = off;
+            buf[HM_SCAN_PAD(tid * PER + q)] = off;
             off += x[q];
         }
         carry += ws[HM_SCAN_THREADS / 64];
+        __syncthreads();
+#pragma unroll
+        for (int q = 0; q < PER; q++) {
+            const uint32_t i = (uint32_t)q * HM_SCAN_THREADS + tid;
+            if (i < m) out[s0 + i] = buf[HM_SCAN_PAD(i)];
+        }
         __syncthreads();
     }
 }
