@@ -1918,7 +1918,7 @@ __global__ __launch_bounds__(256) void k_rs_count(HmRsArgs a)
  * spreads its slices over every wave of the grid. */
 #define HM_RS_SLICE 512
 #ifndef HM_RS_LANE_MAX
-#define HM_RS_LANE_MAX 256  /* one-shard children of at most this many runs: copied 64 children at a time */
+#define HM_RS_LANE_MAX 256  /* children of at most this many runs: copied 64 / S at a time */
 #endif
 
 struct HmRsChild {
@@ -2013,40 +2013,56 @@ __global__ __launch_bounds__(256) void k_rs_copy(HmRsArgs a)
                 m |= 1ull << i;   /* list full: copied here */
             }
         }
-        if (a.shard_bits == 0) {
-            /* one shard per child: a child's runs are one contiguous source
-             * range and one contiguous flat range, so the wave copies the runs
-             * of all its (not big, not hot) children of <= HM_RS_LANE_MAX runs
-             * at once: element x of their concatenation finds its child by a
-             * search over the lanes' inclusive run counts (consecutive children
-             * have adjacent flat ranges: the stores coalesce) */
-            const bool mine = ((m >> lane) & 1ull) && nrl <= HM_RS_LANE_MAX;
-            m &= ~__ballot(mine);
-            uint32_t n = 0;
-            uint64_t src = 0;
-            if (mine) {
-                n = a.nruns[cl];   /* 0: a hot tile (k_hot_runs lists its runs) */
-                const uint64_t p = cl >> a.dbits, d = cl & ((1ull << a.dbits) - 1);
-                const uint32_t t0 = a.parent_item_begin[p];
-                const uint32_t tp = a.parent_item_begin[p + 1] - t0;
-                src = hm_run_base(t0, tp, p, d, a.dbits, 0);
-            }
-            const uint32_t incl = hm_wave_incl_scan(n);
-            const uint32_t tot = __shfl(incl, 63, 64);
-            for (uint32_t x0 = 0; x0 < tot; x0 += 64) {
-                const uint32_t x = x0 + lane;
-                const uint32_t xc = min(x, tot - 1u);
-                uint32_t l = 0;
+        {
+            /* children of <= HM_RS_LANE_MAX runs (not big, not hot) are copied
+             * 64 / S at a time, one (child, shard) per lane: a shard's runs
+             * are one contiguous source range, a child's one contiguous flat
+             * range, so element x of the group's concatenation finds its
+             * (child, shard) by a search over the lanes' inclusive run counts;
+             * consecutive children have adjacent flat ranges, so the stores
+             * coalesce (one child at a time left the wave waiting on each
+             * child's chain of dependent loads) */
+            const uint32_t S = 1u << a.shard_bits, G = 64u / S;   /* (shard_bits <= 6, as below) */
+            const bool mine_l = ((m >> lane) & 1ull) && nrl <= HM_RS_LANE_MAX && G > 0;
+            const uint64_t mineb = __ballot(mine_l);
+            m &= ~mineb;
+            const uint64_t gmask = G >= 64 ? ~0ull : ((1ull << G) - 1ull);
+            for (uint32_t g0 = 0; mineb && g0 < 64; g0 += G) {
+                if (!((mineb >> g0) & gmask)) continue;   /* wave-uniform */
+                const uint32_t ci = g0 + lane / S, sh = lane & (S - 1u);
+                const bool cm = (mineb >> ci) & 1ull;
+                const uint64_t rbc = __shfl(rbl, (int)ci, 64);
+                uint32_t n = 0;
+                uint64_t src = 0;
+                if (cm) {
+                    const uint64_t c = c0 + ci;
+                    n = a.nruns[(c << a.shard_bits) + sh];   /* 0 for a hot tile (k_hot_runs lists its runs) */
+                    const uint64_t p = c >> a.dbits, d = c & ((1ull << a.dbits) - 1);
+                    const uint32_t t0 = a.parent_item_begin[p];
+                    const uint32_t tp = a.parent_item_begin[p + 1] - t0;
+                    const uint64_t cap = ((uint64_t)tp + S - 1) >> a.shard_bits;
+                    src = hm_run_base(t0, tp, p, d, a.dbits, a.shard_bits) + (uint64_t)sh * cap;
+                }
+                const uint32_t incl = hm_wave_incl_scan(n);
+                const int fl = (int)(lane & ~(S - 1u));   /* the child's first lane */
+                const uint32_t cfirst = __shfl(incl, fl, 64) - __shfl(n, fl, 64);
+                const uint64_t dst = rbc + (incl - n - cfirst);
+                const uint32_t tot = __shfl(incl, 63, 64);
+                for (uint32_t x0 = 0; x0 < tot; x0 += 64) {
+                    const uint32_t x = x0 + lane;
+                    const uint32_t xc = min(x, tot - 1u);
+                    uint32_t l = 0;
 #pragma unroll
-                for (int st = 32; st > 0; st >>= 1)
-                    if (__shfl(incl, (int)(l + st - 1), 64) <= xc) l += st;
-                l = min(l, 63u);
-                const uint32_t j = xc - (__shfl(incl, (int)l, 64) - __shfl(n, (int)l, 64));
-                const uint64_t sj = __shfl(src, (int)l, 64) + j, dj = __shfl(rbl, (int)l, 64) + j;
-                if (x < tot) {
-                    const uint2 r = a.runs[sj];
-                    a.flat[dj] = r;
-                    a.cnt[dj] = r.y;
+                    for (int st = 32; st > 0; st >>= 1)
+                        if (__shfl(incl, (int)(l + st - 1), 64) <= xc) l += st;
+                    l = min(l, 63u);
+                    const uint32_t j = xc - (__shfl(incl, (int)l, 64) - __shfl(n, (int)l, 64));
+                    const uint64_t sj = __shfl(src, (int)l, 64) + j, dj = __shfl(dst, (int)l, 64) + j;
+                    if (x < tot) {
+                        const uint2 r = a.runs[sj];
+                        a.flat[dj] = r;
+                        a.cnt[dj] = r.y;
+                    }
                 }
             }
         }
