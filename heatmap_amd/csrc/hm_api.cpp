@@ -106,6 +106,8 @@ enum {
     ST_OVERFLOW = 8,
     ST_NHOT = 9,          /* hot tiles of this call (k_hot_select; low 32 bits) */
     ST_L1TOTAL = 10,      /* level-1 regions' total capacity (k_l1_sizes) */
+    ST_LTOT = 12,         /* 12..14: a partition level's run, key and bucket totals (its run scans),
+                           * read back with the state in one copy */
     ST_COUNT = 16
 };
 
@@ -1154,7 +1156,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ENSURE(B_RUNBASE0 + l, V.nchildren * sizeof(uint64_t), runbase);
         ra.runbase = runbase;
         ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
-        ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+        tot = (uint64_t*)(ctx->state + ST_LTOT);
         hm_launch_rs_count(s, ra);
         /* hot tiles are children of the last level: of their z5 bucket at
          * level 2, of their zs[1] ancestor (kept as a bucket, below) at level 3 */
@@ -1262,10 +1264,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         }
         hm_launch_compact(s, ca);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(down, tot, 3 * sizeof(uint64_t), hipMemcpyDeviceToHost, s));
-        if ((st = read_state(ctx))) return st;
-        level_keys = down[1];
-        const uint64_t tot_h = down[2];
+        if ((st = read_state(ctx))) return st;   /* the level's totals come with it (ST_LTOT) */
+        level_keys = ctx->host_state[ST_LTOT + 1];
+        const uint64_t tot_h = ctx->host_state[ST_LTOT + 2];
         V.count = (uint32_t)(tot_h >> 32);
         V.items = (uint32_t)(tot_h & 0xFFFFFFFFull);
         if (l == L - 1) nslots = (uint32_t)(ctx->host_state[ST_NSLOTS] & 0xFFFFFFFFull);
