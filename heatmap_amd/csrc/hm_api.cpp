@@ -857,8 +857,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             ENSURE(B_FLAT_A, (uint64_t)FS * sizeof(uint2) + 8, ba.runs);
             ENSURE(B_EXCL_A, (uint64_t)FS * sizeof(uint64_t) + 8, ba.excl);
             ENSURE(B_CHILD0, 2 * 4, ba.child_begin);
-            uint64_t* tot;
-            ENSURE(B_TOTAL, 4 * sizeof(uint64_t), tot);
+            uint64_t* tot = (uint64_t*)(ctx->state + ST_LTOT);   /* comes back with the state */
             ba.F = F;
             ba.dbits = V.dbits;
             ba.fill = fill;
@@ -959,7 +958,6 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 auto buckets1 = [&]() -> int {
                     hm_launch_level1_buckets(s, ba);
                     HIPCHK(hipGetLastError());
-                    HIPCHK(hipMemcpyAsync(down, tot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
                     if (L > 1) HIPCHK(hipMemcpyAsync(ctx->host_aux, hist, F * 4, hipMemcpyDeviceToHost, s));
                     return read_state(ctx);
                 };
@@ -1028,8 +1026,8 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             }
             spread = L > 2 && zs[1] - zs[0] < HM_LEVEL_ZOOMS;
             ctx->last_levels = L;
-            V.count = (uint32_t)(down[0] >> 32);
-            V.items = (uint32_t)(down[0] & 0xFFFFFFFFull);
+            V.count = (uint32_t)(ctx->host_state[ST_LTOT] >> 32);
+            V.items = (uint32_t)(ctx->host_state[ST_LTOT] & 0xFFFFFFFFull);
             if (L == 1) nslots = (uint32_t)(ctx->host_state[ST_NSLOTS] & 0xFFFFFFFFull);
             level_keys = total_cap;
             HmBuckets& b = B[0];
