@@ -27,11 +27,11 @@ HM_E_NOMEM = 19
 HM_E_WIDE = 20        # hm_cells_route with u32 counts: a count needs 64 bits
 HM_CELLS_U64, HM_CELLS_U32, HM_CELLS_REC10 = 8, 4, 10   # exchanged cell layouts
 HM_COUNT_MAX_ZOOM = 21
-HM_ABI_VERSION = 5
+HM_ABI_VERSION = 6
 HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy", "hm_ctx_tune",
-           "hm_project", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
+           "hm_project", "hm_project_scalar", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
            "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_cells_merge_runs",
@@ -87,6 +87,8 @@ def load() -> ctypes.CDLL:
         L.hm_ctx_destroy.argtypes = [vp]
         L.hm_ctx_tune.argtypes = [vp, c.c_char_p, c.c_double, P(c.c_double)]
         L.hm_project.argtypes = [vp, vp, vp, c.c_int64, c.c_int, vp, vp, vp]
+        L.hm_project_scalar.argtypes = [c.c_double, c.c_double, c.c_int, vp]
+        L.hm_project_scalar.restype = c.c_int
         L.hm_count.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64),
                                vp, c.c_int64, P(c.c_int64)]
         L.hm_count_tiles.argtypes = [vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64, P(c.c_int64),

@@ -18,7 +18,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
 LIBDIR = os.path.join(HERE, "_lib")
 LIB = os.path.join(LIBDIR, "libheatmap_amd.so")
-SOURCES = ["hm_kernels.hip", "hm_general.hip", "hm_stream.hip", "hm_merge.hip", "hm_api.cpp"]
+SOURCES = ["hm_kernels.hip", "hm_general.hip", "hm_stream.hip", "hm_merge.hip", "hm_api.cpp", "hm_host.c"]
 HEADERS = ["hm_common.h", "hm_device.h", "hm_glibc_emul.h", "hm_branred.h", "hm_project.h", "hm_pipeline.h",
            "hm_ytab.h", "hm_table.h"]
 ARCH = os.environ.get("HM_OFFLOAD_ARCH", "gfx950")
@@ -26,9 +26,14 @@ FLAGS = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "--offload-arch=" + 
          "-Wall", "-Wno-unused-function", "-Wno-unused-variable", "-Wno-unknown-pragmas",
          "-Wno-unused-label"]
 
+HOST_FLAGS = ["-O2", "-fPIC", "-ffp-contract=off", "-std=c11", "-Wall", "-Wno-unused-function", "-Wno-unused-variable",
+              "-Wno-unknown-pragmas"]
+
 
 def _stale() -> bool:
-    if not os.path.exists(LIB):
+    if not os.path.exists(LIB) or not os.path.exists(scalar_module_path()):
+        return True
+    if os.path.getmtime(os.path.join(CSRC, SCALAR_SRC)) > os.path.getmtime(scalar_module_path()):
         return True
     t = os.path.getmtime(LIB)
     deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS]
@@ -48,7 +53,10 @@ def build(force: bool = False, verbose: bool = True, out: str = None, defines=()
     objs, procs = [], []
     for src in SOURCES:   # the translation units compile in parallel
         obj = os.path.join(os.path.dirname(lib), os.path.basename(lib) + "." + src.rsplit(".", 1)[0] + ".o")
-        cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(src_dir, src), "-o", obj]
+        if src.endswith(".c"):   # host C (hm_project_scalar): gcc, contraction off as everywhere
+            cmd = [os.environ.get("CC", "gcc"), *HOST_FLAGS, "-c", os.path.join(src_dir, src), "-o", obj]
+        else:
+            cmd = [hipcc, *FLAGS, *["-D" + d for d in defines], "-c", os.path.join(src_dir, src), "-o", obj]
         if verbose:
             print(" ".join(cmd), flush=True)
         procs.append((subprocess.Popen(cmd), cmd))
@@ -61,7 +69,34 @@ def build(force: bool = False, verbose: bool = True, out: str = None, defines=()
         print(" ".join(cmd), flush=True)
     subprocess.check_call(cmd)
     os.replace(lib + ".tmp", lib)
+    if out is None:
+        build_scalar(verbose)
     return lib
+
+
+SCALAR_SRC = "hm_pyscalar.c"
+
+
+def scalar_module_path() -> str:
+    import sysconfig
+
+    return os.path.join(HERE, "_hm_scalar" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_scalar(verbose: bool = True) -> str:
+    """The CPython binding of hm_project_scalar (per-record Tile calls), linked
+    against the library next to it (rpath $ORIGIN/_lib)."""
+    import sysconfig
+
+    out = scalar_module_path()
+    cmd = [os.environ.get("CC", "gcc"), "-O2", "-fPIC", "-shared", "-Wall", "-I" + sysconfig.get_paths()["include"],
+           os.path.join(CSRC, SCALAR_SRC), "-L" + LIBDIR, "-lheatmap_amd", "-Wl,-rpath,$ORIGIN/_lib",
+           "-o", out + ".tmp"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    subprocess.check_call(cmd)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":

@@ -342,6 +342,25 @@ int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
     return HM_OK;
 }
 
+/* the plan-tuning fields of one context copied to another (a stream's helper
+ * contexts count with the settings of the stream's own) */
+static void ctx_copy_tuning(hm_ctx* d, const hm_ctx* c)
+{
+    d->spread_min_keys = c->spread_min_keys;
+    d->spread_min_cold = c->spread_min_cold;
+    d->sample_log2 = c->sample_log2;
+    d->debug_l1 = c->debug_l1;
+    d->stage_timing = c->stage_timing;
+    d->contig = c->contig;
+    d->ta_min = c->ta_min;
+    d->ta_items = c->ta_items;
+    d->rs_big_min = c->rs_big_min;
+    d->hot = c->hot;
+    d->hot_inv_share = c->hot_inv_share;
+    d->hot_min_keys = c->hot_min_keys;
+    d->run_shard_bits = c->run_shard_bits;
+}
+
 int hm_ctx_destroy(hm_ctx* c)
 {
     if (!c) return HM_OK;
@@ -634,6 +653,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         return HM_E_ARG;
     *n_out = 0;
     *nx_out = 0;
+    /* set again only when THIS attempt re-keys a stream's tail (an attempt
+     * that fails after it, then count_fallback, leaves the keys un-keyed) */
+    ctx->tail_done = 0;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
     const int Z = zmax;
@@ -2052,6 +2074,7 @@ static int stream_fold_parts_par(hm_stream* s, const double* lat, const double* 
             return st;
         }
     }
+    for (int t = 0; t < HMS_PAR; t++) ctx_copy_tuning(s->pctx[t], ctx);   /* hm_ctx_tune of the stream's context */
     if (!s->pev) HIPCHK(hipEventCreateWithFlags(&s->pev, hipEventDisableTiming));
     HIPCHK(hipEventRecord(s->pev, q));   /* the gathered runs are written */
     const uint32_t nall = nparts + 1;    /* + the points not kept (errors only) */

@@ -1,11 +1,14 @@
 """Drop-in for reference tile.py's Tile (projection on the gfx950 device).
 
 Same class and classmethod names, argument meaning and exceptions as
-reference tile.py:3-98.  Projection (row_from_latitude, column_from_longitude,
-tile_id_from_lat_long) runs in the HIP kernel behind hm_project -- bit-exact
-with the reference's glibc arithmetic -- so every call needs the GPU; the
-vectorised forms (rows_from_latitudes, ...) are what callers should use in
-bulk.  Pure string helpers (ids) are plain Python, as in the reference.
+reference tile.py:3-98.  The vectorised projections (rows_from_latitudes,
+columns_from_longitudes, tile_ids_from_lat_longs) run in the HIP kernel behind
+hm_project; the scalar ones (row_from_latitude, column_from_longitude,
+tile_id_from_lat_long), which the reference calls once per record, run the
+same arithmetic (csrc/hm_project.h) compiled for the host behind
+hm_project_scalar, ~1 us a call instead of a launch and a synchronisation.
+Both are bit-exact with the reference's glibc arithmetic.  Pure string
+helpers (ids) are plain Python, as in the reference.
 
 Tile utility API: tile_from_tile_id, parent_id,
 parent, children and tile_ids_for_all_zoom_levels (tile.py:33-98).  Their
@@ -21,15 +24,45 @@ domain, which is what the device uses.
 from __future__ import annotations
 
 import math
+import struct
 
 import numpy as np
 
 from . import _lib, device
 
 
-def _scalar_project(lat, lon, zoom):
-    p = device.project(np.array([float(lat)]), np.array([float(lon)]), int(zoom))
-    return p
+_S = None
+
+
+def _scalar_mod():
+    global _S
+    if _S is None:
+        _lib.load()   # the library (ABI check) that the binding calls into
+        try:
+            from . import _hm_scalar
+        except ImportError as e:   # built by heatmap_amd/build.py with the library
+            raise _lib.DeviceUnavailable("heatmap_amd: the per-record binding _hm_scalar is not built "
+                                         "(python -m heatmap_amd.build): %s" % e) from None
+        _S = _hm_scalar
+    return _S
+
+
+def _bigcol(c):
+    """HM_BIGCOL: the column as an integer-valued double's bits -> the
+    reference's unbounded Python int (tile.py:21)."""
+    return int(struct.unpack("<d", struct.pack("<q", c))[0])
+
+
+def _scalar(lat, lon, zoom):
+    """(status, row, col) of one point by hm_project_scalar: the kernels'
+    arithmetic (csrc/hm_project.h) compiled for the host, so per-record
+    callers pay well under a microsecond, not a launch and a synchronisation."""
+    st, r, c = (_S or _scalar_mod()).project(lat, lon, zoom)
+    if st == _lib.HM_BIGCOL:
+        return _lib.HM_OK, r, _bigcol(c)
+    if st == _lib.HM_E_ARG:
+        raise ValueError("zoom %r outside -30..30" % (zoom,))
+    return st, r, c
 
 
 def _cols(p):
@@ -58,29 +91,31 @@ class Tile:
     @classmethod
     def tile_id_from_lat_long(cls, latitude, longitude, zoom):
         """tile.py:9-13: "z_row_col"; row is evaluated (and raises) first."""
-        p = _scalar_project(latitude, longitude, zoom)
-        st = _status(p)
-        if st != _lib.HM_OK:
-            _lib.raise_for(st)
-        return Tile.tile_id_from_row_column(int(p.row[0]), int(_cols(p)[0]), zoom)
+        st, tid = (_S or _scalar_mod()).tile_id(latitude, longitude, zoom)
+        if st == _lib.HM_OK:
+            return tid
+        if st == _lib.HM_BIGCOL:
+            st, r, c = _scalar(latitude, longitude, zoom)
+            return str(zoom) + "_" + str(r) + "_" + str(c)
+        if st == _lib.HM_E_ARG:
+            raise ValueError("zoom %r outside -30..30" % (zoom,))
+        _lib.raise_for(st)
 
     @classmethod
     def row_from_latitude(cls, latitude, zoom):
         """tile.py:15-17."""
-        p = _scalar_project(latitude, 0.0, zoom)
-        st = int(p.status[0])
-        if st != _lib.HM_OK:
+        st, r, _ = _scalar(latitude, 0.0, zoom)
+        if st:
             _lib.raise_for(st)
-        return int(p.row[0])
+        return r
 
     @classmethod
     def column_from_longitude(cls, longitude, zoom):
         """tile.py:19-21."""
-        p = _scalar_project(0.0, longitude, zoom)
-        st = _status(p)
-        if st != _lib.HM_OK:
+        st, _, c = _scalar(0.0, longitude, zoom)
+        if st:
             _lib.raise_for(st)
-        return int(_cols(p)[0])
+        return c
 
     # vectorised forms: one device call for many points
     @classmethod

@@ -39,7 +39,9 @@
  *     reports its index.
  *   - Thread-compatible: one context per host thread / stream.
  *   - Every call fails loudly (HM_E_HIP) when no gfx950 device is present;
- *     there is no CPU fallback in this library.
+ *     there is no CPU fallback in this library.  (hm_project_scalar is the
+ *     per-record host form of hm_project, not a fallback: it is what a
+ *     one-point call always uses.)
  */
 #ifndef HEATMAP_AMD_H
 #define HEATMAP_AMD_H
@@ -50,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 5
+#define HM_ABI_VERSION 6
 
 /* status / per-point error kinds */
 #define HM_OK 0
@@ -131,6 +133,17 @@ int hm_ctx_tune(hm_ctx* ctx, const char* name, double value, double* old);
  * Replaces Tile.row_from_latitude / column_from_longitude (tile.py:15-21). */
 int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int64_t n, int zoom,
                int64_t* row, int64_t* col, uint8_t* status);
+
+/* One point, on the host: hm_project's arithmetic (csrc/hm_project.h, the
+ * statements the kernels run) compiled for the CPU, for per-record callers
+ * -- the reference's scalar Tile.row_from_latitude / column_from_longitude /
+ * tile_id_from_lat_long (tile.py:9-21, one call per record at
+ * heatmap.py:27) -- for which a launch and a synchronisation would cost
+ * ~100x the reference's ~0.3 us.  row_col: int64[2] (host), row then column
+ * (HM_BIGCOL: the column as an integer-valued double's bits).  Returns the
+ * point's status exactly as hm_project's status[0]; HM_E_ARG for zoom outside
+ * -30..30.  The only host computation in the library; needs no context. */
+int hm_project_scalar(double lat, double lon, int zoom, int64_t* row_col);
 
 /* Count points per (zoom, row, col) for every zoom in [zmin, zmax].
  * keep: uint8[n] or NULL (NULL = keep all); every point is projected (and

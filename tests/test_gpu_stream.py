@@ -270,3 +270,26 @@ def test_stream_exotic_points(gpu):
         _same(s.counts(h), oracle.count(lat, lon, sel.astype(np.uint8), 0, mz + d))
     assert s.rows("alltime") == _reference_rows(lat, lon, keep, users, mz, d)
     s.close()
+
+
+@pytest.mark.parametrize("knobs", [dict(HM_HOT_MIN_KEYS=0, HM_HOT_INV_SHARE=64),
+                                   dict(HM_HOT=0, HM_SPREAD_MIN_KEYS=0, HM_SAMPLE_LOG2=10)])
+def test_stream_forced_plan_on_concurrent_buckets(gpu, knobs):
+    """A 2-3-bucket batch is counted concurrently on helper contexts
+    (stream_fold_parts_par); plan knobs set on the stream's context
+    (device.tuned) reach them, and the forced plans still give the oracle's
+    counts for every hour."""
+    from heatmap_amd import device
+
+    n = 200_000
+    lat, lon = synth.generate("skew", n, seed=11)
+    rng = np.random.default_rng(11)
+    keep = (rng.random(n) > 0.05).astype(np.uint8)
+    with device.tuned(**knobs):
+        s = StreamingHeatmap(0, 18, base_hour=BASE)
+        for nh in (2, 3):
+            hour = (BASE + 4 * nh + rng.integers(0, nh, n)).astype(np.uint32)
+            s.add(lat, lon, keep, hour)
+            for h in range(BASE + 4 * nh, BASE + 5 * nh):
+                _same(s.counts(h), oracle.count(lat, lon, keep & (hour == h).astype(np.uint8), 0, 18))
+        s.close()
