@@ -31,7 +31,8 @@ HM_ABI_VERSION = 6
 HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy", "hm_ctx_tune",
-           "hm_project", "hm_project_scalar", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
+           "hm_project", "hm_project_scalar", "hm_count", "hm_count_tiles", "hm_count_grouped", "hm_count_grouped_tiles",
+           "hm_count_grouped_packed", "hm_count_grouped_packed_tiles", "hm_last_error", "hm_last_stats", "hm_synth",
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
            "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_cells_merge_runs",
@@ -96,6 +97,9 @@ def load() -> ctypes.CDLL:
         L.hm_count_grouped.argtypes = [vp, vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, c.c_int64,
                                        P(c.c_int64)]
         L.hm_count_grouped_tiles.argtypes = L.hm_count_grouped.argtypes
+        L.hm_count_grouped_packed.argtypes = [vp, vp, vp, vp, vp, c.c_int64, c.c_int, c.c_int, vp, vp, c.c_int64,
+                                              P(c.c_int64)]
+        L.hm_count_grouped_packed_tiles.argtypes = L.hm_count_grouped_packed.argtypes
         L.hm_last_error.argtypes = [vp, P(c.c_int64), P(c.c_int)]
         L.hm_last_stats.argtypes = [vp, P(c.c_int64), P(c.c_double), c.c_int]
         L.hm_synth.argtypes = [vp, c.c_int, c.c_uint64, c.c_int64, c.c_int64, vp, vp, vp, c.c_int]

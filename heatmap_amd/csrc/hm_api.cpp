@@ -23,6 +23,7 @@
 #include <vector>
 
 #include "../../include/heatmap_amd.h"
+#include "hm_genkey.h"
 #include "hm_pipeline.h"
 
 namespace {
@@ -89,6 +90,7 @@ struct hm_ctx {
     /* hot tiles (hm_pipeline.h): HM_HOT=0 turns them off; a tile is hot with
      * >= 1/hot_inv_share of the sampled points and >= hot_min_keys estimated */
     int hot = 1;
+    int hot_mid = 1;               /* HM_HOT_MID=0: no hot tiles in 3-level plans (zmax 19-21) */
     double hot_inv_share = 4096;   /* 2048 -> 4096: 291 -> 470 hot tiles on the bench cloud, -0.13 ms */
     double hot_min_keys = 65536;
     int run_shard_bits = -1;   /* HM_RUN_SHARD_BITS: level >= 2 run-counter shards (-1: by plan) */
@@ -257,6 +259,7 @@ int hm_ctx_create(hm_ctx** out, int device, void* stream)
     c->rs_big_min = HM_RS_BIG;
     if (const char* e = getenv("HM_RS_BIG_MIN")) c->rs_big_min = (uint64_t)atoll(e);
     if (const char* e = getenv("HM_HOT")) c->hot = atoi(e);
+    if (const char* e = getenv("HM_HOT_MID")) c->hot_mid = atoi(e);
     if (const char* e = getenv("HM_HOT_INV_SHARE")) c->hot_inv_share = atof(e);
     if (const char* e = getenv("HM_HOT_MIN_KEYS")) c->hot_min_keys = atof(e);
     if (const char* e = getenv("HM_RUN_SHARD_BITS")) c->run_shard_bits = atoi(e);
@@ -324,6 +327,9 @@ int hm_ctx_tune(hm_ctx* c, const char* name, double value, double* old)
     } else if (!strcmp(name, "HM_HOT")) {
         prev = c->hot;
         c->hot = value != 0;
+    } else if (!strcmp(name, "HM_HOT_MID")) {
+        prev = c->hot_mid;
+        c->hot_mid = value != 0;
     } else if (!strcmp(name, "HM_HOT_INV_SHARE")) {
         if (!(value >= 1)) return HM_E_ARG;
         prev = c->hot_inv_share;
@@ -356,6 +362,7 @@ static void ctx_copy_tuning(hm_ctx* d, const hm_ctx* c)
     d->ta_items = c->ta_items;
     d->rs_big_min = c->rs_big_min;
     d->hot = c->hot;
+    d->hot_mid = c->hot_mid;
     d->hot_inv_share = c->hot_inv_share;
     d->hot_min_keys = c->hot_min_keys;
     d->run_shard_bits = c->run_shard_bits;
@@ -505,6 +512,17 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     const bool wide = down[1] != down[3];
     const unsigned __int128 var = ((((unsigned __int128)down[1]) << 64) | down[0]) ^
                                   ((((unsigned __int128)down[3]) << 64) | down[2]);
+    if (e.width == 2) {
+        /* packed records hold HM_KEYs: every key's super tile (its zoom-0
+         * tile) must be (0, 0), i.e. the same super-tile field in all keys
+         * (OR == AND there) and that field the encoding of (0, 0) */
+        const int f0 = 2 * Z + 32;
+        const unsigned __int128 fm = (((unsigned __int128)1 << (5 + HM_GEN_SC_BITS)) - 1) << f0;
+        const unsigned __int128 orv = (((unsigned __int128)down[1]) << 64) | down[0];
+        const unsigned __int128 zero = ((unsigned __int128)((uint64_t)HM_GEN_SR_BIAS << HM_GEN_SC_BITS |
+                                                           (uint64_t)HM_GEN_SC_BIAS)) << f0;
+        if ((var & fm) != 0 || (orv & fm) != zero) return HM_E_EXOTIC;
+    }
     int shs[16], np = 0;
     for (int sh = 0; sh < 128; sh += 8)
         if ((uint64_t)((var >> sh) & 0xFF)) shs[np++] = sh;
@@ -729,8 +747,11 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
     uint32_t* seg1 = nullptr;   /* level-1 items' run tables (k_partition_fr) */
     uint32_t* seg2 = nullptr;   /* level-2 items' run tables after a child-contiguous level */
     bool hot_on = false;        /* hot tiles sampled and looked up by level 1 */
+    bool hot_mid = false;       /* ... at zs[1] of a 3-level plan (they skip level 2 only) */
+    int hz = zb;                /* zoom of the hot tiles: the bucket zoom of level 2 */
     bool spread = false;        /* levels 2.. take fewer zooms (spread_replan) */
     uint32_t nhot = 0;          /* hot tiles found */
+    uint64_t l2_elems = 0;      /* mid-level hot tiles: level 2's key array (elements) */
     int l1_reruns = 0;          /* level-1 re-runs after a region overflow */
     HmHotRunArgs hr;            /* hot tiles as level-2 children */
     memset(&hr, 0, sizeof(hr));
@@ -755,9 +776,15 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             ENSURE(B_L1_RCAP, FS * 4, rcap);
             ENSURE(B_L1_HIST, HM_D1 * 4, hist);
             ENSURE(B_L1_SMASK, HM_D1, smask);
-            /* hot tiles need the two-level plan (level 1 at z1, the last at
-             * zb), a dense zoom-zb sample histogram of <= 4^11 tiles */
-            hot_on = ctx->hot && L == 2 && zb <= 11 && zs[0] == HM_Z1 && n > 0 && V.dbits == 2 * HM_Z1;
+            /* hot tiles are level-2 buckets: zoom zs[1], a dense sample
+             * histogram of <= 4^11 tiles.  In the two-level plan (level 1 at
+             * z1, the last at zb) they skip every partition after level 1; in
+             * a three-level plan (zmax 19-21: z5 -> z11 -> zb) they skip level 2
+             * and join level 3 with the level-2 buckets (HM_HOT_MID) */
+            hot_mid = ctx->hot && ctx->hot_mid && L == 3 && zs[1] <= 11 && zs[0] == HM_Z1 && n > 0 &&
+                      V.dbits == 2 * HM_Z1;
+            hot_on = hot_mid || (ctx->hot && L == 2 && zb <= 11 && zs[0] == HM_Z1 && n > 0 && V.dbits == 2 * HM_Z1);
+            hz = hot_mid ? zs[1] : zb;
             uint32_t* redo_idx = nullptr;
             int64_t *redo_rows = nullptr, *redo_cols = nullptr;
             if (!from_tiles) {
@@ -802,14 +829,15 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             uint8_t* hot_parent = nullptr;
             uint32_t* hot_n = (uint32_t*)(ctx->state + ST_NHOT);
             if (hot_on) {
-                ENSURE(B_HOT_COUNTS, (4ull << (2 * zb)), hot_counts);
+                ENSURE(B_HOT_COUNTS, (4ull << (2 * hz)), hot_counts);
                 ENSURE(B_HOT, (HM_MAX_HOT + HM_HOT_SLOTS + 2 * HM_HOT_CAND + 1) * 4, hot_tiles);
                 ENSURE(B_HOT_PARENT, HM_MAX_F1, hot_parent);
                 hot_hash = hot_tiles + HM_MAX_HOT;
-                hm_fill_add(f1, hot_counts, 0, 4ull << (2 * zb));
+                hm_fill_add(f1, hot_counts, 0, 4ull << (2 * hz));
                 hm_fill_add(f1, hot_hash + HM_HOT_SLOTS + 2 * HM_HOT_CAND, 0, 4);   /* candidates */
                 hm_fill_add(f1, hot_parent, 0, HM_MAX_F1);
-                a.hot_z = zb;
+                a.hot_z = hz;
+                a.hot_bytes = hot_mid ? 4 : 2;
                 a.hot_hash = hot_hash;
                 a.hot_n = hot_n;
             } else {
@@ -822,13 +850,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
             if (hot_on) {
                 hr.tiles = hot_tiles;
                 hr.n = hot_n;
-                hr.zb = zb;
+                hr.zb = hz;
                 hr.z1 = zs[0];
                 hr.fill = fill;
                 hr.rbase = rbase;
                 HmHotArgs ha;
                 ha.counts = hot_counts;
-                ha.zb = zb;
+                ha.zb = hz;
                 ha.z1 = zs[0];
                 const uint64_t m = ((uint64_t)n + stride - 1) / stride;
                 ha.thresh = (uint32_t)std::max<double>(
@@ -922,10 +950,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 ENSURE(slot_k ? B_KEYS_B : B_KEYS_A, (total_cap + 8) * (V.out16 ? 2 : 4), kout);
                 a.keys_out = kout;
                 if (hot_on) {
-                    /* hot keys: u16, straight into the last level's key array
-                     * (level 2 writes the cold keys' positions of it) */
+                    /* hot keys: straight into level 2's output key array (level 2
+                     * writes the cold keys' positions of it): u16 when that is the
+                     * last level's, u32 for mid-level hot tiles -- whose array
+                     * also holds the child-contiguous cold keys above every
+                     * level-1 position (l2_elems) */
                     void* kh = nullptr;
-                    ENSURE(slot_k ? B_KEYS_A : B_KEYS_B, (total_cap + 8) * 2, kh);
+                    if (hot_mid) l2_elems = total_cap + (uint64_t)n + 16;
+                    ENSURE(slot_k ? B_KEYS_A : B_KEYS_B, hot_mid ? l2_elems * 4 : (total_cap + 8) * 2, kh);
                     a.keys_hot = kh;
                 }
                 if (attempt > 0) {
@@ -1032,9 +1064,12 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 if (nx > xl.cap) return HM_E_HIP;   /* cannot happen: the same points */
             }
             nhot = hot_on ? (uint32_t)(ctx->host_state[ST_NHOT] & 0xFFFFFFFFull) : 0u;
+            if (!nhot) hot_mid = false;
             /* levels 2.. may take the spread plan (the level-1 pass is the
              * same under both: its output is u32 keys whenever L > 1) */
-            if (L > 1 && !nhot) {
+            if (hot_mid) {
+                /* the plan stays z5 -> z11 -> zb: the hot tiles are zoom-11 buckets */
+            } else if (L > 1 && !nhot) {
                 spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, true);
             } else if (L > 1) {
                 /* with hot tiles the rest is the cloud's sparse background: 3
@@ -1091,7 +1126,13 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
          * 3-level plan without hot tiles (Z >= 19) writes each child's keys
          * as ONE run, so the last level reads every item from <= 8 runs
          * (k_partition_fr) instead of streaming runs of a few keys each */
-        const bool contig = ctx->contig && l == 1 && L == 3 && !nhot && !V.out16 && seg1 != nullptr;
+        /* (with mid-level hot tiles the cold keys go above every level-1
+         * position, where the hot tiles' keys are: cbase_off) */
+        /* level 1's positions end at its regions' total capacity (k_l1_sizes),
+         * or, after an overflow re-run, at the exact sizes' total (level_keys) */
+        const uint64_t l1_total = l1_reruns ? level_keys : ctx->host_state[ST_L1TOTAL];
+        const bool contig = ctx->contig && l == 1 && L == 3 && (!nhot || hot_mid) && !V.out16 && seg1 != nullptr &&
+                            (!hot_mid || l1_total + (uint64_t)n < 0xFFF00000ull);
         int sb = ctx->run_shard_bits >= 0 ? ctx->run_shard_bits : ((nhot || spread) ? 0 : HM_RUN_SHARD_BITS);
         if (contig) sb = 0;
         while (sb > 0 && (V.nchildren << sb) > (1ull << 25)) sb--;
@@ -1106,9 +1147,9 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         const uint64_t nkeys_out = level_keys;
         /* with hot tiles the last level's keys go where level 1 put the hot
          * tiles' (B); a 3-level plan's middle level then takes a third array */
-        const bool hot3 = nhot && L == 3;
+        const bool hot3 = nhot && L == 3 && !hot_mid;
         const int kslot = hot3 ? (l == 1 ? B_KEYS_C : B_KEYS_B) : (slot_k ? B_KEYS_B : B_KEYS_A);
-        ENSURE(kslot, (nkeys_out + 8) * (V.out16 ? 2 : 4), kout);
+        ENSURE(kslot, std::max<uint64_t>(nkeys_out + 8, (hot_mid && l == 1) ? l2_elems : 0) * (V.out16 ? 2 : 4), kout);
         ENSURE(B_RUNS_SH, run_cap * sizeof(uint2), runs_sh);
         ENSURE(B_NRUNS, (V.nchildren << sb) * sizeof(uint32_t), nruns);
         uint32_t* rs_big;
@@ -1148,6 +1189,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
                 HIPCHK(hipMemsetAsync(a.ctot, 0, V.nchildren * 8, s));
                 HIPCHK(hipMemsetAsync(a.ccur, 0, V.nchildren * 4, s));
                 a.mode = HM_PN_HIST;
+                a.cbase_off = hot_mid ? (uint32_t)l1_total : 0u;
                 hm_launch_partition_hist(s, a);
                 hm_launch_scan(s, (const uint64_t*)a.ctot, V.nchildren, ptl, (uint64_t*)a.cbase, ttl + 3);
                 a.mode = HM_PN_CONTIG;
@@ -1180,18 +1222,18 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         hm_launch_rs_count(s, ra);
         /* hot tiles are children of the last level: of their z5 bucket at
          * level 2, of their zs[1] ancestor (kept as a bucket, below) at level 3 */
-        const bool hot_level = nhot && l == L - 1;
+        const bool hot_level = nhot && l == (hot_mid ? 1 : L - 1);
         if (hot_level) {
             hr.dbits = V.dbits;
             hr.nr = ra.nr;
             hr.zp = zs[l - 1];
-            hr.c2b = (l == 2) ? (const uint32_t*)ctx->bufs[B_C2B].p : nullptr;
+            hr.c2b = (l == 2 && hot3) ? (const uint32_t*)ctx->bufs[B_C2B].p : nullptr;
             hm_launch_hot_nr(s, hr);
         }
         /* a 3-level plan with hot tiles: each hot tile's zs[1] ancestor must be
          * a level-2 bucket (its parent at level 3) even without cold keys */
         uint8_t* force = nullptr;
-        if (nhot && L == 3 && l == 1) {
+        if (hot3 && l == 1) {
             ENSURE(B_HOT_FORCE, V.nchildren, force);
             HIPCHK(hipMemsetAsync(force, 0, V.nchildren, s));
             hr.dbits = V.dbits;
@@ -1274,7 +1316,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         ca.keybase = ckeybase;
         ca.parent_coord = parent_coord;
         ca.child_begin = child_begin;
-        if (nhot && L == 3 && l == 1) ENSURE(B_C2B, V.nchildren * 4, ca.c2b);   /* child -> bucket, for level 3 */
+        if (hot3 && l == 1) ENSURE(B_C2B, V.nchildren * 4, ca.c2b);   /* child -> bucket, for level 3 */
         if (l == L - 1) {
             ENSURE(B_SLOTS, cap * 4, slots);
             ENSURE(B_SLOTBKT, cap * 4, slot_bucket);
@@ -1469,10 +1511,12 @@ extern "C" int hm_count_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* co
 
 static int grouped_impl(hm_ctx* ctx, const double* lat, const double* lon, const int64_t* rows, const int64_t* cols,
                         const uint8_t* keep, const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
-                        int64_t capacity, int64_t* n_out)
+                        int64_t capacity, int64_t* n_out, uint64_t* pkeys = nullptr, uint64_t* pcounts = nullptr)
 {
+    const bool packed = pkeys || pcounts;
     if (!ctx || !n_out || n < 0 || n >= (int64_t)0xFFFFFFF0ll || zmin < 0 || zmax < zmin ||
-        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 || (capacity > 0 && !cells_out))
+        zmax > HM_COUNT_MAX_ZOOM || capacity < 0 ||
+        (capacity > 0 && (packed ? (!pkeys || !pcounts) : !cells_out)))
         return HM_E_ARG;
     *n_out = 0;
     HIPCHK(hipSetDevice(ctx->device));
@@ -1485,6 +1529,12 @@ static int grouped_impl(hm_ctx* ctx, const double* lat, const double* lon, const
     e.cells = cells_out;
     e.capacity = (uint64_t)capacity;
     e.width = 5;
+    if (packed) {
+        e.cells = nullptr;
+        e.keys = pkeys;
+        e.counts = pcounts;
+        e.width = 2;
+    }
     if (rows) {
         int64_t *row, *col, *idx;
         uint32_t* grp;
@@ -1514,6 +1564,37 @@ extern "C" int hm_count_grouped(hm_ctx* ctx, const double* lat, const double* lo
     if (st == HM_E_NOMEM) {
         arena_release(ctx);
         st = grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, cells_out, capacity, n_out);
+    }
+    return st;
+}
+
+extern "C" int hm_count_grouped_packed(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
+                                       const uint32_t* group, int64_t n, int zmin, int zmax, uint64_t* keys_out,
+                                       uint64_t* gcounts_out, int64_t capacity, int64_t* n_out)
+{
+    if (n > 0 && (!lat || !lon)) return HM_E_ARG;
+    int st = grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, nullptr, capacity, n_out,
+                          keys_out, gcounts_out);
+    if (st == HM_E_NOMEM) {
+        arena_release(ctx);
+        st = grouped_impl(ctx, lat, lon, nullptr, nullptr, keep, group, n, zmin, zmax, nullptr, capacity, n_out,
+                          keys_out, gcounts_out);
+    }
+    return st;
+}
+
+extern "C" int hm_count_grouped_packed_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col,
+                                             const uint8_t* keep, const uint32_t* group, int64_t n, int zmin, int zmax,
+                                             uint64_t* keys_out, uint64_t* gcounts_out, int64_t capacity,
+                                             int64_t* n_out)
+{
+    if (n > 0 && (!row || !col)) return HM_E_ARG;
+    int st = grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, nullptr, capacity, n_out,
+                          keys_out, gcounts_out);
+    if (st == HM_E_NOMEM) {
+        arena_release(ctx);
+        st = grouped_impl(ctx, nullptr, nullptr, row, col, keep, group, n, zmin, zmax, nullptr, capacity, n_out,
+                          keys_out, gcounts_out);
     }
     return st;
 }

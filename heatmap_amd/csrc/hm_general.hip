@@ -141,11 +141,18 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 #define HM_CS_FLAG_INC 2ull
 #define HM_CS_VBITS 38
 
-/* one (group,) z, row, col, count record at slot q */
+/* one (group,) z, row, col, count record at slot q; width 2 (packed grouped
+ * records, hm_count_grouped_packed, in-square cells only): keys[q] =
+ * HM_KEY(z, row, col), counts[q] = group << 32 | count */
 __device__ __forceinline__ void hm_put_record(const HmGenEmit& e, uint64_t q, uint32_t g, int z, int64_t row,
                                               int64_t col, uint64_t cnt)
 {
     if (q >= e.capacity) return;
+    if (e.width == 2) {
+        e.keys[q] = ((uint64_t)z << 58) | ((uint64_t)row << 29) | (uint64_t)col;
+        e.counts[q] = ((uint64_t)g << 32) | cnt;
+        return;
+    }
     int64_t* r = e.cells + q * e.width;
     int f = 0;
     if (e.width == 5) r[f++] = (int64_t)g;
@@ -222,7 +229,10 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
     const KT keep_bits = ~((((KT)1) << a.clr) - 1);
     const unsigned long long rb = a.rbase_in ? *a.rbase_in : 0ull;
     const int W = a.e.width;
-    const bool staged = a.emit && !a.e.split, split = a.emit && a.e.split;
+    /* packed records (width 2) go straight from the lanes: consecutive lanes
+     * write consecutive 8-B words of the two arrays */
+    const bool packed = a.emit && W == 2;
+    const bool staged = a.emit && !a.e.split && !packed, split = a.emit && a.e.split;
     if (blockIdx.x == 0 && threadIdx.x == 0 && a.rbase_out) *a.rbase_out = rb + m;
     if (m == 0 && blockIdx.x == 0 && threadIdx.x == 0) *a.m_out = 0u;
     for (;;) {
@@ -276,7 +286,14 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
             uint32_t xs = 0;
             if (a.emit) {
                 const uint64_t cnt = (uint64_t)(e[r] - ep);
-                if (staged) {
+                if (packed) {
+                    uint32_t g = 0;
+                    int64_t row = 0, col = 0;
+                    if (v) {
+                        hm_gen_decode(hm_k128(k[r], a.hic), a.Z, a.zin, &g, &row, &col);
+                        hm_put_record(a.e, rb + i, g, a.zin, row, col, cnt);
+                    }
+                } else if (staged) {
                     /* the wave's 64 records are consecutive: stage them, then
                      * store whole 8-B words across the lanes */
                     const uint64_t i0 = t0 + (uint64_t)r * HM_CS_THREADS + (uint64_t)w * 64;

@@ -503,6 +503,7 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
          * then the stores: no load-use round trip per key */
         OutT* out = (OutT*)a.keys_out;
         uint16_t* hout = (uint16_t*)a.keys_hot;
+        uint32_t* hout32 = (uint32_t*)a.keys_hot;   /* mid-level hot tiles (a.hot_bytes 4) */
         uint32_t sv[HM_P1_PPT], sl[HM_P1_PPT], sb[HM_P1_PPT];
 #pragma unroll
         for (int j = 0; j < HM_P1_PPT; j++) {
@@ -519,6 +520,8 @@ __global__ __launch_bounds__(HM_P1_THREADS, HM_P1_WAVES) void k_project_partitio
             if (i < total && sb[j] != 0xFFFFFFFFu) {
                 if (sl[j] < HM_MAX_F1)
                     out[sb[j] + i] = (OutT)sv[j];
+                else if (a.hot_bytes == 4)
+                    hout32[sb[j] + i] = sv[j];
                 else
                     hout[sb[j] + i] = (uint16_t)sv[j];
             }
@@ -840,10 +843,13 @@ k_l1_fast(HmPart1Args a)
     char* const houtb = (char*)a.keys_hot;
     const uint32_t hm = (1u << hs) - 1u;
     auto put_cold = [&](uint2 e) { *(OutT*)(outb + (uint64_t)e.y * sizeof(OutT)) = (OutT)e.x; };
+    const bool hot32 = a.hot_bytes == 4;   /* block-uniform */
     auto put_hot = [&](uint2 e) {
-        /* (row offset, col offset) in the zoom-zb tile, from the cold key */
+        /* (row offset, col offset) in the hot tile, from the cold key: u16 for
+         * a last-level bucket tile, u32 for a mid-level one */
         const uint32_t hk = (((e.x >> hb) & hm) << hs) | (e.x & hm);
-        *(uint16_t*)(houtb + (uint64_t)e.y * 2u) = (uint16_t)hk;
+        if (hot32) *(uint32_t*)(houtb + (uint64_t)e.y * 4u) = hk;
+        else *(uint16_t*)(houtb + (uint64_t)e.y * 2u) = (uint16_t)hk;
     };
     uint2 e[HM_P1_PPT];
 #pragma unroll
@@ -1739,10 +1745,10 @@ __global__ __launch_bounds__(HM_FR_THREADS, 8) void k_partition_fr(HmPartNArgs a
             const uint64_t child = ((uint64_t)it.bucket << a.dbits) + d;
             if (contig) {
                 /* idx: the key position of this item's range of the child */
-                idx[q] = (uint32_t)a.cbase[child] + atomicAdd(&a.ccur[child], cnt[q]);
+                idx[q] = a.cbase_off + (uint32_t)a.cbase[child] + atomicAdd(&a.ccur[child], cnt[q]);
                 if (atomicCAS(&a.nruns_out[child], 0u, 1u) == 0u) {
                     const uint64_t rb = hm_run_base(tile0, it.nitems, it.bucket, d, a.dbits, 0);
-                    a.runs_out[rb] = make_uint2((uint32_t)a.cbase[child], (uint32_t)a.ctot[child]);
+                    a.runs_out[rb] = make_uint2(a.cbase_off + (uint32_t)a.cbase[child], (uint32_t)a.ctot[child]);
                 }
             } else {
                 idx[q] = atomicAdd(&a.nruns_out[(child << a.shard_bits) + sh], 1u);

@@ -232,6 +232,8 @@ struct HmPart1Args {
     /* hot tiles (hot_z >= 0): keys of hot tile h go to the u16 array keys_hot
      * at the regions of digit HM_MAX_F1 + h (same position space as keys_out) */
     int hot_z;
+    int hot_bytes;              /* 2: u16 keys_hot (hot tiles at the last level's bucket zoom); 4: u32
+                                 * (mid-level hot tiles of a 3-level plan: the middle level's key form) */
     void* keys_hot;
     const uint32_t* hot_hash;   /* [HM_HOT_SLOTS]: bucketed table, tile id << HM_HOT_HBITS | h, HM_HOT_EMPTY */
     const uint32_t* hot_n;      /* device word: number of hot tiles */
@@ -307,6 +309,7 @@ struct HmPartNArgs {
     unsigned long long* ctot;
     const unsigned long long* cbase;
     uint32_t* ccur;
+    uint32_t cbase_off;         /* CONTIG: added to every child base (hot keys hold the positions below it) */
 };
 void hm_launch_partition_hist(hipStream_t s, const HmPartNArgs& a);
 #define HM_PN_RUNS 0

@@ -356,10 +356,7 @@ def count_grouped_device(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 
         kp = _dev(keep, torch.uint8, device)
         if kp.numel() != n:
             raise ValueError("keep must have one entry per point")
-    # records <= points x zooms; start there when it is at most 4 GiB of
-    # records (one pass), else at 2 per point and grow on HM_E_CAPACITY
-    nz = int(zmax) - int(zmin) + 1
-    cap = max(1024, n * nz + 64 if n * nz * 40 <= (4 << 30) else 2 * n + 64)
+    cap = _record_capacity(n, int(zmax) - int(zmin) + 1, 40, device)
     while True:
         cells = torch.empty(5 * cap, dtype=torch.int64, device=a.device)
         nout = ctypes.c_int64(0)
@@ -374,6 +371,58 @@ def count_grouped_device(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 
             _lib.raise_for(rc, idx)
         break
     return cells[:5 * nout.value].view(-1, 5)
+
+
+def _record_capacity(n: int, nz: int, bytes_per: int, device: int) -> int:
+    """First record capacity of a grouped count: every (point, zoom) when that
+    fits half the free device memory (one pass, the usual case on a 288 GB
+    part), else half the free memory's worth (more records: HM_E_CAPACITY and
+    one more pass at the exact size)."""
+    torch = _torch()
+    free, _ = torch.cuda.mem_get_info(device)
+    most = max(1024, int(free // 2) // bytes_per)
+    return max(1024, min(n * nz + 64, most))
+
+
+def count_grouped_packed_device(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,
+                                tiles: bool = False):
+    """hm_count_grouped_packed: (keys, gcounts) int64 CUDA tensors of the
+    records -- keys HM_KEY(zoom, row, col), gcounts group << 32 | count, 16 B
+    per record -- or None when some kept point's tile lies outside
+    [0, 2^zmax)^2 (hm_count_grouped's 5-int64 records hold those)."""
+    torch = _torch()
+    ctx = context(device)
+    dt = torch.int64 if tiles else torch.float64
+    a = _dev(lat, dt, device)
+    b = _dev(lon, dt, device)
+    n = a.numel()
+    g = _dev(np.asarray(group, dtype=np.uint32).view(np.int32) if not isinstance(group, torch.Tensor) else group,
+             torch.int32, device)
+    if b.numel() != n or g.numel() != n:
+        raise ValueError("lat, lon and group must have the same length")
+    kp = None
+    if keep is not None:
+        kp = _dev(keep, torch.uint8, device)
+        if kp.numel() != n:
+            raise ValueError("keep must have one entry per point")
+    cap = _record_capacity(n, int(zmax) - int(zmin) + 1, 16, device)
+    fn = ctx.L.hm_count_grouped_packed_tiles if tiles else ctx.L.hm_count_grouped_packed
+    while True:
+        keys = torch.empty(cap, dtype=torch.int64, device=a.device)
+        gc = torch.empty(cap, dtype=torch.int64, device=a.device)
+        nout = ctypes.c_int64(0)
+        rc = fn(ctx.ptr, _ptr(a), _ptr(b), _ptr(kp), _ptr(g), n, int(zmin), int(zmax), _ptr(keys), _ptr(gc), cap,
+                ctypes.byref(nout))
+        if rc == _lib.HM_E_CAPACITY:
+            del keys, gc
+            cap = int(nout.value) + 64
+            continue
+        if rc == _lib.HM_E_EXOTIC:
+            return None
+        if rc != _lib.HM_OK:
+            idx, kind = ctx.last_error()
+            _lib.raise_for(rc, idx)
+        return keys[:nout.value], gc[:nout.value]
 
 
 def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,

@@ -203,11 +203,22 @@ class Cells:
         z, r, c = (np.asarray(x, np.int64) for x in (self.zoom, self.row, self.col))
         tz, tr, tc = z - d, r >> d, c >> d
         if self.tile_override:
+            # the few overridden bins located by a search over the bins' sorted
+            # (zoom, row, col) rows, not a Python pass over every bin
             tr, tc = tr.copy(), tc.copy()
-            for i in range(z.size):
-                o = self.tile_override.get((int(z[i]), int(r[i]), int(c[i])))
-                if o is not None:
-                    tr[i], tc[i] = o
+            ok = np.array(list(self.tile_override.keys()), np.int64).reshape(-1, 3)
+            ov = np.array(list(self.tile_override.values()), np.int64).reshape(-1, 2)
+            o = np.lexsort((c, r, z))
+            zs, rs, cs = z[o], r[o], c[o]
+            for j in range(ok.shape[0]):
+                lo = np.searchsorted(zs, ok[j, 0], "left")
+                hi = np.searchsorted(zs, ok[j, 0], "right")
+                a = lo + np.searchsorted(rs[lo:hi], ok[j, 1], "left")
+                b = lo + np.searchsorted(rs[lo:hi], ok[j, 1], "right")
+                k = a + np.searchsorted(cs[a:b], ok[j, 2], "left")
+                while k < b and cs[k] == ok[j, 2]:
+                    tr[o[k]], tc[o[k]] = ov[j]
+                    k += 1
         return tz, tr, tc
 
     def __len__(self):
@@ -559,7 +570,13 @@ def _cells_to_table_device(cells: Cells):
             int(sp.max()) >= (1 << 20)):
         return None
     dv = cu(vi)
-    tz, tr, tc = z - d, r >> d, c >> d
+    if cells.tile_override:   # ChainFix: some bins' row tiles are not the shift
+        htz, htr, htc = cells.row_tiles()
+        if min(int(htr.min()), int(htc.min())) < 0 or max(int(htr.max()), int(htc.max())) >= (1 << 29):
+            return None
+        tz, tr, tc = cu(htz), cu(htr), cu(htc)
+    else:
+        tz, tr, tc = z - d, r >> d, c >> d
     perm = torch.arange(z.numel(), device=z.device)
     for key in ((z << 58) | (r << 29) | c, (tz << 58) | (tr << 29) | tc, (lab << 20) | sp):
         perm = perm[torch.sort(key[perm], stable=True).indices]
@@ -583,7 +600,7 @@ def cells_to_table(cells: Cells):
     d = cells.delta
     if len(cells) == 0:
         return pa.table({"id": pa.array([], pa.large_string()), "heatmap": pa.array([], pa.large_string())})
-    if len(cells) >= SUM_BY_CELL_DEVICE_MIN and device.gpu_available() and not cells.tile_override:
+    if len(cells) >= SUM_BY_CELL_DEVICE_MIN and device.gpu_available():
         tab = _cells_to_table_device(cells)
         if tab is not None:
             return tab
@@ -718,7 +735,8 @@ def _ids_gpu(labels, spans, rl, rs, rz, rr, rc):
 def _device_table(labels, keys, counts, grouped, zmax, d, phases):
     """heatmap_table's rows from device-resident counts, end to end on the
     GPU: keys/counts = hm_count's in-square cells (HM_KEY, n) of the kept
-    points; grouped = hm_count_grouped's [m, 5] records.  The 'all' closed
+    points; grouped = hm_count_grouped_packed's (keys, group << 32 | count)
+    or hm_count_grouped's [m, 5] records.  The 'all' closed
     form (combine_cells) by a sort of the cell keys and index_adds, the row
     order by one sort of packed (label, row tile, row, col) keys, the JSON by
     hm_format_bins; only the per-row id fields come back.  None when the keys
@@ -735,9 +753,15 @@ def _device_table(labels, keys, counts, grouped, zmax, d, phases):
     w = torch.ones_like(ks) << (zmax - z)
     a = torch.zeros_like(n)
     u = torch.zeros_like(n)
-    if grouped.numel():
+    if isinstance(grouped, tuple):   # hm_count_grouped_packed: (HM_KEY, group << 32 | count)
+        gk, gcn = grouped
+        gg, gn = gcn >> 32, gcn & 0xFFFFFFFF
+    elif grouped.numel():
         gg, gz, gr, gc, gn = grouped.unbind(1)
         gk = (gz << 58) | (gr << 29) | gc
+    else:
+        gk = None
+    if gk is not None and gk.numel():
         pos = torch.searchsorted(ks, gk)
         lit = gg == 0
         a.index_add_(0, pos[lit], gn[lit])
@@ -804,17 +828,25 @@ def heatmap_table(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None,
     t0 = time.perf_counter()
     m, buf = device.count_device(lat, lon, keep.astype(np.uint8), d + 1, zmax, tiles=tiles)
     keys, counts = buf.keys[:m], buf.counts[:m]
+    packed = None
+    if buf.nx == 0 and plan.grouped.any():
+        # 16-B records (HM_KEY, group | count); None if a kept tile leaves the square
+        packed = device.count_grouped_packed_device(lat, lon, plan.gid, plan.grouped.astype(np.uint8), d + 1, zmax,
+                                                    tiles=tiles)
+    ph["counts (device)"] = time.perf_counter() - t0
+    tab = None
+    if buf.nx == 0 and (packed is not None or not plan.grouped.any()):
+        grouped = packed if packed is not None else keys.new_zeros((0, 5))
+        tab = _device_table(plan.labels, keys, counts, grouped, zmax, d, ph)
+    if tab is not None:
+        return tab
+    t0 = time.perf_counter()
     if plan.grouped.any():
         grouped = device.count_grouped_device(lat, lon, plan.gid, plan.grouped.astype(np.uint8), d + 1, zmax,
                                               tiles=tiles)
     else:
         grouped = keys.new_zeros((0, 5))
-    ph["counts (device)"] = time.perf_counter() - t0
-    tab = None
-    if buf.nx == 0:
-        tab = _device_table(plan.labels, keys, counts, grouped, zmax, d, ph)
-    if tab is not None:
-        return tab
+    ph["counts (device, 5-int64 records)"] = time.perf_counter() - t0
     # host assembly from the same counts
     zk, rk, ck = device.decode_keys(keys.cpu().numpy().view(np.uint64))
     cnt = counts.cpu().numpy()
@@ -873,6 +905,12 @@ def weighted_location_cells(zs, rows, cols, users, weights, zmax, d, project=Non
             j = at[(rows[i], cols[i])]
             T_r[i], T_c[i] = tr[j], tc[j]
     wv = np.asarray(weights, np.float64)
+    # integer-valued counts (dataframe_loader's 1.0s, heatmap_to_locations of
+    # such rows) are summed as int64 -- exact in any order, so on the GPU for
+    # large lists (_sum_by_cell); other floats in float64 on the host, in input
+    # order within a cell as the reference's reduceByKey folds them
+    if np.all(wv == np.trunc(wv)) and float(np.abs(wv).sum()) < 2.0 ** 53:
+        wv = wv.astype(np.int64)
     plan = group_plan(users)
     # every level's tile of each distinct first-level tile: the shift inside
     # the windows, the literal chain outside (ChainFix)
@@ -910,5 +948,8 @@ def weighted_location_cells(zs, rows, cols, users, weights, zmax, d, project=Non
                                         np.concatenate(gc), np.concatenate(gv)[:, None])])
         grp = (kz // 64, kz % 64, kr, kc, kv[:, 0])
     else:
-        grp = (np.zeros(0, np.int64),) * 4 + (np.zeros(0, np.float64),)
+        grp = (np.zeros(0, np.int64),) * 4 + (np.zeros(0, wv.dtype),)
+    if wv.dtype.kind == "i":   # the reference's counts are floats
+        allc = allc[:3] + (allc[3].astype(np.float64),)
+        grp = grp[:4] + (grp[4].astype(np.float64),)
     return combine_cells(plan.labels, allc, grp, zmax, d, exact_levels=over)

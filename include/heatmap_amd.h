@@ -182,6 +182,20 @@ int hm_count_grouped_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, 
                            const uint32_t* group, int64_t n, int zmin, int zmax, int64_t* cells_out,
                            int64_t capacity, int64_t* n_out);
 
+/* hm_count_grouped with a packed output of 16 B per record (SURVEY.md 8(d):
+ * the output cell's 16 B): keys_out[i] = HM_KEY(zoom, row, col) and
+ * gcounts_out[i] = group << 32 | count (u64 device arrays of capacity
+ * entries).  Cells must lie inside [0, 2^z)^2 (every kept point's zoom-zmax
+ * tile in the square): HM_E_EXOTIC otherwise, before any record is written
+ * (use hm_count_grouped).  Records of one zoom are contiguous, zoom zmax
+ * first, in no particular order inside a zoom. */
+int hm_count_grouped_packed(hm_ctx* ctx, const double* lat, const double* lon, const uint8_t* keep,
+                            const uint32_t* group, int64_t n, int zmin, int zmax, uint64_t* keys_out,
+                            uint64_t* gcounts_out, int64_t capacity, int64_t* n_out);
+int hm_count_grouped_packed_tiles(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint8_t* keep,
+                                  const uint32_t* group, int64_t n, int zmin, int zmax, uint64_t* keys_out,
+                                  uint64_t* gcounts_out, int64_t capacity, int64_t* n_out);
+
 /* First failing point of the last call: index in input order (-1 if none)
  * and its HM_E_* kind. */
 int hm_last_error(hm_ctx* ctx, int64_t* index, int* kind);

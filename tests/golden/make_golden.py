@@ -24,6 +24,8 @@ Outputs (data only -- inputs and the reference's outputs):
   heatmap_rows_*.json.gz    build_heatmaps rows for small mixed datasets
   config1_digest.json       1M uniform points: per-zoom counts / digests
   zoom_counts_hotspots.json 100k hotspot points: per-zoom cell digests z0..21
+  weighted_locations.json.gz, weighted_nondyadic.json.gz
+                            build_heatmaps on location lists with float counts
 """
 import argparse
 import collections
@@ -369,6 +371,35 @@ def weighted_locations_golden(hm, rng):
     print("weighted locations:", {k: (len(v["locations"]), len(v["rows"])) for k, v in out.items()})
 
 
+def weighted_nondyadic_golden(hm, rng):
+    """build_heatmaps on locations with NON-dyadic float counts (0.1, 0.3,
+    1/3, 2.7, 0.7): their sums depend on the summation order, which in the
+    reference is Spark's (here the in-memory RDD's input order), so the test
+    compares with a relative tolerance, not bit for bit.  Default constants,
+    MAX_ZOOM_LEVEL = 9; tiles at the detail zoom and two coarser ones."""
+    users = ["x1", "u1", "u2", "rt-9", "all"]
+    hm.MAX_ZOOM_LEVEL = 9
+    try:
+        zmax = 14
+        locs = []
+        for i in range(2000):
+            z = int(rng.choice([zmax, zmax, zmax - 2, 11]))
+            la = float(47.6 + rng.normal(0, 0.2))
+            lo = float(-122.3 + rng.normal(0, 0.2))
+            tid = hm.Tile.tile_id_from_lat_long(la, lo, z)
+            locs.append({"userId": users[int(rng.integers(0, len(users)))], "tileId": tid,
+                         "count": float(rng.choice([0.1, 0.3, 1.0 / 3.0, 2.7, 0.7])), "timespan": "alltime"})
+        res = {}
+        for k, v in hm.build_heatmaps(RDD(locs)):
+            assert k not in res
+            res[k] = v
+    finally:
+        hm.MAX_ZOOM_LEVEL = 16
+    with gzip.open(os.path.join(HERE, "weighted_nondyadic.json.gz"), "wt") as f:
+        json.dump({"max_zoom_level": 9, "locations": locs, "rows": res}, f)
+    print("weighted non-dyadic:", len(locs), len(res))
+
+
 def canonical_digest(items):
     h = hashlib.sha256()
     for it in items:
@@ -477,6 +508,8 @@ def main():
         chain_goldens(hm, np.random.default_rng(20261017))
     if "weighted" in todo or not a.only:
         weighted_locations_golden(hm, np.random.default_rng(20261018))
+    if "weighted_nd" in todo or not a.only:
+        weighted_nondyadic_golden(hm, np.random.default_rng(20261019))
     if "c1" in todo and not a.quick:
         config1_digest(Tile, hm)
 

@@ -108,3 +108,20 @@ def test_fullsize_grouped(gpu):
     rec = cells[:5 * nout.value].reshape(-1, 5)
     gr, z, r, c, cnt = (rec[:, i] for i in range(5))
     assert device_cells_digest(torch, z, (gr << (z + 1)) | r, c, cnt) == g["digest"]
+
+
+def test_fullsize_grouped_packed(gpu):
+    """The same production-zoom grouped count through the 16-B packed records
+    (hm_count_grouped_packed), against the same oracle digest."""
+    torch = gpu
+    g = _golden("grouped_hotspots_1e8_u10000_z6-21")
+    n, users, zmin, zmax = g["n"], g["users"], g["zmin"], g["zmax"]
+    lat = torch.empty(n, dtype=torch.float64, device="cuda")
+    lon = torch.empty(n, dtype=torch.float64, device="cuda")
+    device.synth(g["kind"], lat, lon, seed=g["seed"])
+    grp = (((torch.arange(n, device="cuda", dtype=torch.int64) * 2654435761) >> 7) % users).to(torch.int32)
+    keys, gc = device.count_grouped_packed_device(lat, lon, grp, None, zmin, zmax)
+    del lat, lon, grp
+    z, r, c = keys >> 58, (keys >> 29) & 0x1FFFFFFF, keys & 0x1FFFFFFF
+    gr, cnt = gc >> 32, gc & 0xFFFFFFFF
+    assert device_cells_digest(torch, z, (gr << (z + 1)) | r, c, cnt) == g["digest"]

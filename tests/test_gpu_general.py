@@ -80,6 +80,43 @@ def test_grouped_vs_oracle(gpu, zmin, zmax, groups):
         assert np.array_equal(getattr(got, k), np.concatenate(exp[k])), k
 
 
+@pytest.mark.parametrize("zmin,zmax,groups", [(0, 14, 7), (6, 21, 1000), (3, 18, 1), (6, 21, 5_000_000)])
+def test_grouped_packed_vs_oracle(gpu, zmin, zmax, groups):
+    """hm_count_grouped_packed (16-B records: HM_KEY, group << 32 | count) on
+    in-square points == the oracle per group, and records of one zoom are
+    contiguous, zoom zmax first; groups past 2^22 make the sort's keys 128-bit
+    at zoom 21.  A kept point outside the square: None (HM_E_EXOTIC); an
+    unkept one does not matter."""
+    lat, lon = synth.generate("hotspots", 80_000, seed=groups)
+    rng = np.random.default_rng(groups)
+    g = rng.integers(0, groups, lat.size).astype(np.uint32) * (7919 if groups < 1000 else 1)
+    keep = (rng.random(lat.size) < 0.8).astype(np.uint8)
+    keys, gc = device.count_grouped_packed_device(lat, lon, g, keep, zmin, zmax)
+    k = keys.cpu().numpy().view(np.uint64)
+    z = (k >> np.uint64(58)).astype(np.int32)
+    assert np.all(np.diff(z) <= 0) and z[0] == zmax
+    gcn = gc.cpu().numpy().view(np.uint64)
+    got = device.GroupedCounts((gcn >> np.uint64(32)).astype(np.uint32), z,
+                               ((k >> np.uint64(29)) & np.uint64(0x1FFFFFFF)).astype(np.int64),
+                               (k & np.uint64(0x1FFFFFFF)).astype(np.int64),
+                               (gcn & np.uint64(0xFFFFFFFF)).astype(np.int64)).sorted()
+    ref = device.count_grouped(lat, lon, g, keep, zmin, zmax).sorted()
+    for f in ("group", "zoom", "row", "col", "count"):
+        assert np.array_equal(getattr(got, f), getattr(ref, f)), f
+    if groups <= 7:   # pinned to the oracle directly as well
+        for gid in np.unique(g[keep.astype(bool)])[:3]:
+            o = oracle.count(lat, lon, keep & (g == gid), zmin, zmax)
+            m = got.group == gid
+            assert np.array_equal(got.count[m], o["count"][np.lexsort((o["col"], o["row"], o["zoom"]))])
+    lat2 = lat.copy()
+    lat2[5] = 88.0
+    keep2 = keep.copy()
+    keep2[5] = 1
+    assert device.count_grouped_packed_device(lat2, lon, g, keep2, zmin, zmax) is None
+    keep2[5] = 0
+    assert device.count_grouped_packed_device(lat2, lon, g, keep2, zmin, zmax) is not None
+
+
 def test_grouped_errors(gpu):
     lat, lon = synth.uniform(10000, seed=2)
     lat = lat.copy()
@@ -189,9 +226,11 @@ def test_heat_text_device_matches_host(gpu):
     assert dev.slice(0, 2000).to_pylist() == host
 
 
-def test_cells_to_table_device_matches_host(gpu):
+@pytest.mark.parametrize("override", [False, True])
+def test_cells_to_table_device_matches_host(gpu, override):
     """cells_to_table's device path (order, gathers and JSON on the GPU) gives
-    the host path's table exactly: ids and heatmap strings, row by row."""
+    the host path's table exactly: ids and heatmap strings, row by row; with
+    ChainFix row-tile overrides on some bins too (Cells.row_tiles)."""
     from heatmap_amd import heatmap as hm
 
     g = np.random.default_rng(6)
@@ -204,8 +243,13 @@ def test_cells_to_table_device_matches_host(gpu):
     key = (label << 44) | (span << 43) | (zoom << 38) | (row << 19) | col
     keep = np.unique(key, return_index=True)[1]
     val = g.integers(1, 10 ** 9, keep.size).astype(np.float64)
+    over = None
+    if override:   # a few (zoom, row, col) bins whose row tile is a neighbour of the shift
+        idx = g.choice(keep.size, 40, replace=False)
+        over = {(int(zoom[keep][i]), int(row[keep][i]), int(col[keep][i])):
+                ((int(row[keep][i]) >> 5) ^ 1, int(col[keep][i]) >> 5) for i in idx}
     cells = hm.Cells(["u%d" % i for i in range(50)], label[keep], zoom[keep], row[keep], col[keep], val, 5,
-                     ["alltime", "2024"], span[keep])
+                     ["alltime", "2024"], span[keep], tile_override=over)
     dev = hm._cells_to_table_device(cells)
     old = hm.SUM_BY_CELL_DEVICE_MIN
     hm.SUM_BY_CELL_DEVICE_MIN = 1 << 62

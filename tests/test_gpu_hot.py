@@ -144,3 +144,42 @@ def test_hot_stream_batches(gpu):
         got = s.counts().sorted()
         s.close()
     _same(got, oracle.count(lat, lon, None, 0, 18))
+
+
+@pytest.mark.parametrize("kind,n,zmin,zmax,contig", [("hotspots", 2_000_000, 0, 21, 1), ("hotspots", 2_000_000, 6, 21, 1),
+                                                     ("hotspots", 1_000_000, 0, 19, 1), ("skew", 1_000_000, 0, 20, 1),
+                                                     ("hotspots", 1_000_000, 6, 21, 0), ("hotspots", 800_000, 14, 21, 1)])
+def test_hot_mid_level(gpu, kind, n, zmin, zmax, contig):
+    """Mid-level hot tiles (zmax 19-21, plan z5 -> z11 -> zmax-7): zoom-11
+    tiles with many points skip level 2 -- level 1 writes their keys in level
+    2's u32 form into level 2's output array -- and join level 3 as level-2
+    buckets, next to the cold keys (child-contiguous above every level-1
+    position with HM_CONTIG, at their own positions without)."""
+    lat, lon = synth.generate(kind, n, seed=41)
+    keep = (np.arange(n) % 9 != 2).astype(np.uint8)
+    with device.tuned(HM_HOT_MIN_KEYS=0, HM_CONTIG=contig):
+        got = device.count(lat, lon, keep, zmin, zmax)
+    assert int(got.stage_us[6]) > 0, "no hot tiles"
+    assert int(got.stage_us[7]) == 3
+    _same(got, oracle.count(lat, lon, keep, zmin, zmax))
+    with device.tuned(HM_HOT_MIN_KEYS=0, HM_HOT_MID=0):
+        off = device.count(lat, lon, keep, zmin, zmax)
+    assert int(off.stage_us[6]) == 0
+    _same(off, oracle.count(lat, lon, keep, zmin, zmax))
+
+
+def test_hot_mid_level_tiles_input_and_redo(gpu):
+    """Mid-level hot tiles from tile input with cells outside the square (the
+    partial-tile kernel's u32 hot stores) and guard-band points (k_redo's
+    tiles) at zmax 21."""
+    rng = np.random.default_rng(17)
+    Z = 21
+    n = 1_200_007
+    rows = np.where(rng.random(n) < 0.7, 732467 + rng.integers(-900, 900, n), rng.integers(0, 1 << Z, n))
+    cols = np.where(rng.random(n) < 0.7, 336123 + rng.integers(-900, 900, n), rng.integers(0, 1 << Z, n))
+    out = rng.random(n) < 0.01
+    rows = np.where(out, rows + (1 << Z), rows).astype(np.int64)
+    with device.tuned(HM_HOT_MIN_KEYS=0):
+        got = device.count(rows, cols.astype(np.int64), None, 0, Z, tiles=True)
+    assert int(got.stage_us[6]) > 0
+    _same(got, oracle.count_tiles(rows, cols.astype(np.int64), 0, Z))

@@ -2,7 +2,8 @@
 """The row-producing path (reference heatmap.py:64-75,111-112,120-129): per-user
 counts in one device pass (hm_count_grouped) and heatmap_table end to end.
 
-  device   one step = one hm_count_grouped over N device-resident hotspot
+  device   one step = one hm_count_grouped_packed (--records int64x5:
+           hm_count_grouped) over N device-resident hotspot
            points, each with one of U user groups (a hash of its index): the
            exact projection of every point, 128-bit (group, super-tile, Morton)
            keys, the LSD radix sort and the RLE zoom cascade (hm_general.hip),
@@ -39,19 +40,26 @@ def bench_device(a):
     grp = ((torch.arange(n, device="cuda", dtype=torch.int64) * 2654435761) >> 7) % a.users
     grp = grp.to(torch.int32)
     ctx = device.context(0)
+    w = 2 if a.packed else 5          # int64 words per record: (HM_KEY, group|count) or 5 fields
     buf = {"cap": int(a.cap_factor * n) + 1024}
-    buf["cells"] = torch.empty(5 * buf["cap"], dtype=torch.int64, device="cuda")
+    buf["cells"] = torch.empty(w * buf["cap"], dtype=torch.int64, device="cuda")
     nout = ctypes.c_int64(0)
     p = device._ptr
 
     def step():
         while True:
-            rc = ctx.L.hm_count_grouped(ctx.ptr, p(lat), p(lon), ctypes.c_void_p(0), p(grp), n, a.zmin, a.zmax,
-                                        p(buf["cells"]), buf["cap"], ctypes.byref(nout))
+            if a.packed:
+                c = buf["cells"]
+                rc = ctx.L.hm_count_grouped_packed(ctx.ptr, p(lat), p(lon), ctypes.c_void_p(0), p(grp), n, a.zmin,
+                                                   a.zmax, p(c), ctypes.c_void_p(c.data_ptr() + 8 * buf["cap"]),
+                                                   buf["cap"], ctypes.byref(nout))
+            else:
+                rc = ctx.L.hm_count_grouped(ctx.ptr, p(lat), p(lon), ctypes.c_void_p(0), p(grp), n, a.zmin, a.zmax,
+                                            p(buf["cells"]), buf["cap"], ctypes.byref(nout))
             if rc != _lib.HM_E_CAPACITY:
                 break
             buf["cap"] = int(nout.value * 1.05) + 1024      # warm-up only: the timed steps fit
-            buf["cells"] = torch.empty(5 * buf["cap"], dtype=torch.int64, device="cuda")
+            buf["cells"] = torch.empty(w * buf["cap"], dtype=torch.int64, device="cuda")
         if rc != _lib.HM_OK:
             _lib.raise_for(rc)
 
@@ -69,15 +77,21 @@ def bench_device(a):
     ms = e0.elapsed_time(e1) / a.steps
     m = nout.value
     cells = buf["cells"]
-    tot = int(cells[:5 * m].reshape(-1, 5)[:, 4].sum().item())
-    alg = 16 * n + 4 * n + 40 * m
-    out = {"part": "hm_count_grouped", "value": n / (ms * 1e-3), "unit": "points/s", "ms_per_step": ms,
+    if a.packed:
+        tot = int((cells[buf["cap"]:buf["cap"] + m] & 0xFFFFFFFF).sum().item())
+    else:
+        tot = int(cells[:5 * m].reshape(-1, 5)[:, 4].sum().item())
+    # 16 B of lat/lon + 4 B of group id read per point, 16 B per output cell
+    alg = 16 * n + 4 * n + 16 * m
+    out = {"part": "hm_count_grouped_packed" if a.packed else "hm_count_grouped", "value": n / (ms * 1e-3),
+           "unit": "points/s", "ms_per_step": ms,
            "host_ms_per_step": dt * 1e3 / a.steps, "points": n, "users": a.users, "kind": a.kind,
            "zooms": [a.zmin, a.zmax], "records": m,
            "check": "ok" if tot == n * (a.zmax - a.zmin + 1) else "FAIL sum %d" % tot,
            "roofline": {"bound": "hbm", "alg_bytes": alg, "achieved_GBps": alg / (ms * 1e-3) / 1e9,
                         "frac": alg / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
-                        "alg_bytes_note": "16 B lat/lon + 4 B group per point read, 40 B per output record"}}
+                        "alg_bytes_note": "SURVEY 8(d): 16 B lat/lon + 4 B group per point read, 16 B per "
+                                          "output cell (the record layout written: %d B)" % (8 * w)}}
     print(json.dumps(out), flush=True)
     del lat, lon, grp, cells
     torch.cuda.empty_cache()
@@ -118,7 +132,10 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cap-factor", type=float, default=2.0, help="first record capacity per point")
     ap.add_argument("--no-table", action="store_true")
+    ap.add_argument("--records", choices=["packed", "int64x5"], default="packed",
+                    help="hm_count_grouped_packed (16 B per record) or hm_count_grouped (40 B)")
     a = ap.parse_args()
+    a.packed = a.records == "packed"
     bench_device(a)
     if not a.no_table:
         bench_table(a)
