@@ -25,7 +25,7 @@ HM_E_CAPACITY = 17
 HM_E_HIP = 18
 HM_E_NOMEM = 19
 HM_E_WIDE = 20        # hm_cells_route with u32 counts: a count needs 64 bits
-HM_CELLS_U64, HM_CELLS_U32, HM_CELLS_REC10 = 8, 4, 10   # exchanged cell layouts
+HM_CELLS_U64, HM_CELLS_U32, HM_CELLS_REC10, HM_CELLS_G12 = 8, 4, 10, 12   # exchanged cell layouts
 HM_COUNT_MAX_ZOOM = 21
 HM_ABI_VERSION = 6
 HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4

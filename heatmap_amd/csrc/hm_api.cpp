@@ -1627,10 +1627,11 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
                               int delta, int dense_zmax, uint64_t* grid, void* keys_out, void* counts_out,
                               int layout, int64_t* send_counts)
 {
-    const bool rec = layout == HM_CELLS_REC10;
+    const bool rec = layout == HM_CELLS_REC10, grp = layout == HM_CELLS_G12;
     if (!ctx || n < 0 || nranks < 1 || nranks > 64 || delta < 0 || delta > 28 || dense_zmax > 14 ||
-        (layout != HM_CELLS_U32 && layout != HM_CELLS_U64 && !rec) || (dense_zmax >= 0 && !grid) ||
-        !send_counts || (n > 0 && (!keys || !counts || !keys_out || (!rec && !counts_out))))
+        (layout != HM_CELLS_U32 && layout != HM_CELLS_U64 && !rec && !grp) || (dense_zmax >= 0 && !grid) ||
+        (grp && dense_zmax >= 0) || !send_counts ||
+        (n > 0 && (!keys || !counts || !keys_out || (!rec && !counts_out))))
         return HM_E_ARG;
     HIPCHK(hipSetDevice(ctx->device));
     hipStream_t s = ctx->stream;
@@ -1665,6 +1666,7 @@ extern "C" int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t*
         } else {
             a.keys_out = (uint64_t*)keys_out;
             a.counts_out32 = (uint32_t*)counts_out;
+            a.grouped = grp;
         }
         a.wide = (unsigned long long*)(off + m + 1);
         HIPCHK(hipMemsetAsync(a.wide, 0, 8, s));

@@ -28,12 +28,13 @@
 #define HM_ROUTE_THREADS 256
 #define HM_MAX_RANKS 64
 
-/* owner rank of a cell: multiplicative hash of its heatmap-row key */
-__device__ __forceinline__ uint32_t hm_owner(uint64_t key, int delta, int nranks)
+/* owner rank of a cell: multiplicative hash of its heatmap-row key (and, for
+ * grouped cells, the group: the row id is user|alltime|tile, heatmap.py:55) */
+__device__ __forceinline__ uint32_t hm_owner(uint64_t key, int delta, int nranks, uint64_t gmix = 0)
 {
     const int64_t z = (int64_t)(key >> 58);
     const int64_t r = (int64_t)((key >> 29) & 0x1FFFFFFFull), c = (int64_t)(key & 0x1FFFFFFFull);
-    const int64_t rk = (z << 48) ^ ((r >> delta) << 24) ^ (c >> delta);
+    const int64_t rk = ((z << 48) ^ ((r >> delta) << 24) ^ (c >> delta)) + (int64_t)(gmix * 0xD6E8FEB86659FD93ull);
     const int64_t h = (int64_t)((uint64_t)rk * 0x9E3779B97F4A7C15ull) >> 33;   /* wrapping multiply */
     const int64_t m = h % nranks;
     return (uint32_t)(m < 0 ? m + nranks : m);
@@ -106,13 +107,17 @@ __global__ __launch_bounds__(HM_ROUTE_THREADS) void k_cells_route(HmRouteArgs a)
                       (unsigned long long)a.counts[i]);
         }
         const bool sp = in && !dense;
-        const uint32_t o = sp ? hm_owner(k, a.delta, a.nranks) : 0u;
+        const uint32_t g = a.grouped && in ? (uint32_t)(a.counts[i] >> 32) : 0u;
+        const uint32_t o = sp ? hm_owner(k, a.delta, a.nranks, a.grouped ? (uint64_t)g + 1 : 0ull) : 0u;
         if (SCATTER) {
             const uint32_t pos = hm_lds_claim(hist, HM_MAX_RANKS, o, sp);
             if (sp) {
                 const uint64_t q = base[o] + pos;
                 if (a.rec_out) {
                     hm_rec_put(a.rec_out + 5 * q, k, (uint32_t)a.counts[i]);
+                } else if (a.grouped) {
+                    a.keys_out[q] = hm_gkey(k, g);
+                    a.counts_out32[q] = (uint32_t)a.counts[i];
                 } else {
                     a.keys_out[q] = k;
                     if (a.counts_out32) a.counts_out32[q] = (uint32_t)a.counts[i];
@@ -123,9 +128,11 @@ __global__ __launch_bounds__(HM_ROUTE_THREADS) void k_cells_route(HmRouteArgs a)
             hm_lds_count(hist, HM_MAX_RANKS, o, sp);
             /* wide: a count needs 64 bits, or (10-byte records) a key does not
              * fit 48 bits (zoom > 21, row or column >= 2^21) */
-            const bool kw = a.rec_out && (z > 21 || ((k >> 29) & 0x1FFFFFFFull) >= (1ull << 21) ||
-                                          (k & 0x1FFFFFFFull) >= (1ull << 21));
-            if (a.wide && __any(sp && ((a.counts[i] >> 32) != 0ull || kw)) && (tid & 63) == 0)
+            const bool kw = (a.rec_out || a.grouped) && (z > 21 || ((k >> 29) & 0x1FFFFFFFull) >= (1ull << 21) ||
+                                                         (k & 0x1FFFFFFFull) >= (1ull << 21));
+            /* grouped: the count field is 32 bits already; the group must fit the merge key */
+            const bool cw = a.grouped ? g >= (1u << HM_GKEY_GROUP_BITS) : (a.counts[i] >> 32) != 0ull;
+            if (a.wide && __any(sp && (cw || kw)) && (tid & 63) == 0)
                 atomicOr(a.wide, 1ull);
         }
     }

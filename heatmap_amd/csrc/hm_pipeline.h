@@ -665,7 +665,15 @@ struct HmRouteArgs {
     uint32_t* counts_out32;    /* u32 counts, or */
     uint16_t* rec_out;         /* 10-B records (48-bit key, u32 count; hm_rec_put) */
     unsigned long long* wide;  /* u32 counts: set when a sent count needs 64 bits */
+    int grouped;               /* HM_CELLS_G12: counts = group << 32 | count (hm_count_grouped_packed);
+                                  the owner hashes (group, row key); keys_out = hm_gkey packed merge keys */
 };
+/* grouped exchange key: group (17 bits) | zoom (5) | row (21) | col (21) */
+#define HM_GKEY_GROUP_BITS 17
+__host__ __device__ inline uint64_t hm_gkey(uint64_t hmkey, uint32_t g)
+{
+    return ((uint64_t)g << 47) | ((hmkey >> 58) << 42) | (((hmkey >> 29) & 0x1FFFFFull) << 21) | (hmkey & 0x1FFFFFull);
+}
 unsigned hm_route_blocks(uint64_t n);
 /* bucketed merge of (key, count) cells: hash-partition into 2^lb buckets
  * (count + scatter passes over nblocks input chunks), then one block per

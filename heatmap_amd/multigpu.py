@@ -83,6 +83,27 @@ class DeviceOps:
         parts = [(rec[:5 * m].view(torch.uint8), 10)] if narrow else [(ko[:m], 1), (co[:m], 1)]
         return grid[:gsz], parts, sent, wide
 
+    def route_grouped(self, keys, gcounts, ws):
+        """hm_cells_route of grouped cells (HM_CELLS_G12): keys HM_KEY and
+        gcounts group << 32 | count (hm_count_grouped_packed) -> (parts,
+        group sizes, wide): parts [(u64 merge keys, 1), (u32 counts, 1)] grouped
+        by owner; wide: a group id or a zoom past the merge key (exchange
+        those records as int64 instead)."""
+        from . import _lib
+
+        n = keys.numel()
+        ko = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
+        co = torch.empty(max(n, 1), dtype=torch.int32, device=keys.device)
+        send = (ctypes.c_int64 * ws)()
+        rc = self.L.hm_cells_route(self.ctx.ptr, self._p(keys), self._p(gcounts), n, ws, DELTA, -1, ctypes.c_void_p(0),
+                                   self._p(ko), self._p(co), _lib.HM_CELLS_G12, send)
+        wide = rc == _lib.HM_E_WIDE
+        if not wide:
+            self._check(rc)
+        sent = list(send)
+        m = sum(sent)
+        return [(ko[:m], 1), (co[:m], 1)], sent, wide
+
     def merge(self, keys, counts=None, runs=None, out=None):
         """Sum equal keys.  keys int64 with counts int32 or int64, or (counts
         None) keys = 10-byte records (HM_CELLS_REC10, uint8); the sums are
@@ -339,3 +360,57 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         buffers.xcells[:x.numel()] = x.reshape(-1)
         buffers.nx = x.shape[0]
     return n
+
+
+GKEY_GROUP_BITS = 17
+
+
+def grouped_owner(keys: torch.Tensor, groups: torch.Tensor, ws: int) -> torch.Tensor:
+    """Owner rank of grouped in-square cells (HM_KEY keys, group ids): the
+    hash hm_cells_route computes for HM_CELLS_G12 (the row key of
+    heatmap.py:55 -- user, timespan, tile -- holds the group)."""
+    z, r, c = keys >> 58, (keys >> 29) & 0x1FFFFFFF, keys & 0x1FFFFFFF
+    gm = (groups + 1) * -2960836687051489901          # wrapping (group + 1) * 0xD6E8FEB86659FD93
+    rk = ((z << 48) ^ ((r >> DELTA) << 24) ^ (c >> DELTA)) + gm
+    h = (rk * -7046029254386353131) >> 33
+    return torch.remainder(h, ws)
+
+
+def merge_grouped(keys: torch.Tensor, gcounts: torch.Tensor, ws: int, rank: int, ops=None):
+    """Exchange and merge grouped cells -- hm_count_grouped_packed's keys
+    (HM_KEY) and gcounts (group << 32 | count) on every rank -- so that each
+    (group, cell) ends on the rank owning its heatmap row (the reference's
+    reduceByKey / groupByKey on user|alltime|tile keys, heatmap.py:54-55,
+    111-112).  Returns this rank's (keys, groups, counts) int64 tensors
+    (counts summed over ranks: int64).  Device route into 12-byte records
+    (u64 merge key of group, zoom, row, col; u32 count), ONE all-to-all of
+    sizes + the wide flag, one of keys, one of counts, and hm_cells_merge_runs
+    on the owner; if any rank holds a group id past 2^17 (the merge key's
+    field) every rank exchanges (key, group, count) int64 records and sums
+    them with torch ops instead."""
+    if ops is None:
+        ops = DeviceOps(keys.device.index or 0)
+    parts, sent, wide = ops.route_grouped(keys, gcounts, ws)
+    send = torch.tensor([[s, int(wide)] for s in sent], dtype=torch.int64, device=keys.device)
+    recv = torch.empty_like(send)
+    dist.all_to_all_single(recv, send)
+    recv = recv.cpu()
+    rl = recv[:, 0].tolist()
+    if bool(recv[:, 1].any()):
+        g = gcounts >> 32
+        rows = torch.stack([keys, g, gcounts & 0xFFFFFFFF], 1)
+        got = _exchange(rows, grouped_owner(keys, g, ws), ws)
+        if got.shape[0] == 0:
+            return got[:, 0], got[:, 1], got[:, 2]
+        u, inv = torch.unique(got[:, :2], dim=0, return_inverse=True)
+        tot = torch.zeros(u.shape[0], dtype=torch.int64, device=got.device).index_add_(0, inv, got[:, 2])
+        return u[:, 0], u[:, 1], tot
+    got = []
+    for t, w in parts:
+        r = torch.empty(sum(rl) * w, dtype=t.dtype, device=keys.device)
+        dist.all_to_all_single(r, t, [x * w for x in rl], [x * w for x in sent])
+        got.append(r)
+    mk, mc = ops.merge(got[0], got[1], runs=rl)
+    g = mk >> 47
+    hk = (((mk >> 42) & 31) << 58) | (((mk >> 21) & 0x1FFFFF) << 29) | (mk & 0x1FFFFF)
+    return hk, g, mc

@@ -302,6 +302,12 @@ int64_t hm_dense_grid_size(int dense_zmax);
 #define HM_CELLS_U64 8
 #define HM_CELLS_U32 4
 #define HM_CELLS_REC10 10
+#define HM_CELLS_G12 12  /* hm_cells_route of grouped cells (hm_count_grouped_packed's keys and
+                            group << 32 | count): owner by (group, heatmap row); keys_out = u64
+                            merge keys group << 47 | zoom << 42 | row << 21 | col, counts_out =
+                            u32 counts (12 B a cell); no dense grid (dense_zmax -1); HM_E_WIDE
+                            when a group passes 2^17 or a cell passes zoom 21 (exchange those as
+                            int64 records) */
 int hm_cells_route(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks, int delta,
                    int dense_zmax, uint64_t* grid, void* keys_out, void* counts_out, int layout,
                    int64_t* send_counts);

@@ -217,3 +217,81 @@ def test_pipelined_steps_over_rccl(gpu, nccl_world):
                         (k & np.uint64(0x1FFFFFFF)).astype(np.int64), bufs.counts[:m].cpu().numpy(), 0, []).sorted()
     for f in ("zoom", "row", "col", "count"):
         assert np.array_equal(getattr(got, f), getattr(ref, f)), f
+
+
+def _grouped(n, seed, users):
+    lat, lon = synth.generate("hotspots", n, seed=seed)
+    grp = (((np.arange(n) * 2654435761) >> 7) % users).astype(np.uint32)
+    return lat, lon, grp
+
+
+@pytest.mark.parametrize("ws,users", [(1, 1000), (5, 1000), (8, 30), (8, 200_000)])
+def test_route_grouped_kernel_contract(gpu, ws, users):
+    """hm_cells_route of grouped cells (HM_CELLS_G12) == the CPU stand-in:
+    the same owner group sizes and, per owner, the same (merge key, count)
+    multiset; group ids past 2^17 answer wide."""
+    lat, lon, grp = _grouped(300_000, ws, users)
+    keys, gc = device.count_grouped_packed_device(lat, lon, grp, None, 6, 21)
+    parts, sent, wide = multigpu.DeviceOps(0).route_grouped(keys, gc, ws)
+    rparts, rsent, rwide = TorchOps.route_grouped(keys.cpu(), gc.cpu(), ws)
+    assert wide == rwide == (users > (1 << 17))
+    assert sent == rsent
+    if wide:
+        return
+    sk, sc = parts[0][0].cpu(), parts[1][0].cpu().to(torch.int64)
+    rk, rc = rparts[0][0], rparts[1][0].to(torch.int64)
+    at = 0
+    for m in sent:
+        a, b = torch.argsort(sk[at:at + m]), torch.argsort(rk[at:at + m])
+        assert torch.equal(sk[at:at + m][a], rk[at:at + m][b]) and torch.equal(sc[at:at + m][a], rc[at:at + m][b])
+        at += m
+
+
+@pytest.mark.parametrize("users", [1000, 200_000])
+def test_merge_grouped_over_rccl(gpu, nccl_world, users):
+    """merge_grouped over a real RCCL group of world size 1: the device route,
+    the all-to-alls and hm_cells_merge_runs (or, past 2^17 groups, the int64
+    records) give back exactly the grouped count."""
+    lat, lon, grp = _grouped(500_000, 3, users)
+    keys, gc = device.count_grouped_packed_device(lat, lon, grp, None, 6, 21)
+    k, g, c = multigpu.merge_grouped(keys, gc, 1, 0)
+    got = np.lexsort((k.cpu().numpy(), g.cpu().numpy()))
+    ref = np.lexsort((keys.cpu().numpy(), (gc >> 32).cpu().numpy()))
+    assert np.array_equal(k.cpu().numpy()[got], keys.cpu().numpy()[ref])
+    assert np.array_equal(g.cpu().numpy()[got], (gc >> 32).cpu().numpy()[ref])
+    assert np.array_equal(c.cpu().numpy()[got], (gc & 0xFFFFFFFF).cpu().numpy()[ref])
+
+
+def test_grouped_exchange_8_emulated_ranks(gpu):
+    """The grouped pyramid sharded over 8 emulated ranks on one GPU: each
+    shard's hm_count_grouped_packed, routed by hm_cells_route(G12, nranks=8);
+    owner o merges group o of every shard (hm_cells_merge_runs).  Every
+    (group, cell) has one owner and the union equals one grouped count of all
+    points (heatmap.py:54-55,111-112)."""
+    ws, n, users = 8, 2_000_000, 5000
+    lat, lon, grp = _grouped(n, 9, users)
+    ops = multigpu.DeviceOps(0)
+    per = n // ws
+    routed = []
+    for r in range(ws):
+        sl = slice(r * per, (r + 1) * per)
+        k, gc = device.count_grouped_packed_device(lat[sl], lon[sl], grp[sl], None, 6, 21)
+        parts, sent, wide = ops.route_grouped(k, gc, ws)
+        assert not wide
+        routed.append((parts[0][0].clone(), parts[1][0].clone(), [0] + np.cumsum(sent).tolist(), sent))
+    allk, allg, allc = [], [], []
+    for o in range(ws):
+        mk = torch.cat([x[0][x[2][o]:x[2][o + 1]] for x in routed])
+        mc = torch.cat([x[1][x[2][o]:x[2][o + 1]] for x in routed])
+        uk, uc = ops.merge(mk, mc, [x[3][o] for x in routed])
+        g = uk >> 47
+        hk = (((uk >> 42) & 31) << 58) | (((uk >> 21) & 0x1FFFFF) << 29) | (uk & 0x1FFFFF)
+        assert bool((multigpu.grouped_owner(hk, g, ws) == o).all())
+        allk.append(hk.cpu().numpy())
+        allg.append(g.cpu().numpy())
+        allc.append(uc.cpu().numpy())
+    ks, gs, cs = np.concatenate(allk), np.concatenate(allg), np.concatenate(allc)
+    keys, gc = device.count_grouped_packed_device(lat, lon, grp, None, 6, 21)
+    rk, rg, rc = keys.cpu().numpy(), (gc >> 32).cpu().numpy(), (gc & 0xFFFFFFFF).cpu().numpy()
+    a, b = np.lexsort((ks, gs)), np.lexsort((rk, rg))
+    assert np.array_equal(ks[a], rk[b]) and np.array_equal(gs[a], rg[b]) and np.array_equal(cs[a], rc[b])

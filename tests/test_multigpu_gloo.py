@@ -73,6 +73,16 @@ class TorchOps:
         return grid, parts, torch.bincount(own, minlength=ws).tolist(), wide
 
     @staticmethod
+    def route_grouped(keys, gcounts, ws):
+        g = gcounts >> 32
+        z, r, c = keys >> 58, (keys >> 29) & M29, keys & M29
+        wide = bool((g >= 1 << multigpu.GKEY_GROUP_BITS).any() or (z > 21).any())
+        own = multigpu.grouped_owner(keys, g, ws)
+        o = torch.argsort(own, stable=True)
+        mk = (g << 47) | (z << 42) | (r << 21) | c
+        return [(mk[o], 1), ((gcounts & 0xFFFFFFFF)[o].to(torch.int32), 1)], torch.bincount(own, minlength=ws).tolist(), wide
+
+    @staticmethod
     def merge(keys, counts=None, runs=None):
         if counts is None:                      # HM_CELLS_REC10 records
             keys, counts = multigpu.unpack_records(keys)
@@ -185,3 +195,57 @@ def test_records_round_trip():
     assert rec.dtype == torch.uint8 and rec.numel() == 10 * keys.numel()
     k2, c2 = multigpu.unpack_records(rec)
     assert torch.equal(k2, keys) and torch.equal(c2, counts)
+
+
+def _grouped_cells(lat, lon, grp, zmin, zmax):
+    """(HM_KEY keys, groups, counts) per (group, zoom, row, col): the oracle's
+    projection at zmax and every coarser zoom by the shift (the oracle's own
+    pyramid is pinned in tests/test_oracle.py; this is the exchange's input)."""
+    r, c, st, _ = oracle.project(lat, lon, zmax)
+    assert (st == 0).all()
+    ks = []
+    for z in range(zmin, zmax + 1):
+        ks.append((np.int64(z) << 58) | ((r >> (zmax - z)) << 29) | (c >> (zmax - z)))
+    k = np.concatenate(ks)
+    g = np.tile(grp.astype(np.int64), zmax - zmin + 1)
+    u, cnt = np.unique(np.stack([g, k], 1), axis=0, return_counts=True)
+    return u[:, 1], u[:, 0], cnt.astype(np.int64)
+
+
+def _grouped_worker(rank, ws, port, n, zmin, zmax, users, out):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=ws)
+    per = n // ws
+    lat, lon = synth.generate("hotspots", per, seed=3, start=rank * per)
+    grp = ((np.arange(rank * per, (rank + 1) * per) * 2654435761) >> 7) % users
+    k, g, c = _grouped_cells(lat, lon, grp, zmin, zmax)   # stands in for hm_count_grouped_packed
+    k, g, c = multigpu.merge_grouped(torch.from_numpy(k), torch.from_numpy((g << 32) | c), ws, rank, ops=TorchOps())
+    out[rank] = (k.numpy().copy(), g.numpy().copy(), c.numpy().copy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("ws,users", [(2, 7), (2, 200_000), (3, 50)])
+def test_merge_grouped_ranks(ws, users):
+    """Grouped cells (hm_count_grouped_packed's records) exchanged over ws gloo
+    ranks: every (group, cell) has one owner, the owner is the hash of (group,
+    heatmap row), and the union equals one per-group count of all points;
+    200,000 users pass the merge key's 2^17 groups, so every rank takes the
+    int64-record exchange."""
+    n, zmin, zmax = 24000, 6, 21
+    mgr = mp.Manager()
+    out = mgr.dict()
+    mp.start_processes(_grouped_worker, args=(ws, _port(), n, zmin, zmax, users, out), nprocs=ws, join=True,
+                       start_method="spawn")
+    ks = np.concatenate([out[r][0] for r in range(ws)])
+    gs = np.concatenate([out[r][1] for r in range(ws)])
+    cs = np.concatenate([out[r][2] for r in range(ws)])
+    for r in range(ws):
+        own = multigpu.grouped_owner(torch.from_numpy(out[r][0]), torch.from_numpy(out[r][1]), ws)
+        assert bool((own == r).all())
+    per = n // ws
+    lat, lon = synth.generate("hotspots", per * ws, seed=3)
+    grp = ((np.arange(per * ws) * 2654435761) >> 7) % users
+    ek, eg, ec = _grouped_cells(lat, lon, grp, zmin, zmax)
+    o = np.lexsort((ks, gs))
+    assert np.array_equal(gs[o], eg) and np.array_equal(ks[o], ek) and np.array_equal(cs[o], ec)
