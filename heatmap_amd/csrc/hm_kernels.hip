@@ -591,7 +591,7 @@ static_assert(HM_L1_SLOTS % HM_P1_THREADS == 0, "slots per thread");
 #ifndef HM_L1_WAVES
 #define HM_L1_WAVES 4                       /* k_l1_fast: waves per SIMD its registers allow (4: 2 blocks of 8 waves per CU) */
 #endif
-template <typename OutT>
+template <typename OutT, bool KEEP>
 __global__ __launch_bounds__(HM_P1_THREADS) __attribute__((amdgpu_waves_per_eu(HM_L1_WAVES, HM_L1_WAVES))) void
 k_l1_fast(HmPart1Args a)
 {
@@ -638,8 +638,8 @@ k_l1_fast(HmPart1Args a)
         return sl < HM_MAX_HOT ? sl < H : (sl - HM_MAX_HOT) < (uint32_t)F;
     };
     /* keep bytes, then the tables, then the points (vmcnt retires in order) */
-    uint32_t kp[HM_P1_PPT / 2];
-    if (a.keep) {
+    uint32_t kp[HM_P1_PPT / 2];   /* KEEP: the keep bytes (a keep-less call compiles the test away) */
+    if (KEEP) {
         const uint16_t* kp2 = (const uint16_t*)(a.keep + base);
 #pragma unroll
         for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = kp2[k * HM_P1_THREADS + tid];
@@ -727,7 +727,9 @@ k_l1_fast(HmPart1Args a)
         /* column: y = (lon + 180) / 360 * 2^z within 2^(z-51.3); guard 2^(z-49) */
         const double y = fma(po, kz, c180);
         const double fc = __builtin_amdgcn_fract(y);
-        const bool ok = (int)(fabs(pa) <= HM_LAT_SQ) & (int)(fabs(fr - 0.5) < ghalf) & (int)(fabs(po) < 180.0) &
+        /* |lat| <= HM_LAT_SQ as dd >= 90 - HM_LAT_SQ: both differences are
+         * exact for |lat| in [45, 180] (Sterbenz), dd >= 45 below, NaN fails */
+        const bool ok = (int)(dd >= 90.0 - HM_LAT_SQ) & (int)(fabs(fr - 0.5) < ghalf) & (int)(fabs(po) < 180.0) &
                         (int)(fabs(fc - 0.5) < ghalf2);
         const uint32_t r = (uint32_t)(int32_t)R;   /* truncation = floor: R, y > 0 when ok */
         const uint32_t c = (uint32_t)(int32_t)y;
@@ -3440,8 +3442,13 @@ void hm_launch_part1(hipStream_t s, const HmPart1Args& a0, uint32_t grid, bool o
     } while (0)
     if (full) {
         if (mode == 0 && HM_L1_FAST) {
-            if (out16) hipLaunchKernelGGL(k_l1_fast<uint16_t>, dim3(full), b, 0, s, a);
-            else hipLaunchKernelGGL(k_l1_fast<uint32_t>, dim3(full), b, 0, s, a);
+            if (out16) {
+                if (a.keep) hipLaunchKernelGGL((k_l1_fast<uint16_t, true>), dim3(full), b, 0, s, a);
+                else hipLaunchKernelGGL((k_l1_fast<uint16_t, false>), dim3(full), b, 0, s, a);
+            } else {
+                if (a.keep) hipLaunchKernelGGL((k_l1_fast<uint32_t, true>), dim3(full), b, 0, s, a);
+                else hipLaunchKernelGGL((k_l1_fast<uint32_t, false>), dim3(full), b, 0, s, a);
+            }
         } else if (out16) HM_P1_MODES(uint16_t, true, full);
         else HM_P1_MODES(uint32_t, true, full);
     }

@@ -52,8 +52,15 @@ static_assert(HM_MAX_HOT <= 1024 && (HM_MAX_HOT & 255) == 0, "hot tiles");
 /* bucket of zoom-zb tile (rs, cs), zb <= HM_HOT_BBITS */
 __host__ __device__ inline uint32_t hm_hot_bucket(uint32_t rs, uint32_t cs)
 {
-    return (rs * HM_HOT_MULT + cs) & (HM_HOT_BUCKETS - 1u);   /* v_mad_u32_u24 */
+    /* rs < 2^16 and HM_HOT_MULT < 2^24: a 24-bit multiply-add (the compiler,
+     * unable to bound rs, otherwise picks a 64-bit v_mad_u64_u32) */
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (__umul24(rs, HM_HOT_MULT) + cs) & (HM_HOT_BUCKETS - 1u);
+#else
+    return (rs * HM_HOT_MULT + cs) & (HM_HOT_BUCKETS - 1u);
+#endif
 }
+static_assert(HM_HOT_MULT < (1u << 24), "24-bit hash multiplier");
 static_assert(HM_HOT_BUCKETS == 1 << HM_HOT_BBITS, "hot-tile table");
 /* level-1 (digit, shard) arrays (fill, rbase, rcap) are shard-major: the
  * digits one wave reserves for sit in consecutive words, so its returning
