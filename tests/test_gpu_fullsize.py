@@ -125,3 +125,44 @@ def test_fullsize_grouped_packed(gpu):
     z, r, c = keys >> 58, (keys >> 29) & 0x1FFFFFFF, keys & 0x1FFFFFFF
     gr, cnt = gc >> 32, gc & 0xFFFFFFFF
     assert device_cells_digest(torch, z, (gr << (z + 1)) | r, c, cnt) == g["digest"]
+
+
+def test_fullsize_stream_multi_hour_batches(gpu):
+    """The same 20 x 10M-point stream with 2 or 3 hours per batch (alternating),
+    the concurrent per-bucket path (stream_fold_parts_par: one context, HIP
+    stream and host thread per bucket run): the alltime cells equal the
+    oracle's digest of all 200M points, and the hours of batches 0 and 19,
+    summed (hm_cells_merge), equal their batches' digests."""
+    torch = gpu
+    from heatmap_amd import multigpu
+    from heatmap_amd.stream import ALLTIME, StreamingHeatmap
+
+    base = 480000
+    g = _golden("hotspots_2e8_z0-18_stream20x10M")
+    b = 10_000_000
+    s = StreamingHeatmap(0, 18, base_hour=base, initial_cells=1 << 26)
+    lat = torch.empty(b, dtype=torch.float64, device="cuda")
+    lon = torch.empty(b, dtype=torch.float64, device="cuda")
+    first = {}
+    h0 = base
+    for k in range(20):
+        nh = 2 + (k & 1)
+        first[k] = (h0, nh)
+        device.synth("hotspots", lat, lon, seed=0, start=k * b)
+        hour = (h0 + torch.arange(b, device="cuda", dtype=torch.int64) % nh).to(torch.int32)
+        s.add(lat, lon, hour=hour)
+        h0 += nh
+    n, keys, counts = s.extract_device(ALLTIME)[:3]
+    assert device_digest(torch, keys[:n], counts[:n]) == g["digest"]
+    ops = multigpu.DeviceOps(0)
+    for k, name in ((0, "hotspots_1e7_start0_z0-18"), (19, "hotspots_1e7_start190M_z0-18")):
+        h, nh = first[k]
+        parts = []
+        for j in range(nh):   # (copies: a rollup's outputs may live in the stream's scratch)
+            m, kk, cc = s.extract_device(h + j)[:3]
+            parts.append((kk[:m].clone(), cc[:m].clone()))
+        mk = torch.cat([p[0] for p in parts])
+        mc = torch.cat([p[1] for p in parts])
+        uk, uc = ops.merge(mk, mc)
+        assert device_digest(torch, uk, uc) == _golden(name)["digest"], name
+    s.close()
