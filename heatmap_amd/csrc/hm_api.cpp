@@ -456,6 +456,9 @@ extern "C" int hm_project(hm_ctx* ctx, const double* lat, const double* lon, int
 /* [zmin, Z] (hm_general.hip).  *total = records (all of them, even past the   */
 /* capacity).  Errors (tiles beyond the key's range) go to the error word.      */
 /* ------------------------------------------------------------------------ */
+#ifndef HM_CS_FUSE
+#define HM_CS_FUSE 1   /* packed grouped records: two zoom steps per cascade launch (k_cascade2) */
+#endif
 static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const uint32_t* group, const int64_t* index,
                      uint64_t n, int Z, int zmin, const HmGenEmit& e, uint64_t* total, const double* lat = nullptr,
                      const double* lon = nullptr, const uint8_t* keep = nullptr)
@@ -537,43 +540,58 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     const uint64_t ntc = hm_cascade_tiles(n);
     uint8_t* cs;
     uint32_t *e0, *e1;
-    ENSURE(B_GEN_FLAG, 512 + ntc * 8, cs);
+    ENSURE(B_GEN_FLAG, 512 + 2 * ntc * 8, cs);
     ENSURE(B_GEN_IDX, n * 4, e0);
     ENSURE(B_GEN_C, n * 4, e1);
     unsigned* tick = (unsigned*)cs;
     uint32_t* mdev = (uint32_t*)(cs + 128);
     unsigned long long* rbase = (unsigned long long*)(cs + 256);
     static_assert(HM_MAX_ZOOM + 3 <= 32, "cascade state slots");
-    HIPCHK(hipMemsetAsync(cs, 0, 512 + ntc * 8, s));
+    HIPCHK(hipMemsetAsync(cs, 0, 512 + 2 * ntc * 8, s));
     HmCascArgs ca;
     memset(&ca, 0, sizeof(ca));
     ca.tstat = (uint64_t*)(cs + 512);
+    ca.tstat2 = ca.tstat + ntc;
     ca.e = e;
     ca.hic = down[1];
-    int in = cur;   /* buffer of the step's input keys */
-    for (int k = 0; k <= K; k++) {
+    /* packed records: two zoom steps per launch where two levels of records
+     * are left before the last (k_cascade2) */
+    const bool fuse = HM_CS_FUSE && e.width == 2 && !e.split;
+    int in = cur;                       /* key buffer of the launch's input */
+    uint32_t* ecur = nullptr;           /* ENDs of the input cells (none: raw keys) */
+    uint32_t* eb[2] = {e0, e1};
+    int eo = 0;
+    int slot = 0;                       /* launch index: its count, record base, ticket and epoch */
+    for (int kz = 0;;) {                /* the input level is zoom Z - kz + 1 (kz >= 1), raw keys at kz = 0 */
+        const bool last = kz == K;
+        const bool two = fuse && kz >= 1 && kz + 2 <= K;
         ca.kin_lo = klo[in];
         ca.kin_hi = khi[in];
-        ca.ein = k ? (k & 1 ? e0 : e1) : nullptr;
-        ca.m_in = k ? mdev + (k - 1) : nullptr;
+        ca.ein = ecur;
+        ca.m_in = slot ? mdev + (slot - 1) : nullptr;
         ca.m_host = n;
-        ca.clr = 2 * k;
+        ca.clr = 2 * (two ? kz + 1 : kz);
         ca.Z = Z;
-        ca.zin = Z - k + 1;
-        ca.emit = k > 0;
+        ca.zin = Z - kz + 1;
+        ca.emit = kz > 0;
         ca.kout_lo = klo[1 - in];
         ca.kout_hi = khi[1 - in];
-        ca.eout = k & 1 ? e1 : e0;
-        ca.m_out = mdev + k;
-        ca.epoch = (uint64_t)k + 1;
-        ca.ticket = tick + k;
-        ca.rbase_in = k ? rbase + k : nullptr;
-        ca.rbase_out = k ? rbase + k + 1 : nullptr;
-        hm_launch_cascade(s, ca, n, k == K, wide);
+        ca.eout = eb[eo];
+        ca.m_out = mdev + slot;
+        ca.epoch = (uint64_t)slot + 1;
+        ca.ticket = tick + slot;
+        ca.rbase_in = slot ? rbase + slot : nullptr;
+        ca.rbase_out = slot ? rbase + slot + 1 : nullptr;
+        hm_launch_cascade(s, ca, n, last ? 1 : (two ? 2 : 0), wide);
         HIPCHK(hipGetLastError());
+        slot++;
+        if (last) break;
         in = 1 - in;
+        ecur = eb[eo];
+        eo ^= 1;
+        kz += two ? 2 : 1;
     }
-    HIPCHK(hipMemcpyAsync(down, rbase + K + 1, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(down, rbase + slot, sizeof(uint64_t), hipMemcpyDeviceToHost, s));
     HIPCHK(hm_sync(s));
     *total = down[0];
     return HM_OK;

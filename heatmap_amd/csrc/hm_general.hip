@@ -415,6 +415,196 @@ __global__ __launch_bounds__(HM_CS_THREADS) void k_cascade(HmCascArgs a)
     }
 }
 
+/* Two zoom steps per launch (packed records, width 2): the sorted level-zin
+ * cells in, the records of levels zin AND zin - 1 out, and the level-(zin - 2)
+ * cells for the next launch -- the level-(zin - 1) cells are never written
+ * and read back (24 of every 80 bytes a pair of single steps moves).
+ * A level-(zin - 1) cell holds at most 4 input cells (one zoom, one group),
+ * so the last input cell of its run finds the END before the run at most 4
+ * items back (lane shuffles; lanes 0..3 read the previous fragment's last 4
+ * items from LDS) and writes the record; its slot is the number of
+ * level-(zin - 1) heads up to it, from a second look-back (tstat2, wave 1)
+ * beside the output level's (tstat, wave 0).  a.clr: low key bits cleared
+ * for the OUTPUT level (zin - 2). */
+#ifndef HM_CS2_IT
+#define HM_CS2_IT 16                /* k_cascade2: items per thread of a tile */
+#endif
+#define HM_CS2_TILE (HM_CS_THREADS * HM_CS2_IT)
+template <typename KT>
+__device__ __forceinline__ KT hm_kshfl_up_d(KT k, int d);
+template <>
+__device__ __forceinline__ uint64_t hm_kshfl_up_d<uint64_t>(uint64_t k, int d)
+{
+    return __shfl_up((unsigned long long)k, d, 64);
+}
+template <>
+__device__ __forceinline__ hm_u128 hm_kshfl_up_d<hm_u128>(hm_u128 k, int d)
+{
+    return ((hm_u128)__shfl_up((unsigned long long)(k >> 64), d, 64) << 64) |
+           (hm_u128)__shfl_up((unsigned long long)k, d, 64);
+}
+
+template <typename KT>
+__global__ __launch_bounds__(HM_CS_THREADS) void k_cascade2(HmCascArgs a)
+{
+    constexpr int NW = HM_CS_THREADS / 64, NF = HM_CS2_IT * NW;   /* (round, wave) fragments of a tile */
+    __shared__ uint32_t wtot[NF], wtot1[NF];
+    __shared__ KT kfirst[NF + 1];
+    __shared__ KT klast4[NF + 1][4];      /* [f + 1][j]: lane 60 + j of fragment f; [0]: items t0 - 4 .. t0 - 1 */
+    __shared__ uint32_t elast4[NF + 1][4];
+    __shared__ uint32_t tile_s;
+    __shared__ uint64_t excl_s, excl1_s;
+    const uint64_t m = a.m_in ? (uint64_t)*a.m_in : a.m_host;
+    const uint64_t ntiles = (m + HM_CS2_TILE - 1) / HM_CS2_TILE;
+    const int lane = hm_lane(), w = threadIdx.x >> 6;
+    const KT keep1 = ~((((KT)1) << (a.clr - 2)) - 1);   /* level zin - 1 */
+    const KT keep2 = ~((((KT)1) << a.clr) - 1);         /* level zin - 2 (the output) */
+    const unsigned long long rb = *a.rbase_in, rb1 = rb + m;
+    if (m == 0 && blockIdx.x == 0 && threadIdx.x == 0) {
+        *a.m_out = 0u;
+        *a.rbase_out = rb1;
+    }
+    for (;;) {
+        if (threadIdx.x == 0) tile_s = atomicAdd(a.ticket, 1u);
+        __syncthreads();
+        const uint64_t tile = tile_s;
+        if (tile >= ntiles) break;
+        const uint64_t t0 = tile * HM_CS2_TILE;
+        KT k[HM_CS2_IT];
+        uint32_t e[HM_CS2_IT];
+#pragma unroll
+        for (int r = 0; r < HM_CS2_IT; r++) {
+            const uint64_t i = t0 + (uint64_t)r * HM_CS_THREADS + threadIdx.x;
+            const bool v = i < m;
+            k[r] = v ? hm_kld<KT>(a.kin_lo, a.kin_hi, i) : (KT)0;
+            e[r] = v ? a.ein[i] : 0u;
+        }
+        if (threadIdx.x < 4) {
+            const int64_t j = (int64_t)t0 - 4 + (int64_t)threadIdx.x;
+            klast4[0][threadIdx.x] = j >= 0 ? hm_kld<KT>(a.kin_lo, a.kin_hi, (uint64_t)j) : (KT)0;
+            elast4[0][threadIdx.x] = j >= 0 ? a.ein[j] : 0u;
+        }
+        if (threadIdx.x == HM_CS_THREADS - 1)
+            kfirst[NF] = t0 + HM_CS2_TILE < m ? hm_kld<KT>(a.kin_lo, a.kin_hi, t0 + HM_CS2_TILE) : (KT)0;
+#pragma unroll
+        for (int r = 0; r < HM_CS2_IT; r++) {
+            const int f = r * NW + w;
+            if (lane == 0) kfirst[f] = k[r];
+            if (lane >= 60) {
+                klast4[f + 1][lane - 60] = k[r];
+                elast4[f + 1][lane - 60] = e[r];
+            }
+        }
+        __syncthreads();
+        uint32_t fl[HM_CS2_IT];
+#pragma unroll
+        for (int r = 0; r < HM_CS2_IT; r++) {
+            const int f = r * NW + w;
+            const uint64_t i = t0 + (uint64_t)r * HM_CS_THREADS + threadIdx.x;
+            const bool v = i < m;
+            KT kp = hm_kshfl_up(k[r]), kn = hm_kshfl_down(k[r]);
+            uint32_t ep = __shfl_up(e[r], 1, 64);
+            if (lane == 0) {
+                kp = klast4[f][3];
+                ep = elast4[f][3];
+            }
+            if (lane == 63) kn = kfirst[f + 1];
+            const KT k1 = k[r] & keep1, k2 = k[r] & keep2;
+            const bool head1 = v && (i == 0 || (kp & keep1) != k1);
+            const bool tail1 = v && (i + 1 == m || (kn & keep1) != k1);
+            const bool head2 = v && (i == 0 || (kp & keep2) != k2);
+            const bool tail2 = v && (i + 1 == m || (kn & keep2) != k2);
+            /* the input level's record (its cells are compact: slot rb + i) */
+            if (v) {
+                uint32_t g;
+                int64_t row, col;
+                hm_gen_decode(hm_k128(k[r], a.hic), a.Z, a.zin, &g, &row, &col);
+                hm_put_record(a.e, rb + i, g, a.zin, row, col, (uint64_t)(e[r] - (i ? ep : 0u)));
+            }
+            const uint64_t hb1 = __builtin_amdgcn_ballot_w64(head1), hb2 = __builtin_amdgcn_ballot_w64(head2);
+            /* the lane of this cell's level-(zin - 1) run head, 64: before the fragment */
+            const uint64_t below = hb1 & (((2ull << lane) - 1ull) | (lane == 63 ? ~0ull : 0ull));
+            const uint32_t hl = below ? 63u - (uint32_t)__builtin_clzll(below) : 64u;
+            if (lane == 0) {
+                wtot[f] = (uint32_t)__popcll(hb2);
+                wtot1[f] = (uint32_t)__popcll(hb1);
+            }
+            fl[r] = (uint32_t)head2 | ((uint32_t)tail2 << 1) | (hm_mbcnt(hb2) << 2) | ((uint32_t)tail1 << 9) |
+                    ((hm_mbcnt(hb1) + (uint32_t)head1) << 10) | (hl << 17);
+        }
+        __syncthreads();
+        if (w < 2) {
+            /* wave 0: the output level's heads; wave 1: level zin - 1's */
+            uint32_t* wt = w ? wtot1 : wtot;
+            uint64_t* st = w ? a.tstat2 : a.tstat;
+            const uint32_t x = lane < NF ? wt[lane] : 0u;
+            uint32_t inc = x;
+#pragma unroll
+            for (int o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o, 64);
+                if (lane >= o) inc += y;
+            }
+            const uint64_t agg = __shfl(inc, 63, 64);
+            if (lane < NF) wt[lane] = inc - x;
+            if (lane == 0)
+                __hip_atomic_store(st + tile, hm_cs_word(a.epoch, tile ? HM_CS_FLAG_AGG : HM_CS_FLAG_INC, agg),
+                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t excl = tile ? hm_cs_lookback(st, (int64_t)tile, a.epoch) : 0ull;
+            if (lane == 0) {
+                if (tile)
+                    __hip_atomic_store(st + tile, hm_cs_word(a.epoch, HM_CS_FLAG_INC, excl + agg), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+                if (w == 0) {
+                    if (tile + 1 == ntiles) *a.m_out = (uint32_t)(excl + agg);
+                    excl_s = excl;
+                } else {
+                    if (tile + 1 == ntiles) *a.rbase_out = rb1 + excl + agg;
+                    excl1_s = excl;
+                }
+            }
+        }
+        __syncthreads();
+        const uint64_t excl = excl_s, excl1 = excl1_s;
+#pragma unroll
+        for (int r = 0; r < HM_CS2_IT; r++) {
+            const int f = r * NW + w;
+            const uint64_t j = excl + wtot[r * NW + w] + ((fl[r] >> 2) & 0x7fu);
+            if (fl[r] & 1u) hm_kst(a.kout_lo, a.kout_hi, j, k[r] & keep2);
+            if (fl[r] & 2u) a.eout[j + (fl[r] & 1u) - 1] = e[r];
+            /* the END before this cell's level-(zin - 1) run: its head's
+             * predecessor (one lane shuffle, every lane active), the previous
+             * fragment's last item for a head at lane 0, and for a run that
+             * began before the fragment (lanes 0..2: runs hold <= 4 cells)
+             * the first of that fragment's last items with another key */
+            const uint32_t hl = fl[r] >> 17;
+            uint32_t eb = __shfl(e[r], hl >= 1u && hl < 64u ? (int)hl - 1 : 0, 64);
+            if ((fl[r] >> 9) & 1u) {
+                const KT k1 = k[r] & keep1;
+                if (hl == 0u) {
+                    eb = elast4[f][3];
+                } else if (hl == 64u) {
+                    const int64_t i0 = (int64_t)t0 + (int64_t)f * 64;   /* item of lane 0 */
+                    eb = 0u;
+                    for (int jj = 3; jj >= 0; jj--) {
+                        if (i0 - 4 + jj < 0) break;
+                        if ((klast4[f][jj] & keep1) != k1) {
+                            eb = elast4[f][jj];
+                            break;
+                        }
+                    }
+                }
+                /* the level-(zin - 1) record, by the last cell of its run */
+                const uint64_t q = excl1 + wtot1[f] + ((fl[r] >> 10) & 0x7fu) - 1;
+                uint32_t g;
+                int64_t row, col;
+                hm_gen_decode(hm_k128(k1, a.hic), a.Z, a.zin - 1, &g, &row, &col);
+                hm_put_record(a.e, rb1 + q, g, a.zin - 1, row, col, (uint64_t)(e[r] - eb));
+            }
+        }
+        __syncthreads();
+    }
+}
+
 /* the records of the last level (nothing below it to fold into); split mode
  * reserves its slots once per block and kind */
 template <typename KT>
@@ -769,6 +959,15 @@ int hm_launch_rx_sort(hipStream_t s, bool wide, uint64_t* const* lo, uint64_t* c
 
 void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only, bool wide)
 {
+    if (emit_only == 2) {   /* two zoom steps (k_cascade2) */
+        if (wide)
+            hipLaunchKernelGGL(k_cascade2<hm_u128>, dim3(hm_ggrid(bound, HM_CS2_TILE, 2048)), dim3(HM_CS_THREADS), 0,
+                               s, a);
+        else
+            hipLaunchKernelGGL(k_cascade2<uint64_t>, dim3(hm_ggrid(bound, HM_CS2_TILE, 2048)), dim3(HM_CS_THREADS), 0,
+                               s, a);
+        return;
+    }
     if (emit_only) {
         if (wide)
             hipLaunchKernelGGL(k_cascade_emit<hm_u128>, dim3(hm_ggrid(bound, 256, 4096)), dim3(256), 0, s, a);
@@ -784,7 +983,12 @@ void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int e
     }
 }
 
-uint64_t hm_cascade_tiles(uint64_t n) { return (n + HM_CS_TILE - 1) / HM_CS_TILE; }
+/* look-back words per level: sized for the smaller of the two kernels' tiles */
+uint64_t hm_cascade_tiles(uint64_t n)
+{
+    constexpr uint64_t t = HM_CS_TILE < HM_CS2_TILE ? HM_CS_TILE : HM_CS2_TILE;
+    return (n + t - 1) / t;
+}
 
 void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
                           const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,

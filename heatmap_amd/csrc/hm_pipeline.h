@@ -649,12 +649,15 @@ struct HmCascArgs {
     uint32_t* eout;
     uint32_t* m_out;
     uint64_t* tstat;            /* look-back words, one per tile */
+    uint64_t* tstat2;           /* k_cascade2: the middle level's look-back words */
     uint64_t epoch;             /* distinct per step of a call (tstat zeroed per call) */
     unsigned* ticket;
     const unsigned long long* rbase_in;   /* record offset of the input level */
     unsigned long long* rbase_out;        /* = rbase_in + m (offset of the next level) */
     HmGenEmit e;
 };
+/* emit_only: 0 one zoom step (k_cascade), 1 the last level's records (k_cascade_emit), 2 two zoom steps
+ * (k_cascade2, packed records) */
 void hm_launch_cascade(hipStream_t s, const HmCascArgs& a, uint64_t bound, int emit_only, bool wide);
 uint64_t hm_cascade_tiles(uint64_t n);
 

@@ -66,6 +66,9 @@ VARIANTS = {
     "os24": ["HM_OS_IT=24"],                # one-sweep radix tiles of 6144 keys
     "os32": ["HM_OS_IT=32"],                # one-sweep radix tiles of 8192 keys
     "l1n6": ["HM_L1_NARROW=1", "HM_L1_WAVES=6"],   # k_l1_fast with 4-B staging, 3 blocks per CU (spills)
+    "nofuse": ["HM_CS_FUSE=0"],                      # packed grouped records: one zoom step per cascade launch
+    "cs2it8": ["HM_CS2_IT=8"],                       # k_cascade2: 2048-item tiles
+    "cs2it12": ["HM_CS2_IT=12"],
     "l1nt0": ["HM_L1_NT=0"],                        # K1's point loads without the non-temporal hint
     "l1n4": ["HM_L1_NARROW=1", "HM_L1_WAVES=4"],   # 4-B staging at 2 blocks per CU               # 16K-key partition items (half the (item, child) pairs)                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
 }
