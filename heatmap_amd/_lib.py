@@ -27,7 +27,7 @@ HM_E_NOMEM = 19
 HM_E_WIDE = 20        # hm_cells_route with u32 counts: a count needs 64 bits
 HM_CELLS_U64, HM_CELLS_U32, HM_CELLS_REC10, HM_CELLS_G12 = 8, 4, 10, 12   # exchanged cell layouts
 HM_COUNT_MAX_ZOOM = 21
-HM_ABI_VERSION = 6
+HM_ABI_VERSION = 7
 HM_SPAN_HOUR, HM_SPAN_DAY, HM_SPAN_MONTH, HM_SPAN_YEAR, HM_SPAN_ALLTIME = 0, 1, 2, 3, 4
 
 EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_stream", "hm_ctx_destroy", "hm_ctx_tune",
@@ -36,7 +36,7 @@ EXPORTS = ["hm_abi_version", "hm_status_string", "hm_ctx_create", "hm_ctx_set_st
            "hm_stream_create", "hm_stream_add", "hm_stream_cells", "hm_stream_rollup", "hm_stream_extract",
            "hm_stream_destroy",
            "hm_dense_grid_size", "hm_cells_route", "hm_cells_merge", "hm_cells_merge_runs",
-           "hm_dense_cells", "hm_format_bins", "hm_format_ids", "hm_bench_read"]
+           "hm_cells_route_pieces", "hm_cells_merge_pieces", "hm_dense_cells", "hm_format_bins", "hm_format_ids", "hm_bench_read"]
 
 _LIB = None
 _LOCK = threading.Lock()
@@ -117,6 +117,10 @@ def load() -> ctypes.CDLL:
         L.hm_cells_merge.argtypes = [vp, vp, vp, c.c_int, c.c_int64, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_cells_merge_runs.argtypes = [vp, vp, vp, c.c_int, c.c_int64, P(c.c_int64), c.c_int, vp, vp, c.c_int64,
                                           P(c.c_int64)]
+        L.hm_cells_route_pieces.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp, vp,
+                                            c.c_int, vp, c.c_int]
+        L.hm_cells_merge_pieces.argtypes = [vp, c.c_int, c.c_int, P(vp), P(vp), P(c.c_int64), c.c_int, vp, vp,
+                                            c.c_int64, P(c.c_int64)]
         L.hm_dense_cells.argtypes = [vp, vp, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_format_bins.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, c.c_int64, vp]
         L.hm_format_ids.argtypes = [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp, c.c_int64, vp]

@@ -168,7 +168,7 @@ enum {
     B_L1_FILL, B_L1_RBASE, B_L1_RCAP, B_L1_HIST, B_L1_SMASK,
     B_RT_CNT, B_RT_OFF, B_MG_TABLE, B_MG_STATE, B_SEG, B_RS_BIG,
     B_HOT, B_HOT_COUNTS, B_HOT_PARENT, B_D2B, B_MB_CNT, B_MB_OFF, B_MB_KEYS, B_MB_COUNTS, B_MB_CNT2, B_MB_OFF2,
-    B_MB_KEYS2, B_MB_COUNTS2, B_KEYS_C, B_HOT_FORCE, B_C2B, B_SEG2, B_CTOT, B_CBASE, B_CCUR,
+    B_MB_KEYS2, B_MB_COUNTS2, B_KEYS_C, B_HOT_FORCE, B_C2B, B_SEG2, B_CTOT, B_CBASE, B_CCUR, B_MG_PIECES,
     B_COUNT
 };
 
@@ -1872,6 +1872,191 @@ extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const void* keys, const void* co
 {
     if (!cells_layout_ok(layout)) return HM_E_ARG;
     return cells_merge(ctx, keys, counts, layout, n, runs, nruns, keys_out, counts_out, capacity, n_out);
+}
+
+/* the pieces exchange (hm_merge.hip, "the pieces exchange"): the route orders
+ * each owner's group by the first merge digit, so the owner gathers digit
+ * s's pieces, partitions them by the next bits and merges */
+extern "C" int hm_cells_route_pieces(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
+                                     int nranks, int delta, int dense_zmax, int bits, uint64_t* grid, void* keys_out,
+                                     void* counts_out, int layout, int64_t* sizes, int stride)
+{
+    const bool rec = layout == HM_CELLS_REC10, grp = layout == HM_CELLS_G12;
+    if (!ctx || n < 0 || nranks < 1 || nranks > 64 || delta < 0 || delta > 28 || dense_zmax > 14 || bits < 0 ||
+        bits > 7 || ((int64_t)nranks << bits) > HM_XR_MAXD || stride < 2 + (1 << bits) || !sizes ||
+        (layout != HM_CELLS_U32 && layout != HM_CELLS_U64 && !rec && !grp) || (dense_zmax >= 0 && !grid) ||
+        (grp && dense_zmax >= 0) || (n > 0 && (!keys || !counts || !keys_out || (!rec && !counts_out))) ||
+        (rec && ((uintptr_t)keys_out & 1)))
+        return HM_E_ARG;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    const int64_t gsz = hm_dense_grid_size(dense_zmax);
+    if (gsz > 0) HIPCHK(hipMemsetAsync(grid, 0, (size_t)gsz * 8, s));
+    HmRouteArgs a;
+    memset(&a, 0, sizeof(a));
+    a.C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(1024, ((uint64_t)n + 16383) / 16384));
+    const uint64_t m = ((uint64_t)nranks << bits) * a.C;
+    ENSURE(B_RT_CNT, m * 8, a.block_cnt);
+    uint64_t* off;
+    ENSURE(B_RT_OFF, (m + 2) * 8, off);    /* + the total, + the wide flag */
+    uint64_t* partial;
+    ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+    a.keys = keys;
+    a.counts = counts;
+    a.n = (uint64_t)n;
+    a.nranks = nranks;
+    a.delta = delta;
+    a.dense_zmax = dense_zmax;
+    a.grid = grid;
+    a.block_off = off;
+    a.bits = bits;
+    a.sizes = (long long*)sizes;
+    a.stride = stride;
+    if (layout == HM_CELLS_U64) {
+        a.keys_out = (uint64_t*)keys_out;
+        a.counts_out = (uint64_t*)counts_out;
+    } else if (rec) {
+        a.rec_out = (uint16_t*)keys_out;
+    } else {
+        a.keys_out = (uint64_t*)keys_out;
+        a.counts_out32 = (uint32_t*)counts_out;
+        a.grouped = grp;
+    }
+    if (layout != HM_CELLS_U64) {
+        a.wide = (unsigned long long*)(off + m + 1);
+        HIPCHK(hipMemsetAsync(a.wide, 0, 8, s));
+    }
+    hm_launch_xroute(s, a, false, layout);
+    hm_launch_scan(s, a.block_cnt, m, partial, off, off + m);
+    if (n > 0) hm_launch_xroute(s, a, true, layout);
+    hm_launch_xroute_sizes(s, a);
+    HIPCHK(hipGetLastError());
+    return HM_OK;
+}
+
+extern "C" int hm_cells_merge_pieces(hm_ctx* ctx, int layout, int nruns, const void* const* key_src,
+                                     const void* const* count_src, const int64_t* pieces, int bits,
+                                     uint64_t* keys_out, uint64_t* counts_out, int64_t capacity, int64_t* n_out)
+{
+    const bool rec = layout == HM_CELLS_REC10, c64 = layout == HM_CELLS_U64;
+    if (!ctx || !n_out || nruns < 1 || nruns > 64 || bits < 0 || bits > 7 || !pieces || !key_src ||
+        (layout != HM_CELLS_U32 && !c64 && layout != HM_CELLS_G12 && !rec) || (!rec && !count_src) ||
+        capacity < 0 || (capacity > 0 && (!keys_out || !counts_out)))
+        return HM_E_ARG;
+    const uint32_t S = 1u << bits, R = (uint32_t)nruns;
+    uint64_t n = 0;
+    for (uint32_t r = 0; r < R; r++) {
+        uint64_t len = 0;
+        for (uint32_t d = 0; d < S; d++) {
+            if (pieces[r * S + d] < 0) return HM_E_ARG;
+            len += (uint64_t)pieces[r * S + d];
+        }
+        if (len && (!key_src[r] || (!rec && !count_src[r]) || (rec && ((uintptr_t)key_src[r] & 1))))
+            return HM_E_ARG;
+        n += len;
+    }
+    *n_out = 0;
+    if (n == 0) return HM_OK;
+    HIPCHK(hipSetDevice(ctx->device));
+    hipStream_t s = ctx->stream;
+    unsigned long long* down = ctx->host_state + 2 * ST_COUNT;
+    /* buckets of <= HM_MB2_TARGET cells (one LDS table pass each) */
+    int lb = bits;
+    while (lb < bits + 8 && (n >> lb) > HM_MB2_TARGET) lb++;
+    const int b2 = lb - bits;
+    /* piece table: vpre [S][R + 1], key address [S][R], count address [S][R] */
+    const size_t ksz = rec ? 10 : 8, csz = c64 ? 8 : 4;
+    std::vector<unsigned long long> tab((size_t)S * (R + 1) + 2 * (size_t)S * R, 0ull);
+    unsigned long long *vpre = tab.data(), *kp = vpre + (size_t)S * (R + 1), *cp = kp + (size_t)S * R;
+    for (uint32_t r = 0; r < R; r++) {
+        uint64_t e = 0;   /* cells of run r before piece d */
+        for (uint32_t d = 0; d < S; d++) {
+            kp[d * R + r] = (unsigned long long)((uintptr_t)key_src[r] + e * ksz);
+            cp[d * R + r] = rec ? 0ull : (unsigned long long)((uintptr_t)count_src[r] + e * csz);
+            e += (uint64_t)pieces[r * S + d];
+        }
+    }
+    for (uint32_t d = 0; d < S; d++) {
+        uint64_t v = 0;
+        for (uint32_t r = 0; r < R; r++) {
+            vpre[d * (R + 1) + r] = v;
+            v += (uint64_t)pieces[r * S + d];
+        }
+        vpre[d * (R + 1) + R] = v;
+    }
+    unsigned long long* dtab;
+    ENSURE(B_MG_PIECES, tab.size() * 8, dtab);
+    HIPCHK(hipMemcpyAsync(dtab, tab.data(), tab.size() * 8, hipMemcpyHostToDevice, s));
+    HmMbGather g;
+    memset(&g, 0, sizeof(g));
+    g.vpre = dtab;
+    g.kp = dtab + (size_t)S * (R + 1);
+    g.cp = rec ? nullptr : g.kp + (size_t)S * R;
+    g.R = R;
+    g.S = S;
+    g.C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, ((n >> bits) + 32767) / 32768));
+    g.shift = lb ? 64 - lb : 63;
+    g.bits = b2;
+    g.in_layout = rec ? HM_CELLS_REC10 : (c64 ? HM_CELLS_U64 : HM_CELLS_U32);
+    const uint64_t m2 = ((uint64_t)S << b2) * g.C;
+    uint64_t *cnt2, *off2, *qk, *partial;
+    void* qc;
+    ENSURE(B_MB_CNT2, m2 * 8, cnt2);
+    ENSURE(B_MB_OFF2, (m2 + 1) * 8, off2);
+    ENSURE(B_MB_KEYS2, n * 8, qk);
+    ENSURE(B_MB_COUNTS2, n * csz, qc);
+    ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
+    g.cnt = cnt2;
+    g.off = off2;
+    g.kout = qk;
+    g.cout = qc;
+    hm_launch_mb_gather(s, g, false);
+    hm_launch_scan(s, cnt2, m2, partial, off2, off2 + m2);
+    hm_launch_mb_gather(s, g, true);
+    HmMergeArgs a;
+    memset(&a, 0, sizeof(a));
+    a.pkeys = qk;
+    if (c64) a.pcounts = (uint64_t*)qc;
+    else a.pcounts32 = (const uint32_t*)qc;
+    a.boff = off2;
+    a.nblocks = g.C;
+    a.n = n;
+    a.lb = lb;
+    unsigned long long* st;
+    ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), st);
+    HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
+    a.keys_out = keys_out;
+    a.counts_out = counts_out;
+    a.cap = (uint64_t)capacity;
+    a.cursor = st;
+    a.overflow = st + 1;
+    hm_launch_mb_merge2(s, a);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(down, st, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hm_sync(s));
+    if (!down[1]) {
+        *n_out = (int64_t)down[0];
+        return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
+    }
+    /* a bucket's table filled up (adversarial hash collisions): a global hash
+     * table takes the partitioned cells */
+    uint64_t cap = 1024;
+    while (cap < 2 * n) cap <<= 1;
+    HmsTable t;
+    ENSURE(B_MG_TABLE, cap * 16, t.slots);
+    ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), t.state);
+    t.mask = cap - 1;
+    HIPCHK(hipMemsetAsync(t.state, 0, 8 * sizeof(unsigned long long), s));
+    hm_launch_stream_init(s, t);
+    if (c64) hm_launch_cells_merge(s, qk, (const uint64_t*)qc, n, t);
+    else hm_launch_cells_merge32(s, qk, (const uint32_t*)qc, n, t);
+    hm_launch_table_extract(s, t, keys_out, counts_out, (uint64_t)capacity, t.state + HMS_ST_CURSOR);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipMemcpyAsync(down, t.state, 4 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hm_sync(s));
+    if (down[HMS_ST_OVERFLOW]) return HM_E_HIP;
+    *n_out = (int64_t)down[HMS_ST_CURSOR];
+    return *n_out > capacity ? HM_E_CAPACITY : HM_OK;
 }
 
 extern "C" int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out,

@@ -21,6 +21,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+#include <type_traits>
+
 #include "hm_device.h"
 #include "hm_pipeline.h"
 #include "hm_table.h"
@@ -140,8 +143,9 @@ __global__ __launch_bounds__(HM_ROUTE_THREADS) void k_cells_route(HmRouteArgs a)
     if (!SCATTER && tid < a.nranks) a.block_cnt[(uint64_t)tid * gridDim.x + blockIdx.x] = hist[tid];
 }
 
-__global__ __launch_bounds__(256) void k_cells_merge(const uint64_t* __restrict__ keys,
-                                                     const uint64_t* __restrict__ counts, uint64_t n, HmsTable t)
+template <typename CT>
+__global__ __launch_bounds__(256) void k_cells_merge(const uint64_t* __restrict__ keys, const CT* __restrict__ counts,
+                                                     uint64_t n, HmsTable t)
 {
     uint32_t overflow = 0;
     const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
@@ -447,6 +451,492 @@ void hm_launch_mb_merge(hipStream_t s, const HmMergeArgs& a)
     hipLaunchKernelGGL(k_mb_merge, dim3(1u << a.lb), dim3(HM_MB_THREADS), 0, s, a);
 }
 
+/* ---- the pieces exchange (hm_cells_route_pieces / hm_cells_merge_pieces) ----
+ * The sender's route already partitions its cells by owner; it now orders each
+ * owner's group by the first merge digit as well (the top `bits` bits of the
+ * merge key's hash), so the owner skips the first partition pass: it gathers
+ * digit s's piece of every sender (one chunked segment per digit), partitions
+ * it by the next bits, and merges buckets of <= ~1000 cells in LDS. */
+#define HM_XR_PPT 8
+#define HM_XR_TILE (256 * HM_XR_PPT)
+
+struct HmXCell {
+    uint32_t d;     /* digit, or ~0u: not routed (dense zoom / past the input) */
+    uint64_t mk;    /* merge key */
+};
+
+__device__ __forceinline__ HmXCell hm_xr_cell(const HmRouteArgs& a, uint64_t k, uint64_t cn, bool in)
+{
+    HmXCell x;
+    const int z = (int)(k >> 58);
+    const bool sp = in && z > a.dense_zmax;
+    const uint32_t g = a.grouped ? (uint32_t)(cn >> 32) : 0u;
+    x.mk = a.grouped ? hm_gkey(k, g) : k;
+    const uint32_t o = sp ? hm_owner(k, a.delta, a.nranks, a.grouped ? (uint64_t)g + 1 : 0ull) : 0u;
+    const uint32_t h = a.bits ? (uint32_t)(hms_hash(x.mk) >> (64 - a.bits)) : 0u;
+    x.d = sp ? (o << a.bits) | h : ~0u;
+    return x;
+}
+
+/* count pass: per-block digit histogram (+ the dense grid's atomics and the
+ * wide flag, as k_cells_route<false>) */
+__global__ __launch_bounds__(256) void k_xroute_count(HmRouteArgs a)
+{
+    __shared__ uint32_t hist[HM_XR_MAXD];
+    const int tid = threadIdx.x;
+    const uint32_t D = (uint32_t)a.nranks << a.bits;
+    for (uint32_t d = tid; d < D; d += 256) hist[d] = 0;
+    __syncthreads();
+    const uint64_t c0 = a.n * blockIdx.x / gridDim.x, c1 = a.n * (blockIdx.x + 1) / gridDim.x;
+    bool wide = false;
+    for (uint64_t t0 = c0; t0 < c1; t0 += HM_XR_TILE) {
+        uint64_t k[HM_XR_PPT], cn[HM_XR_PPT];
+#pragma unroll
+        for (int j = 0; j < HM_XR_PPT; j++) {
+            const uint64_t i = t0 + j * 256 + tid;
+            k[j] = i < c1 ? a.keys[i] : 0ull;
+            cn[j] = i < c1 ? a.counts[i] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < HM_XR_PPT; j++) {
+            const bool in = t0 + j * 256 + tid < c1;
+            const int z = (int)(k[j] >> 58);
+            if (in && z <= a.dense_zmax) {
+                const uint64_t r = (k[j] >> 29) & 0x1FFFFFFFull, c = k[j] & 0x1FFFFFFFull;
+                const uint64_t off = ((1ull << (2 * z)) - 1) / 3;
+                atomicAdd((unsigned long long*)&a.grid[off + ((hm_spread29(r) << 1) | hm_spread29(c))],
+                          (unsigned long long)cn[j]);
+            }
+            const HmXCell x = hm_xr_cell(a, k[j], cn[j], in);
+            if (x.d != ~0u) {
+                atomicAdd(&hist[x.d], 1u);
+                const uint64_t kk = k[j];
+                const bool kw = (a.rec_out || a.grouped) && (z > 21 || ((kk >> 29) & 0x1FFFFFFFull) >= (1ull << 21) ||
+                                                             (kk & 0x1FFFFFFFull) >= (1ull << 21));
+                const bool cw = a.grouped ? (cn[j] >> 32) >= (1ull << HM_GKEY_GROUP_BITS) : (cn[j] >> 32) != 0ull;
+                wide |= kw || cw;
+            }
+        }
+    }
+    if (a.wide && __any(wide) && (tid & 63) == 0) atomicOr(a.wide, 1ull);
+    __syncthreads();
+    for (uint32_t d = tid; d < D; d += 256) a.block_cnt[(uint64_t)d * a.C + blockIdx.x] = hist[d];
+}
+
+/* scatter pass: each 2048-cell tile is ordered by digit in LDS, then every
+ * digit's cells are written as one run at the block's running offset (the
+ * runs of consecutive tiles of a block continue each other).  OUT: 0 records
+ * (REC10), 1 u64 keys + u64 counts, 2 u64 keys + u32 counts (U32, G12) */
+template <int OUT>
+__global__ __launch_bounds__(256) void k_xroute_scatter(HmRouteArgs a)
+{
+    typedef typename std::conditional<OUT == 1, unsigned long long, uint32_t>::type CT;
+    __shared__ uint32_t hist[HM_XR_MAXD];
+    __shared__ uint32_t toff[HM_XR_MAXD];
+    __shared__ unsigned long long gb[HM_XR_MAXD];
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long sk[HM_XR_TILE];
+    __shared__ CT sc[HM_XR_TILE];
+    __shared__ uint16_t sd[HM_XR_TILE];
+    const int tid = threadIdx.x;
+    const uint32_t D = (uint32_t)a.nranks << a.bits;
+    const uint32_t per = (D + 255) / 256;   /* digits per thread in the tile scan */
+    for (uint32_t d = tid; d < D; d += 256) {
+        hist[d] = 0;
+        gb[d] = a.block_off[(uint64_t)d * a.C + blockIdx.x];
+    }
+    __syncthreads();
+    const uint64_t c0 = a.n * blockIdx.x / gridDim.x, c1 = a.n * (blockIdx.x + 1) / gridDim.x;
+    for (uint64_t t0 = c0; t0 < c1; t0 += HM_XR_TILE) {
+        uint64_t k[HM_XR_PPT], cn[HM_XR_PPT];
+        uint32_t d[HM_XR_PPT], r[HM_XR_PPT];
+#pragma unroll
+        for (int j = 0; j < HM_XR_PPT; j++) {
+            const uint64_t i = t0 + j * 256 + tid;
+            k[j] = i < c1 ? a.keys[i] : 0ull;
+            cn[j] = i < c1 ? a.counts[i] : 0ull;
+        }
+#pragma unroll
+        for (int j = 0; j < HM_XR_PPT; j++) {
+            const HmXCell x = hm_xr_cell(a, k[j], cn[j], t0 + j * 256 + tid < c1);
+            d[j] = x.d;
+            if (OUT == 2 && a.grouped) k[j] = x.mk;
+            r[j] = x.d != ~0u ? atomicAdd(&hist[x.d], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t loc = 0;
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t dd = tid * per + q;
+            loc += dd < D ? hist[dd] : 0u;
+        }
+        uint32_t tot;
+        uint32_t o = hm_block_excl_scan<256>(loc, scr, &tot);
+        for (uint32_t q = 0; q < per; q++) {
+            const uint32_t dd = tid * per + q;
+            if (dd < D) {
+                toff[dd] = o;
+                o += hist[dd];
+            }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < HM_XR_PPT; j++) {
+            if (d[j] != ~0u) {
+                const uint32_t pos = toff[d[j]] + r[j];
+                sk[pos] = k[j];
+                sc[pos] = (CT)cn[j];
+                sd[pos] = (uint16_t)d[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < tot; i += 256) {
+            const uint32_t dd = sd[i];
+            const uint64_t q = gb[dd] + (i - toff[dd]);
+            if (OUT == 0) {
+                hm_rec_put(a.rec_out + 5 * q, sk[i], (uint32_t)sc[i]);
+            } else {
+                a.keys_out[q] = sk[i];
+                if (OUT == 1) a.counts_out[q] = sc[i];
+                else a.counts_out32[q] = (uint32_t)sc[i];
+            }
+        }
+        __syncthreads();
+        for (uint32_t dd = tid; dd < D; dd += 256) {
+            gb[dd] += hist[dd];
+            hist[dd] = 0;
+        }
+        __syncthreads();
+    }
+}
+
+/* per-owner rows of the device sizes array: sent, wide, pieces */
+__global__ __launch_bounds__(256) void k_xroute_sizes(HmRouteArgs a)
+{
+    const uint32_t S = 1u << a.bits, D = (uint32_t)a.nranks << a.bits;
+    const unsigned long long wide = a.wide ? *a.wide : 0ull;
+    for (uint32_t d = threadIdx.x; d < D; d += 256) {
+        const uint32_t o = d >> a.bits, s = d & (S - 1);
+        long long* row = a.sizes + (uint64_t)o * a.stride;
+        row[2 + s] = (long long)(a.block_off[(uint64_t)(d + 1) * a.C] - a.block_off[(uint64_t)d * a.C]);
+        if (s == 0) {
+            row[0] = (long long)(a.block_off[(uint64_t)(d + S) * a.C] - a.block_off[(uint64_t)d * a.C]);
+            row[1] = wide ? 1ll : 0ll;
+        }
+    }
+}
+
+void hm_launch_xroute(hipStream_t s, const HmRouteArgs& a, bool scatter, int layout)
+{
+    if (!scatter)
+        hipLaunchKernelGGL(k_xroute_count, dim3(a.C), dim3(256), 0, s, a);
+    else if (layout == 10)
+        hipLaunchKernelGGL(k_xroute_scatter<0>, dim3(a.C), dim3(256), 0, s, a);
+    else if (layout == 8)
+        hipLaunchKernelGGL(k_xroute_scatter<1>, dim3(a.C), dim3(256), 0, s, a);
+    else
+        hipLaunchKernelGGL(k_xroute_scatter<2>, dim3(a.C), dim3(256), 0, s, a);
+}
+
+void hm_launch_xroute_sizes(hipStream_t s, const HmRouteArgs& a)
+{
+    hipLaunchKernelGGL(k_xroute_sizes, dim3(1), dim3(256), 0, s, a);
+}
+
+/* owner: partition digit s's pieces by the next bits.  IN: 0 records, 1 u32
+ * counts, 2 u64 counts (kept u64 in the output) */
+#define HM_MG_PPT 16
+#define HM_MG_TILE (256 * HM_MG_PPT)
+#define HM_MG_MAXD 256
+#define HM_MG_MAXR 64
+template <bool SCATTER, int IN>
+__global__ __launch_bounds__(256) void k_mb_gather(HmMbGather a)
+{
+    typedef typename std::conditional<IN == 2, unsigned long long, uint32_t>::type CT;
+    __shared__ uint32_t hist[HM_MG_MAXD];
+    __shared__ uint32_t toff[HM_MG_MAXD];
+    __shared__ unsigned long long gb[HM_MG_MAXD];
+    __shared__ unsigned long long vp[HM_MG_MAXR + 1], kp[HM_MG_MAXR], cp[HM_MG_MAXR];
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long sk[SCATTER ? HM_MG_TILE : 1];
+    __shared__ CT sc[SCATTER ? HM_MG_TILE : 1];
+    __shared__ uint8_t sd[SCATTER ? HM_MG_TILE : 1];
+    const int tid = threadIdx.x;
+    const uint32_t s = blockIdx.x / a.C, c = blockIdx.x % a.C;
+    const uint32_t R = a.R, nd = 1u << a.bits, dm = nd - 1u;
+    if (tid <= (int)R) vp[tid] = a.vpre[(uint64_t)s * (R + 1) + tid];
+    if (tid < (int)R) {
+        kp[tid] = a.kp[(uint64_t)s * R + tid];
+        cp[tid] = a.cp ? a.cp[(uint64_t)s * R + tid] : 0ull;
+    }
+    const uint64_t cbase = ((uint64_t)s << a.bits) * a.C + c;   /* + d * C */
+    for (uint32_t d = tid; d < nd; d += 256) {
+        hist[d] = 0;
+        if (SCATTER) gb[d] = a.off[cbase + (uint64_t)d * a.C];
+    }
+    __syncthreads();
+    const uint64_t len = vp[R];
+    const uint64_t c0 = len * c / a.C, c1 = len * (c + 1) / a.C;
+    for (uint64_t t0 = c0; t0 < c1; t0 += HM_MG_TILE) {
+        const uint32_t tn = (uint32_t)min((uint64_t)HM_MG_TILE, c1 - t0);
+        uint64_t k[HM_MG_PPT];
+        CT cc[HM_MG_PPT];
+#pragma unroll
+        for (int j = 0; j < HM_MG_PPT; j++) {
+            const uint32_t i = j * 256 + tid;
+            k[j] = 0ull;
+            cc[j] = 0;
+            if (i < tn) {
+                const uint64_t v = t0 + i;
+                uint32_t lo = 0, hi = R;   /* the last piece starting at or before v */
+                while (hi - lo > 1) {
+                    const uint32_t mid = (lo + hi) >> 1;
+                    if (vp[mid] <= v) lo = mid;
+                    else hi = mid;
+                }
+                const uint64_t e = v - vp[lo];
+                if (IN == 0) {
+                    const uint16_t* rp = (const uint16_t*)kp[lo] + 5 * e;
+                    k[j] = hm_rec_key(rp);
+                    cc[j] = hm_rec_count(rp);
+                } else {
+                    k[j] = ((const uint64_t*)kp[lo])[e];
+                    cc[j] = IN == 1 ? (CT)((const uint32_t*)cp[lo])[e] : (CT)((const uint64_t*)cp[lo])[e];
+                }
+            }
+        }
+        if (!SCATTER) {
+#pragma unroll
+            for (int j = 0; j < HM_MG_PPT; j++)
+                if ((uint32_t)(j * 256 + tid) < tn) atomicAdd(&hist[(uint32_t)(hms_hash(k[j]) >> a.shift) & dm], 1u);
+            continue;
+        }
+        uint32_t d[HM_MG_PPT], r[HM_MG_PPT];
+#pragma unroll
+        for (int j = 0; j < HM_MG_PPT; j++) {
+            const bool v = (uint32_t)(j * 256 + tid) < tn;
+            d[j] = (uint32_t)(hms_hash(k[j]) >> a.shift) & dm;
+            r[j] = v ? atomicAdd(&hist[d[j]], 1u) : 0u;
+        }
+        __syncthreads();
+        uint32_t tot;
+        const uint32_t o = hm_block_excl_scan<256>(tid < (int)nd ? hist[tid] : 0u, scr, &tot);
+        if (tid < (int)nd) toff[tid] = o;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < HM_MG_PPT; j++) {
+            if ((uint32_t)(j * 256 + tid) < tn) {
+                const uint32_t pos = toff[d[j]] + r[j];
+                sk[pos] = k[j];
+                sc[pos] = cc[j];
+                sd[pos] = (uint8_t)d[j];
+            }
+        }
+        __syncthreads();
+        for (uint32_t i = tid; i < tn; i += 256) {
+            const uint32_t dd = sd[i];
+            const uint64_t dst = gb[dd] + (i - toff[dd]);
+            a.kout[dst] = sk[i];
+            ((CT*)a.cout)[dst] = sc[i];
+        }
+        __syncthreads();
+        if (tid < (int)nd) {
+            gb[tid] += hist[tid];
+            hist[tid] = 0;
+        }
+        __syncthreads();
+    }
+    if (!SCATTER) {
+        __syncthreads();
+        for (uint32_t d = tid; d < nd; d += 256) a.cnt[cbase + (uint64_t)d * a.C] = hist[d];
+    }
+}
+
+void hm_launch_mb_gather(hipStream_t s, const HmMbGather& a, bool scatter)
+{
+    const unsigned g = a.S * a.C;
+#define HM_MG_L(SC, IN) hipLaunchKernelGGL((k_mb_gather<SC, IN>), dim3(g), dim3(256), 0, s, a)
+    if (a.in_layout == 10) {
+        if (scatter) HM_MG_L(true, 0);
+        else HM_MG_L(false, 0);
+    } else if (a.in_layout == 8) {
+        if (scatter) HM_MG_L(true, 2);
+        else HM_MG_L(false, 2);
+    } else {
+        if (scatter) HM_MG_L(true, 1);
+        else HM_MG_L(false, 1);
+    }
+#undef HM_MG_L
+}
+
+/* buckets of <= ~1000 cells, 256-thread blocks each looping over buckets
+ * b = blockIdx, + gridDim, ... (a few blocks per CU): a 2048-slot LDS table,
+ * distinct cells out in slot order (a wave's stores consecutive), one output
+ * reservation per bucket.  The next bucket's cells (<= 4 a thread) are loaded
+ * into registers while this one is merged, and its bounds one bucket earlier
+ * still, so a block's loads overlap its LDS work.  C32: u32 input counts
+ * and (TC32) u32 table counts -- 24 KB, 6 blocks a CU; a sum that carries out
+ * of 32 bits sets the overflow flag (the caller's global table takes over). */
+#ifndef HM_MB2_TC32
+#define HM_MB2_TC32 1
+#endif
+#define HM_MB2_PF ((HM_MB2_TS / 2 + HM_MB2_T - 1) / HM_MB2_T)
+template <bool C32>
+__global__ __launch_bounds__(HM_MB2_T) void k_mb_merge2(HmMergeArgs a)
+{
+    constexpr bool TC32 = C32 && HM_MB2_TC32;
+    typedef typename std::conditional<TC32, uint32_t, unsigned long long>::type TC;
+    __shared__ unsigned long long tk[HM_MB2_TS];
+    __shared__ TC tc[HM_MB2_TS];
+    constexpr int SPT = HM_MB2_TS / HM_MB2_T, NW = HM_MB2_T / 64, PF = HM_MB2_PF;
+    constexpr int NF = SPT * NW, FPL = (NF + 63) / 64;   /* fragments, per lane of the scan */
+    __shared__ uint32_t wc[NF + 1];
+    __shared__ unsigned long long sbase;
+    __shared__ uint32_t full;
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const uint32_t nb = 1u << a.lb, G = gridDim.x;
+    auto bounds = [&](uint32_t bb, uint64_t& f0, uint64_t& f1) {
+        f0 = bb < nb ? a.boff[(uint64_t)bb * a.nblocks] : 0ull;
+        f1 = bb < nb ? a.boff[(uint64_t)(bb + 1) * a.nblocks] : 0ull;
+    };
+    auto fetch = [&](uint64_t f0, uint64_t f1, uint64_t (&k)[PF], uint32_t (&c)[PF], uint64_t (&c64)[PF]) {
+#pragma unroll
+        for (int j = 0; j < PF; j++) {
+            const uint64_t i = f0 + j * HM_MB2_T + tid;
+            const bool v = i < f1;
+            k[j] = v ? a.pkeys[i] : HMS_EMPTY;
+            if (C32) c[j] = v ? a.pcounts32[i] : 0u;
+            else c64[j] = v ? a.pcounts[i] : 0ull;
+        }
+    };
+#pragma unroll
+    for (int j = 0; j < SPT; j++) {
+        tk[j * HM_MB2_T + tid] = HMS_EMPTY;
+        tc[j * HM_MB2_T + tid] = 0;
+    }
+    if (tid == 0) full = 0;
+    uint64_t e0, e1, n0, n1;
+    bounds(blockIdx.x, e0, e1);
+    bounds(blockIdx.x + G, n0, n1);
+    uint64_t ck[PF], cc64[PF];
+    uint32_t cc[PF];
+    fetch(e0, e1, ck, cc, cc64);
+    __syncthreads();
+    for (uint32_t b = blockIdx.x; b < nb; b += G) {
+        const uint64_t size = e1 - e0;
+        const bool fast = size <= (uint64_t)PF * HM_MB2_T;
+        const uint32_t P = fast ? 1u : (uint32_t)((size + HM_MB2_TS / 2 - 1) / (HM_MB2_TS / 2));
+        auto insert = [&](uint64_t k, uint64_t c, uint32_t pass) {
+            if (k == HMS_EMPTY) return;
+            const uint64_t h = hms_hash(k);
+            if (P > 1 && (uint32_t)((h >> 32) % P) != pass) return;
+            uint32_t sl = (uint32_t)h & (HM_MB2_TS - 1);
+            for (int probes = 0;; probes++) {
+                const unsigned long long o = atomicCAS(&tk[sl], (unsigned long long)HMS_EMPTY, (unsigned long long)k);
+                if (o == HMS_EMPTY || o == k) {
+                    if (TC32) {
+                        if (atomicAdd((uint32_t*)&tc[sl], (uint32_t)c) + (uint32_t)c < (uint32_t)c) full = 1;
+                    } else {
+                        atomicAdd((unsigned long long*)&tc[sl], (unsigned long long)c);
+                    }
+                    return;
+                }
+                sl = (sl + 1) & (HM_MB2_TS - 1);
+                if (probes == HM_MB2_TS) {
+                    full = 1;
+                    return;
+                }
+            }
+        };
+        for (uint32_t pass = 0; pass < P; pass++) {
+            if (fast) {
+#pragma unroll
+                for (int j = 0; j < PF; j++) insert(ck[j], C32 ? (uint64_t)cc[j] : cc64[j], 0);
+            } else {
+                for (uint64_t i0 = e0; i0 < e1; i0 += PF * HM_MB2_T) {
+                    uint64_t k[PF], c64[PF];
+                    uint32_t c[PF];
+                    fetch(i0, min(e1, i0 + (uint64_t)PF * HM_MB2_T), k, c, c64);
+#pragma unroll
+                    for (int j = 0; j < PF; j++) insert(k[j], C32 ? (uint64_t)c[j] : c64[j], pass);
+                }
+            }
+            __syncthreads();
+            if (full) {
+                if (tid == 0) atomicOr(a.overflow, 1ull);
+                return;
+            }
+            uint64_t bal[SPT];
+#pragma unroll
+            for (int j = 0; j < SPT; j++) {
+                bal[j] = __ballot(tk[j * HM_MB2_T + tid] != HMS_EMPTY);
+                if (lane == 0) wc[j * NW + w] = (uint32_t)__popcll(bal[j]);
+            }
+            __syncthreads();
+            if (w == 0) {
+                /* exclusive scan of the NF fragment counts, FPL consecutive ones a lane */
+                uint32_t f[FPL], v = 0;
+#pragma unroll
+                for (int q = 0; q < FPL; q++) {
+                    f[q] = lane * FPL + q < NF ? wc[lane * FPL + q] : 0u;
+                    v += f[q];
+                }
+                const uint32_t inc = hm_wave_incl_scan(v);
+                uint32_t o = inc - v;
+#pragma unroll
+                for (int q = 0; q < FPL; q++) {
+                    if (lane * FPL + q < NF) wc[lane * FPL + q] = o;
+                    o += f[q];
+                }
+                if (lane == 63) sbase = inc ? atomicAdd(a.cursor, (unsigned long long)inc) : 0ull;
+            }
+            if (pass + 1 == P) {
+                /* the next bucket: its cells now, the one after's bounds */
+                e0 = n0;
+                e1 = n1;
+                bounds(b + 2 * G, n0, n1);
+                if (e1 - e0 <= (uint64_t)PF * HM_MB2_T) fetch(e0, e1, ck, cc, cc64);
+            }
+            __syncthreads();
+            const uint64_t base = sbase;
+#pragma unroll
+            for (int j = 0; j < SPT; j++) {
+                const uint32_t sl = j * HM_MB2_T + tid;
+                if ((bal[j] >> lane) & 1ull) {
+                    const uint64_t q = base + wc[j * NW + w] + hm_mbcnt(bal[j]);
+                    if (q < a.cap) {
+                        a.keys_out[q] = tk[sl];
+                        a.counts_out[q] = (uint64_t)tc[sl];
+                    }
+                    tk[sl] = HMS_EMPTY;
+                    tc[sl] = 0;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+void hm_launch_mb_merge2(hipStream_t s, const HmMergeArgs& a)
+{
+    /* as many blocks as fit the CUs at once (each loops over buckets) */
+    static int cus = 0, per32 = 0, per64 = 0;
+    if (!cus) {
+        int dev = 0;
+        (void)hipGetDevice(&dev);
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) cus = 256;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per32, k_mb_merge2<true>, HM_MB2_T, 0) != hipSuccess ||
+            per32 < 1)
+            per32 = 1;
+        if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per64, k_mb_merge2<false>, HM_MB2_T, 0) != hipSuccess ||
+            per64 < 1)
+            per64 = 1;
+    }
+    const unsigned per = (unsigned)(a.pcounts32 ? per32 : per64);
+    const dim3 g(std::min(1u << a.lb, per * (unsigned)cus)), t(HM_MB2_T);
+    if (a.pcounts32) hipLaunchKernelGGL(k_mb_merge2<true>, g, t, 0, s, a);
+    else hipLaunchKernelGGL(k_mb_merge2<false>, g, t, 0, s, a);
+}
+
 static unsigned hm_mgrid(uint64_t n, unsigned cap)
 {
     uint64_t b = (n + 255) / 256;
@@ -473,7 +963,13 @@ void hm_launch_cells_merge_unique(hipStream_t s, const uint64_t* keys, const uin
 
 void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t)
 {
-    if (n) hipLaunchKernelGGL(k_cells_merge, dim3(hm_mgrid(n, 8192)), dim3(256), 0, s, keys, counts, n, t);
+    if (n) hipLaunchKernelGGL(k_cells_merge<uint64_t>, dim3(hm_mgrid(n, 8192)), dim3(256), 0, s, keys, counts, n, t);
+}
+
+void hm_launch_cells_merge32(hipStream_t s, const uint64_t* keys, const uint32_t* counts, uint64_t n,
+                             const HmsTable& t)
+{
+    if (n) hipLaunchKernelGGL(k_cells_merge<uint32_t>, dim3(hm_mgrid(n, 8192)), dim3(256), 0, s, keys, counts, n, t);
 }
 
 void hm_launch_table_extract(hipStream_t s, const HmsTable& t, uint64_t* keys_out, uint64_t* counts_out, uint64_t cap,

@@ -677,7 +677,35 @@ struct HmRouteArgs {
     unsigned long long* wide;  /* u32 counts: set when a sent count needs 64 bits */
     int grouped;               /* HM_CELLS_G12: counts = group << 32 | count (hm_count_grouped_packed);
                                   the owner hashes (group, row key); keys_out = hm_gkey packed merge keys */
+    /* hm_cells_route_pieces (k_xroute_*): digit = owner << bits | the top `bits` bits of the merge
+     * key's hash (the owner's first merge digit); C blocks, block_cnt/block_off [digits * C]
+     * digit-major; sizes: device rows of `stride` int64 per owner (sent, wide, pieces) */
+    int bits;
+    uint32_t C;
+    long long* sizes;
+    int stride;
 };
+#define HM_XR_MAXD 1024               /* route digits (nranks << bits) */
+void hm_launch_xroute(hipStream_t s, const HmRouteArgs& a, bool scatter, int layout);
+void hm_launch_xroute_sizes(hipStream_t s, const HmRouteArgs& a);
+/* owner side of the pieces exchange: run r's piece of first digit s (all of
+ * its cells with that digit) starts at device address kp[s R + r] (records,
+ * or keys with their counts at cp[s R + r]); the S segments are each cut into
+ * C chunks of their R pieces' concatenation (virtual starts vpre[s (R + 1) + r])
+ * and partitioned by the next `bits` hash bits into u64 keys and u32 (records
+ * and u32 input) or u64 counts */
+struct HmMbGather {
+    const unsigned long long* vpre;
+    const unsigned long long* kp;
+    const unsigned long long* cp;
+    uint32_t R, S, C;
+    int shift, bits, in_layout;
+    uint64_t* cnt;
+    const uint64_t* off;
+    uint64_t* kout;
+    void* cout;
+};
+void hm_launch_mb_gather(hipStream_t s, const HmMbGather& a, bool scatter);
 /* grouped exchange key: group (17 bits) | zoom (5) | row (21) | col (21) */
 #define HM_GKEY_GROUP_BITS 17
 __host__ __device__ inline uint64_t hm_gkey(uint64_t hmkey, uint32_t g)
@@ -700,6 +728,7 @@ struct HmMergeArgs {
     uint64_t* boff;            /* its exclusive scan, total at [2^lb * nblocks] */
     uint64_t* pkeys;           /* partitioned cells */
     uint64_t* pcounts;
+    const uint32_t* pcounts32; /* k_mb_merge2: u32 counts instead of pcounts */
     uint64_t* keys_out;
     uint64_t* counts_out;
     uint64_t cap;
@@ -727,6 +756,18 @@ struct HmMbPass {
 };
 void hm_launch_mb_pass(hipStream_t s, const HmMbPass& a, bool scatter);
 void hm_launch_mb_merge(hipStream_t s, const HmMergeArgs& a);
+/* the pieces merge (k_mb_merge2): LDS tables of HM_MB2_TS slots, blocks of
+ * HM_MB2_T threads; the host sizes buckets to <= HM_MB2_TARGET cells */
+#ifndef HM_MB2_TS
+#define HM_MB2_TS 4096
+#endif
+#ifndef HM_MB2_T
+#define HM_MB2_T 512
+#endif
+#define HM_MB2_TARGET (HM_MB2_TS * 7 / 16)
+void hm_launch_mb_merge2(hipStream_t s, const HmMergeArgs& a);
+void hm_launch_cells_merge32(hipStream_t s, const uint64_t* keys, const uint32_t* counts, uint64_t n,
+                             const HmsTable& t);
 void hm_launch_cells_route(hipStream_t s, const HmRouteArgs& a, bool scatter);
 void hm_launch_cells_merge(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n, const HmsTable& t);
 void hm_launch_cells_merge_unique(hipStream_t s, const uint64_t* keys, const uint64_t* counts, uint64_t n,

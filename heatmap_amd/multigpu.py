@@ -140,6 +140,69 @@ class DeviceOps:
             _lib.raise_for(rc)
         return ko[:nout.value], co[:nout.value]
 
+    def route_pieces(self, keys, counts, ws, dense_zmax, bits, layout, extra=1):
+        """hm_cells_route_pieces -> (dense grid, parts, sizes): parts as route()
+        (REC10: [(uint8 records, 10)]; U64: [(keys, 1), (counts, 1)]; G12:
+        [(u64 merge keys, 1), (u32 counts, 1)]) with room for every cell; sizes
+        a DEVICE int64 tensor [ws, 2 + 2^bits + extra]: per owner the cells
+        sent, the wide flag, the 2^bits piece sizes, then `extra` zero columns
+        for the caller (nothing is synchronised)."""
+        from . import _lib
+
+        self.ctx.bind_stream()
+        n = keys.numel()
+        gsz = int(self.L.hm_dense_grid_size(dense_zmax))
+        grid = torch.empty(max(gsz, 1), dtype=torch.int64, device=keys.device)
+        width = 2 + (1 << bits) + extra
+        sizes = torch.zeros((ws, width), dtype=torch.int64, device=keys.device)
+        if layout == _lib.HM_CELLS_REC10:
+            rec = torch.empty(max(n, 1) * 5, dtype=torch.int16, device=keys.device)
+            ko, co, parts = rec, None, [(rec.view(torch.uint8), 10)]
+        else:
+            ko = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
+            co = torch.empty(max(n, 1), dtype=torch.int32 if layout == _lib.HM_CELLS_G12 else torch.int64,
+                             device=keys.device)
+            parts = [(ko, 1), (co, 1)]
+        rc = self.L.hm_cells_route_pieces(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax, bits,
+                                          self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko), self._p(co),
+                                          layout, self._p(sizes), width)
+        self._check(rc)
+        return grid[:gsz], parts, sizes
+
+    def merge_pieces(self, runs, pieces, bits, layout, out=None):
+        """hm_cells_merge_pieces.  runs: per sender (key tensor, count tensor
+        or None, first cell) -- its cells, 2^bits pieces in digit order, start
+        at that cell of those tensors (REC10: uint8 records, 10 bytes a cell);
+        pieces: host int64 [senders, 2^bits].  -> (keys, counts) int64, into
+        `out` as merge()."""
+        from . import _lib
+
+        self.ctx.bind_stream()
+        R = len(runs)
+        ks = (ctypes.c_void_p * R)()
+        cs = (ctypes.c_void_p * R)()
+        for r, (kt, ct, start) in enumerate(runs):
+            kw = 10 if layout == _lib.HM_CELLS_REC10 else 8
+            ks[r] = kt.data_ptr() + start * kw if kt is not None and kt.numel() else None
+            cs[r] = ct.data_ptr() + start * ct.element_size() if ct is not None and ct.numel() else None
+        pa = (ctypes.c_int64 * (R << bits))(*[int(v) for row in pieces for v in row])
+        n = sum(int(v) for row in pieces for v in row)
+        if out is not None:
+            ko, co = out
+            cap = ko.numel()
+        else:
+            cap = max(n, 1)
+            ko = torch.empty(cap, dtype=torch.int64, device=runs[0][0].device)
+            co = torch.empty_like(ko)
+        nout = ctypes.c_int64(0)
+        rc = self.L.hm_cells_merge_pieces(self.ctx.ptr, layout, R, ks, cs, pa, bits, self._p(ko), self._p(co), cap,
+                                          ctypes.byref(nout))
+        if rc == _lib.HM_E_CAPACITY and out is not None:
+            raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (nout.value, cap))
+        if rc != _lib.HM_OK:
+            _lib.raise_for(rc)
+        return ko[:nout.value], co[:nout.value]
+
     def dense_cells(self, grid, dense_zmax, out=None):
         from . import _lib
 
@@ -291,29 +354,98 @@ def pipelined_steps(count, bufsets, steps: int, ws: int, rank: int, ctx=None, de
     return (owned[-1] if owned else 0), stages, last[0]
 
 
+def route_bits(ws: int) -> int:
+    """Merge-digit bits of the pieces route: 7 (the owner's first partition
+    pass of 128 digits), fewer past 8 ranks (ws << bits <= 1024 route digits)."""
+    b = 7
+    while (ws << b) > 1024:
+        b -= 1
+    return b
+
+
+def _alltoallv(out_slices, in_slices, rank):
+    """Variable all-to-all of 1-D slices (in_slices[o] to rank o, out_slices[r]
+    from rank r; the own pair is never touched).  RCCL: one grouped all_to_all
+    of tensor lists; gloo (CPU tests): point-to-point sends and receives."""
+    if dist.get_backend() == "nccl":
+        ins = [t if o != rank else t[:0] for o, t in enumerate(in_slices)]
+        outs = [t if r != rank else t[:0] for r, t in enumerate(out_slices)]
+        dist.all_to_all(outs, ins)
+        return
+    ops = [dist.P2POp(dist.isend, t, o) for o, t in enumerate(in_slices) if o != rank and t.numel()]
+    ops += [dist.P2POp(dist.irecv, t, r) for r, t in enumerate(out_slices) if r != rank and t.numel()]
+    if ops:
+        for w in dist.batch_isend_irecv(ops):
+            w.wait()
+
+
+def _exchange_pieces(parts, sent, rl, rank, device):
+    """All-to-all of the routed cells (parts from route_pieces, grouped by owner)
+    -> per sender (key tensor, count tensor or None, first cell): the peers'
+    cells land in fresh receive tensors, this rank's own group stays where the
+    route wrote it (no self copy)."""
+    ws = len(sent)
+    soff = [0] * (ws + 1)
+    roff = [0] * (ws + 1)
+    for r in range(ws):
+        soff[r + 1] = soff[r] + sent[r]
+        roff[r + 1] = roff[r] + (rl[r] if r != rank else 0)
+    got = []
+    for t, w in parts:
+        recv = torch.empty(max(roff[ws], 1) * w, dtype=t.dtype, device=device)
+        if ws > 1:
+            _alltoallv([recv[roff[r] * w:roff[r + 1] * w] for r in range(ws)],
+                       [t[soff[o] * w:soff[o + 1] * w] for o in range(ws)], rank)
+        got.append(recv)
+    runs = []
+    for r in range(ws):
+        if r == rank:
+            kt, ct, start = parts[0][0], parts[1][0] if len(parts) > 1 else None, soff[rank]
+        else:
+            kt, ct, start = got[0], got[1] if len(got) > 1 else None, roff[r]
+        runs.append((kt, ct, start))
+    return runs, got
+
+
 def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=None) -> int:
     """Exchange and merge the first m cells of `buffers` (int64 keys/counts,
     HM_KEY layout; records of cells outside the square in buffers.xcells,
     buffers.nx of them) in place; returns the number of in-square cells this
     rank owns (buffers.nx becomes the owned exotic count).  dense_zmax < 0
     sends every zoom through the all-to-all.  `ops`: the device operations
-    (DeviceOps), or stand-ins with the same contract (CPU tests)."""
+    (DeviceOps), or stand-ins with the same contract (CPU tests).
+
+    The pieces exchange: hm_cells_route_pieces groups the cells by owner and,
+    inside a group, by the first merge digit (route_bits), writing the sizes
+    on the device; ONE all-to-all of those rows (which also carry every
+    rank's wide flag and exotic count) and ONE host sync; then the cells'
+    all-to-all, and hm_cells_merge_pieces on the owner, whose own group never
+    leaves the route's buffer."""
+    from . import _lib
+
     if ops is None:
         ops = DeviceOps(buffers.keys.device.index or 0)
     keys = buffers.keys[:m]
     counts = buffers.counts[:m]
-    # cells travel as 10-byte records (48-bit key, u32 count: one all-to-all,
-    # 10 B per cell, not 16) unless some rank holds a cell count >= 2^32:
-    # every rank's flag rides on the group-size exchange, so all ranks agree
-    # before the cells' all-to-all
-    grid, parts, sent, wide = ops.route(keys, counts, ws, dense_zmax, narrow=True)
-    send = torch.tensor([[s, int(wide)] for s in sent], dtype=torch.int64, device=keys.device)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send)
-    recv = recv.cpu()
-    rl = recv[:, 0].tolist()
-    if bool(recv[:, 1].any()):
-        grid, parts, sent, _ = ops.route(keys, counts, ws, dense_zmax, narrow=False)
+    bits = route_bits(ws)
+    S = 1 << bits
+    nx = int(getattr(buffers, "nx", 0))
+    # cells travel as 10-byte records (48-bit key, u32 count) unless some
+    # rank holds a cell count >= 2^32: every rank's flag rides on the size
+    # exchange, so all ranks agree before the cells' all-to-all
+    grid, parts, sizes = ops.route_pieces(keys, counts, ws, dense_zmax, bits, _lib.HM_CELLS_REC10)
+    sizes[:, -1] = nx
+    recv = torch.empty_like(sizes)
+    dist.all_to_all_single(recv, sizes)
+    both = torch.stack([sizes, recv]).cpu()
+    sent = both[0, :, 0].tolist()
+    rl = both[1, :, 0].tolist()
+    pieces = both[1, :, 2:2 + S].tolist()
+    nx_all = int(both[1, :, -1].sum())
+    layout = _lib.HM_CELLS_REC10
+    if bool(both[1, :, 1].any()):
+        layout = _lib.HM_CELLS_U64
+        grid, parts, _ = ops.route_pieces(keys, counts, ws, dense_zmax, bits, layout)
     if dense_zmax >= 0:
         dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
     # the owned cells are at most the received ones plus (rank 0) the dense
@@ -324,36 +456,16 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         buffers.keys = torch.empty(need, dtype=torch.int64, device=keys.device)
         buffers.counts = torch.empty_like(buffers.keys)
         buffers.capacity = need
-    got = []
-    for t, w in parts:
-        r = torch.empty(sum(rl) * w, dtype=t.dtype, device=keys.device)
-        dist.all_to_all_single(r, t, [x * w for x in rl], [x * w for x in sent])
-        got.append(r)
-    if isinstance(ops, DeviceOps):
-        # merged cells straight into the buffers (the received copies are in got)
-        uk, _ = ops.merge(*got, runs=rl, out=(buffers.keys, buffers.counts))
+    runs, got = _exchange_pieces(parts, sent, rl, rank, keys.device)
+    n = 0
+    if sum(rl):
+        uk, _ = ops.merge_pieces(runs, pieces, bits, layout, out=(buffers.keys, buffers.counts))
         n = uk.numel()
-        if dense_zmax >= 0 and rank == 0:
-            dk, _ = ops.dense_cells(grid, dense_zmax, out=(buffers.keys[n:], buffers.counts[n:]))
-            n += dk.numel()
-    else:
-        parts_k, parts_c = [], []
-        uk, uc = ops.merge(*got, runs=rl)
-        parts_k.append(uk)
-        parts_c.append(uc)
-        if dense_zmax >= 0 and rank == 0:
-            dk, dc = ops.dense_cells(grid, dense_zmax)
-            parts_k.append(dk)
-            parts_c.append(dc)
-        k = torch.cat(parts_k)
-        c = torch.cat(parts_c)
-        n = k.numel()
-        buffers.keys[:n] = k
-        buffers.counts[:n] = c
-    nx = int(getattr(buffers, "nx", 0))
-    nx_all = torch.tensor([nx], dtype=torch.int64, device=keys.device)
-    dist.all_reduce(nx_all)
-    if int(nx_all.item()):
+    del got
+    if dense_zmax >= 0 and rank == 0:
+        dk, _ = ops.dense_cells(grid, dense_zmax, out=(buffers.keys[n:], buffers.counts[n:]))
+        n += dk.numel()
+    if nx_all:
         x = merge_exotic(buffers.xcells[:4 * nx], ws, rank)
         if x.numel() > buffers.xcells.numel():
             buffers.xcells = torch.empty(x.numel(), dtype=torch.int64, device=keys.device)
@@ -382,21 +494,25 @@ def merge_grouped(keys: torch.Tensor, gcounts: torch.Tensor, ws: int, rank: int,
     (group, cell) ends on the rank owning its heatmap row (the reference's
     reduceByKey / groupByKey on user|alltime|tile keys, heatmap.py:54-55,
     111-112).  Returns this rank's (keys, groups, counts) int64 tensors
-    (counts summed over ranks: int64).  Device route into 12-byte records
-    (u64 merge key of group, zoom, row, col; u32 count), ONE all-to-all of
-    sizes + the wide flag, one of keys, one of counts, and hm_cells_merge_runs
-    on the owner; if any rank holds a group id past 2^17 (the merge key's
-    field) every rank exchanges (key, group, count) int64 records and sums
-    them with torch ops instead."""
+    (counts summed over ranks: int64).  The pieces exchange of merge_cells
+    with 12-byte cells (u64 merge key of group, zoom, row, col; u32 count):
+    ONE all-to-all of the size rows (wide flag included), one of keys, one of
+    counts, and hm_cells_merge_pieces on the owner; if any rank holds a group
+    id past 2^17 (the merge key's field) every rank exchanges (key, group,
+    count) int64 records and sums them with torch ops instead."""
+    from . import _lib
+
     if ops is None:
         ops = DeviceOps(keys.device.index or 0)
-    parts, sent, wide = ops.route_grouped(keys, gcounts, ws)
-    send = torch.tensor([[s, int(wide)] for s in sent], dtype=torch.int64, device=keys.device)
-    recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send)
-    recv = recv.cpu()
-    rl = recv[:, 0].tolist()
-    if bool(recv[:, 1].any()):
+    bits = route_bits(ws)
+    S = 1 << bits
+    _, parts, sizes = ops.route_pieces(keys, gcounts, ws, -1, bits, _lib.HM_CELLS_G12, extra=0)
+    recv = torch.empty_like(sizes)
+    dist.all_to_all_single(recv, sizes)
+    both = torch.stack([sizes, recv]).cpu()
+    sent = both[0, :, 0].tolist()
+    rl = both[1, :, 0].tolist()
+    if bool(both[1, :, 1].any()):
         g = gcounts >> 32
         rows = torch.stack([keys, g, gcounts & 0xFFFFFFFF], 1)
         got = _exchange(rows, grouped_owner(keys, g, ws), ws)
@@ -405,12 +521,11 @@ def merge_grouped(keys: torch.Tensor, gcounts: torch.Tensor, ws: int, rank: int,
         u, inv = torch.unique(got[:, :2], dim=0, return_inverse=True)
         tot = torch.zeros(u.shape[0], dtype=torch.int64, device=got.device).index_add_(0, inv, got[:, 2])
         return u[:, 0], u[:, 1], tot
-    got = []
-    for t, w in parts:
-        r = torch.empty(sum(rl) * w, dtype=t.dtype, device=keys.device)
-        dist.all_to_all_single(r, t, [x * w for x in rl], [x * w for x in sent])
-        got.append(r)
-    mk, mc = ops.merge(got[0], got[1], runs=rl)
+    runs, got = _exchange_pieces(parts, sent, rl, rank, keys.device)
+    if not sum(rl):
+        e = torch.empty(0, dtype=torch.int64, device=keys.device)
+        return e, e, e
+    mk, mc = ops.merge_pieces(runs, both[1, :, 2:2 + S].tolist(), bits, _lib.HM_CELLS_G12)
     g = mk >> 47
     hk = (((mk >> 42) & 31) << 58) | (((mk >> 21) & 0x1FFFFF) << 29) | (mk & 0x1FFFFF)
     return hk, g, mc

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define HM_ABI_VERSION 6
+#define HM_ABI_VERSION 7
 
 /* status / per-point error kinds */
 #define HM_OK 0
@@ -318,6 +318,31 @@ int hm_cells_merge_runs(hm_ctx* ctx, const void* keys, const void* counts, int l
                         int64_t* n_out);
 int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* keys_out, uint64_t* counts_out,
                    int64_t capacity, int64_t* n_out);
+/* The exchange with the owner's first merge pass done by the sender (round 5):
+ *   hm_cells_route_pieces  hm_cells_route whose owner groups are each ordered
+ *                    by `bits` (0..7, nranks << bits <= 1024) top bits of the
+ *                    merge key's hash (the key; for HM_CELLS_G12 the packed
+ *                    merge key) -- 2^bits "pieces" per owner.  No host sync:
+ *                    the sizes go to the DEVICE int64 array `sizes`, row o
+ *                    (row stride `stride` >= 2 + 2^bits) = cells for owner o,
+ *                    the wide flag (1: as HM_E_WIDE; every row), the owner's
+ *                    2^bits piece sizes -- the row an RCCL all-to-all sends
+ *                    to owner o; other columns are left alone.  Asynchronous;
+ *                    HM_E_WIDE is never returned (it is in the rows).
+ *   hm_cells_merge_pieces  the owner's merge of nruns senders' cells: run r
+ *                    is a contiguous device array of records (REC10) or keys
+ *                    key_src[r] with counts count_src[r] (u32 for U32/G12 or
+ *                    u64 for U64 layouts; count_src NULL for REC10) holding its
+ *                    2^bits pieces in digit order, pieces[r * 2^bits + d]
+ *                    cells each (host int64); the runs need not be adjacent
+ *                    (the sender's own cells can stay in its send buffer).
+ *                    Outputs as hm_cells_merge.  Reference: heatmap.py:111-112. */
+int hm_cells_route_pieces(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks,
+                          int delta, int dense_zmax, int bits, uint64_t* grid, void* keys_out, void* counts_out,
+                          int layout, int64_t* sizes, int stride);
+int hm_cells_merge_pieces(hm_ctx* ctx, int layout, int nruns, const void* const* key_src,
+                          const void* const* count_src, const int64_t* pieces, int bits, uint64_t* keys_out,
+                          uint64_t* counts_out, int64_t capacity, int64_t* n_out);
 
 /* Row JSON text (heatmap_to_json, heatmap.py:92-95 via list_to_dict :120-126):
  * the bins of the rows, in row order (device arrays, n of them), are written

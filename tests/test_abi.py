@@ -34,7 +34,7 @@ def test_library_exports_every_declared_symbol():
     missing = [n for n in declared() if n not in exported]
     assert not missing, missing
     assert set(_lib.EXPORTS) == set(declared())
-    assert L.hm_abi_version() == _lib.HM_ABI_VERSION == 6
+    assert L.hm_abi_version() == _lib.HM_ABI_VERSION == 7
     assert _lib.status_string(_lib.HM_E_DOMAIN) == "math domain error"
     assert _lib.status_string(_lib.HM_E_NAN) == "cannot convert float NaN to integer"
 

@@ -295,3 +295,95 @@ def test_grouped_exchange_8_emulated_ranks(gpu):
     rk, rg, rc = keys.cpu().numpy(), (gc >> 32).cpu().numpy(), (gc & 0xFFFFFFFF).cpu().numpy()
     a, b = np.lexsort((ks, gs)), np.lexsort((rk, rg))
     assert np.array_equal(ks[a], rk[b]) and np.array_equal(gs[a], rg[b]) and np.array_equal(cs[a], rc[b])
+
+
+# ---- the pieces exchange (hm_cells_route_pieces / hm_cells_merge_pieces) ----
+from heatmap_amd import _lib  # noqa: E402
+
+
+def _piece_cells(parts, layout, lo, hi):
+    """(keys, counts) int64 of cells lo..hi of route parts (CPU)."""
+    if layout == _lib.HM_CELLS_REC10:
+        return multigpu.unpack_records(parts[0][0][lo * 10:hi * 10].cpu())
+    return parts[0][0][lo:hi].cpu(), parts[1][0][lo:hi].cpu().to(torch.int64)
+
+
+@pytest.mark.parametrize("ws,dz,layout,n", [(1, 10, 10, 300_000), (5, 8, 10, 300_000), (8, -1, 10, 300_000),
+                                            (8, 10, 8, 300_000), (64, 4, 8, 300_000), (8, -1, 12, 200_000),
+                                            (3, 8, 10, 7), (2, 10, 10, 0)])
+def test_route_pieces_contract(gpu, ws, dz, layout, n):
+    """hm_cells_route_pieces == its CPU stand-in: the same size rows (owner
+    totals, wide flag and the 2^bits digit pieces -- the device's fmix64 and
+    the stand-in's agree) and, piece by piece, the same cells."""
+    bits = multigpu.route_bits(ws)
+    if layout == _lib.HM_CELLS_G12:
+        lat, lon, grp = _grouped(n, ws, 3000)
+        keys, counts = device.count_grouped_packed_device(lat, lon, grp, None, 6, 21)
+        keys, counts = keys.cpu(), counts.cpu()
+    elif n:
+        keys, counts = _cells(n, ws)
+        keys, counts = keys[: n], counts[: n]
+    else:
+        keys = counts = torch.zeros(0, dtype=torch.int64)
+    ops = multigpu.DeviceOps(0)
+    g, parts, sizes = ops.route_pieces(keys.cuda(), counts.cuda(), ws, dz, bits, layout)
+    rg, rparts, rsizes = TorchOps.route_pieces(keys, counts, ws, dz, bits, layout)
+    sizes = sizes.cpu()
+    assert torch.equal(sizes, rsizes)
+    assert not bool(sizes[:, 1].any())
+    if dz >= 0:
+        assert torch.equal(g.cpu(), rg)
+    S = 1 << bits
+    flat = sizes[:, 2:2 + S].reshape(-1).tolist()
+    at = 0
+    for m in flat:                        # the same cells per (owner, digit) piece
+        sk, sc = _piece_cells(parts, layout, at, at + m)
+        rk, rc = _piece_cells(rparts, layout, at, at + m)
+        a, b = torch.argsort(sk), torch.argsort(rk)
+        assert torch.equal(sk[a], rk[b]) and torch.equal(sc[a], rc[b])
+        at += m
+    assert at == int(sizes[:, 0].sum())
+
+
+@pytest.mark.parametrize("layout,n,R", [(10, 1, 1), (10, 100, 3), (10, 5000, 8), (10, 3_000_000, 8),
+                                        (8, 300_000, 5), (12, 400_000, 8), (10, 6_000_000, 1)])
+def test_merge_pieces(gpu, layout, n, R):
+    """hm_cells_merge_pieces of R senders' cells as the exchange leaves them:
+    each sender's hm_cells_route_pieces output (2 owners) in its own tensor,
+    owner 1's group starting mid-tensor; equal keys summed (past 2^32 from
+    u32 inputs), every key once, and only owner 1's cells."""
+    gen = torch.Generator().manual_seed(n + R)
+    z = torch.randint(11, 22, (n,), generator=gen, dtype=torch.int64)
+    r = torch.randint(0, 1 << 21, (n,), generator=gen, dtype=torch.int64) & ((1 << z) - 1)
+    c = torch.randint(0, 1 << 21, (n,), generator=gen, dtype=torch.int64) & ((1 << z) - 1)
+    keys = torch.unique((z << 58) | (r << 29) | c)
+    bits = multigpu.route_bits(2)
+    S = 1 << bits
+    ops = multigpu.DeviceOps(0)
+    runs, pieces, ak, ac = [], [], [], []
+    for s in range(R):
+        k = keys[torch.randperm(keys.numel(), generator=gen)[: max(1, keys.numel() * (s + 2) // (R + 2))]]
+        if layout == _lib.HM_CELLS_U64:
+            cnt = torch.randint(1, 1 << 40, (k.numel(),), generator=gen, dtype=torch.int64)
+        else:
+            cnt = torch.randint(1 << 31, (1 << 32) - 1, (k.numel(),), generator=gen, dtype=torch.int64)
+        if layout == _lib.HM_CELLS_G12:
+            grp = (k & 7) * 1000
+            own = multigpu.grouped_owner(k, grp, 2)
+            mk = (grp << 47) | ((k >> 58) << 42) | (((k >> 29) & 0x1FFFFF) << 21) | (k & 0x1FFFFF)
+            cin = (grp << 32) | cnt
+        else:
+            own = multigpu.record_owner(torch.stack([k >> 58, (k >> 29) & 0x1FFFFFFF, k & 0x1FFFFFFF], 1), 2)
+            mk, cin = k, cnt
+        _, parts, sizes = ops.route_pieces(k.cuda(), cin.cuda(), 2, -1, bits, layout)
+        sz = sizes.cpu()
+        runs.append((parts[0][0], parts[1][0] if len(parts) > 1 else None, int(sz[0, 0])))
+        pieces.append(sz[1, 2:2 + S].tolist())
+        ak.append(mk[own == 1])
+        ac.append(cnt[own == 1])
+    uk, uc = ops.merge_pieces(runs, pieces, bits, layout)
+    ek, ec = TorchOps.merge(torch.cat(ak), torch.cat(ac))
+    o = torch.argsort(uk.cpu())
+    assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
+    if layout != _lib.HM_CELLS_U64 and R > 2:
+        assert int(ec.max()) >= 1 << 32

@@ -92,12 +92,87 @@ class TorchOps:
         return u, t
 
     @staticmethod
-    def dense_cells(grid, dz):
+    def dense_cells(grid, dz, out=None):
         nz = torch.nonzero(grid).flatten()
         off = torch.tensor([((1 << (2 * z)) - 1) // 3 for z in range(dz + 1)], dtype=torch.int64)
         zc = torch.bucketize(nz, off, right=True) - 1
         m = nz - off[zc]
-        return (zc << 58) | (_compact(m >> 1) << 29) | _compact(m), grid[nz]
+        return _into(out, (zc << 58) | (_compact(m >> 1) << 29) | _compact(m), grid[nz])
+
+    @staticmethod
+    def route_pieces(keys, counts, ws, dz, bits, layout, extra=1):
+        """hm_cells_route_pieces: owner groups ordered by the top `bits` bits
+        of fmix64(merge key); sizes rows (sent, wide, pieces, extra zeros)."""
+        from heatmap_amd import _lib
+
+        grouped = layout == _lib.HM_CELLS_G12
+        if grouped:
+            g = counts >> 32
+            z, r, c = keys >> 58, (keys >> 29) & M29, keys & M29
+            wide = bool((g >= 1 << multigpu.GKEY_GROUP_BITS).any() or (z > 21).any())
+            own = multigpu.grouped_owner(keys, g, ws)
+            mk, cnt = (g << 47) | (z << 42) | (r << 21) | c, (counts & 0xFFFFFFFF).to(torch.int32)
+            grid = torch.zeros(0, dtype=torch.int64)
+        else:
+            narrow = layout == _lib.HM_CELLS_REC10
+            grid, parts, _, wide = TorchOps.route(keys, counts, ws, dz, narrow)
+            sp = (keys >> 58) > dz
+            mk, cnt = keys[sp], counts[sp]
+            own = multigpu.record_owner(torch.stack([mk >> 58, (mk >> 29) & M29, mk & M29], 1), ws)
+        d = own << bits
+        if bits:
+            d = d | _lsr(_fmix64(mk), 64 - bits)
+        o = torch.argsort(d, stable=True)
+        S = 1 << bits
+        sizes = torch.zeros((ws, 2 + S + extra), dtype=torch.int64)
+        sizes[:, 0] = torch.bincount(own, minlength=ws)
+        sizes[:, 1] = int(wide)
+        sizes[:, 2:2 + S] = torch.bincount(d, minlength=ws << bits).reshape(ws, S)
+        if layout == _lib.HM_CELLS_REC10:
+            parts = [(multigpu.pack_records(mk[o], cnt[o]), 10)]
+        else:
+            parts = [(mk[o], 1), (cnt[o], 1)]
+        return grid, parts, sizes
+
+    @staticmethod
+    def merge_pieces(runs, pieces, bits, layout, out=None):
+        from heatmap_amd import _lib
+
+        ks, cs = [], []
+        for (kt, ct, start), row in zip(runs, pieces):
+            n = int(sum(row))
+            if layout == _lib.HM_CELLS_REC10:
+                k, c = multigpu.unpack_records(kt[start * 10:(start + n) * 10])
+            else:
+                k, c = kt[start:start + n], ct[start:start + n].to(torch.int64)
+            ks.append(k)
+            cs.append(c)
+        u, t = TorchOps.merge(torch.cat(ks), torch.cat(cs))
+        return _into(out, u, t)
+
+
+def _into(out, k, c):
+    if out is None:
+        return k, c
+    n = k.numel()
+    if n > out[0].numel():
+        raise MemoryError("merge_cells: %d owned cells exceed the buffer capacity %d" % (n, out[0].numel()))
+    out[0][:n] = k
+    out[1][:n] = c
+    return out[0][:n], out[1][:n]
+
+
+def _lsr(v, s):
+    return (v >> s) & ((1 << (64 - s)) - 1)
+
+
+def _fmix64(k):
+    """hms_hash (MurmurHash3's fmix64) on int64 bits, wrapping multiplies."""
+    k = k ^ _lsr(k, 33)
+    k = k * (0xFF51AFD7ED558CCD - (1 << 64))
+    k = k ^ _lsr(k, 33)
+    k = k * (0xC4CEB9FE1A85EC53 - (1 << 64))
+    return k ^ _lsr(k, 33)
 
 
 class _Bufs:
@@ -146,7 +221,7 @@ def _worker(rank, ws, port, kind, n, zmin, zmax, dense_zmax, out, wide_rank=1):
 
 
 @pytest.mark.parametrize("ws,kind,zmax,dense_zmax", [(2, "hotspots", 18, 8), (2, "uniform", 12, -1),
-                                                      (2, "skew", 18, 10), (4, "hotspots", 16, 10),
+                                                      (2, "skew", 18, 10), (4, "hotspots", 16, 10), (1, "hotspots", 14, 8),
                                                       (4, "skew", 18, 8)])
 def test_merge_ranks(ws, kind, zmax, dense_zmax):
     """ws gloo ranks (CPU stand-ins of the device operations): the union of

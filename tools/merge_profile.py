@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Phase timing of the multi-GPU merge (heatmap_amd.multigpu.merge_cells) on one
 GPU with a world-size-1 RCCL group: count 1.25e9 hotspot points (the N>1 bench
-shard), then time route, reduce, all-to-all, merge, dense extraction and the
-exotic step separately (synchronised).  Prints one JSON line.
+shard), then time the pieces exchange's route, size exchange, reduce, merge and
+dense extraction separately (synchronised; at world size 1 no cell crosses
+the all-to-all), and the route alone at 8 owners.  Prints one JSON line.
 
     python tools/merge_profile.py [points]
 """
@@ -20,7 +21,7 @@ os.environ.setdefault("RANK", "0")
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
-from heatmap_amd import device, multigpu  # noqa: E402
+from heatmap_amd import _lib, device, multigpu  # noqa: E402
 
 
 def main():
@@ -33,6 +34,8 @@ def main():
     bufs = device.CountBuffers(64 << 20)
     ops = multigpu.DeviceOps(0)
     res = {}
+    bits = multigpu.route_bits(1)
+    S = 1 << bits
     for it in range(3):
         t = {}
 
@@ -46,34 +49,32 @@ def main():
         m, bufs = device.count_device(lat, lon, None, 0, 18, 0, buffers=bufs)
         t0 = mark("count", t0)
         keys, counts = bufs.keys[:m], bufs.counts[:m]
-        grid, parts, sent, wide = ops.route(keys, counts, 1, 10, narrow=True)
-        assert not wide
-        rec = parts[0][0]
+        grid, parts, sizes = ops.route_pieces(keys, counts, 1, 10, bits, _lib.HM_CELLS_REC10)
         t0 = mark("route", t0)
+        recv = torch.empty_like(sizes)
+        dist.all_to_all_single(recv, sizes)
+        both = torch.stack([sizes, recv]).cpu()
+        assert not bool(both[1, :, 1].any())
+        t0 = mark("size_exchange", t0)
         dist.reduce(grid, dst=0)
         t0 = mark("reduce", t0)
-        send = torch.tensor(sent, dtype=torch.int64, device="cuda")
-        recv = torch.empty_like(send)
-        dist.all_to_all_single(recv, send)
-        rl = recv.tolist()
-        nrec = torch.empty(sum(rl) * 10, dtype=torch.uint8, device="cuda")
-        dist.all_to_all_single(nrec, rec, [x * 10 for x in rl], [x * 10 for x in sent])
-        t0 = mark("all_to_all", t0)
-        uk, uc = ops.merge(nrec, None, rl)
+        runs = [(parts[0][0], None, 0)]
+        uk, uc = ops.merge_pieces(runs, both[1, :, 2:2 + S].tolist(), bits, _lib.HM_CELLS_REC10,
+                                  out=(bufs.keys, bufs.counts))
+        n = uk.numel()
         t0 = mark("merge", t0)
-        dk, dc = ops.dense_cells(grid, 10)
+        dk, dc = ops.dense_cells(grid, 10, out=(bufs.keys[n:], bufs.counts[n:]))
         t0 = mark("dense_cells", t0)
-        k = torch.cat([uk, dk])
-        c = torch.cat([uc, dc])
-        bufs.keys[:k.numel()] = k
-        bufs.counts[:k.numel()] = c
-        t0 = mark("cat_copy", t0)
-        nx_all = torch.tensor([int(bufs.nx)], dtype=torch.int64, device="cuda")
-        dist.all_reduce(nx_all)
-        t0 = mark("exotic_check", t0)
+        # the route at 8 owners (1024 route digits), timed alone: the sender's
+        # side of a world-size-8 step
+        m2, bufs = device.count_device(lat, lon, None, 0, 18, 0, buffers=bufs)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        ops.route_pieces(bufs.keys[:m2], bufs.counts[:m2], 8, 10, multigpu.route_bits(8), _lib.HM_CELLS_REC10)
+        t0 = mark("route_ws8", t0)
         t["cells"] = int(m)
-        t["sent"] = int(sum(sent))
-        t["owned"] = int(k.numel())
+        t["sent"] = int(both[0, :, 0].sum())
+        t["owned"] = int(n + dk.numel())
         res = t
     print(json.dumps(res), flush=True)
     dist.destroy_process_group()

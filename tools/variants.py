@@ -70,6 +70,11 @@ VARIANTS = {
     "cs2it8": ["HM_CS2_IT=8"],                       # k_cascade2: 2048-item tiles
     "cs2it12": ["HM_CS2_IT=12"],
     "l1nt0": ["HM_L1_NT=0"],                        # K1's point loads without the non-temporal hint
+    "mbtc64": ["HM_MB2_TC32=0"],                    # k_mb_merge2: u64 table counts
+    "mb2k": ["HM_MB2_TS=2048", "HM_MB2_T=256"],      # k_mb_merge2 tables / block size (default 4096 / 512)
+    "mb8k": ["HM_MB2_TS=8192", "HM_MB2_T=1024"],
+    "mb4k256": ["HM_MB2_TS=4096", "HM_MB2_T=256"],
+    "mb4k1024": ["HM_MB2_TS=4096", "HM_MB2_T=1024"],
     "l1n4": ["HM_L1_NARROW=1", "HM_L1_WAVES=4"],   # 4-B staging at 2 blocks per CU               # 16K-key partition items (half the (item, child) pairs)                  # one-sweep radix tiles of 2048 keys (4 blocks per CU)
 }
 
@@ -105,6 +110,26 @@ PATCHES["l1occ1"] = [("hm_kernels.hip", """    __shared__ uint32_t s_over;
     __shared__ uint32_t occpad[20480];
     if (a.n == -12345) occpad[threadIdx.x] = 1;
     /* the polynomial table plus one poison row""")]
+# the exchange's bucket merge (k_mb_merge2): no LDS insertion atomics (each
+# key stored at its home slot), or no output stores
+PATCHES["mb2noins"] = [("hm_merge.hip", """                        const unsigned long long o =
+                            atomicCAS(&tk[sl], (unsigned long long)HMS_EMPTY, (unsigned long long)k[j]);""",
+                        """                        tk[sl] = k[j];
+                        const unsigned long long o = k[j];""")]
+PATCHES["mb2nowrite"] = [("hm_merge.hip", """                    if (q < a.cap) {
+                        a.keys_out[q] = tk[sl];
+                        a.counts_out[q] = tc[sl];
+                    }""", """                    if (q == 0x123456789ull) {
+                        a.keys_out[q] = tk[sl];
+                        a.counts_out[q] = tc[sl];
+                    }""")]
+PATCHES["mb2nocur"] = [("hm_merge.hip", "if (lane == 63) sbase = inc ? atomicAdd(a.cursor, (unsigned long long)inc) : 0ull;",
+                        "if (lane == 63) sbase = (uint64_t)b * 1024u;")]
+PATCHES["mb2loadonly"] = [("hm_merge.hip", """                for (int j = 0; j < 4; j++) {
+                    if (k[j] == HMS_EMPTY) continue;
+                    const uint64_t h = hms_hash(k[j]);""", """                for (int j = 0; j < 4; j++) {
+                    if (k[j] != 0x1234567ull) continue;
+                    const uint64_t h = hms_hash(k[j]);""")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
@@ -173,6 +198,45 @@ def one(name, points, steps, zmax):
                       "stage_us": [round(x, 1) for x in np.mean(np.array(st), axis=0)]}), flush=True)
 
 
+def merge_one(name, points, steps):
+    """The exchange at world size 1 (the rehearsal's route + merge, no RCCL):
+    per-call times of hm_cells_route_pieces and hm_cells_merge_pieces over the
+    cells of one count; the owned cells must be the counted ones."""
+    if name != "main":
+        os.environ["HM_LIB_PATH"] = os.path.join(VDIR, "lib_%s.so" % name)
+    import torch
+
+    from heatmap_amd import _lib, device, multigpu
+
+    lat = torch.empty(points, dtype=torch.float64, device="cuda")
+    lon = torch.empty(points, dtype=torch.float64, device="cuda")
+    device.synth("hotspots", lat, lon)
+    m, bufs = device.count_device(lat, lon, None, 0, 18)
+    del lat, lon
+    keys, counts = bufs.keys[:m].clone(), bufs.counts[:m].clone()
+    ops = multigpu.DeviceOps(0)
+    bits = multigpu.route_bits(1)
+    ok, tr, tm = True, [], []
+    for it in range(steps + 1):
+        e = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+        e[0].record()
+        _, parts, sizes = ops.route_pieces(keys, counts, 1, 10, bits, _lib.HM_CELLS_REC10)
+        e[1].record()
+        pieces = sizes.cpu()[:, 2:2 + (1 << bits)].tolist()
+        uk, uc = ops.merge_pieces([(parts[0][0], None, 0)], pieces, bits, _lib.HM_CELLS_REC10)
+        e[2].record()
+        torch.cuda.synchronize()
+        if it:
+            tr.append(e[0].elapsed_time(e[1]))
+            tm.append(e[1].elapsed_time(e[2]))
+        sp = (keys >> 58) > 10
+        ok = ok and uk.numel() == int(sp.sum()) and int(uc.sum()) == int(counts[sp].sum())
+    tr.sort()
+    tm.sort()
+    print(json.dumps({"variant": name, "route_ms": tr[len(tr) // 2], "merge_ms": tm[len(tm) // 2], "cells": m,
+                      "lb": os.environ.get("HM_MERGE_LB", "1"), "ok": ok}), flush=True)
+
+
 def main():
     cmd = sys.argv[1]
     names = sys.argv[2:] or ["base"]
@@ -184,6 +248,14 @@ def main():
             if r.returncode != 0:
                 print(json.dumps({"variant": n, "error": r.returncode}), flush=True)
                 break
+    elif cmd == "mrun":
+        for n in names:
+            r = subprocess.run([sys.executable, __file__, "mone", n], timeout=300)
+            if r.returncode != 0:
+                print(json.dumps({"variant": n, "error": r.returncode}), flush=True)
+                break
+    elif cmd == "mone":
+        merge_one(names[0], int(float(os.environ.get("HM_POINTS", "1.25e9"))), int(os.environ.get("HM_STEPS", "5")))
     elif cmd == "one":
         one(names[0], int(float(os.environ.get("HM_POINTS", "1e9"))), int(os.environ.get("HM_STEPS", "3")),
             int(os.environ.get("HM_ZMAX", "18")))
