@@ -1994,46 +1994,96 @@ extern "C" int hm_cells_merge_pieces(hm_ctx* ctx, int layout, int nruns, const v
     g.cp = rec ? nullptr : g.kp + (size_t)S * R;
     g.R = R;
     g.S = S;
-    g.C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, ((n >> bits) + 32767) / 32768));
+#ifndef HM_MG_CHUNK
+#define HM_MG_CHUNK 16384
+#endif
+    g.C = (uint32_t)std::max<uint64_t>(1, std::min<uint64_t>(64, ((n >> bits) + HM_MG_CHUNK - 1) / HM_MG_CHUNK));
     g.shift = lb ? 64 - lb : 63;
     g.bits = b2;
     g.in_layout = rec ? HM_CELLS_REC10 : (c64 ? HM_CELLS_U64 : HM_CELLS_U32);
-    const uint64_t m2 = ((uint64_t)S << b2) * g.C;
-    uint64_t *cnt2, *off2, *qk, *partial;
+    uint64_t *partial, *qk;
     void* qc;
-    ENSURE(B_MB_CNT2, m2 * 8, cnt2);
-    ENSURE(B_MB_OFF2, (m2 + 1) * 8, off2);
-    ENSURE(B_MB_KEYS2, n * 8, qk);
-    ENSURE(B_MB_COUNTS2, n * csz, qc);
+    unsigned long long* st;
     ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
-    g.cnt = cnt2;
-    g.off = off2;
-    g.kout = qk;
-    g.cout = qc;
-    hm_launch_mb_gather(s, g, false);
-    hm_launch_scan(s, cnt2, m2, partial, off2, off2 + m2);
-    hm_launch_mb_gather(s, g, true);
+    ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), st);
     HmMergeArgs a;
     memset(&a, 0, sizeof(a));
-    a.pkeys = qk;
-    if (c64) a.pcounts = (uint64_t*)qc;
-    else a.pcounts32 = (const uint32_t*)qc;
-    a.boff = off2;
-    a.nblocks = g.C;
     a.n = n;
     a.lb = lb;
-    unsigned long long* st;
-    ENSURE(B_MG_STATE, 8 * sizeof(unsigned long long), st);
-    HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
     a.keys_out = keys_out;
     a.counts_out = counts_out;
     a.cap = (uint64_t)capacity;
     a.cursor = st;
     a.overflow = st + 1;
+    /* fill mode: no count pass -- buckets of a fixed capacity (the mean
+     * + 1/4 + 64; hash buckets are near the mean), claimed per tile; a bucket
+     * past it (st[2]) or a full LDS table sends the call to the counted form */
+    const char* fe = getenv("HM_GATHER_FILL");   /* 0: always the counted form (A/B) */
+    const char* be = getenv("HM_GATHER_BCAP");   /* test hook: a bucket capacity (forces the fallback) */
+    const uint64_t nbk = 1ull << lb;
+    const bool fill = (!fe || atoi(fe) != 0) && n >= 4096;
+    auto counted = [&]() -> int {
+        const uint64_t m2 = ((uint64_t)S << b2) * g.C;
+        uint64_t *cnt2, *off2;
+        ENSURE(B_MB_CNT2, m2 * 8, cnt2);
+        ENSURE(B_MB_OFF2, (m2 + 1) * 8, off2);
+        ENSURE(B_MB_KEYS2, n * 8, qk);
+        ENSURE(B_MB_COUNTS2, n * csz, qc);
+        g.cnt = cnt2;
+        g.off = off2;
+        g.kout = qk;
+        g.cout = qc;
+        g.fill = nullptr;
+        hm_launch_mb_gather(s, g, false);
+        hm_launch_scan(s, cnt2, m2, partial, off2, off2 + m2);
+        hm_launch_mb_gather(s, g, true);
+        a.boff = off2;
+        a.nblocks = g.C;
+        a.bfill = nullptr;
+        return HM_OK;
+    };
+    HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
+    if (fill) {
+        const uint64_t mean = (n + nbk - 1) / nbk;
+        const uint64_t bcap = be && atoll(be) > 0 ? (uint64_t)atoll(be) : mean + mean / 4 + 64;
+        unsigned long long* fc;
+        ENSURE(B_MB_CNT2, nbk * 8, fc);
+        ENSURE(B_MB_KEYS2, nbk * bcap * 8, qk);
+        ENSURE(B_MB_COUNTS2, nbk * bcap * csz, qc);
+        HIPCHK(hipMemsetAsync(fc, 0, nbk * 8, s));
+        g.kout = qk;
+        g.cout = qc;
+        g.fill = fc;
+        g.bcap = bcap;
+        g.over = st + 2;
+        hm_launch_mb_gather(s, g, true);
+        a.bfill = fc;
+        a.bcap = bcap;
+    } else {
+        int st2 = counted();
+        if (st2 != HM_OK) return st2;
+    }
+    if (c64) a.pcounts = (uint64_t*)qc;
+    else a.pcounts32 = (const uint32_t*)qc;
+    a.pkeys = qk;
     hm_launch_mb_merge2(s, a);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipMemcpyAsync(down, st, 2 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(down, st, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(hm_sync(s));
+    if (fill && (down[1] || down[2])) {
+        /* a bucket past its capacity, or a full table: partition again with the
+         * count pass (contiguous buckets, which the global table below can take) */
+        HIPCHK(hipMemsetAsync(st, 0, 8 * sizeof(unsigned long long), s));
+        int st2 = counted();
+        if (st2 != HM_OK) return st2;
+        a.pkeys = qk;
+        if (c64) a.pcounts = (uint64_t*)qc;
+        else a.pcounts32 = (const uint32_t*)qc;
+        hm_launch_mb_merge2(s, a);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(down, st, 3 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+        HIPCHK(hm_sync(s));
+    }
     if (!down[1]) {
         *n_out = (int64_t)down[0];
         return *n_out > capacity ? HM_E_CAPACITY : HM_OK;

@@ -82,6 +82,22 @@ __device__ __forceinline__ uint64_t hm_rec_key(const uint16_t* r)
 }
 __device__ __forceinline__ uint32_t hm_rec_count(const uint16_t* r) { return (uint32_t)r[3] | ((uint32_t)r[4] << 16); }
 
+/* a record through the two aligned 8-byte words around it (2 loads, not 5
+ * strided u16 ones; reads up to 6 bytes either side, inside the record's
+ * 8-byte words -- the caller takes the u16 form for a run's last record) */
+__device__ __forceinline__ void hm_rec_load(const uint16_t* r, uint64_t& key, uint32_t& cnt)
+{
+    const uintptr_t A = (uintptr_t)r;
+    const uint64_t* q = (const uint64_t*)(A & ~(uintptr_t)7);
+    const uint32_t sh = (uint32_t)(A & 7) * 8;
+    const uint64_t q0 = q[0], q1 = q[1];
+    const uint64_t lo = sh ? (q0 >> sh) | (q1 << (64 - sh)) : q0;
+    const uint32_t hi = (uint32_t)(q1 >> sh) & 0xFFFFu;
+    const uint64_t p = lo & 0xFFFFFFFFFFFFull;
+    key = ((p >> 42) << 58) | (((p >> 21) & 0x1FFFFFull) << 29) | (p & 0x1FFFFFull);
+    cnt = (uint32_t)(lo >> 48) | (hi << 16);
+}
+
 /* pass 1 (count) / pass 2 (scatter) over the same block-contiguous cells:
  * both passes see identical per-block owner counts, so pass 1's block totals,
  * scanned owner-major, are pass 2's reservations (slots inside a block's
@@ -457,8 +473,13 @@ void hm_launch_mb_merge(hipStream_t s, const HmMergeArgs& a)
  * merge key's hash), so the owner skips the first partition pass: it gathers
  * digit s's piece of every sender (one chunked segment per digit), partitions
  * it by the next bits, and merges buckets of <= ~1000 cells in LDS. */
-#define HM_XR_PPT 8
+#ifndef HM_XR_PPT
+#define HM_XR_PPT 16
+#endif
 #define HM_XR_TILE (256 * HM_XR_PPT)
+#ifndef HM_XRC_PPT
+#define HM_XRC_PPT 16                /* the count pass's cells in flight a thread */
+#endif
 
 struct HmXCell {
     uint32_t d;     /* digit, or ~0u: not routed (dense zoom / past the input) */
@@ -489,16 +510,16 @@ __global__ __launch_bounds__(256) void k_xroute_count(HmRouteArgs a)
     __syncthreads();
     const uint64_t c0 = a.n * blockIdx.x / gridDim.x, c1 = a.n * (blockIdx.x + 1) / gridDim.x;
     bool wide = false;
-    for (uint64_t t0 = c0; t0 < c1; t0 += HM_XR_TILE) {
-        uint64_t k[HM_XR_PPT], cn[HM_XR_PPT];
+    for (uint64_t t0 = c0; t0 < c1; t0 += 256 * HM_XRC_PPT) {
+        uint64_t k[HM_XRC_PPT], cn[HM_XRC_PPT];
 #pragma unroll
-        for (int j = 0; j < HM_XR_PPT; j++) {
+        for (int j = 0; j < HM_XRC_PPT; j++) {
             const uint64_t i = t0 + j * 256 + tid;
             k[j] = i < c1 ? a.keys[i] : 0ull;
             cn[j] = i < c1 ? a.counts[i] : 0ull;
         }
 #pragma unroll
-        for (int j = 0; j < HM_XR_PPT; j++) {
+        for (int j = 0; j < HM_XRC_PPT; j++) {
             const bool in = t0 + j * 256 + tid < c1;
             const int z = (int)(k[j] >> 58);
             if (in && z <= a.dense_zmax) {
@@ -644,7 +665,9 @@ void hm_launch_xroute_sizes(hipStream_t s, const HmRouteArgs& a)
 
 /* owner: partition digit s's pieces by the next bits.  IN: 0 records, 1 u32
  * counts, 2 u64 counts (kept u64 in the output) */
-#define HM_MG_PPT 16
+#ifndef HM_MG_PPT
+#define HM_MG_PPT 8
+#endif
 #define HM_MG_TILE (256 * HM_MG_PPT)
 #define HM_MG_MAXD 256
 #define HM_MG_MAXR 64
@@ -671,7 +694,7 @@ __global__ __launch_bounds__(256) void k_mb_gather(HmMbGather a)
     const uint64_t cbase = ((uint64_t)s << a.bits) * a.C + c;   /* + d * C */
     for (uint32_t d = tid; d < nd; d += 256) {
         hist[d] = 0;
-        if (SCATTER) gb[d] = a.off[cbase + (uint64_t)d * a.C];
+        if (SCATTER && !a.fill) gb[d] = a.off[cbase + (uint64_t)d * a.C];
     }
     __syncthreads();
     const uint64_t len = vp[R];
@@ -696,8 +719,14 @@ __global__ __launch_bounds__(256) void k_mb_gather(HmMbGather a)
                 const uint64_t e = v - vp[lo];
                 if (IN == 0) {
                     const uint16_t* rp = (const uint16_t*)kp[lo] + 5 * e;
-                    k[j] = hm_rec_key(rp);
-                    cc[j] = hm_rec_count(rp);
+                    if (v + 1 < vp[lo + 1]) {
+                        uint32_t c32;
+                        hm_rec_load(rp, k[j], c32);
+                        cc[j] = c32;
+                    } else {   /* a piece's last record: nothing read past it */
+                        k[j] = hm_rec_key(rp);
+                        cc[j] = hm_rec_count(rp);
+                    }
                 } else {
                     k[j] = ((const uint64_t*)kp[lo])[e];
                     cc[j] = IN == 1 ? (CT)((const uint32_t*)cp[lo])[e] : (CT)((const uint64_t*)cp[lo])[e];
@@ -720,7 +749,21 @@ __global__ __launch_bounds__(256) void k_mb_gather(HmMbGather a)
         __syncthreads();
         uint32_t tot;
         const uint32_t o = hm_block_excl_scan<256>(tid < (int)nd ? hist[tid] : 0u, scr, &tot);
-        if (tid < (int)nd) toff[tid] = o;
+        if (tid < (int)nd) {
+            toff[tid] = o;
+            if (a.fill) {
+                /* fill mode: this tile's run of digit tid, claimed in its bucket */
+                const uint32_t h = hist[tid];
+                const uint64_t bk = ((uint64_t)s << a.bits) + tid;
+                const uint64_t at = h ? atomicAdd(a.fill + bk, (unsigned long long)h) : 0ull;
+                if (at + h > a.bcap) {
+                    atomicOr(a.over, 1ull);
+                    gb[tid] = ~0ull;
+                } else {
+                    gb[tid] = bk * a.bcap + at;
+                }
+            }
+        }
         __syncthreads();
 #pragma unroll
         for (int j = 0; j < HM_MG_PPT; j++) {
@@ -734,13 +777,14 @@ __global__ __launch_bounds__(256) void k_mb_gather(HmMbGather a)
         __syncthreads();
         for (uint32_t i = tid; i < tn; i += 256) {
             const uint32_t dd = sd[i];
+            if (a.fill && gb[dd] == ~0ull) continue;
             const uint64_t dst = gb[dd] + (i - toff[dd]);
             a.kout[dst] = sk[i];
             ((CT*)a.cout)[dst] = sc[i];
         }
         __syncthreads();
         if (tid < (int)nd) {
-            gb[tid] += hist[tid];
+            if (!a.fill) gb[tid] += hist[tid];
             hist[tid] = 0;
         }
         __syncthreads();
@@ -795,8 +839,13 @@ __global__ __launch_bounds__(HM_MB2_T) void k_mb_merge2(HmMergeArgs a)
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     const uint32_t nb = 1u << a.lb, G = gridDim.x;
     auto bounds = [&](uint32_t bb, uint64_t& f0, uint64_t& f1) {
-        f0 = bb < nb ? a.boff[(uint64_t)bb * a.nblocks] : 0ull;
-        f1 = bb < nb ? a.boff[(uint64_t)(bb + 1) * a.nblocks] : 0ull;
+        if (a.bfill) {
+            f0 = (uint64_t)bb * a.bcap;
+            f1 = bb < nb ? f0 + min((uint64_t)a.bfill[bb], a.bcap) : f0;
+        } else {
+            f0 = bb < nb ? a.boff[(uint64_t)bb * a.nblocks] : 0ull;
+            f1 = bb < nb ? a.boff[(uint64_t)(bb + 1) * a.nblocks] : 0ull;
+        }
     };
     auto fetch = [&](uint64_t f0, uint64_t f1, uint64_t (&k)[PF], uint32_t (&c)[PF], uint64_t (&c64)[PF]) {
 #pragma unroll

@@ -704,6 +704,13 @@ struct HmMbGather {
     const uint64_t* off;
     uint64_t* kout;
     void* cout;
+    /* fill mode (no count pass): bucket (s, d) holds <= bcap cells at
+     * kout/cout + (s << bits | d) * bcap, claimed per tile from fill[]; a
+     * bucket that would pass bcap sets *over (the caller partitions again
+     * with the count pass) */
+    unsigned long long* fill;
+    uint64_t bcap;
+    unsigned long long* over;
 };
 void hm_launch_mb_gather(hipStream_t s, const HmMbGather& a, bool scatter);
 /* grouped exchange key: group (17 bits) | zoom (5) | row (21) | col (21) */
@@ -729,6 +736,8 @@ struct HmMergeArgs {
     uint64_t* pkeys;           /* partitioned cells */
     uint64_t* pcounts;
     const uint32_t* pcounts32; /* k_mb_merge2: u32 counts instead of pcounts */
+    const unsigned long long* bfill;   /* k_mb_merge2: buckets of bfill[b] cells at b * bcap (else boff) */
+    uint64_t bcap;
     uint64_t* keys_out;
     uint64_t* counts_out;
     uint64_t cap;

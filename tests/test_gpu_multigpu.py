@@ -387,3 +387,13 @@ def test_merge_pieces(gpu, layout, n, R):
     assert torch.equal(uk.cpu()[o], ek) and torch.equal(uc.cpu()[o], ec)
     if layout != _lib.HM_CELLS_U64 and R > 2:
         assert int(ec.max()) >= 1 << 32
+
+
+@pytest.mark.parametrize("env", [{"HM_GATHER_BCAP": "64"}, {"HM_GATHER_FILL": "0"}])
+def test_merge_pieces_counted_forms(gpu, env, monkeypatch):
+    """hm_cells_merge_pieces' other partitions: buckets of a fixed capacity
+    overflowing (HM_GATHER_BCAP, a test hook) fall back to the counted
+    partition; HM_GATHER_FILL=0 always counts.  Same cells either way."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    test_merge_pieces(gpu, 10, 300_000, 4)

@@ -70,6 +70,12 @@ VARIANTS = {
     "cs2it8": ["HM_CS2_IT=8"],                       # k_cascade2: 2048-item tiles
     "cs2it12": ["HM_CS2_IT=12"],
     "l1nt0": ["HM_L1_NT=0"],                        # K1's point loads without the non-temporal hint
+    "xr16": ["HM_XR_PPT=16"],                        # route scatter: 4096-cell tiles (default 2048)
+    "xr4": ["HM_XR_PPT=4"],
+    "xrc8": ["HM_XRC_PPT=8"],                        # route count: 8 cells a thread in flight (default 16)
+    "mg16": ["HM_MG_PPT=16"],                        # k_mb_gather: 4096-cell tiles (default 2048)
+    "mg4": ["HM_MG_PPT=4"],
+    "mgc32": ["HM_MG_CHUNK=32768"],                   # 32K-cell chunks a block (default 16K)
     "mbtc64": ["HM_MB2_TC32=0"],                    # k_mb_merge2: u64 table counts
     "mb2k": ["HM_MB2_TS=2048", "HM_MB2_T=256"],      # k_mb_merge2 tables / block size (default 4096 / 512)
     "mb8k": ["HM_MB2_TS=8192", "HM_MB2_T=1024"],
@@ -130,6 +136,10 @@ PATCHES["mb2loadonly"] = [("hm_merge.hip", """                for (int j = 0; j 
                     const uint64_t h = hms_hash(k[j]);""", """                for (int j = 0; j < 4; j++) {
                     if (k[j] != 0x1234567ull) continue;
                     const uint64_t h = hms_hash(k[j]);""")]
+# the route's scatter without its record stores
+PATCHES["xrnostore"] = [("hm_merge.hip", """            if (OUT == 0) {
+                hm_rec_put(a.rec_out + 5 * q, sk[i], (uint32_t)sc[i]);""", """            if (OUT == 0) {
+                if (q == 0x123456789ull) hm_rec_put(a.rec_out + 5 * q, sk[i], (uint32_t)sc[i]);""")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
