@@ -509,37 +509,32 @@ __global__ __launch_bounds__(256) void k_xroute_count(HmRouteArgs a)
     for (uint32_t d = tid; d < D; d += 256) hist[d] = 0;
     __syncthreads();
     const uint64_t c0 = a.n * blockIdx.x / gridDim.x, c1 = a.n * (blockIdx.x + 1) / gridDim.x;
-    bool wide = false;
     for (uint64_t t0 = c0; t0 < c1; t0 += 256 * HM_XRC_PPT) {
-        uint64_t k[HM_XRC_PPT], cn[HM_XRC_PPT];
+        uint64_t k[HM_XRC_PPT];
 #pragma unroll
         for (int j = 0; j < HM_XRC_PPT; j++) {
             const uint64_t i = t0 + j * 256 + tid;
             k[j] = i < c1 ? a.keys[i] : 0ull;
-            cn[j] = i < c1 ? a.counts[i] : 0ull;
         }
 #pragma unroll
         for (int j = 0; j < HM_XRC_PPT; j++) {
-            const bool in = t0 + j * 256 + tid < c1;
+            const uint64_t i = t0 + j * 256 + tid;
+            const bool in = i < c1;
             const int z = (int)(k[j] >> 58);
-            if (in && z <= a.dense_zmax) {
+            const bool dense = in && z <= a.dense_zmax;
+            /* counts: the dense cells' (grid sums) and grouped cells' (the group
+             * picks the owner); the wide checks are the scatter pass's */
+            const uint64_t cn = (dense || (in && a.grouped)) ? a.counts[i] : 0ull;
+            if (dense) {
                 const uint64_t r = (k[j] >> 29) & 0x1FFFFFFFull, c = k[j] & 0x1FFFFFFFull;
                 const uint64_t off = ((1ull << (2 * z)) - 1) / 3;
                 atomicAdd((unsigned long long*)&a.grid[off + ((hm_spread29(r) << 1) | hm_spread29(c))],
-                          (unsigned long long)cn[j]);
+                          (unsigned long long)cn);
             }
-            const HmXCell x = hm_xr_cell(a, k[j], cn[j], in);
-            if (x.d != ~0u) {
-                atomicAdd(&hist[x.d], 1u);
-                const uint64_t kk = k[j];
-                const bool kw = (a.rec_out || a.grouped) && (z > 21 || ((kk >> 29) & 0x1FFFFFFFull) >= (1ull << 21) ||
-                                                             (kk & 0x1FFFFFFFull) >= (1ull << 21));
-                const bool cw = a.grouped ? (cn[j] >> 32) >= (1ull << HM_GKEY_GROUP_BITS) : (cn[j] >> 32) != 0ull;
-                wide |= kw || cw;
-            }
+            const HmXCell x = hm_xr_cell(a, k[j], cn, in);
+            if (x.d != ~0u) atomicAdd(&hist[x.d], 1u);
         }
     }
-    if (a.wide && __any(wide) && (tid & 63) == 0) atomicOr(a.wide, 1ull);
     __syncthreads();
     for (uint32_t d = tid; d < D; d += 256) a.block_cnt[(uint64_t)d * a.C + blockIdx.x] = hist[d];
 }
@@ -577,13 +572,26 @@ __global__ __launch_bounds__(256) void k_xroute_scatter(HmRouteArgs a)
             k[j] = i < c1 ? a.keys[i] : 0ull;
             cn[j] = i < c1 ? a.counts[i] : 0ull;
         }
+        bool wide = false;
 #pragma unroll
         for (int j = 0; j < HM_XR_PPT; j++) {
             const HmXCell x = hm_xr_cell(a, k[j], cn[j], t0 + j * 256 + tid < c1);
             d[j] = x.d;
+            if (x.d != ~0u && OUT != 1) {
+                /* wide: a count needs 64 bits, a grouped cell's group passes the
+                 * merge key's field, or (records and grouped keys) the key
+                 * passes 48 bits (zoom > 21, row or column >= 2^21) */
+                const uint64_t kk = k[j];
+                const bool kw = (OUT == 0 || a.grouped) &&
+                                ((kk >> 58) > 21 || ((kk >> 29) & 0x1FFFFFFFull) >= (1ull << 21) ||
+                                 (kk & 0x1FFFFFFFull) >= (1ull << 21));
+                const bool cw = a.grouped ? (cn[j] >> 32) >= (1ull << HM_GKEY_GROUP_BITS) : (cn[j] >> 32) != 0ull;
+                wide |= kw || cw;
+            }
             if (OUT == 2 && a.grouped) k[j] = x.mk;
             r[j] = x.d != ~0u ? atomicAdd(&hist[x.d], 1u) : 0u;
         }
+        if (OUT != 1 && a.wide && __any(wide) && (tid & 63) == 0) atomicOr(a.wide, 1ull);
         __syncthreads();
         uint32_t loc = 0;
         for (uint32_t q = 0; q < per; q++) {
