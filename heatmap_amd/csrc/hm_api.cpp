@@ -483,9 +483,24 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     HIPCHK(hipMemcpyAsync(orand, up, 4 * 8, hipMemcpyHostToDevice, s));
     if (lat) {
         /* points: projected straight into keys (the kept ones, compacted) */
+        HmPkArgs pk;
+        pk.lat = lat;
+        pk.lon = lon;
+        pk.keep = keep;
+        pk.group = group;
+        pk.n = (int64_t)n;
+        pk.Z = Z;
+        pk.klo = klo[0];
+        pk.khi = khi[0];
+        pk.count = ctx->state + ST_XCOUNT;
+        pk.err_word = ctx->state + ST_ERR;
+        pk.orand = orand;
+        pk.redo_cap = std::min<uint64_t>(n, std::max<uint64_t>(1u << 16, n / 256));
+        ENSURE(B_REDO_IDX, pk.redo_cap * sizeof(uint32_t) + 4, pk.redo_idx);
+        pk.redo_count = ctx->state + ST_REDO;
         HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, sizeof(unsigned long long), s));
-        hm_launch_project_keys(s, lat, lon, keep, group, (int64_t)n, Z, klo[0], khi[0], ctx->state + ST_XCOUNT,
-                               ctx->state + ST_ERR, orand);
+        HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, sizeof(unsigned long long), s));
+        hm_launch_project_keys(s, pk);
     } else {
         HmGenArgs ga;
         ga.row = row;

@@ -3675,15 +3675,151 @@ __global__ __launch_bounds__(256) void k_project_keys(const double* lat, const d
     }
 }
 
-void hm_launch_project_keys(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
-                            const uint32_t* group, int64_t n, int Z, uint64_t* klo, uint64_t* khi,
-                            unsigned long long* count, unsigned long long* err_word, unsigned long long* orand)
+/* The keys' fast form: hm_project_fast (no transcendental, no call) for
+ * every point; the points it cannot settle (guard band, |lat| > 85.05, a tile
+ * outside the square, non-finite input: a few per million) are listed for
+ * k_project_keys_slow, which takes them through k_project_keys' exact code --
+ * the keys are a multiset (sorted next), so where a key lands in the
+ * compacted list is free, and errors go by input index (atomicMin) either
+ * way.  (k_project_keys with the exact chain inline ran at 2 waves a SIMD:
+ * 2.1 ms for 1e8 points.) */
+#define HM_PK_PPT 8
+__global__ __launch_bounds__(256) void k_project_keys_fast(HmPkArgs a)
 {
-    int64_t blocks = (n + 256 * HM_PL_PPT - 1) / (256 * HM_PL_PPT);
-    if (blocks > 4096) blocks = 4096;
+    __shared__ double tab[HM_YTAB_N];
+    __shared__ uint32_t scr[256 / 64 + 1];
+    __shared__ unsigned long long base_s;
+    hm_load_ytab(tab);
+    __syncthreads();
+    const double scale = hm_exp2i(a.Z), kz = HM_INV360 * scale;
+    unsigned long long o_lo = 0, o_hi = 0, n_lo = ~0ull, n_hi = ~0ull;
+    constexpr int64_t TILE = 256 * HM_PK_PPT;
+    for (int64_t t0 = (int64_t)blockIdx.x * TILE; t0 < a.n; t0 += (int64_t)gridDim.x * TILE) {
+        hm_u128 k[HM_PK_PPT];
+        uint32_t pm = 0, sm = 0;
+#pragma unroll
+        for (int j = 0; j < HM_PK_PPT; j++) {
+            const int64_t i = t0 + (int64_t)j * 256 + threadIdx.x;
+            k[j] = 0;
+            if (i < a.n) {
+                int32_t r, c;
+                const int fast = hm_project_fast(a.lat[i], a.lon[i], scale, kz, &r, &c, tab);
+                sm |= (uint32_t)(!fast) << j;
+                if (fast && (!a.keep || a.keep[i])) {
+                    bool ok = false;
+                    k[j] = hm_gen_key(r, c, a.group ? a.group[i] : 0u, a.Z, &ok);
+                    if (!ok) atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)HM_E_RANGE);
+                    pm |= (uint32_t)ok << j;
+                    if (ok) {
+                        o_lo |= (unsigned long long)k[j];
+                        o_hi |= (unsigned long long)(k[j] >> 64);
+                        n_lo &= (unsigned long long)k[j];
+                        n_hi &= (unsigned long long)(k[j] >> 64);
+                    }
+                }
+            }
+        }
+        /* the unsettled points, one list reservation a wave */
+#pragma unroll
+        for (int j = 0; j < HM_PK_PPT; j++) {
+            const bool sl = (sm >> j) & 1u;
+            const uint64_t m = __ballot(sl);
+            if (!m) continue;
+            unsigned long long at = 0;
+            if (hm_lane() == 0) at = atomicAdd(a.redo_count, (unsigned long long)__popcll(m));
+            at = __shfl(at, 0, 64) + hm_mbcnt(m);
+            if (sl && at < a.redo_cap) a.redo_idx[at] = (uint32_t)(t0 + (int64_t)j * 256 + threadIdx.x);
+        }
+        uint32_t tot;
+        uint32_t pos = hm_block_excl_scan<256>((uint32_t)__popc(pm), scr, &tot);
+        if (threadIdx.x == 0) base_s = tot ? atomicAdd(a.count, (unsigned long long)tot) : 0ull;
+        __syncthreads();
+        const unsigned long long b = base_s;
+        __syncthreads();
+#pragma unroll
+        for (int j = 0; j < HM_PK_PPT; j++)
+            if ((pm >> j) & 1u) {
+                a.klo[b + pos] = (uint64_t)k[j];
+                a.khi[b + pos] = (uint64_t)(k[j] >> 64);
+                pos++;
+            }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        o_lo |= __shfl_xor(o_lo, o, 64);
+        o_hi |= __shfl_xor(o_hi, o, 64);
+        n_lo &= __shfl_xor(n_lo, o, 64);
+        n_hi &= __shfl_xor(n_hi, o, 64);
+    }
+    if (hm_lane() == 0) {
+        atomicOr(&a.orand[0], o_lo);
+        atomicOr(&a.orand[1], o_hi);
+        atomicAnd(&a.orand[2], n_lo);
+        atomicAnd(&a.orand[3], n_hi);
+    }
+}
+
+/* the listed points through the exact chain (k_project_keys' per-point code);
+ * a list that overflowed its capacity: every point the fast form cannot
+ * settle, found again by a sweep of the whole input */
+__global__ __launch_bounds__(256) void k_project_keys_slow(HmPkArgs a)
+{
+    __shared__ double tab[HM_YTAB_N];
+    hm_load_ytab(tab);
+    __syncthreads();
+    const uint64_t listed = *a.redo_count;
+    const bool sweep = listed > a.redo_cap;
+    const uint64_t m = sweep ? (uint64_t)a.n : listed;
+    const double scale = hm_exp2i(a.Z), kz = HM_INV360 * scale;
+    unsigned long long o_lo = 0, o_hi = 0, n_lo = ~0ull, n_hi = ~0ull;
+    for (uint64_t v = (uint64_t)blockIdx.x * 256 + threadIdx.x; v < m; v += (uint64_t)gridDim.x * 256) {
+        const int64_t i = sweep ? (int64_t)v : (int64_t)a.redo_idx[v];
+        if (sweep) {
+            int32_t r, c;
+            if (hm_project_fast(a.lat[i], a.lon[i], scale, kz, &r, &c, tab)) continue;
+        }
+        int64_t r = 0, c = 0;
+        int slow = 0;
+        int st = hm_project_point(a.lat[i], a.lon[i], a.Z, &r, &c, &slow, tab);
+        bool ok = false;
+        hm_u128 k = 0;
+        if (st == HM_OK && (!a.keep || a.keep[i])) {
+            k = hm_gen_key(r, c, a.group ? a.group[i] : 0u, a.Z, &ok);
+            if (!ok) st = HM_E_RANGE;
+        }
+        if (st != HM_OK) atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
+        if (ok) {
+            const unsigned long long q = atomicAdd(a.count, 1ull);
+            a.klo[q] = (uint64_t)k;
+            a.khi[q] = (uint64_t)(k >> 64);
+            o_lo |= (unsigned long long)k;
+            o_hi |= (unsigned long long)(k >> 64);
+            n_lo &= (unsigned long long)k;
+            n_hi &= (unsigned long long)(k >> 64);
+        }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        o_lo |= __shfl_xor(o_lo, o, 64);
+        o_hi |= __shfl_xor(o_hi, o, 64);
+        n_lo &= __shfl_xor(n_lo, o, 64);
+        n_hi &= __shfl_xor(n_hi, o, 64);
+    }
+    if (hm_lane() == 0 && (o_lo | o_hi)) {
+        atomicOr(&a.orand[0], o_lo);
+        atomicOr(&a.orand[1], o_hi);
+        atomicAnd(&a.orand[2], n_lo);
+        atomicAnd(&a.orand[3], n_hi);
+    }
+}
+
+void hm_launch_project_keys(hipStream_t s, const HmPkArgs& a)
+{
+    int64_t blocks = (a.n + 256 * HM_PK_PPT - 1) / (256 * HM_PK_PPT);
+    if (blocks > 8192) blocks = 8192;
     if (blocks < 1) blocks = 1;
-    hipLaunchKernelGGL(k_project_keys, dim3((unsigned)blocks), dim3(256), 0, s, lat, lon, keep, group, n, Z, klo,
-                       khi, count, err_word, orand);
+    hipLaunchKernelGGL(k_project_keys_fast, dim3((unsigned)blocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_project_keys_slow, dim3(1024), dim3(256), 0, s, a);
 }
 
 void hm_launch_partN(hipStream_t s, const HmPartNArgs& a, uint32_t items, bool out16, bool few_runs)

@@ -624,9 +624,24 @@ struct HmGenEmit {
     unsigned long long* xcursor;
 };
 void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a);
-void hm_launch_project_keys(hipStream_t s, const double* lat, const double* lon, const uint8_t* keep,
-                            const uint32_t* group, int64_t n, int Z, uint64_t* klo, uint64_t* khi,
-                            unsigned long long* count, unsigned long long* err_word, unsigned long long* orand);
+/* points -> general-path keys (k_project_keys_fast + k_project_keys_slow) */
+struct HmPkArgs {
+    const double* lat;
+    const double* lon;
+    const uint8_t* keep;
+    const uint32_t* group;
+    int64_t n;
+    int Z;
+    uint64_t* klo;
+    uint64_t* khi;
+    unsigned long long* count;      /* keys written (zeroed) */
+    unsigned long long* err_word;
+    unsigned long long* orand;
+    uint32_t* redo_idx;             /* points the fast form leaves to the exact chain */
+    unsigned long long* redo_count; /* (zeroed) */
+    uint64_t redo_cap;
+};
+void hm_launch_project_keys(hipStream_t s, const HmPkArgs& a);
 void hm_launch_tiles_list(hipStream_t s, const int64_t* rows, const int64_t* cols, const uint8_t* keep,
                           const uint32_t* group, int64_t n, int64_t* row, int64_t* col, uint32_t* grp, int64_t* idx,
                           unsigned long long* count);

@@ -117,6 +117,20 @@ def test_grouped_packed_vs_oracle(gpu, zmin, zmax, groups):
     assert device.count_grouped_packed_device(lat2, lon, g, keep2, zmin, zmax) is not None
 
 
+def test_grouped_many_unsettled_points(gpu):
+    """More points than the fast projection's list holds (2^16 here) left to
+    the exact chain -- 60% polar or beyond +-180: the exact pass sweeps the
+    whole input again; the counts still equal the oracle's per group."""
+    lat, lon = _exotic_cloud(150_000, seed=77, frac=0.6)
+    g = (np.arange(lat.size) % 3).astype(np.uint32) * 11
+    got = device.count_grouped(lat, lon, g, None, 4, 18).sorted()
+    for gid in (0, 11, 22):
+        ref = oracle.count(lat, lon, (g == gid).astype(np.uint8), 4, 18)
+        m = got.group == gid
+        for k in ("zoom", "row", "col", "count"):
+            assert np.array_equal(getattr(got, k)[m], ref[k]), k
+
+
 def test_grouped_errors(gpu):
     lat, lon = synth.uniform(10000, seed=2)
     lat = lat.copy()
