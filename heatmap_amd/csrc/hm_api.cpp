@@ -498,9 +498,24 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
         pk.redo_cap = std::min<uint64_t>(n, std::max<uint64_t>(1u << 16, n / 256));
         ENSURE(B_REDO_IDX, pk.redo_cap * sizeof(uint32_t) + 4, pk.redo_idx);
         pk.redo_count = ctx->state + ST_REDO;
+        pk.dense = keep == nullptr;
+        pk.write_hi = 0;
         HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, sizeof(unsigned long long), s));
         HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, sizeof(unsigned long long), s));
         hm_launch_project_keys(s, pk);
+        HIPCHK(hipGetLastError());
+        unsigned long long* dn = ctx->host_state + 2 * ST_COUNT;
+        HIPCHK(hipMemcpyAsync(dn, orand, 4 * 8, hipMemcpyDeviceToHost, s));
+        HIPCHK(hm_sync(s));
+        if (dn[1] != dn[3]) {
+            /* wide keys (groups past 2^22 at zoom 21, tiles outside the
+             * square): again, with the high halves */
+            HIPCHK(hipMemcpyAsync(orand, up, 4 * 8, hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemsetAsync(ctx->state + ST_XCOUNT, 0, sizeof(unsigned long long), s));
+            HIPCHK(hipMemsetAsync(ctx->state + ST_REDO, 0, sizeof(unsigned long long), s));
+            pk.write_hi = 1;
+            hm_launch_project_keys(s, pk);
+        }
     } else {
         HmGenArgs ga;
         ga.row = row;
@@ -521,7 +536,7 @@ static int gen_count(hm_ctx* ctx, const int64_t* row, const int64_t* col, const 
     int st;
     if ((st = read_state(ctx))) return st;
     if ((st = take_error(ctx))) return st;
-    if (lat) {
+    if (lat && keep) {
         n = ctx->host_state[ST_XCOUNT];
         if (n == 0) return HM_OK;
     }

@@ -90,6 +90,42 @@ __device__ __forceinline__ void hm_orand_flush(unsigned long long* orand, unsign
     }
 }
 
+/* the same, one set of atomics per 256-thread block (every thread calls):
+ * same-address atomics serialise (~88 per us a word) */
+__device__ __forceinline__ void hm_orand_flush_block(unsigned long long* orand, unsigned long long o_lo,
+                                                     unsigned long long o_hi, unsigned long long n_lo,
+                                                     unsigned long long n_hi)
+{
+    __shared__ unsigned long long red[4][4];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        o_lo |= __shfl_xor(o_lo, o, 64);
+        o_hi |= __shfl_xor(o_hi, o, 64);
+        n_lo &= __shfl_xor(n_lo, o, 64);
+        n_hi &= __shfl_xor(n_hi, o, 64);
+    }
+    const int w = threadIdx.x >> 6;
+    if (hm_lane() == 0) {
+        red[0][w] = o_lo;
+        red[1][w] = o_hi;
+        red[2][w] = n_lo;
+        red[3][w] = n_hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < 4; q++) {
+            o_lo |= red[0][q];
+            o_hi |= red[1][q];
+            n_lo &= red[2][q];
+            n_hi &= red[3][q];
+        }
+        atomicOr(&orand[0], o_lo);
+        atomicOr(&orand[1], o_hi);
+        atomicAnd(&orand[2], n_lo);
+        atomicAnd(&orand[3], n_hi);
+    }
+}
+
 __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
 {
     const uint64_t n = a.n;
@@ -111,7 +147,7 @@ __global__ __launch_bounds__(256) void k_gen_keys(HmGenArgs a)
         n_lo &= (unsigned long long)k;
         n_hi &= (unsigned long long)(k >> 64);
     }
-    hm_orand_flush(a.orand, o_lo, o_hi, n_lo, n_hi);
+    hm_orand_flush_block(a.orand, o_lo, o_hi, n_lo, n_hi);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -907,7 +943,7 @@ static unsigned hm_ggrid(uint64_t n, unsigned per, unsigned cap)
 
 void hm_launch_gen_keys(hipStream_t s, const HmGenArgs& a)
 {
-    hipLaunchKernelGGL(k_gen_keys, dim3(hm_ggrid(a.n, 256, 8192)), dim3(256), 0, s, a);
+    hipLaunchKernelGGL(k_gen_keys, dim3(hm_ggrid(a.n, 256, 4096)), dim3(256), 0, s, a);
 }
 
 uint64_t hm_rx_os_tiles(uint64_t n) { return (n + HM_OS_TILE_MIN - 1) / HM_OS_TILE_MIN; }

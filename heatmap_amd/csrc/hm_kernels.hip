@@ -3682,7 +3682,12 @@ __global__ __launch_bounds__(256) void k_project_keys(const double* lat, const d
  * the keys are a multiset (sorted next), so where a key lands in the
  * compacted list is free, and errors go by input index (atomicMin) either
  * way.  (k_project_keys with the exact chain inline ran at 2 waves a SIMD:
- * 2.1 ms for 1e8 points.) */
+ * 2.1 ms for 1e8 points.)  Dense (no keep mask): every point's key goes to
+ * its own index -- no compaction, no per-tile cursor atomic (one address:
+ * 49K of them took ~0.5 ms for 1e8 points).  write_hi = 0: the high halves
+ * are not stored (the caller runs the pass again with them when the keys
+ * turn out wide; narrow keys share one high half, which the sort and the
+ * cascade take as a constant). */
 #define HM_PK_PPT 8
 __global__ __launch_bounds__(256) void k_project_keys_fast(HmPkArgs a)
 {
@@ -3730,6 +3735,17 @@ __global__ __launch_bounds__(256) void k_project_keys_fast(HmPkArgs a)
             at = __shfl(at, 0, 64) + hm_mbcnt(m);
             if (sl && at < a.redo_cap) a.redo_idx[at] = (uint32_t)(t0 + (int64_t)j * 256 + threadIdx.x);
         }
+        if (a.dense) {
+            /* no keep mask: every point has a key (or the call fails), at its index */
+#pragma unroll
+            for (int j = 0; j < HM_PK_PPT; j++)
+                if ((pm >> j) & 1u) {
+                    const int64_t i = t0 + (int64_t)j * 256 + threadIdx.x;
+                    a.klo[i] = (uint64_t)k[j];
+                    if (a.write_hi) a.khi[i] = (uint64_t)(k[j] >> 64);
+                }
+            continue;
+        }
         uint32_t tot;
         uint32_t pos = hm_block_excl_scan<256>((uint32_t)__popc(pm), scr, &tot);
         if (threadIdx.x == 0) base_s = tot ? atomicAdd(a.count, (unsigned long long)tot) : 0ull;
@@ -3740,7 +3756,7 @@ __global__ __launch_bounds__(256) void k_project_keys_fast(HmPkArgs a)
         for (int j = 0; j < HM_PK_PPT; j++)
             if ((pm >> j) & 1u) {
                 a.klo[b + pos] = (uint64_t)k[j];
-                a.khi[b + pos] = (uint64_t)(k[j] >> 64);
+                if (a.write_hi) a.khi[b + pos] = (uint64_t)(k[j] >> 64);
                 pos++;
             }
     }
@@ -3751,7 +3767,24 @@ __global__ __launch_bounds__(256) void k_project_keys_fast(HmPkArgs a)
         n_lo &= __shfl_xor(n_lo, o, 64);
         n_hi &= __shfl_xor(n_hi, o, 64);
     }
+    /* one OR / AND per block: these four words take every block's atomics
+     * (per wave they were 32K same-address atomics a word for 1e8 points) */
+    __shared__ unsigned long long red[4][4];
+    const int w = threadIdx.x >> 6;
     if (hm_lane() == 0) {
+        red[0][w] = o_lo;
+        red[1][w] = o_hi;
+        red[2][w] = n_lo;
+        red[3][w] = n_hi;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int q = 1; q < 4; q++) {
+            o_lo |= red[0][q];
+            o_hi |= red[1][q];
+            n_lo &= red[2][q];
+            n_hi &= red[3][q];
+        }
         atomicOr(&a.orand[0], o_lo);
         atomicOr(&a.orand[1], o_hi);
         atomicAnd(&a.orand[2], n_lo);
@@ -3789,9 +3822,9 @@ __global__ __launch_bounds__(256) void k_project_keys_slow(HmPkArgs a)
         }
         if (st != HM_OK) atomicMin(a.err_word, ((unsigned long long)i << 8) | (unsigned long long)st);
         if (ok) {
-            const unsigned long long q = atomicAdd(a.count, 1ull);
+            const unsigned long long q = a.dense ? (unsigned long long)i : atomicAdd(a.count, 1ull);
             a.klo[q] = (uint64_t)k;
-            a.khi[q] = (uint64_t)(k >> 64);
+            if (a.write_hi) a.khi[q] = (uint64_t)(k >> 64);
             o_lo |= (unsigned long long)k;
             o_hi |= (unsigned long long)(k >> 64);
             n_lo &= (unsigned long long)k;
@@ -3816,7 +3849,7 @@ __global__ __launch_bounds__(256) void k_project_keys_slow(HmPkArgs a)
 void hm_launch_project_keys(hipStream_t s, const HmPkArgs& a)
 {
     int64_t blocks = (a.n + 256 * HM_PK_PPT - 1) / (256 * HM_PK_PPT);
-    if (blocks > 8192) blocks = 8192;
+    if (blocks > 2048) blocks = 2048;
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_project_keys_fast, dim3((unsigned)blocks), dim3(256), 0, s, a);
     hipLaunchKernelGGL(k_project_keys_slow, dim3(1024), dim3(256), 0, s, a);

@@ -637,6 +637,8 @@ struct HmPkArgs {
     unsigned long long* count;      /* keys written (zeroed) */
     unsigned long long* err_word;
     unsigned long long* orand;
+    int dense;                      /* no keep mask: key of point i at i (count untouched) */
+    int write_hi;                   /* store the high halves (wide keys) */
     uint32_t* redo_idx;             /* points the fast form leaves to the exact chain */
     unsigned long long* redo_count; /* (zeroed) */
     uint64_t redo_cap;
