@@ -136,6 +136,11 @@ PATCHES["mb2loadonly"] = [("hm_merge.hip", """                for (int j = 0; j 
                     const uint64_t h = hms_hash(k[j]);""", """                for (int j = 0; j < 4; j++) {
                     if (k[j] != 0x1234567ull) continue;
                     const uint64_t h = hms_hash(k[j]);""")]
+# hm_count's emit reservations without the cursor atomic (timing only)
+PATCHES["emitnocur"] = [("hm_kernels.hip", "if (lane == NW - 1) *sbase = incl ? atomicAdd(o.cursor, (unsigned long long)incl) : 0ull;",
+                         "if (lane == NW - 1) *sbase = (uint64_t)(hm_block_id() & 4095u) * 16384u;"),
+                        ("hm_kernels.hip", "if (threadIdx.x == 0) *sbase = atomicAdd(o.cursor, (unsigned long long)tot);",
+                         "if (threadIdx.x == 0) *sbase = (uint64_t)(hm_block_id() & 4095u) * 16384u;")]
 # the route's scatter without its record stores
 PATCHES["xrnostore"] = [("hm_merge.hip", """            if (OUT == 0) {
                 hm_rec_put(a.rec_out + 5 * q, sk[i], (uint32_t)sc[i]);""", """            if (OUT == 0) {
