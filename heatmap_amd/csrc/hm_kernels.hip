@@ -588,6 +588,9 @@ static_assert(HM_L1_SLOTS % HM_P1_THREADS == 0, "slots per thread");
 #ifndef HM_L1_FAST
 #define HM_L1_FAST 1                        /* 0: k_project_partition, 1: k_l1_fast */
 #endif
+#ifndef HM_L1_LATE_DEST
+#define HM_L1_LATE_DEST 1                   /* destinations resolved after the staging (see the staging) */
+#endif
 #ifndef HM_L1_WAVES
 #define HM_L1_WAVES 4                       /* k_l1_fast: waves per SIMD its registers allow (4: 2 blocks of 8 waves per CU) */
 #endif
@@ -826,33 +829,50 @@ k_l1_fast(HmPart1Args a)
         }
     }
     bool over = false;
+    /* a slot's destination delta: its region base + reservation - stage
+     * offset; a region that overflowed: destinations >= 0xFFF00000 (no key
+     * position reaches it), dropped by the copy-out */
+    auto deltas = [&]() {
+#pragma unroll
+        for (int q = 0; q < PERD; q++) {
+            const uint32_t sl = q * HM_P1_THREADS + tid;
+            if (live(sl)) {
+                const uint32_t rc = smk[q] != 0 ? rcap2[q][1] : rcap2[q][0];
+                const uint32_t rb = smk[q] != 0 ? rbase2[q][1] : rbase2[q][0];
+                const bool fits = (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rc;
+                over |= cnt[q] && !fits;
+                cw[HM_L1_CW + sl] = (fits ? rb + gpos[q] : 0xFFF00000u) - offq[q];
+            }
+        }
+        if (over) {
+            atomicOr(a.overflow, 1ull);
+            s_over = 1;
+        }
+    };
 #pragma unroll
     for (int q = 0; q < PERD; q++) {
         const uint32_t sl = q * HM_P1_THREADS + tid;
-        if (live(sl)) {
-            const uint32_t rc = smk[q] != 0 ? rcap2[q][1] : rcap2[q][0];
-            const uint32_t rb = smk[q] != 0 ? rbase2[q][1] : rbase2[q][0];
-            const bool fits = (uint64_t)gpos[q] + cnt[q] <= (uint64_t)rc;
-            over |= cnt[q] && !fits;
-            cw[sl] = offq[q];
-            /* a region that overflowed: destinations >= 0xFFF00000 (no key
-             * position reaches it), dropped by the copy-out */
-            cw[HM_L1_CW + sl] = (fits ? rb + gpos[q] : 0xFFF00000u) - offq[q];
-        }
+        if (live(sl)) cw[sl] = offq[q];
     }
-    if (over) {
-        atomicOr(a.overflow, 1ull);
-        s_over = 1;
-    }
+    if (!HM_L1_LATE_DEST) deltas();
     hm_lds_barrier();
     HM_STAMP_M(4, 4);
-    /* staging, branch-free: a point that stages nothing writes its lane's pad entry */
+    /* staging, branch-free: a point that stages nothing writes its lane's pad
+     * entry.  HM_L1_LATE_DEST: the entry holds its slot, and the destination
+     * deltas are written after the staging, so the reservation atomics'
+     * round trip overlaps it (the copy-out looks the delta up per key) */
 #pragma unroll
     for (int k = 0; k < HM_P1_PPT; k++) {
-        const uint32_t o = cw[slot[k]], dl = cw[HM_L1_CW + slot[k]];   /* (dummies: in range, unused) */
+        const uint32_t o = cw[slot[k]];   /* (dummies: in range, unused) */
         const uint32_t pos = slot[k] < HM_L1_SLOTS ? o + rank[k] : HM_T1 + (uint32_t)hm_lane();
-        ent[pos] = make_uint2(key[k], dl + pos);
+        if (HM_L1_LATE_DEST) {
+            ent[pos] = make_uint2(key[k], slot[k]);
+        } else {
+            const uint32_t dl = cw[HM_L1_CW + slot[k]];
+            ent[pos] = make_uint2(key[k], dl + pos);
+        }
     }
+    if (HM_L1_LATE_DEST) deltas();
     hm_lds_barrier();
     HM_STAMP_M(4, 5);
     /* copy-out: a wave stores 64 consecutive staged keys -- cold keys in [0, C)
@@ -872,7 +892,11 @@ k_l1_fast(HmPart1Args a)
     };
     uint2 e[HM_P1_PPT];
 #pragma unroll
-    for (int j = 0; j < HM_P1_PPT; j++) e[j] = ent[j * HM_P1_THREADS + tid];   /* past total: unused */
+    for (int j = 0; j < HM_P1_PPT; j++) {
+        const uint32_t i = j * HM_P1_THREADS + tid;
+        e[j] = ent[i];   /* past total: unused */
+        if (HM_L1_LATE_DEST) e[j].y = i < total ? cw[HM_L1_CW + e[j].y] + i : 0u;
+    }
     const uint32_t wofs = (uint32_t)tid & ~63u;
     if (!s_over) {
 #pragma unroll
