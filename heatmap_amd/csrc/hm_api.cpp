@@ -927,7 +927,7 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
              * (digit, shard) entries are non-empty, and sum sqrt(e stride) <=
              * sqrt(M nn stride) (Cauchy-Schwarz) */
             const double nn = (double)n + (double)(F + (hot_on ? HM_MAX_HOT : 0)) * (double)stride;
-            const double M = F + std::min((double)F, nn / (64.0 * HM_T1)) * (HM_L1_SHARDS - 1) +
+            const double M = F + std::min((double)F, nn / ((double)HM_L1_SHARD_TILES * HM_T1)) * (HM_L1_SHARDS - 1) +
                              (hot_on ? (double)HM_MAX_HOT * HM_L1_SHARDS : 0.0);
             double bound = nn * 17.0 / 16.0 + 8.0 * sqrt(M * nn * (double)stride) + M * 2.0 * HM_T1 +
                            (double)(F + (hot_on ? HM_MAX_HOT : 0)) * HM_L1_ZERO_SAMPLES * (double)stride + 1024.0;

@@ -1117,7 +1117,7 @@ void hm_launch_hot_select(hipStream_t s, const HmHotArgs& a)
 __device__ __forceinline__ uint32_t hm_l1_cap(uint32_t hist, uint64_t stride, int* ns)
 {
     const double est = (double)hist * (double)stride;
-    *ns = est > 64.0 * HM_T1 ? HM_L1_SHARDS : 1;
+    *ns = est > (double)HM_L1_SHARD_TILES * HM_T1 ? HM_L1_SHARDS : 1;
     const double e = est / *ns;
     /* + HM_L1_ZERO_SAMPLES strides per digit: a digit with few or no samples
      * may still hold that many strides of points (P(0 samples | 24) = 4e-11);

@@ -21,6 +21,9 @@
 #define HM_P1_WAVES 1                       /* waves per SIMD the register budget targets */
 #endif
 #define HM_L1_SHARDS 8                      /* sub-regions of a hot level-1 digit */
+#ifndef HM_L1_SHARD_TILES
+#define HM_L1_SHARD_TILES 16                /* a digit of more points than this many tiles is sharded (64 until round 5) */
+#endif
 #define HM_L1_ZERO_SAMPLES 24               /* level-1 region slack per digit, in sample strides */
 #define HM_Z1 5                             /* level-1 digit: zoom-5 tile */
 #define HM_MAX_F1 1024

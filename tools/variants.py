@@ -70,7 +70,11 @@ VARIANTS = {
     "cs2it8": ["HM_CS2_IT=8"],                       # k_cascade2: 2048-item tiles
     "cs2it12": ["HM_CS2_IT=12"],
     "l1nt0": ["HM_L1_NT=0"],                        # K1's point loads without the non-temporal hint
-    "l1early": ["HM_L1_LATE_DEST=0"],                # K1: destinations before the staging (round 4)
+    "l1early": ["HM_L1_LATE_DEST=0"],
+    "sh8": ["HM_L1_SHARD_TILES=8"],                 # level-1 digits sharded above 8 tiles of points (default 64)
+    "sh2": ["HM_L1_SHARD_TILES=2"],
+    "sh4": ["HM_L1_SHARD_TILES=4"],
+    "sh16": ["HM_L1_SHARD_TILES=16"],                # K1: destinations before the staging (round 4)
     "xr16": ["HM_XR_PPT=16"],                        # route scatter: 4096-cell tiles (default 2048)
     "xr4": ["HM_XR_PPT=4"],
     "xrc8": ["HM_XRC_PPT=8"],                        # route count: 8 cells a thread in flight (default 16)
