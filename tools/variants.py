@@ -141,6 +141,9 @@ PATCHES["mb2loadonly"] = [("hm_merge.hip", """                for (int j = 0; j 
                     const uint64_t h = hms_hash(k[j]);""", """                for (int j = 0; j < 4; j++) {
                     if (k[j] != 0x1234567ull) continue;
                     const uint64_t h = hms_hash(k[j]);""")]
+# k_aggregate: multi-item buckets without their global histogram adds (timing only)
+PATCHES["agnoslot"] = [("hm_kernels.hip", "            if (i < ncell && x[k]) atomicAdd(&g[i], x[k]);",
+                        "            if (i < ncell && x[k] == 0xFFFFFFFFu) atomicAdd(&g[i], x[k]);")]
 # hm_count's emit reservations without the cursor atomic (timing only)
 PATCHES["emitnocur"] = [("hm_kernels.hip", "if (lane == NW - 1) *sbase = incl ? atomicAdd(o.cursor, (unsigned long long)incl) : 0ull;",
                          "if (lane == NW - 1) *sbase = (uint64_t)(hm_block_id() & 4095u) * 16384u;"),
