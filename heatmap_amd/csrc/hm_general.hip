@@ -705,6 +705,9 @@ __global__ __launch_bounds__(256) void k_cascade_emit(HmCascArgs a)
  * and 8 B written per narrow key (16 + 16 wide), plus 2 KB of look-back
  * words per tile. */
 #define HM_OS_THREADS 256
+#ifndef HM_OS_LB
+#define HM_OS_LB 4                  /* one-sweep look-back: predecessors per round trip */
+#endif
 /* keys per thread: 32 narrow keys (211 VGPRs, 72 KB of LDS: 2 blocks per
  * CU; 16 measured 1.1 ms slower per grouped call), 16 wide ones */
 template <typename KT> struct HmOs {
@@ -836,17 +839,31 @@ __global__ __launch_bounds__(HM_OS_THREADS) void k_rx_onesweep(HmRxPass a)
         uint64_t* st = a.tstat + tile * 256 + d;
         __hip_atomic_store(st, hm_cs_word(a.epoch, tile ? HM_CS_FLAG_AGG : HM_CS_FLAG_INC, cnt), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
+        /* look back HM_OS_LB predecessors per round trip (a tile mostly finds
+         * a run of aggregate-only predecessors before an inclusive one; one
+         * load per step made the walk 35% of a pass) */
         uint64_t excl = 0;
         for (int64_t p = (int64_t)tile - 1; p >= 0;) {
-            const uint64_t wv = __hip_atomic_load(a.tstat + (uint64_t)p * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint64_t f = (wv >> 40) == a.epoch ? (wv >> HM_CS_VBITS) & 3ull : 0ull;
-            if (!f) {
-                __builtin_amdgcn_s_sleep(1);
-                continue;
+            uint64_t wv[HM_OS_LB];
+#pragma unroll
+            for (int q = 0; q < HM_OS_LB; q++)
+                wv[q] = p - q >= 0 ? __hip_atomic_load(a.tstat + (uint64_t)(p - q) * 256 + d, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : hm_cs_word(a.epoch, HM_CS_FLAG_INC, 0);
+            int adv = 0;
+            bool done = false;
+#pragma unroll
+            for (int q = 0; q < HM_OS_LB; q++) {
+                if (done || adv < q) break;
+                const uint64_t f = (wv[q] >> 40) == a.epoch ? (wv[q] >> HM_CS_VBITS) & 3ull : 0ull;
+                if (!f) break;
+                excl += wv[q] & ((1ull << HM_CS_VBITS) - 1);
+                adv++;
+                done = f == HM_CS_FLAG_INC;
             }
-            excl += wv & ((1ull << HM_CS_VBITS) - 1);
-            if (f == HM_CS_FLAG_INC) break;
-            p--;
+            if (done) break;
+            if (!adv) __builtin_amdgcn_s_sleep(1);
+            p -= adv;
         }
         if (tile)
             __hip_atomic_store(st, hm_cs_word(a.epoch, HM_CS_FLAG_INC, excl + cnt), __ATOMIC_RELAXED,

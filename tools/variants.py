@@ -73,6 +73,8 @@ VARIANTS = {
     "l1early": ["HM_L1_LATE_DEST=0"],
     "sh8": ["HM_L1_SHARD_TILES=8"],                 # level-1 digits sharded above 8 tiles of points (default 64)
     "sh2": ["HM_L1_SHARD_TILES=2"],
+    "lb1": ["HM_OS_LB=1"],                           # one-sweep look-back: one predecessor per round trip
+    "lb8": ["HM_OS_LB=8"],
     "sh4": ["HM_L1_SHARD_TILES=4"],
     "sh16": ["HM_L1_SHARD_TILES=16"],                # K1: destinations before the staging (round 4)
     "xr16": ["HM_XR_PPT=16"],                        # route scatter: 4096-cell tiles (default 2048)
@@ -141,6 +143,11 @@ PATCHES["mb2loadonly"] = [("hm_merge.hip", """                for (int j = 0; j 
                     const uint64_t h = hms_hash(k[j]);""", """                for (int j = 0; j < 4; j++) {
                     if (k[j] != 0x1234567ull) continue;
                     const uint64_t h = hms_hash(k[j]);""")]
+# one-sweep radix passes without the decoupled look-back (timing only: wrong offsets)
+PATCHES["rxnolb"] = [("hm_general.hip", """        for (int64_t p = (int64_t)tile - 1; p >= 0;) {
+            const uint64_t wv = __hip_atomic_load(a.tstat + (uint64_t)p * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);""",
+                      """        for (int64_t p = (int64_t)tile - 1; p >= 0 && p == 0x7FFFFFFFFFFF;) {
+            const uint64_t wv = __hip_atomic_load(a.tstat + (uint64_t)p * 256 + d, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);""")]
 # k_aggregate: multi-item buckets without their global histogram adds (timing only)
 PATCHES["agnoslot"] = [("hm_kernels.hip", "            if (i < ncell && x[k]) atomicAdd(&g[i], x[k]);",
                         "            if (i < ncell && x[k] == 0xFFFFFFFFu) atomicAdd(&g[i], x[k]);")]
