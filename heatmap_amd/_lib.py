@@ -117,8 +117,8 @@ def load() -> ctypes.CDLL:
         L.hm_cells_merge.argtypes = [vp, vp, vp, c.c_int, c.c_int64, vp, vp, c.c_int64, P(c.c_int64)]
         L.hm_cells_merge_runs.argtypes = [vp, vp, vp, c.c_int, c.c_int64, P(c.c_int64), c.c_int, vp, vp, c.c_int64,
                                           P(c.c_int64)]
-        L.hm_cells_route_pieces.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, c.c_int, vp, vp, vp,
-                                            c.c_int, vp, c.c_int]
+        L.hm_cells_route_pieces.argtypes = [vp, vp, vp, c.c_int64, c.c_int, c.c_int, c.c_int, c.c_int, c.c_int, vp,
+                                            vp, vp, c.c_int, vp, c.c_int]
         L.hm_cells_merge_pieces.argtypes = [vp, c.c_int, c.c_int, P(vp), P(vp), P(c.c_int64), c.c_int, vp, vp,
                                             c.c_int64, P(c.c_int64)]
         L.hm_dense_cells.argtypes = [vp, vp, c.c_int, vp, vp, c.c_int64, P(c.c_int64)]

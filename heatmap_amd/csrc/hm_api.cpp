@@ -1908,11 +1908,12 @@ extern "C" int hm_cells_merge_runs(hm_ctx* ctx, const void* keys, const void* co
  * each owner's group by the first merge digit, so the owner gathers digit
  * s's pieces, partitions them by the next bits and merges */
 extern "C" int hm_cells_route_pieces(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n,
-                                     int nranks, int delta, int dense_zmax, int bits, uint64_t* grid, void* keys_out,
-                                     void* counts_out, int layout, int64_t* sizes, int stride)
+                                     int nranks, int delta, int dense_zmax, int bits, int self_rank, uint64_t* grid,
+                                     void* keys_out, void* counts_out, int layout, int64_t* sizes, int stride)
 {
     const bool rec = layout == HM_CELLS_REC10, grp = layout == HM_CELLS_G12;
     if (!ctx || n < 0 || nranks < 1 || nranks > 64 || delta < 0 || delta > 28 || dense_zmax > 14 || bits < 0 ||
+        self_rank < -1 || self_rank >= nranks ||
         bits > 7 || ((int64_t)nranks << bits) > HM_XR_MAXD || stride < 2 + (1 << bits) || !sizes ||
         (layout != HM_CELLS_U32 && layout != HM_CELLS_U64 && !rec && !grp) || (dense_zmax >= 0 && !grid) ||
         (grp && dense_zmax >= 0) || (n > 0 && (!keys || !counts || !keys_out || (!rec && !counts_out))) ||
@@ -1942,6 +1943,7 @@ extern "C" int hm_cells_route_pieces(hm_ctx* ctx, const uint64_t* keys, const ui
     a.bits = bits;
     a.sizes = (long long*)sizes;
     a.stride = stride;
+    a.self = self_rank;
     if (layout == HM_CELLS_U64) {
         a.keys_out = (uint64_t*)keys_out;
         a.counts_out = (uint64_t*)counts_out;

@@ -495,7 +495,9 @@ __device__ __forceinline__ HmXCell hm_xr_cell(const HmRouteArgs& a, uint64_t k, 
     x.mk = a.grouped ? hm_gkey(k, g) : k;
     const uint32_t o = sp ? hm_owner(k, a.delta, a.nranks, a.grouped ? (uint64_t)g + 1 : 0ull) : 0u;
     const uint32_t h = a.bits ? (uint32_t)(hms_hash(x.mk) >> (64 - a.bits)) : 0u;
-    x.d = sp ? (o << a.bits) | h : ~0u;
+    /* group position of owner o: rank order, or (self >= 0) that owner last */
+    const uint32_t po = a.self < 0 ? o : (o == (uint32_t)a.self ? (uint32_t)a.nranks - 1u : o - (o > (uint32_t)a.self));
+    x.d = sp ? (po << a.bits) | h : ~0u;
     return x;
 }
 
@@ -644,7 +646,8 @@ __global__ __launch_bounds__(256) void k_xroute_sizes(HmRouteArgs a)
     const uint32_t S = 1u << a.bits, D = (uint32_t)a.nranks << a.bits;
     const unsigned long long wide = a.wide ? *a.wide : 0ull;
     for (uint32_t d = threadIdx.x; d < D; d += 256) {
-        const uint32_t o = d >> a.bits, s = d & (S - 1);
+        const uint32_t p = d >> a.bits, s = d & (S - 1);   /* group position p -> owner o */
+        const uint32_t o = a.self < 0 ? p : (p == (uint32_t)a.nranks - 1u ? (uint32_t)a.self : p + (p >= (uint32_t)a.self));
         long long* row = a.sizes + (uint64_t)o * a.stride;
         row[2 + s] = (long long)(a.block_off[(uint64_t)(d + 1) * a.C] - a.block_off[(uint64_t)d * a.C]);
         if (s == 0) {

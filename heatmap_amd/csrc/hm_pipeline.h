@@ -704,6 +704,7 @@ struct HmRouteArgs {
     uint32_t C;
     long long* sizes;
     int stride;
+    int self;                  /* >= 0: that owner's group goes last (the others in rank order) */
 };
 #define HM_XR_MAXD 1024               /* route digits (nranks << bits) */
 void hm_launch_xroute(hipStream_t s, const HmRouteArgs& a, bool scatter, int layout);

@@ -140,13 +140,14 @@ class DeviceOps:
             _lib.raise_for(rc)
         return ko[:nout.value], co[:nout.value]
 
-    def route_pieces(self, keys, counts, ws, dense_zmax, bits, layout, extra=1):
+    def route_pieces(self, keys, counts, ws, dense_zmax, bits, layout, extra=1, self_rank=-1):
         """hm_cells_route_pieces -> (dense grid, parts, sizes): parts as route()
         (REC10: [(uint8 records, 10)]; U64: [(keys, 1), (counts, 1)]; G12:
         [(u64 merge keys, 1), (u32 counts, 1)]) with room for every cell; sizes
         a DEVICE int64 tensor [ws, 2 + 2^bits + extra]: per owner the cells
         sent, the wide flag, the 2^bits piece sizes, then `extra` zero columns
-        for the caller (nothing is synchronised)."""
+        for the caller (nothing is synchronised).  self_rank >= 0: the groups
+        leave in rank order with that owner's group last."""
         from . import _lib
 
         self.ctx.bind_stream()
@@ -164,8 +165,8 @@ class DeviceOps:
                              device=keys.device)
             parts = [(ko, 1), (co, 1)]
         rc = self.L.hm_cells_route_pieces(self.ctx.ptr, self._p(keys), self._p(counts), n, ws, DELTA, dense_zmax, bits,
-                                          self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko), self._p(co),
-                                          layout, self._p(sizes), width)
+                                          self_rank, self._p(grid) if gsz > 0 else ctypes.c_void_p(0), self._p(ko),
+                                          self._p(co), layout, self._p(sizes), width)
         self._check(rc)
         return grid[:gsz], parts, sizes
 
@@ -365,47 +366,32 @@ def route_bits(ws: int) -> int:
     return b
 
 
-def _alltoallv(out_slices, in_slices, rank):
-    """Variable all-to-all of 1-D slices (in_slices[o] to rank o, out_slices[r]
-    from rank r; the own pair is never touched).  RCCL: one grouped all_to_all
-    of tensor lists; gloo (CPU tests): point-to-point sends and receives."""
-    if dist.get_backend() == "nccl":
-        ins = [t if o != rank else t[:0] for o, t in enumerate(in_slices)]
-        outs = [t if r != rank else t[:0] for r, t in enumerate(out_slices)]
-        dist.all_to_all(outs, ins)
-        return
-    ops = [dist.P2POp(dist.isend, t, o) for o, t in enumerate(in_slices) if o != rank and t.numel()]
-    ops += [dist.P2POp(dist.irecv, t, r) for r, t in enumerate(out_slices) if r != rank and t.numel()]
-    if ops:
-        for w in dist.batch_isend_irecv(ops):
-            w.wait()
-
-
 def _exchange_pieces(parts, sent, rl, rank, device):
-    """All-to-all of the routed cells (parts from route_pieces, grouped by owner)
-    -> per sender (key tensor, count tensor or None, first cell): the peers'
-    cells land in fresh receive tensors, this rank's own group stays where the
-    route wrote it (no self copy)."""
+    """All-to-all of the routed cells (parts from route_pieces with
+    self_rank = rank: the peers' groups in rank order, this rank's own group
+    last) -> per sender (key tensor, count tensor or None, first cell): the
+    peers' cells land in fresh receive tensors by one all_to_all_single with
+    a zero own split, this rank's own group stays where the route wrote it
+    (no self copy)."""
     ws = len(sent)
-    soff = [0] * (ws + 1)
+    others = sum(sent) - sent[rank]
     roff = [0] * (ws + 1)
     for r in range(ws):
-        soff[r + 1] = soff[r] + sent[r]
         roff[r + 1] = roff[r] + (rl[r] if r != rank else 0)
     got = []
     for t, w in parts:
         recv = torch.empty(max(roff[ws], 1) * w, dtype=t.dtype, device=device)
         if ws > 1:
-            _alltoallv([recv[roff[r] * w:roff[r + 1] * w] for r in range(ws)],
-                       [t[soff[o] * w:soff[o + 1] * w] for o in range(ws)], rank)
+            dist.all_to_all_single(recv[:roff[ws] * w], t[:others * w],
+                                   [(rl[r] if r != rank else 0) * w for r in range(ws)],
+                                   [(sent[o] if o != rank else 0) * w for o in range(ws)])
         got.append(recv)
     runs = []
     for r in range(ws):
         if r == rank:
-            kt, ct, start = parts[0][0], parts[1][0] if len(parts) > 1 else None, soff[rank]
+            runs.append((parts[0][0], parts[1][0] if len(parts) > 1 else None, others))
         else:
-            kt, ct, start = got[0], got[1] if len(got) > 1 else None, roff[r]
-        runs.append((kt, ct, start))
+            runs.append((got[0], got[1] if len(got) > 1 else None, roff[r]))
     return runs, got
 
 
@@ -435,7 +421,7 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
     # cells travel as 10-byte records (48-bit key, u32 count) unless some
     # rank holds a cell count >= 2^32: every rank's flag rides on the size
     # exchange, so all ranks agree before the cells' all-to-all
-    grid, parts, sizes = ops.route_pieces(keys, counts, ws, dense_zmax, bits, _lib.HM_CELLS_REC10)
+    grid, parts, sizes = ops.route_pieces(keys, counts, ws, dense_zmax, bits, _lib.HM_CELLS_REC10, self_rank=rank)
     sizes[:, -1] = nx
     recv = torch.empty_like(sizes)
     dist.all_to_all_single(recv, sizes)
@@ -447,7 +433,7 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
     layout = _lib.HM_CELLS_REC10
     if bool(both[1, :, 1].any()):
         layout = _lib.HM_CELLS_U64
-        grid, parts, _ = ops.route_pieces(keys, counts, ws, dense_zmax, bits, layout)
+        grid, parts, _ = ops.route_pieces(keys, counts, ws, dense_zmax, bits, layout, self_rank=rank)
     if dense_zmax >= 0:
         dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
     # the owned cells are at most the received ones plus (rank 0) the dense
@@ -508,7 +494,7 @@ def merge_grouped(keys: torch.Tensor, gcounts: torch.Tensor, ws: int, rank: int,
         ops = DeviceOps(keys.device.index or 0)
     bits = route_bits(ws)
     S = 1 << bits
-    _, parts, sizes = ops.route_pieces(keys, gcounts, ws, -1, bits, _lib.HM_CELLS_G12, extra=0)
+    _, parts, sizes = ops.route_pieces(keys, gcounts, ws, -1, bits, _lib.HM_CELLS_G12, extra=0, self_rank=rank)
     recv = torch.empty_like(sizes)
     dist.all_to_all_single(recv, sizes)
     both = torch.stack([sizes, recv]).cpu()

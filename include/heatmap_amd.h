@@ -329,6 +329,10 @@ int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* 
  *                    2^bits piece sizes -- the row an RCCL all-to-all sends
  *                    to owner o; other columns are left alone.  Asynchronous;
  *                    HM_E_WIDE is never returned (it is in the rows).
+ *                    self_rank >= 0: the groups leave in rank order with
+ *                    owner self_rank's group moved to the end, so the others
+ *                    are one contiguous all-to-all input with a zero own split
+ *                    and the own group stays in place (-1: rank order).
  *   hm_cells_merge_pieces  the owner's merge of nruns senders' cells: run r
  *                    is a contiguous device array of records (REC10) or keys
  *                    key_src[r] with counts count_src[r] (u32 for U32/G12 or
@@ -338,8 +342,8 @@ int hm_dense_cells(hm_ctx* ctx, const uint64_t* grid, int dense_zmax, uint64_t* 
  *                    (the sender's own cells can stay in its send buffer).
  *                    Outputs as hm_cells_merge.  Reference: heatmap.py:111-112. */
 int hm_cells_route_pieces(hm_ctx* ctx, const uint64_t* keys, const uint64_t* counts, int64_t n, int nranks,
-                          int delta, int dense_zmax, int bits, uint64_t* grid, void* keys_out, void* counts_out,
-                          int layout, int64_t* sizes, int stride);
+                          int delta, int dense_zmax, int bits, int self_rank, uint64_t* grid, void* keys_out,
+                          void* counts_out, int layout, int64_t* sizes, int stride);
 int hm_cells_merge_pieces(hm_ctx* ctx, int layout, int nruns, const void* const* key_src,
                           const void* const* count_src, const int64_t* pieces, int bits, uint64_t* keys_out,
                           uint64_t* counts_out, int64_t capacity, int64_t* n_out);

@@ -308,10 +308,11 @@ def _piece_cells(parts, layout, lo, hi):
     return parts[0][0][lo:hi].cpu(), parts[1][0][lo:hi].cpu().to(torch.int64)
 
 
-@pytest.mark.parametrize("ws,dz,layout,n", [(1, 10, 10, 300_000), (5, 8, 10, 300_000), (8, -1, 10, 300_000),
-                                            (8, 10, 8, 300_000), (64, 4, 8, 300_000), (8, -1, 12, 200_000),
-                                            (3, 8, 10, 7), (2, 10, 10, 0)])
-def test_route_pieces_contract(gpu, ws, dz, layout, n):
+@pytest.mark.parametrize("ws,dz,layout,n,me", [(1, 10, 10, 300_000, -1), (5, 8, 10, 300_000, 2),
+                                               (8, -1, 10, 300_000, -1), (8, 10, 8, 300_000, 0),
+                                               (64, 4, 8, 300_000, 63), (8, -1, 12, 200_000, 5),
+                                               (3, 8, 10, 7, 1), (2, 10, 10, 0, -1)])
+def test_route_pieces_contract(gpu, ws, dz, layout, n, me):
     """hm_cells_route_pieces == its CPU stand-in: the same size rows (owner
     totals, wide flag and the 2^bits digit pieces -- the device's fmix64 and
     the stand-in's agree) and, piece by piece, the same cells."""
@@ -326,15 +327,16 @@ def test_route_pieces_contract(gpu, ws, dz, layout, n):
     else:
         keys = counts = torch.zeros(0, dtype=torch.int64)
     ops = multigpu.DeviceOps(0)
-    g, parts, sizes = ops.route_pieces(keys.cuda(), counts.cuda(), ws, dz, bits, layout)
-    rg, rparts, rsizes = TorchOps.route_pieces(keys, counts, ws, dz, bits, layout)
+    g, parts, sizes = ops.route_pieces(keys.cuda(), counts.cuda(), ws, dz, bits, layout, self_rank=me)
+    rg, rparts, rsizes = TorchOps.route_pieces(keys, counts, ws, dz, bits, layout, self_rank=me)
     sizes = sizes.cpu()
     assert torch.equal(sizes, rsizes)
     assert not bool(sizes[:, 1].any())
     if dz >= 0:
         assert torch.equal(g.cpu(), rg)
     S = 1 << bits
-    flat = sizes[:, 2:2 + S].reshape(-1).tolist()
+    order = [o for o in range(ws) if o != me] + ([me] if me >= 0 else [])   # the groups' order in the output
+    flat = sizes[order, 2:2 + S].reshape(-1).tolist()
     at = 0
     for m in flat:                        # the same cells per (owner, digit) piece
         sk, sc = _piece_cells(parts, layout, at, at + m)

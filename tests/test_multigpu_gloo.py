@@ -100,9 +100,10 @@ class TorchOps:
         return _into(out, (zc << 58) | (_compact(m >> 1) << 29) | _compact(m), grid[nz])
 
     @staticmethod
-    def route_pieces(keys, counts, ws, dz, bits, layout, extra=1):
+    def route_pieces(keys, counts, ws, dz, bits, layout, extra=1, self_rank=-1):
         """hm_cells_route_pieces: owner groups ordered by the top `bits` bits
-        of fmix64(merge key); sizes rows (sent, wide, pieces, extra zeros)."""
+        of fmix64(merge key), in rank order or (self_rank >= 0) with that
+        owner's group last; sizes rows (sent, wide, pieces, extra zeros) by owner."""
         from heatmap_amd import _lib
 
         grouped = layout == _lib.HM_CELLS_G12
@@ -119,15 +120,14 @@ class TorchOps:
             sp = (keys >> 58) > dz
             mk, cnt = keys[sp], counts[sp]
             own = multigpu.record_owner(torch.stack([mk >> 58, (mk >> 29) & M29, mk & M29], 1), ws)
-        d = own << bits
-        if bits:
-            d = d | _lsr(_fmix64(mk), 64 - bits)
-        o = torch.argsort(d, stable=True)
+        h = _lsr(_fmix64(mk), 64 - bits) if bits else torch.zeros_like(own)
+        pos = own if self_rank < 0 else torch.where(own == self_rank, ws - 1, own - (own > self_rank).to(own.dtype))
+        o = torch.argsort((pos << bits) | h, stable=True)
         S = 1 << bits
         sizes = torch.zeros((ws, 2 + S + extra), dtype=torch.int64)
         sizes[:, 0] = torch.bincount(own, minlength=ws)
         sizes[:, 1] = int(wide)
-        sizes[:, 2:2 + S] = torch.bincount(d, minlength=ws << bits).reshape(ws, S)
+        sizes[:, 2:2 + S] = torch.bincount((own << bits) | h, minlength=ws << bits).reshape(ws, S)
         if layout == _lib.HM_CELLS_REC10:
             parts = [(multigpu.pack_records(mk[o], cnt[o]), 10)]
         else:
