@@ -38,7 +38,8 @@
 #ifdef HM_STAMPS
 /* phase timing (profiling builds only, tools/stamps.py): thread 0 of the first
  * HM_STAMP_BLOCKS blocks of one kernel records s_memtime at up to 12 points.
- * HM_STAMPS = 1: k_partition, 2: k_project_partition, 3: k_partition_fr, 4: k_l1_fast */
+ * HM_STAMPS = 1: k_partition, 2: k_project_partition, 3: k_partition_fr, 4: k_l1_fast,
+ * 5: k_aggregate */
 #define HM_STAMP_BLOCKS 65536
 __device__ unsigned long long g_stamps[HM_STAMP_BLOCKS * 12];
 #define HM_STAMP_M(m, k)                                                                       \
@@ -46,12 +47,18 @@ __device__ unsigned long long g_stamps[HM_STAMP_BLOCKS * 12];
         if (HM_STAMPS == (m) && threadIdx.x == 0 && hm_block_id() < HM_STAMP_BLOCKS)           \
             g_stamps[hm_block_id() * 12 + (k)] = __builtin_amdgcn_s_memtime();                 \
     } while (0)
+#define HM_STAMP_V(m, k, v)                                                                    \
+    do {                                                                                       \
+        if (HM_STAMPS == (m) && threadIdx.x == 0 && hm_block_id() < HM_STAMP_BLOCKS)           \
+            g_stamps[hm_block_id() * 12 + (k)] = (v);                                          \
+    } while (0)
 extern "C" int hm_debug_stamps(void* host, size_t bytes)
 {
     return (int)hipMemcpyFromSymbol(host, HIP_SYMBOL(g_stamps), bytes, 0, hipMemcpyDeviceToHost);
 }
 #else
 #define HM_STAMP_M(m, k) do { } while (0)
+#define HM_STAMP_V(m, k, v) do { } while (0)
 #endif
 #define HM_STAMP(k) HM_STAMP_M(1, k)
 
@@ -2654,24 +2661,147 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
  * item's u16 keys in an LDS 2^lg x 2^lg histogram.  The rows are padded to
  * 2^lg + 8 words (cell (r, c) at r (2^lg + 8) + c: a cluster's cells in one
  * column fall in different banks, the row stride no longer being a multiple
- * of the 64 banks); the padding is squeezed out before the pyramid.  A
- * single-item bucket emits its pyramid; an item of a multi-item bucket adds
- * its histogram into the bucket's slot and k_aggregate_merged emits it. */
+ * of the 64 banks).  A single-item bucket emits its pyramid, at lg = 7 from
+ * registers straight off the padded rows (hm_reg_pyramid7), below that from
+ * the squeezed histogram; an item of a multi-item bucket adds its squeezed
+ * histogram into the bucket's slot and k_aggregate_merged emits it. */
 #define HM_AG_ROW(lg) ((1u << (lg)) + 8u)
 #define HM_AG_PADDED (128u * (128u + 8u))
 static_assert(HM_AG_LG == 7 && HM_AG_CELLS == 128 * 128, "padded histogram");
+
+/* The lg = 7 bucket pyramid from registers (k_aggregate's single-item
+ * buckets): thread t holds the 4 x 4 block (t >> 5, t & 31) of the padded
+ * 128 x 128 histogram, so zooms z_top-1 and z_top-2 are in-register sums; wave
+ * 0 takes the 32 x 32 level (through s19) on to the bucket total, its lanes'
+ * 4 x 4 blocks giving z_top-3 and z_top-4 and lane shuffles z_top-5, z_top-6
+ * and the total.  Two barriers and one output reservation (hm_bucket_pyramid:
+ * a barrier per level and LDS passes over every level twice); each level's
+ * non-empty cells are ballot-compacted per wave, so the stores stay
+ * coalesced.  Emits zooms z_top .. z_top-6 within [zmin, zmax] and returns the
+ * bucket total (zoom z_top-7) in wave 0.  Every thread calls; the histogram's
+ * rows are ROW words apart; s19 is 1024 words of 16-B-aligned scratch LDS. */
+template <uint32_t ROW>
+__device__ __forceinline__ uint64_t hm_reg_pyramid7(const uint32_t* grid, int z_top, uint64_t prefix, const HmOut& o,
+                                                    uint32_t* s19, uint32_t* scr, unsigned long long* sbase)
+{
+    constexpr int NW = HM_AG_THREADS / 64;
+    static_assert(HM_AG_THREADS == 1024, "one 4 x 4 block per thread");
+    const int tid = threadIdx.x, lane = hm_lane(), w = tid >> 6;
+    const uint32_t br = (uint32_t)tid >> 5, bc = (uint32_t)tid & 31u;
+    auto in = [&](int z) { return z >= o.zmin && z <= o.zmax; };
+    auto nnz = [](bool nz) { return (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(nz)); };
+    uint32_t c[16], d[4];
+#pragma unroll
+    for (int y = 0; y < 4; y++) {
+        const uint4 q = *(const uint4*)&grid[(4u * br + y) * ROW + 4u * bc];
+        c[4 * y] = q.x;
+        c[4 * y + 1] = q.y;
+        c[4 * y + 2] = q.z;
+        c[4 * y + 3] = q.w;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int r = 8 * (j >> 1) + 2 * (j & 1);
+        d[j] = c[r] + c[r + 1] + c[r + 4] + c[r + 5];
+    }
+    const uint32_t e = d[0] + d[1] + d[2] + d[3];
+    s19[tid] = e;
+    const bool i0 = in(z_top), i1 = in(z_top - 1), i2 = in(z_top - 2);
+    uint32_t n = 0;
+    if (i0)
+#pragma unroll
+        for (int j = 0; j < 16; j++) n += nnz(c[j] != 0);
+    if (i1)
+#pragma unroll
+        for (int j = 0; j < 4; j++) n += nnz(d[j] != 0);
+    if (i2) n += nnz(e != 0);
+    if (lane == 0) scr[w] = n;
+    __syncthreads();
+    /* wave 0: lane l the 4 x 4 block (l >> 3, l & 7) of the 32 x 32 level */
+    const uint32_t R = (uint32_t)lane >> 3, C = (uint32_t)lane & 7u;
+    const bool l5 = (lane & 9) == 0, l6 = (lane & 27) == 0;
+    const bool i3 = in(z_top - 3), i4 = in(z_top - 4), i5 = in(z_top - 5), i6 = in(z_top - 6);
+    uint32_t g[4] = {0u, 0u, 0u, 0u}, h = 0, h5 = 0, h6 = 0, tot = 0;
+    if (w == 0) {
+        uint32_t f[16];
+#pragma unroll
+        for (int y = 0; y < 4; y++) {
+            const uint4 q = *(const uint4*)&s19[(4u * R + y) * 32u + 4u * C];
+            f[4 * y] = q.x;
+            f[4 * y + 1] = q.y;
+            f[4 * y + 2] = q.z;
+            f[4 * y + 3] = q.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int r = 8 * (j >> 1) + 2 * (j & 1);
+            g[j] = f[r] + f[r + 1] + f[r + 4] + f[r + 5];
+        }
+        h = g[0] + g[1] + g[2] + g[3];                 /* z_top-4: (R, C) of 8 x 8 */
+        uint32_t s = h + __shfl_xor(h, 1, 64);
+        h5 = s + __shfl_xor(s, 8, 64);                 /* z_top-5: (R/2, C/2), lanes & 9 == 0 */
+        s = h5 + __shfl_xor(h5, 2, 64);
+        h6 = s + __shfl_xor(s, 16, 64);                /* z_top-6: (R/4, C/4), lanes & 27 == 0 */
+        s = h6 + __shfl_xor(h6, 4, 64);
+        tot = s + __shfl_xor(s, 32, 64);
+        uint32_t ns = 0;
+        if (i3)
+#pragma unroll
+            for (int j = 0; j < 4; j++) ns += nnz(g[j] != 0);
+        if (i4) ns += nnz(h != 0);
+        if (i5) ns += nnz(l5 && h5 != 0);
+        if (i6) ns += nnz(l6 && h6 != 0);
+        /* the waves' counts, then the small levels (slot NW) */
+        const uint32_t x = lane < NW ? scr[lane] : lane == NW ? ns : 0u;
+        const uint32_t incl = hm_wave_incl_scan(x);
+        if (lane <= NW) scr[lane] = incl - x;
+        if (lane == NW) *sbase = incl ? atomicAdd(o.cursor, (unsigned long long)incl) : 0ull;
+    }
+    __syncthreads();
+    uint64_t base = *sbase + scr[w];
+    auto put = [&](bool nz, int z, int lg, uint32_t i, uint32_t v) {
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+        const uint64_t pos = base + hm_mbcnt(m);
+        if (nz && pos < o.capacity) {
+            o.keys[pos] = hm_cell_key(z, prefix, lg, i);
+            o.counts[pos] = v;
+        }
+        base += (uint32_t)__builtin_popcountll(m);
+    };
+    if (i0)
+#pragma unroll
+        for (int j = 0; j < 16; j++)
+            put(c[j] != 0, z_top, 7, (4u * br + (j >> 2)) * 128u + 4u * bc + (j & 3), c[j]);
+    if (i1)
+#pragma unroll
+        for (int j = 0; j < 4; j++) put(d[j] != 0, z_top - 1, 6, (2u * br + (j >> 1)) * 64u + 2u * bc + (j & 1), d[j]);
+    if (i2) put(e != 0, z_top - 2, 5, br * 32u + bc, e);
+    if (w == 0) {
+        base = *sbase + scr[NW];
+        if (i3)
+#pragma unroll
+            for (int j = 0; j < 4; j++) put(g[j] != 0, z_top - 3, 4, (2u * R + (j >> 1)) * 16u + 2u * C + (j & 1), g[j]);
+        if (i4) put(h != 0, z_top - 4, 3, R * 8u + C, h);
+        if (i5) put(l5 && h5 != 0, z_top - 5, 2, (R >> 1) * 4u + (C >> 1), h5);
+        if (i6) put(l6 && h6 != 0, z_top - 6, 1, (R >> 2) * 2u + (C >> 2), h6);
+    }
+    return tot;
+}
 __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
 {
-    __shared__ uint32_t grid[HM_AG_PADDED + 64];   /* + 64 dummy words (hm_lds_count) */
+    __shared__ alignas(16) uint32_t grid[HM_AG_PADDED + 64];   /* + 64 dummy words (hm_lds_count) */
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
-    __shared__ HmRunLds<256> L;
+    __shared__ alignas(16) HmRunLds<256> L;                     /* after the count: hm_reg_pyramid7's s19 */
+    static_assert(sizeof(HmRunLds<256>) >= 1024 * sizeof(uint32_t), "s19 in the run chunk");
     const int tid = threadIdx.x;
     const uint32_t side = 1u << a.lg, ncell = side * side, npad = side * HM_AG_ROW(a.lg);
+    HM_STAMP_M(5, 0);
     for (uint32_t i = tid; i < npad; i += HM_AG_THREADS) grid[i] = 0;
     __syncthreads();
     if (hm_block_id() >= a.items) return;   /* block-uniform */
     const HmItem it = hm_item(a.B, hm_block_id());
+    HM_STAMP_M(5, 1);
     struct {
         uint32_t* grid;
         uint32_t dummy;
@@ -2698,6 +2828,18 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
         }
     } f{grid, HM_AG_PADDED, a.lg};
     hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);
+    HM_STAMP_M(5, 2);
+    HM_STAMP_V(5, 5, (unsigned long long)(it.b - it.a));
+    HM_STAMP_V(5, 6, (unsigned long long)(it.r1 - it.r0));
+    HM_STAMP_V(5, 7, (unsigned long long)it.nitems);
+    if (it.nitems == 1 && a.lg == HM_AG_LG) {   /* block-uniform */
+        const uint64_t t = hm_reg_pyramid7<HM_AG_ROW(7)>(grid, a.Z, a.B.coord[it.bucket], a.out, (uint32_t*)&L, scr,
+                                                         &sbase);
+        if (tid == 0) a.totals[it.bucket] = t;
+        HM_STAMP_M(5, 3);
+        HM_STAMP_M(5, 4);
+        return;
+    }
     /* squeeze the padding out: cell i back at i */
     constexpr int CPT = HM_AG_CELLS / HM_AG_THREADS;
     uint32_t x[CPT];
@@ -2721,6 +2863,8 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
         }
         s = hm_wave_sum(s);
         if (hm_lane() == 0 && s) atomicAdd(&a.totals[it.bucket], (unsigned long long)s);
+        HM_STAMP_M(5, 3);
+        HM_STAMP_M(5, 4);
         return;
     }
     __syncthreads();
@@ -2730,13 +2874,16 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
         if (i < ncell) grid[i] = x[k];
     }
     __syncthreads();
+    HM_STAMP_M(5, 3);
     const uint64_t t = hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[it.bucket], a.out, scr, &sbase);
     if (tid == 0) a.totals[it.bucket] = t;
+    HM_STAMP_M(5, 4);
 }
 /* one block per multi-item bucket: its summed histogram, then its pyramid */
 __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
 {
-    __shared__ uint32_t grid[HM_AG_CELLS];
+    __shared__ alignas(16) uint32_t grid[HM_AG_CELLS];
+    __shared__ alignas(16) uint32_t s19[1024];
     __shared__ uint32_t scr[HM_AG_THREADS / 64 + 1];
     __shared__ unsigned long long sbase;
     const uint32_t ncell = 1u << (2 * a.lg);
@@ -2745,7 +2892,10 @@ __global__ __launch_bounds__(HM_AG_THREADS) void k_aggregate_merged(HmAggArgs a)
     const uint4* g = (const uint4*)(a.gslots + (uint64_t)hm_block_id() * HM_AG_CELLS);
     for (uint32_t v = threadIdx.x; v < ncell / 4; v += HM_AG_THREADS) ((uint4*)grid)[v] = g[v];
     __syncthreads();
-    hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[b], a.out, scr, &sbase);
+    if (a.lg == HM_AG_LG)
+        hm_reg_pyramid7<1u << HM_AG_LG>(grid, a.Z, a.B.coord[b], a.out, s19, scr, &sbase);
+    else
+        hm_bucket_pyramid<HM_AG_THREADS>(grid, a.lg, a.Z, a.B.coord[b], a.out, scr, &sbase);
 }
 
 /* ------------------------------------------------------------------------ */

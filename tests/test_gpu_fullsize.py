@@ -23,6 +23,23 @@ pytestmark = pytest.mark.gpu
 from digest import device_cells_digest, device_digest  # noqa: E402
 
 
+@pytest.fixture(autouse=True)
+def _release_device_memory():
+    """Each full-size case starts on an emptied device: the library's cached
+    contexts (their count buffers sized by the last 1e9-point call) and
+    torch's cached blocks are released after every case.  The concurrent
+    per-bucket stream allocates one context per bucket, and after the grouped
+    cases it ran out of device memory when this file ran first."""
+    yield
+    import gc
+
+    import torch
+
+    device._CTX.clear()
+    gc.collect()
+    torch.cuda.empty_cache()
+
+
 def _golden(name):
     path = os.path.join(GOLDEN, "big_digests.json")
     d = json.load(open(path))

@@ -29,6 +29,7 @@ NAMES = {
     "stamps2": ["start", "item+loads_issue+init", "count_rank(loads)", "barrier", "scan+run_atomics", "scatter",
                 "copy+runs"],
     "stamps4": ["start", "issue+lds_setup", "project(loads)", "redo+count_rank", "reserve+scan", "stage", "copy"],
+    "stamps5": ["start", "zero+item", "count(stream_runs)", "squeeze", "pyramid+emit"],
 }[VAR]
 K = len(NAMES)
 n = int(float(os.environ.get("HM_POINTS", "2.5e8")))
@@ -43,9 +44,11 @@ L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 st = np.zeros(65536 * 12, np.uint64)
 assert L.hm_debug_stamps(st.ctypes.data, st.nbytes) == 0
 st = st.reshape(-1, 12).astype(np.int64)
+extra = st[:, K:K + 3].copy()
 st = st[:, :K]
 ok = (st[:, 0] > 0) & (st[:, K - 1] > 0)
 st = st[ok]
+extra = extra[ok]
 print(VAR, "blocks", len(st))
 # missing intermediate stamps (no chunk) -> carry previous
 for k in range(1, K):
@@ -56,3 +59,14 @@ for k in range(K - 1):
     print("%-22s mean %8.0f  median %8.0f" % (NAMES[k + 1], d[:, k].mean(), np.median(d[:, k])))
 tot = st[:, K - 1] - st[:, 0]
 print("%-16s mean %8.0f  median %8.0f cycles" % ("total", tot.mean(), np.median(tot)))
+if VAR == "stamps5":
+    # k_aggregate: phase cycles by the item's key count (keys, runs, items of its bucket)
+    keys, runs, nit = extra[:, 0], extra[:, 1], extra[:, 2]
+    print("items: keys mean %.0f median %.0f; runs mean %.0f median %.0f; multi-item %.3f"
+          % (keys.mean(), np.median(keys), runs.mean(), np.median(runs), (nit > 1).mean()))
+    edges = [0, 1024, 4096, 16384, 65536, 1 << 30]
+    for lo, hi in zip(edges[:-1], edges[1:]):
+        m = (keys >= lo) & (keys < hi)
+        if m.sum():
+            print("keys [%7d,%10d): %6d items, runs %7.0f, " % (lo, hi, m.sum(), runs[m].mean())
+                  + ", ".join("%s %.0f" % (NAMES[k + 1], d[m, k].mean()) for k in range(K - 1)))

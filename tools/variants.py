@@ -23,6 +23,7 @@ VARIANTS = {
     "stamps1": ["HM_STAMPS=2"],              # k_project_partition
     "stamps2": ["HM_STAMPS=3"],              # k_partition_fr
     "stamps4": ["HM_STAMPS=4"],              # k_l1_fast
+    "stamps5": ["HM_STAMPS=5"],              # k_aggregate
     "l1old": ["HM_L1_FAST=0"],               # level 1 through k_project_partition (round 3)
     "l1m3": ["HM_L1_MERGE_MIN=3"],
     "l1m12": ["HM_L1_MERGE_MIN=12"],
@@ -160,6 +161,10 @@ PATCHES["emitnocur"] = [("hm_kernels.hip", "if (lane == NW - 1) *sbase = incl ? 
 PATCHES["xrnostore"] = [("hm_merge.hip", """            if (OUT == 0) {
                 hm_rec_put(a.rec_out + 5 * q, sk[i], (uint32_t)sc[i]);""", """            if (OUT == 0) {
                 if (q == 0x123456789ull) hm_rec_put(a.rec_out + 5 * q, sk[i], (uint32_t)sc[i]);""")]
+# hm_emit_cells (k_aggregate's pyramid emission) without its cell stores (timing only)
+PATCHES["agnoemit"] = [("hm_kernels.hip", """        if (nz && pos < o.capacity) {
+            o.keys[pos] = k;""", """        if (nz && pos == 0x123456789ull) {
+            o.keys[pos] = k;""")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
