@@ -1476,9 +1476,11 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
             L.pn[2 * i + 1] = lg ? cnt - head - nv * V : 0u;
         }
         __syncthreads();
+        if (sizeof(InT) == 2 && rc == it.r0) HM_STAMP_M(5, 8);
         if (w == 0) hm_wave_prefix(L.bn, m, L.pre);
         if (w == 1 || NW == 1) hm_wave_prefix(L.pn, 2 * m, L.ppre);
         __syncthreads();
+        if (sizeof(InT) == 2 && rc == it.r0) HM_STAMP_M(5, 9);
         const uint32_t nb = m, np = 2 * m;
         const uint32_t total = L.pre[nb];
         const uint32_t pbase = carry + V * total;
@@ -1505,6 +1507,7 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
             }
         }
         if (sizeof(InT) == 4 && rc == it.r0) HM_STAMP(5);
+        if (sizeof(InT) == 2 && rc == it.r0) HM_STAMP_M(5, 10);
         /* pieces: a wave takes 64 at a time, scans their lengths and hands
          * consecutive keys to consecutive lanes (piece found by a 6-step
          * shuffle search), 4 loads per lane in flight */
@@ -1552,6 +1555,7 @@ __device__ __forceinline__ void hm_stream_runs(const HmItem& it, const InT* __re
             }
         }
         if (sizeof(InT) == 4 && rc == it.r0) HM_STAMP(6);
+        if (sizeof(InT) == 2 && rc == it.r0) HM_STAMP_M(5, 11);
         carry = pbase + L.ppre[np];
         __syncthreads();
     }

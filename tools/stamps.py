@@ -44,6 +44,7 @@ L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 st = np.zeros(65536 * 12, np.uint64)
 assert L.hm_debug_stamps(st.ctypes.data, st.nbytes) == 0
 st = st.reshape(-1, 12).astype(np.int64)
+st_all = st.copy()
 extra = st[:, K:K + 3].copy()
 st = st[:, :K]
 ok = (st[:, 0] > 0) & (st[:, K - 1] > 0)
@@ -64,6 +65,17 @@ if VAR == "stamps5":
     keys, runs, nit = extra[:, 0], extra[:, 1], extra[:, 2]
     print("items: keys mean %.0f median %.0f; runs mean %.0f median %.0f; multi-item %.3f"
           % (keys.mean(), np.median(keys), runs.mean(), np.median(runs), (nit > 1).mean()))
+    # inside the count, first run chunk (0 when the item takes the few-runs path):
+    # staged descriptors, prefixes, bodies, pieces
+    sub = st_all[ok][:, 8:12].astype(np.int64)
+    c0 = st[:, 1]
+    many = sub[:, 0] > 0
+    if many.any():
+        s = sub[many]
+        seg = np.diff(np.concatenate([c0[many, None], s], axis=1), axis=1)
+        for k, nm in enumerate(["descriptors+barrier", "prefix+barrier", "bodies", "pieces"]):
+            print("  first chunk %-20s mean %8.0f  median %8.0f  (%d items)" % (nm, seg[:, k].mean(), np.median(seg[:, k]),
+                                                                          many.sum()))
     edges = [0, 1024, 4096, 16384, 65536, 1 << 30]
     for lo, hi in zip(edges[:-1], edges[1:]):
         m = (keys >= lo) & (keys < hi)
