@@ -1052,36 +1052,58 @@ __global__ __launch_bounds__(1024) void k_hot_hash(HmHotArgs a)
     __shared__ uint32_t fill[HM_HOT_BUCKETS];
     __shared__ uint32_t bins[256];
     __shared__ uint32_t nh, cut;
+    static_assert(HM_HOT_CAND <= 4 * 1024, "4 candidates a thread");
     const int tid = threadIdx.x;
     for (int i = tid; i < HM_HOT_SLOTS; i += 1024) tab[i] = HM_HOT_EMPTY;
     for (int i = tid; i < HM_HOT_BUCKETS; i += 1024) fill[i] = 0;
     for (int i = tid; i < 256; i += 1024) bins[i] = 0;
     if (tid == 0) nh = 0;
-    __syncthreads();
+    /* the thread's candidates j = tid + 1024 u, read once for the three passes */
     const uint32_t nc = min(a.cand[2 * HM_HOT_CAND], (uint32_t)HM_HOT_CAND);
-    for (uint32_t j = tid; j < nc; j += 1024) atomicAdd(&bins[hm_hot_bin(a.cand[2 * j + 1])], 1u);
+    uint32_t ct[4], cc[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint32_t j = tid + 1024u * u;
+        const uint2 v = j < nc ? ((const uint2*)a.cand)[j] : make_uint2(0u, 0u);
+        ct[u] = v.x;
+        cc[u] = v.y;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < 4; u++)
+        if (tid + 1024u * u < nc) atomicAdd(&bins[hm_hot_bin(cc[u])], 1u);
     __syncthreads();
     if (tid < 64) {
-        /* cutoff: the highest bin at which the candidates from the top reach HM_MAX_HOT */
-        uint32_t acc = 0, c = 0;
-        if (tid == 0) {
-            for (int b = 255; b >= 0; b--) {
-                acc += bins[b];
-                if (acc >= HM_HOT_LIMIT) {
-                    c = (uint32_t)b;
-                    break;
-                }
-            }
-            cut = c;
+        /* cutoff: the highest bin b whose candidates from the top (bins >= b)
+         * reach HM_HOT_LIMIT, 0 if none -- lane l holds bins 4l .. 4l+3, the
+         * bins above them a reversed-lane scan */
+        const int l = tid;
+        uint32_t s = 0;
+        uint32_t bv[4];
+#pragma unroll
+        for (int k = 0; k < 4; k++) s += (bv[k] = bins[4 * l + k]);
+        const uint32_t rs = __shfl(s, 63 - l, 64);              /* lane l: the sum of lane 63 - l */
+        const uint32_t incl = hm_wave_incl_scan(rs);              /* lanes 63-l .. 63 from the top */
+        const uint32_t above = __shfl(incl, 62 - l < 0 ? 0 : 62 - l, 64);   /* bins of lanes > l */
+        uint32_t acc = l == 63 ? 0u : above;
+        int best = -1;
+#pragma unroll
+        for (int k = 3; k >= 0; k--) {
+            acc += bv[k];
+            if (best < 0 && acc >= HM_HOT_LIMIT) best = 4 * l + k;
         }
+        for (int o = 32; o > 0; o >>= 1) best = max(best, __shfl_xor(best, o, 64));
+        if (l == 0) cut = best < 0 ? 0u : (uint32_t)best;
     }
     __syncthreads();
     /* pass 0: above the cutoff bin; 1: at it; 2: below it (only while hot
      * digits are left: candidates whose bucket was full leave room) */
     for (int pass = 0; pass < 3; pass++) {
         if (pass == 2 && nh >= HM_HOT_LIMIT) break;   /* (block-uniform: read after the barrier) */
-        for (uint32_t j = tid; j < nc; j += 1024) {
-            const uint32_t t = a.cand[2 * j], c = a.cand[2 * j + 1];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (tid + 1024u * u >= nc) continue;
+            const uint32_t t = ct[u], c = cc[u];
             const uint32_t bn = hm_hot_bin(c);
             if (pass == 0 ? bn <= cut : pass == 1 ? bn != cut : bn >= cut) continue;
             const uint32_t tr = t >> a.zb, tc = t & ((1u << a.zb) - 1u);
