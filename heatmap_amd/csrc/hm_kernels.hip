@@ -2402,11 +2402,14 @@ __global__ __launch_bounds__(1024) void k_scan_one(const uint64_t* v, uint32_t n
 /* block b: its chunk in sub-chunks of HM_SCAN_ITEMS, carrying the prefix.
  * The sub-chunk passes through LDS both ways (padded one word per 16), so
  * global loads and stores are lane-consecutive while each thread scans 16
- * consecutive values */
+ * consecutive values.  SUM (grids of <= HM_SCAN_THREADS blocks): the block
+ * sums the partials before it itself, and the last block writes the total --
+ * no k_scan_one dispatch between the two passes */
 #define HM_SCAN_PAD(i) ((i) + ((i) >> 4))
+template <bool SUM>
 __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v, uint64_t n, uint64_t chunk,
                                                                const uint64_t* partial, uint64_t* out,
-                                                               const uint64_t* ndev)
+                                                               const uint64_t* ndev, uint64_t* total)
 {
     __shared__ uint64_t ws[HM_SCAN_THREADS / 64 + 1];
     __shared__ uint64_t buf[HM_SCAN_PAD(HM_SCAN_ITEMS)];
@@ -2415,7 +2418,20 @@ __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v
     const uint32_t tid = threadIdx.x;
     const uint64_t c0 = (uint64_t)blockIdx.x * chunk;
     const uint64_t c1 = min(c0 + chunk, n);
-    uint64_t carry = partial[blockIdx.x];
+    uint64_t carry;
+    if (SUM) {
+        uint64_t p = tid < blockIdx.x ? partial[tid] : 0ull;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) p += __shfl_xor(p, o, 64);
+        if (hm_lane() == 0) ws[tid >> 6] = p;
+        __syncthreads();
+        carry = 0;
+#pragma unroll
+        for (int k = 0; k < HM_SCAN_THREADS / 64; k++) carry += ws[k];
+        __syncthreads();
+    } else {
+        carry = partial[blockIdx.x];
+    }
     for (uint64_t s0 = c0; s0 < c1; s0 += HM_SCAN_ITEMS) {
         const uint64_t m = min<uint64_t>(c1 - s0, HM_SCAN_ITEMS);
 #pragma unroll
@@ -2460,6 +2476,7 @@ __global__ __launch_bounds__(HM_SCAN_THREADS) void k_scan_down(const uint64_t* v
         }
         __syncthreads();
     }
+    if (SUM && blockIdx.x == gridDim.x - 1 && tid == 0) *total = carry;
 }
 
 /* compaction of non-empty children into the bucket list B_l (parent-major) */
@@ -4111,8 +4128,14 @@ void hm_launch_scan(hipStream_t s, const uint64_t* v, uint64_t n, uint64_t* part
     const uint32_t nb = (uint32_t)((n + chunk - 1) / chunk);
     const uint32_t g = nb ? nb : 1;
     hipLaunchKernelGGL(k_scan_reduce, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, ndev);
+    if (g <= HM_SCAN_THREADS) {
+        hipLaunchKernelGGL(k_scan_down<true>, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out, ndev,
+                           total);
+        return;
+    }
     hipLaunchKernelGGL(k_scan_one<4>, dim3(1), dim3(1024), 0, s, partial, g, partial, total, nullptr);
-    hipLaunchKernelGGL(k_scan_down, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out, ndev);
+    hipLaunchKernelGGL(k_scan_down<false>, dim3(g), dim3(HM_SCAN_THREADS), 0, s, v, n, chunk, partial, out, ndev,
+                       total);
 }
 
 void hm_launch_compact(hipStream_t s, const HmCompactArgs& a)
