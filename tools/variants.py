@@ -165,6 +165,23 @@ PATCHES["xrnostore"] = [("hm_merge.hip", """            if (OUT == 0) {
 PATCHES["agnoemit"] = [("hm_kernels.hip", """        if (nz && pos < o.capacity) {
             o.keys[pos] = k;""", """        if (nz && pos == 0x123456789ull) {
             o.keys[pos] = k;""")]
+# K1 phase-lockstep probe: the first round's second block of a CU starts ~16 us
+# late, so the two resident blocks alternate load and compute phases from then on
+PATCHES["l1stag256"] = [("hm_kernels.hip", """    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);""", """    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);
+    if (blockIdx.x >= 256 && blockIdx.x < 512)
+        for (int z = 0; z < 5; z++) __builtin_amdgcn_s_sleep(127);""")]
+PATCHES["l1stagodd"] = [("hm_kernels.hip", """    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);""", """    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);
+    if (blockIdx.x < 512 && (blockIdx.x & 1))
+        for (int z = 0; z < 5; z++) __builtin_amdgcn_s_sleep(127);""")]
+PATCHES["l1stagall"] = [("hm_kernels.hip", """    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);""", """    const int64_t base = (a.tile0 + (int64_t)blockIdx.x) * HM_T1;
+    HM_STAMP_M(4, 0);
+    if (blockIdx.x < 512)
+        for (int z = 0; z < (int)(blockIdx.x & 7); z++) __builtin_amdgcn_s_sleep(127);""")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
