@@ -52,7 +52,11 @@ def test_tile_big_column_ids(gpu):
 @pytest.mark.parametrize("kind,n,zmin,zmax", [("uniform", 20000, 0, 14), ("hotspots", 200000, 0, 18),
                                                ("hotspots", 50000, 3, 21), ("skew", 100000, 0, 18),
                                                ("uniform", 1000, 0, 5), ("hotspots", 3000, 0, 0),
-                                               ("uniform", 100000, 10, 14)])
+                                               ("uniform", 100000, 10, 14),
+                                               # zmin inside the final 7-zoom pyramid of k_aggregate's
+                                               # dense buckets (single- and multi-item): the register
+                                               # pyramid's per-level zoom filter
+                                               ("hotspots", 2_000_000, 14, 18), ("hotspots", 1_000_000, 17, 21)])
 def test_count_vs_oracle(gpu, kind, n, zmin, zmax):
     lat, lon = synth.generate(kind, n, seed=3)
     keep = (np.arange(n) % 7 != 3).astype(np.uint8)
