@@ -2858,16 +2858,37 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
                 hm_lds_count(grid, dummy, sl(k), v);
         }
         __device__ __forceinline__ void key(uint32_t k, bool v, uint32_t) { cnt(k, v); }
+        __device__ __forceinline__ void add(uint32_t k, bool v) { atomicAdd(&grid[v ? sl(k) : dummy + (uint32_t)hm_lane()], 1u); }
+        /* 8 keys: the wave tests its first key only -- more than HM_MERGE_MIN
+         * lanes on lane 0's key (a skewed cloud's hot cell) sends all 8 through
+         * the merging count, otherwise they are 8 plain atomics (1e9 hotspots:
+         * aggregation 762-770 -> 710-723 us at zooms 0-18, 3.58 -> 3.48 ms at
+         * 6-21; skew unchanged; plain atomics on every vector took the skewed
+         * cloud's aggregation 6.1 -> 8.6 ms) */
         __device__ __forceinline__ void vec(const uint4& x, bool v, uint32_t)
         {
-            cnt(x.x & 0xFFFFu, v);
-            cnt(x.x >> 16, v);
-            cnt(x.y & 0xFFFFu, v);
-            cnt(x.y >> 16, v);
-            cnt(x.z & 0xFFFFu, v);
-            cnt(x.z >> 16, v);
-            cnt(x.w & 0xFFFFu, v);
-            cnt(x.w >> 16, v);
+            const uint32_t k0 = x.x & 0xFFFFu;
+            const uint64_t m = __builtin_amdgcn_ballot_w64(v && k0 == __builtin_amdgcn_readfirstlane(k0));
+            if (!HM_AG_FAST || (uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32)) >
+                                   HM_MERGE_MIN) {
+                cnt(x.x & 0xFFFFu, v);
+                cnt(x.x >> 16, v);
+                cnt(x.y & 0xFFFFu, v);
+                cnt(x.y >> 16, v);
+                cnt(x.z & 0xFFFFu, v);
+                cnt(x.z >> 16, v);
+                cnt(x.w & 0xFFFFu, v);
+                cnt(x.w >> 16, v);
+            } else {
+                add(x.x & 0xFFFFu, v);
+                add(x.x >> 16, v);
+                add(x.y & 0xFFFFu, v);
+                add(x.y >> 16, v);
+                add(x.z & 0xFFFFu, v);
+                add(x.z >> 16, v);
+                add(x.w & 0xFFFFu, v);
+                add(x.w >> 16, v);
+            }
         }
     } f{grid, HM_AG_PADDED, a.lg};
     hm_stream_runs<uint16_t, HM_AG_THREADS, 256, false>(it, a.keys, a.in, L, scr, f);

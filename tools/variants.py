@@ -182,6 +182,11 @@ PATCHES["l1stagall"] = [("hm_kernels.hip", """    const int64_t base = (a.tile0 
     HM_STAMP_M(4, 0);
     if (blockIdx.x < 512)
         for (int z = 0; z < (int)(blockIdx.x & 7); z++) __builtin_amdgcn_s_sleep(127);""")]
+# k_aggregate's count without any wave merging: one plain LDS atomic per key
+PATCHES["agplain"] = [("hm_kernels.hip", """            if (HM_AG_FAST)
+                hm_lds_count_fast(grid, dummy + (uint32_t)hm_lane(), sl(k), v);
+            else
+                hm_lds_count(grid, dummy, sl(k), v);""", """            atomicAdd(&grid[v ? sl(k) : dummy + (uint32_t)hm_lane()], 1u);""")]
 # compile-time macros added to a patched build
 PATCH_DEFINES = {}
 
