@@ -19,6 +19,7 @@
 #include <chrono>
 #include <string>
 #include <thread>
+#include <unordered_map>
 #include <unordered_set>
 #include <vector>
 
@@ -2245,7 +2246,128 @@ struct hm_stream {
     hm_ctx* pctx[HMS_PAR] = {};
     Buf pk[HMS_PAR], pc[HMS_PAR];
     hipEvent_t pev = nullptr;
+    /* the log arrays as growable reservations (log_alloc): base -> its
+     * reservation, so a full log maps more pages behind its cells instead of
+     * being copied into a buffer twice the size */
+    struct VArr {
+        size_t reserved = 0, mapped = 0;
+        std::vector<std::pair<hipMemGenericAllocationHandle_t, size_t>> chunks;
+    };
+    std::unordered_map<void*, VArr> varr;
+    bool vmm = true;                      /* HM_STREAM_VMM=0: plain allocations, grown by copying */
 };
+
+/* ---- the log's growable arrays ---- */
+static hipMemAllocationProp log_prop(int device)
+{
+    hipMemAllocationProp prop = {};
+    prop.type = hipMemAllocationTypePinned;
+    prop.location.type = hipMemLocationTypeDevice;
+    prop.location.id = device;
+    return prop;
+}
+
+/* map [mapped, bytes) of reservation v at base p (bytes: a granularity multiple) */
+static bool log_map(hm_stream* s, void* p, hm_stream::VArr& v, size_t bytes)
+{
+    if (bytes <= v.mapped) return true;
+    if (bytes > v.reserved) return false;
+    const hipMemAllocationProp prop = log_prop(s->ctx->device);
+    const size_t add = bytes - v.mapped;
+    hipMemGenericAllocationHandle_t h;
+    if (hipMemCreate(&h, add, &prop, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    char* at = (char*)p + v.mapped;
+    hipMemAccessDesc d = {};
+    d.location = prop.location;
+    d.flags = hipMemAccessFlagsProtReadWrite;
+    if (hipMemMap(at, add, 0, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipMemRelease(h);
+        return false;
+    }
+    if (hipMemSetAccess(at, add, &d, 1) != hipSuccess) {
+        (void)hipGetLastError();
+        (void)hipMemUnmap(at, add);
+        (void)hipMemRelease(h);
+        return false;
+    }
+    v.chunks.push_back({h, add});
+    v.mapped = bytes;
+    return true;
+}
+
+static size_t log_round(hm_stream* s, size_t bytes)
+{
+    const hipMemAllocationProp prop = log_prop(s->ctx->device);
+    size_t g = 0;
+    if (hipMemGetAllocationGranularity(&g, &prop, hipMemAllocationGranularityRecommended) != hipSuccess || !g) {
+        (void)hipGetLastError();
+        g = 2u << 20;
+    }
+    return (bytes + g - 1) / g * g;
+}
+
+static void log_free(hm_stream* s, void* p)
+{
+    if (!p) return;
+    auto it = s->varr.find(p);
+    if (it == s->varr.end()) {
+        (void)hipFree(p);
+        return;
+    }
+    size_t off = 0;
+    for (auto& c : it->second.chunks) {
+        (void)hipMemUnmap((char*)p + off, c.second);
+        (void)hipMemRelease(c.first);
+        off += c.second;
+    }
+    (void)hipMemAddressFree(p, it->second.reserved);
+    s->varr.erase(it);
+}
+
+/* n cells: a reservation of 64x that (at most the device's memory) with the
+ * first n mapped, or a plain allocation when reservations are off or fail */
+static int log_alloc(hm_stream* s, uint64_t n, uint64_t** out)
+{
+    *out = nullptr;
+    if (s->vmm) {
+        size_t total = 0, freeb = 0;
+        if (hipMemGetInfo(&freeb, &total) != hipSuccess) {
+            (void)hipGetLastError();
+            total = 0;
+        }
+        const size_t want = log_round(s, (size_t)n * 8);
+        size_t res = log_round(s, std::max<size_t>(want, std::min<size_t>((size_t)n * 8 * 64, total ? total : want)));
+        void* p = nullptr;
+        if (hipMemAddressReserve(&p, res, 0, nullptr, 0) == hipSuccess) {
+            hm_stream::VArr v;
+            v.reserved = res;
+            if (log_map(s, p, v, want)) {
+                s->varr[p] = std::move(v);
+                *out = (uint64_t*)p;
+                return HM_OK;
+            }
+            (void)hipMemAddressFree(p, res);
+        }
+        (void)hipGetLastError();
+    }
+    if (hipMalloc((void**)out, n * 8) != hipSuccess) {
+        (void)hipGetLastError();
+        *out = nullptr;
+        return HM_E_NOMEM;
+    }
+    return HM_OK;
+}
+
+/* grow the array at p to n cells in place; false: not a reservation, or it is too small */
+static bool log_grow(hm_stream* s, uint64_t* p, uint64_t n)
+{
+    auto it = s->varr.find((void*)p);
+    return it != s->varr.end() && log_map(s, p, it->second, log_round(s, (size_t)n * 8));
+}
 
 static int stream_sync_state(hm_stream* s)
 {
@@ -2271,13 +2393,12 @@ static int stream_buf(hm_stream* s, Buf& b, size_t bytes)
     return HM_OK;
 }
 
-static int stream_alloc2(uint64_t n, uint64_t** k, uint64_t** c)
+static int stream_alloc2(hm_stream* s, uint64_t n, uint64_t** k, uint64_t** c)
 {
     *k = nullptr;
     *c = nullptr;
-    if (hipMalloc((void**)k, n * 8) != hipSuccess || hipMalloc((void**)c, n * 8) != hipSuccess) {
-        (void)hipGetLastError();
-        if (*k) (void)hipFree(*k);
+    if (log_alloc(s, n, k) != HM_OK || log_alloc(s, n, c) != HM_OK) {
+        log_free(s, *k);
         *k = nullptr;
         *c = nullptr;
         return HM_E_NOMEM;
@@ -2294,7 +2415,7 @@ static int stream_compact(hm_stream* s)
         return HM_OK;
     }
     int st;
-    if (!s->akeys && (st = stream_alloc2(s->lcap, &s->akeys, &s->acounts))) return st;
+    if (!s->akeys && (st = stream_alloc2(s, s->lcap, &s->akeys, &s->acounts))) return st;
     int64_t m = 0;
     if ((st = cells_merge(s->ctx, s->lkeys, s->lcounts, HM_CELLS_U64, (int64_t)s->llen, nullptr, 0, s->akeys, s->acounts,
                           (int64_t)s->lcap, &m)))
@@ -2315,16 +2436,27 @@ static int stream_room(hm_stream* s, uint64_t need)
     if (s->lcap - s->llen >= need) return HM_OK;
     uint64_t cap = s->lcap ? s->lcap : 1024;
     while (cap - s->llen < need) cap <<= 1;
+    /* reservations: more pages behind the cells, no copy and no sync (the
+     * compaction target, when there is one, grows with them or is dropped) */
+    if (log_grow(s, s->lkeys, cap) && log_grow(s, s->lcounts, cap)) {
+        if (s->akeys && !(log_grow(s, s->akeys, cap) && log_grow(s, s->acounts, cap))) {
+            HIPCHK(hm_sync(s->ctx->stream));
+            log_free(s, s->akeys);
+            log_free(s, s->acounts);
+            s->akeys = s->acounts = nullptr;
+        }
+        s->lcap = cap;
+        return HM_OK;
+    }
     uint64_t *k, *c;
-    if ((st = stream_alloc2(cap, &k, &c))) return st;
+    if ((st = stream_alloc2(s, cap, &k, &c))) return st;
     hipStream_t q = s->ctx->stream;
     if (s->llen) {
         HIPCHK(hipMemcpyAsync(k, s->lkeys, s->llen * 8, hipMemcpyDeviceToDevice, q));
         HIPCHK(hipMemcpyAsync(c, s->lcounts, s->llen * 8, hipMemcpyDeviceToDevice, q));
     }
     HIPCHK(hm_sync(q));
-    for (uint64_t* p : {s->lkeys, s->lcounts, s->akeys, s->acounts})
-        if (p) (void)hipFree(p);
+    for (uint64_t* p : {s->lkeys, s->lcounts, s->akeys, s->acounts}) log_free(s, p);
     s->lkeys = k;
     s->lcounts = c;
     s->akeys = s->acounts = nullptr;   /* the compaction target, at the new size when needed */
@@ -2635,12 +2767,13 @@ extern "C" int hm_stream_create(hm_ctx* ctx, int zmin, int zmax, uint32_t base_h
     s->bk.mask = nb - 1;
     s->lcap = std::max<uint64_t>(1024, (uint64_t)initial_cells);
     if (const char* e = getenv("HM_STREAM_PAR")) s->par = atoi(e) != 0;
+    if (const char* e = getenv("HM_STREAM_VMM")) s->vmm = atoi(e) != 0;
     int st = HM_OK;
     if (hipMalloc((void**)&s->state, HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc((void**)&s->hstate, 2 * HMS_ST_COUNT * sizeof(unsigned long long)) != hipSuccess ||
         hipMalloc((void**)&s->bk.keys, nb * 8) != hipSuccess || hipMalloc((void**)&s->bflag, nb * 4) != hipSuccess ||
         hipMalloc((void**)&s->blist, nb * 4) != hipSuccess || hipMalloc((void**)&s->bloc, nb * 4) != hipSuccess ||
-        stream_alloc2(s->lcap, &s->lkeys, &s->lcounts) != HM_OK) {
+        stream_alloc2(s, s->lcap, &s->lkeys, &s->lcounts) != HM_OK) {
         (void)hipGetLastError();
         hm_stream_destroy(s);
         return HM_E_NOMEM;
@@ -2836,10 +2969,11 @@ extern "C" int hm_stream_destroy(hm_stream* s)
     if (!s) return HM_OK;
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
-    for (void* p : {(void*)s->state, (void*)s->bk.keys, (void*)s->bflag, (void*)s->blist, (void*)s->bloc,
-                    (void*)s->lkeys, (void*)s->lcounts, (void*)s->akeys, (void*)s->acounts, s->bids.p, s->rec.p,
-                    s->plat.p, s->plon.p, s->pkeep.p, s->pstart.p, s->pcnt.p, s->rk.p, s->rc.p, s->mk.p, s->mc.p})
+    for (void* p : {(void*)s->state, (void*)s->bk.keys, (void*)s->bflag, (void*)s->blist, (void*)s->bloc, s->bids.p,
+                    s->rec.p, s->plat.p, s->plon.p, s->pkeep.p, s->pstart.p, s->pcnt.p, s->rk.p, s->rc.p, s->mk.p,
+                    s->mc.p})
         if (p) (void)hipFree(p);
+    for (void* p : {(void*)s->lkeys, (void*)s->lcounts, (void*)s->akeys, (void*)s->acounts}) log_free(s, p);
     if (s->hstate) (void)hipHostFree(s->hstate);
     for (int t = 0; t < HMS_PAR; t++) {
         for (void* p : {s->pk[t].p, s->pc[t].p})

@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--zmin", type=int, default=0)
     ap.add_argument("--zmax", type=int, default=18)
     ap.add_argument("--kind", default="hotspots")
+    ap.add_argument("--initial-cells", type=float, default=float(1 << 26),
+                    help="the resident log's first capacity (it doubles when full)")
     a = ap.parse_args()
     n = int(a.batch)
     total = a.warmup + a.batches
@@ -49,7 +51,7 @@ def main():
         device.synth(a.kind, lat[b], lon[b], seed=0, start=b * n)
         h = BASE + b * a.hours + (torch.arange(n, device="cuda", dtype=torch.int64) % a.hours)
         hrs.append(h.to(torch.int32))
-    s = StreamingHeatmap(a.zmin, a.zmax, base_hour=BASE, initial_cells=1 << 26)
+    s = StreamingHeatmap(a.zmin, a.zmax, base_hour=BASE, initial_cells=int(a.initial_cells))
     for b in range(a.warmup):
         s.add(lat[b], lon[b], hour=hrs[b])
     torch.cuda.synchronize()
