@@ -2255,7 +2255,15 @@ struct hm_stream {
     };
     std::unordered_map<void*, VArr> varr;
     bool vmm = true;                      /* HM_STREAM_VMM=0: plain allocations, grown by copying */
+    /* maps the log's next extent ahead of need, on a host thread, while the
+     * batches run (every varr access joins it first) */
+    std::thread premap;
 };
+
+static void premap_join(hm_stream* s)
+{
+    if (s->premap.joinable()) s->premap.join();
+}
 
 /* ---- the log's growable arrays ---- */
 static hipMemAllocationProp log_prop(int device)
@@ -2312,6 +2320,7 @@ static size_t log_round(hm_stream* s, size_t bytes)
 
 static void log_free(hm_stream* s, void* p)
 {
+    premap_join(s);
     if (!p) return;
     auto it = s->varr.find(p);
     if (it == s->varr.end()) {
@@ -2332,6 +2341,7 @@ static void log_free(hm_stream* s, void* p)
  * first n mapped, or a plain allocation when reservations are off or fail */
 static int log_alloc(hm_stream* s, uint64_t n, uint64_t** out)
 {
+    premap_join(s);
     *out = nullptr;
     if (s->vmm) {
         size_t total = 0, freeb = 0;
@@ -2365,6 +2375,7 @@ static int log_alloc(hm_stream* s, uint64_t n, uint64_t** out)
 /* grow the array at p to n cells in place; false: not a reservation, or it is too small */
 static bool log_grow(hm_stream* s, uint64_t* p, uint64_t n)
 {
+    premap_join(s);
     auto it = s->varr.find((void*)p);
     return it != s->varr.end() && log_map(s, p, it->second, log_round(s, (size_t)n * 8));
 }
@@ -2428,9 +2439,32 @@ static int stream_compact(hm_stream* s)
 }
 
 /* room for `need` more cells at the log's tail: compact first, then grow */
+/* the log will be over 3/4 full: map the next doubling's pages now, on a
+ * host thread (hipMemCreate of a few hundred MB costs about a batch) */
+static void premap_ahead(hm_stream* s, uint64_t need)
+{
+    if (!s->vmm || s->premap.joinable() || s->lcap - s->llen - need >= s->lcap / 4) return;
+    auto ik = s->varr.find((void*)s->lkeys), ic = s->varr.find((void*)s->lcounts);
+    if (ik == s->varr.end() || ic == s->varr.end()) return;
+    const size_t bytes = log_round(s, (size_t)s->lcap * 16);
+    if (bytes > ik->second.reserved || bytes > ic->second.reserved) return;
+    if (ik->second.mapped >= bytes && ic->second.mapped >= bytes) return;
+    hm_stream::VArr *vk = &ik->second, *vc = &ic->second;   /* (stable: every insert or erase joins first) */
+    void *pk = s->lkeys, *pc = s->lcounts;
+    const int dev = s->ctx->device;
+    s->premap = std::thread([s, vk, vc, pk, pc, bytes, dev]() {
+        (void)hipSetDevice(dev);
+        if (log_map(s, pk, *vk, bytes)) (void)log_map(s, pc, *vc, bytes);
+    });
+}
+
 static int stream_room(hm_stream* s, uint64_t need)
 {
-    if (s->lcap - s->llen >= need) return HM_OK;
+    if (s->lcap - s->llen >= need) {
+        premap_ahead(s, need);
+        return HM_OK;
+    }
+    premap_join(s);
     int st;
     if ((st = stream_compact(s))) return st;
     if (s->lcap - s->llen >= need) return HM_OK;
@@ -2967,6 +3001,7 @@ extern "C" int hm_stream_extract(hm_stream* s, int64_t hour, uint64_t* keys_out,
 extern "C" int hm_stream_destroy(hm_stream* s)
 {
     if (!s) return HM_OK;
+    premap_join(s);
     if (s->ctx) (void)hipSetDevice(s->ctx->device);
     if (s->ctx && s->ctx->stream) (void)hipStreamSynchronize(s->ctx->stream);
     for (void* p : {(void*)s->state, (void*)s->bk.keys, (void*)s->bflag, (void*)s->blist, (void*)s->bloc, s->bids.p,
