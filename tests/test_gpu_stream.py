@@ -67,6 +67,33 @@ def test_stream_matches_oracle(gpu, kind, zmin, zmax, initial):
     s.close()
 
 
+@pytest.mark.parametrize("vmm", ["1", "0"])
+def test_stream_log_growth(gpu, monkeypatch, vmm):
+    """The cell log grown from 1024 cells over one-hour batches, as virtual
+    address reservations mapped in place (and ahead, on a host thread) or, with
+    HM_STREAM_VMM=0, as plain allocations copied into twice the size: the same
+    cells as the oracle either way, and a late batch of an older hour (the
+    compaction target allocated and grown with the log) after that."""
+    monkeypatch.setenv("HM_STREAM_VMM", vmm)
+    n, nb = 30000, 8
+    s = StreamingHeatmap(0, 18, base_hour=BASE, initial_cells=1024)
+    lats, lons, hours = [], [], []
+    for b in range(nb + 1):
+        lat, lon = synth.generate("hotspots", n, seed=5, start=b * n)
+        hour = np.full(n, BASE + (b if b < nb else 2), np.uint32)   # the last batch: hour 2 again
+        s.add(lat, lon, None, hour)
+        lats.append(lat)
+        lons.append(lon)
+        hours.append(hour)
+        cells, cap = s.cells()
+        assert cells <= cap
+    lat, lon, hour = np.concatenate(lats), np.concatenate(lons), np.concatenate(hours)
+    _same(s.counts(ALLTIME), oracle.count(lat, lon, None, 0, 18))
+    for h in (BASE, BASE + 2, BASE + nb - 1):
+        _same(s.counts(h), oracle.count(lat, lon, (hour == h).astype(np.uint8), 0, 18))
+    s.close()
+
+
 def test_stream_alltime_only_and_errors(gpu):
     lat, lon = synth.generate("hotspots", 30000, seed=2)
     s = StreamingHeatmap(0, 16, base_hour=BASE)
