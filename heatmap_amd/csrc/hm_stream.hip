@@ -198,7 +198,9 @@ __global__ __launch_bounds__(256) void k_stream_batch_list(const uint32_t* __res
 }
 
 /* points per run: the kept points of each of the batch's buckets, and (run
- * nparts) the points not kept; a block histogram, one atomic per run */
+ * nparts) the points not kept; a block histogram over 4096-point chunks (a
+ * thread's 16 bucket ids and keep bytes loaded before their run lookups),
+ * one atomic per run */
 __global__ __launch_bounds__(256) void k_stream_part_count(HmsScatterArgs a)
 {
     __shared__ uint32_t h[HMS_MAX_PARTS + 1 + 64];
@@ -206,13 +208,22 @@ __global__ __launch_bounds__(256) void k_stream_part_count(HmsScatterArgs a)
     const uint32_t np = a.nparts + 1;
     if (tid < (int)np) h[tid] = 0;
     __syncthreads();
-    const uint64_t stride = (uint64_t)gridDim.x * 256;
-    const uint64_t n_up = (a.n + 255) & ~255ull;
-    for (uint64_t i = (uint64_t)blockIdx.x * 256 + tid; i < n_up; i += stride) {
-        const bool in = i < a.n;
-        const bool kept = in && (!a.keep || a.keep[i]);
-        const uint32_t part = in ? (kept ? a.loc[a.bids[i]] : a.nparts) : 0u;
-        hm_lds_count(h, HMS_MAX_PARTS + 1, part, in);
+    const uint64_t chunk = 256 * 16;
+    for (uint64_t c0 = (uint64_t)blockIdx.x * chunk; c0 < a.n; c0 += (uint64_t)gridDim.x * chunk) {
+        uint32_t bid[16];
+        bool kept[16];
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const uint64_t i = c0 + (uint64_t)k * 256 + tid;
+            bid[k] = i < a.n ? a.bids[i] : 0u;
+            kept[k] = i < a.n && (!a.keep || a.keep[i]);
+        }
+#pragma unroll
+        for (int k = 0; k < 16; k++) {
+            const bool in = c0 + (uint64_t)k * 256 + tid < a.n;
+            const uint32_t part = in ? (kept[k] ? a.loc[bid[k]] : a.nparts) : 0u;
+            hm_lds_count(h, HMS_MAX_PARTS + 1, part, in);
+        }
     }
     __syncthreads();
     if (tid < (int)np && h[tid]) atomicAdd(&a.cursor[tid], (unsigned long long)h[tid]);
@@ -492,8 +503,8 @@ void hm_launch_stream_batch_list(hipStream_t s, const uint32_t* list, uint32_t n
 
 void hm_launch_stream_part_count(hipStream_t s, const HmsScatterArgs& a)
 {
-    uint64_t b = (a.n + 32767) / 32768;
-    if (b > 512) b = 512;
+    uint64_t b = (a.n + 4095) / 4096;
+    if (b > 2048) b = 2048;
     if (a.n) hipLaunchKernelGGL(k_stream_part_count, dim3((unsigned)(b ? b : 1)), dim3(256), 0, s, a);
 }
 
