@@ -50,6 +50,7 @@ VARIANTS = {
     "p1ilp2": ["HM_P1_ILP=2"],
     "frg8": ["HM_FR_GROUP=8"],
     "fr512_4k": ["HM_FR_THREADS=512", "HM_TN=4096"],
+    "fr512": ["HM_FR_THREADS=512"],                 # k_partition_fr: 512-thread blocks, 16 keys a thread
     "ta64k": ["HM_TA=65536"],
     "ta128k": ["HM_TA=131072"],
     "lz3": ["HM_LEVEL_ZOOMS=3"],            # levels z5, z8, z11 (zmax 18)
