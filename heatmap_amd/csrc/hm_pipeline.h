@@ -105,14 +105,16 @@ __host__ __device__ inline uint32_t hm_l1i(uint32_t d, uint32_t sh) { return sh 
 #define HM_TA (1u << 18)                    /* keys per aggregation work item */
 #endif
 /* buckets of <= HM_SP_MAX keys get no dense work item: one wavefront sorts
- * each (k_small_sort / k_small_emit) */
+ * each (k_small_sort / k_small_emit); larger ones go to k_aggregate (512
+ * against 2048: 1-hour stream batches 0.57-0.59 -> 0.52-0.53 ms, 1e9 hotspot
+ * aggregation -50 us, uniform 6e8 -0.9 ms, skew unchanged;
+ * profiles/r5_reentry/sp_*_ab.*) */
 #ifndef HM_SP_MAX
-#define HM_SP_MAX 2048
+#define HM_SP_MAX 512
 #endif
 /* small final buckets (k_small_sort / k_small_emit): one wavefront per bucket */
 #ifndef HM_SPW_MAX
-#define HM_SPW_MAX HM_SP_MAX                /* <= 2048 keys: 32 per lane (a 512-2048-key
-                                               block pyramid was 0.17 ms slower per 10M) */
+#define HM_SPW_MAX HM_SP_MAX                /* up to 2048 keys supported: 32 per lane */
 #endif
 /* buckets of <= HM_SPW_SPLIT keys: the narrow (high-occupancy) instantiation */
 #ifndef HM_SPW_SPLIT

@@ -56,6 +56,7 @@ VARIANTS = {
     "lz3": ["HM_LEVEL_ZOOMS=3"],            # levels z5, z8, z11 (zmax 18)
     "split256": ["HM_SPW_SPLIT=256"],       # narrow small-bucket instantiation up to 256 keys
     "sp1024": ["HM_SP_MAX=1024"],           # buckets of 1025-2048 keys to k_aggregate
+    "sp512": ["HM_SP_MAX=512"],             # buckets of 513-2048 keys to k_aggregate
     "agslow": ["HM_AG_FAST=0"],             # k_aggregate with the lane-0 merge on every key
     "agm4": ["HM_MERGE_MIN=4"],
     "agm16": ["HM_MERGE_MIN=16"],
