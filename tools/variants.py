@@ -57,6 +57,7 @@ VARIANTS = {
     "split256": ["HM_SPW_SPLIT=256"],       # narrow small-bucket instantiation up to 256 keys
     "sp1024": ["HM_SP_MAX=1024"],           # buckets of 1025-2048 keys to k_aggregate
     "sp512": ["HM_SP_MAX=512"],             # buckets of 513-2048 keys to k_aggregate
+    "sp256": ["HM_SP_MAX=256", "HM_SPW_SPLIT=256"],   # buckets of 257-2048 keys to k_aggregate
     "agslow": ["HM_AG_FAST=0"],             # k_aggregate with the lane-0 merge on every key
     "agm4": ["HM_MERGE_MIN=4"],
     "agm16": ["HM_MERGE_MIN=16"],
