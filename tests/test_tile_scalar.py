@@ -66,11 +66,14 @@ def test_scalar_row_and_column_forms():
 def test_scalar_call_cost():
     """A per-record tile_id_from_lat_long costs about a microsecond (the
     reference's CPython math: ~2.7 us with its string building)."""
-    n = 100_000
+    n = 20_000
     Tile.tile_id_from_lat_long(1.0, 2.0, 3)
-    t = time.perf_counter()
-    for i in range(n):
-        Tile.tile_id_from_lat_long(47.6 + i * 1e-7, -122.3, 21)
-    us = (time.perf_counter() - t) / n * 1e6
+    best = float("inf")
+    for _ in range(5):          # best of 5: robust to a loaded host (pytest -n)
+        t = time.perf_counter()
+        for i in range(n):
+            Tile.tile_id_from_lat_long(47.6 + i * 1e-7, -122.3, 21)
+        best = min(best, time.perf_counter() - t)
+    us = best / n * 1e6
     print("tile_id_from_lat_long: %.2f us per call" % us)
     assert us < 3.0
