@@ -10,6 +10,7 @@
  * integer-valued double (the caller makes the unbounded int). */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
+#include <math.h>
 #include <stdint.h>
 
 int hm_project_scalar(double lat, double lon, int zoom, int64_t* row_col);
@@ -24,8 +25,24 @@ static int args3(PyObject* const* args, Py_ssize_t n, double* lat, double* lon, 
     if (*lat == -1.0 && PyErr_Occurred()) return -1;
     *lon = PyFloat_AsDouble(args[1]);
     if (*lon == -1.0 && PyErr_Occurred()) return -1;
-    const long z = PyLong_AsLong(args[2]);
-    if (z == -1 && PyErr_Occurred()) return -1;
+    /* zoom: an int (or any index type), or an integral float (the
+     * reference's 2 ** zoom takes floats); out of range, huge or non-integral:
+     * 1000, which hm_project_scalar answers with HM_E_ARG (ValueError in
+     * tile.py) */
+    PyObject* o = args[2];
+    long z = 1000;
+    if (PyFloat_Check(o)) {
+        const double d = PyFloat_AS_DOUBLE(o);
+        if (d == floor(d) && fabs(d) <= 1000.0) z = (long)d;
+    } else {
+        PyObject* i = PyNumber_Index(o);   /* TypeError for non-numbers, as int(zoom) */
+        if (!i) return -1;
+        int overflow = 0;
+        z = PyLong_AsLongAndOverflow(i, &overflow);
+        Py_DECREF(i);
+        if (z == -1 && PyErr_Occurred()) return -1;
+        if (overflow) z = 1000;
+    }
     *zoom = (z < -1000 || z > 1000) ? 1000 : (int)z;   /* out of range: HM_E_ARG below */
     return 0;
 }

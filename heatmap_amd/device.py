@@ -370,7 +370,20 @@ def count_grouped_device(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 
             idx, kind = ctx.last_error()
             _lib.raise_for(rc, idx)
         break
-    return cells[:5 * nout.value].view(-1, 5)
+    return _exact(cells, 5 * nout.value).view(-1, 5)
+
+
+def _exact(buf, m: int):
+    """buf[:m], copied out at its exact size when the first capacity guess
+    (_record_capacity: up to half the free memory) left more than 256 MiB and
+    a quarter of the buffer unused -- a slice would keep the whole allocation
+    alive for the caller's later sorts and the library's own buffers."""
+    waste = (buf.numel() - m) * buf.element_size()
+    if waste > (256 << 20) and 4 * (buf.numel() - m) > buf.numel():
+        out = buf[:m].clone()
+        del buf
+        return out
+    return buf[:m]
 
 
 def _record_capacity(n: int, nz: int, bytes_per: int, device: int) -> int:
@@ -422,7 +435,8 @@ def count_grouped_packed_device(lat, lon, group, keep=None, zmin: int = 0, zmax:
         if rc != _lib.HM_OK:
             idx, kind = ctx.last_error()
             _lib.raise_for(rc, idx)
-        return keys[:nout.value], gc[:nout.value]
+        m = nout.value
+        return _exact(keys, m), _exact(gc, m)
 
 
 def count_grouped(lat, lon, group, keep=None, zmin: int = 0, zmax: int = 18, device: int = 0,

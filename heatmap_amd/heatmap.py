@@ -840,6 +840,7 @@ def heatmap_table(lat, lon, user_id, keep=None, max_zoom_level=None, delta=None,
         tab = _device_table(plan.labels, keys, counts, grouped, zmax, d, ph)
     if tab is not None:
         return tab
+    packed = grouped = None   # free the packed records before the 5-int64 pass sizes itself
     t0 = time.perf_counter()
     if plan.grouped.any():
         grouped = device.count_grouped_device(lat, lon, plan.gid, plan.grouped.astype(np.uint8), d + 1, zmax,

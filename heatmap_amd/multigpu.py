@@ -21,7 +21,9 @@ reference (reduceByKey at heatmap.py:111, groupByKey at :112):
 
 Every output cell, and every heatmap row, ends with exactly one owner rank.
 torch.distributed is the plumbing ("nccl" = RCCL on ROCm; "gloo" in the CPU
-tests, which pass torch stand-ins for the three device operations).
+tests, which pass torch stand-ins for the three device operations, and in the
+2-process GPU test of the glue with the device operations, where gloo -- which
+has no device all-to-all or reduce -- gets host copies: _all_to_all / _reduce).
 """
 from __future__ import annotations
 
@@ -31,6 +33,33 @@ import torch
 import torch.distributed as dist
 
 DELTA = 5
+
+
+def _host_staged(t: torch.Tensor) -> bool:
+    """A device tensor under a backend without device collectives (gloo):
+    the collective runs on a host copy.  RCCL ("nccl") takes the tensor as is."""
+    return t.is_cuda and dist.get_backend() == "gloo"
+
+
+def _all_to_all(out: torch.Tensor, inp: torch.Tensor, out_splits=None, in_splits=None):
+    """dist.all_to_all_single, staged through host memory under gloo."""
+    if not _host_staged(out):
+        dist.all_to_all_single(out, inp, out_splits, in_splits)
+        return
+    o = torch.empty(out.shape, dtype=out.dtype)
+    dist.all_to_all_single(o, inp.cpu(), out_splits, in_splits)
+    out.copy_(o)
+
+
+def _reduce(t: torch.Tensor, dst: int):
+    """dist.reduce (sum into dst), staged through host memory under gloo."""
+    if not _host_staged(t):
+        dist.reduce(t, dst=dst)
+        return
+    c = t.cpu()
+    dist.reduce(c, dst=dst)
+    if dist.get_rank() == dst:
+        t.copy_(c)
 
 
 class DeviceOps:
@@ -257,11 +286,11 @@ def _exchange(rows: torch.Tensor, owner: torch.Tensor, ws: int) -> torch.Tensor:
     rows = rows[order]
     send = torch.bincount(owner, minlength=ws)
     recv = torch.empty_like(send)
-    dist.all_to_all_single(recv, send)
+    _all_to_all(recv, send)
     sl, rl = send.tolist(), recv.tolist()
     w = rows.shape[1]
     out = torch.empty(sum(rl) * w, dtype=rows.dtype, device=rows.device)
-    dist.all_to_all_single(out, rows.reshape(-1).contiguous(), [x * w for x in rl], [x * w for x in sl])
+    _all_to_all(out, rows.reshape(-1).contiguous(), [x * w for x in rl], [x * w for x in sl])
     return out.reshape(-1, w)
 
 
@@ -382,7 +411,7 @@ def _exchange_pieces(parts, sent, rl, rank, device):
     for t, w in parts:
         recv = torch.empty(max(roff[ws], 1) * w, dtype=t.dtype, device=device)
         if ws > 1:
-            dist.all_to_all_single(recv[:roff[ws] * w], t[:others * w],
+            _all_to_all(recv[:roff[ws] * w], t[:others * w],
                                    [(rl[r] if r != rank else 0) * w for r in range(ws)],
                                    [(sent[o] if o != rank else 0) * w for o in range(ws)])
         got.append(recv)
@@ -424,7 +453,7 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
     grid, parts, sizes = ops.route_pieces(keys, counts, ws, dense_zmax, bits, _lib.HM_CELLS_REC10, self_rank=rank)
     sizes[:, -1] = nx
     recv = torch.empty_like(sizes)
-    dist.all_to_all_single(recv, sizes)
+    _all_to_all(recv, sizes)
     both = torch.stack([sizes, recv]).cpu()
     sent = both[0, :, 0].tolist()
     rl = both[1, :, 0].tolist()
@@ -435,7 +464,7 @@ def merge_cells(buffers, m: int, ws: int, rank: int, dense_zmax: int = 10, ops=N
         layout = _lib.HM_CELLS_U64
         grid, parts, _ = ops.route_pieces(keys, counts, ws, dense_zmax, bits, layout, self_rank=rank)
     if dense_zmax >= 0:
-        dist.reduce(grid, dst=0)                    # RCCL reduce of the dense zooms over xGMI
+        _reduce(grid, 0)                            # RCCL reduce of the dense zooms over xGMI
     # the owned cells are at most the received ones plus (rank 0) the dense
     # grid's: grow this rank's buffers first (a local decision -- a rank that
     # raised here instead would leave its peers blocked in the next collective)
@@ -496,7 +525,7 @@ def merge_grouped(keys: torch.Tensor, gcounts: torch.Tensor, ws: int, rank: int,
     S = 1 << bits
     _, parts, sizes = ops.route_pieces(keys, gcounts, ws, -1, bits, _lib.HM_CELLS_G12, extra=0, self_rank=rank)
     recv = torch.empty_like(sizes)
-    dist.all_to_all_single(recv, sizes)
+    _all_to_all(recv, sizes)
     both = torch.stack([sizes, recv]).cpu()
     sent = both[0, :, 0].tolist()
     rl = both[1, :, 0].tolist()
@@ -514,6 +543,6 @@ def merge_grouped(keys: torch.Tensor, gcounts: torch.Tensor, ws: int, rank: int,
         e = torch.empty(0, dtype=torch.int64, device=keys.device)
         return e, e, e
     mk, mc = ops.merge_pieces(runs, both[1, :, 2:2 + S].tolist(), bits, _lib.HM_CELLS_G12)
-    g = mk >> 47
+    g = (mk >> 47) & 0x1FFFF   # the 17-bit group field (bits 47-63; >> on int64 is arithmetic)
     hk = (((mk >> 42) & 31) << 58) | (((mk >> 21) & 0x1FFFFF) << 29) | (mk & 0x1FFFFF)
     return hk, g, mc

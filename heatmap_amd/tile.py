@@ -61,7 +61,7 @@ def _scalar(lat, lon, zoom):
     if st == _lib.HM_BIGCOL:
         return _lib.HM_OK, r, _bigcol(c)
     if st == _lib.HM_E_ARG:
-        raise ValueError("zoom %r outside -30..30" % (zoom,))
+        raise ValueError("zoom %r outside -30..30 or not integral" % (zoom,))
     return st, r, c
 
 
@@ -92,13 +92,13 @@ class Tile:
     def tile_id_from_lat_long(cls, latitude, longitude, zoom):
         """tile.py:9-13: "z_row_col"; row is evaluated (and raises) first."""
         st, tid = (_S or _scalar_mod()).tile_id(latitude, longitude, zoom)
-        if st == _lib.HM_OK:
+        if st == _lib.HM_OK and type(zoom) is int:
             return tid
-        if st == _lib.HM_BIGCOL:
+        if st == _lib.HM_BIGCOL or st == _lib.HM_OK:   # (an integral float zoom keeps str(zoom): "10.0_r_c")
             st, r, c = _scalar(latitude, longitude, zoom)
             return str(zoom) + "_" + str(r) + "_" + str(c)
         if st == _lib.HM_E_ARG:
-            raise ValueError("zoom %r outside -30..30" % (zoom,))
+            raise ValueError("zoom %r outside -30..30 or not integral" % (zoom,))
         _lib.raise_for(st)
 
     @classmethod

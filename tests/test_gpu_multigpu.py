@@ -262,13 +262,15 @@ def test_merge_grouped_over_rccl(gpu, nccl_world, users):
     assert np.array_equal(c.cpu().numpy()[got], (gc & 0xFFFFFFFF).cpu().numpy()[ref])
 
 
-def test_grouped_exchange_8_emulated_ranks(gpu):
+@pytest.mark.parametrize("users", [5000, 100_000])
+def test_grouped_exchange_8_emulated_ranks(gpu, users):
     """The grouped pyramid sharded over 8 emulated ranks on one GPU: each
     shard's hm_count_grouped_packed, routed by hm_cells_route(G12, nranks=8);
     owner o merges group o of every shard (hm_cells_merge_runs).  Every
     (group, cell) has one owner and the union equals one grouped count of all
-    points (heatmap.py:54-55,111-112)."""
-    ws, n, users = 8, 2_000_000, 5000
+    points (heatmap.py:54-55,111-112).  100,000 users: group ids in [2^16,
+    2^17), the merge key's top bit set, still on the packed route."""
+    ws, n = 8, 2_000_000
     lat, lon, grp = _grouped(n, 9, users)
     ops = multigpu.DeviceOps(0)
     per = n // ws
@@ -284,7 +286,7 @@ def test_grouped_exchange_8_emulated_ranks(gpu):
         mk = torch.cat([x[0][x[2][o]:x[2][o + 1]] for x in routed])
         mc = torch.cat([x[1][x[2][o]:x[2][o + 1]] for x in routed])
         uk, uc = ops.merge(mk, mc, [x[3][o] for x in routed])
-        g = uk >> 47
+        g = (uk >> 47) & 0x1FFFF
         hk = (((uk >> 42) & 31) << 58) | (((uk >> 21) & 0x1FFFFF) << 29) | (uk & 0x1FFFFF)
         assert bool((multigpu.grouped_owner(hk, g, ws) == o).all())
         allk.append(hk.cpu().numpy())

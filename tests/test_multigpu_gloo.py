@@ -300,12 +300,14 @@ def _grouped_worker(rank, ws, port, n, zmin, zmax, users, out):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("ws,users", [(2, 7), (2, 200_000), (3, 50)])
+@pytest.mark.parametrize("ws,users", [(2, 7), (2, 100_000), (2, 200_000), (3, 50)])
 def test_merge_grouped_ranks(ws, users):
     """Grouped cells (hm_count_grouped_packed's records) exchanged over ws gloo
     ranks: every (group, cell) has one owner, the owner is the hash of (group,
     heatmap row), and the union equals one per-group count of all points;
-    200,000 users pass the merge key's 2^17 groups, so every rank takes the
+    100,000 users put group ids in [2^16, 2^17) through the packed exchange (the
+    merge key's top bit set: the decode must not sign-extend it); 200,000
+    users pass the merge key's 2^17 groups, so every rank takes the
     int64-record exchange."""
     n, zmin, zmax = 24000, 6, 21
     mgr = mp.Manager()

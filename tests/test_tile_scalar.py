@@ -77,3 +77,20 @@ def test_scalar_call_cost():
     us = best / n * 1e6
     print("tile_id_from_lat_long: %.2f us per call" % us)
     assert us < 3.0
+
+
+def test_scalar_zoom_forms():
+    """zoom as the reference's `2 ** zoom` takes it (tile.py:9-21): an integral
+    float projects like the int and keeps str(zoom) in the id; numpy integers
+    are accepted; a non-integral, huge or out-of-range zoom is a ValueError,
+    a non-number a TypeError (as int(zoom) would raise)."""
+    lat, lon = 47.6062, -122.3321
+    r, c = Tile.row_from_latitude(lat, 12), Tile.column_from_longitude(lon, 12)
+    assert Tile.row_from_latitude(lat, 12.0) == r and Tile.column_from_longitude(lon, 12.0) == c
+    assert Tile.tile_id_from_lat_long(lat, lon, 12.0) == "12.0_%d_%d" % (r, c)
+    assert Tile.tile_id_from_lat_long(lat, lon, np.int64(12)) == "12_%d_%d" % (r, c)
+    for z in (12.5, 10 ** 30, -(10 ** 30), 31, float("inf"), float("nan")):
+        with pytest.raises(ValueError):
+            Tile.row_from_latitude(lat, z)
+    with pytest.raises(TypeError):
+        Tile.row_from_latitude(lat, "12")
