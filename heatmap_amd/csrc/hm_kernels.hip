@@ -933,6 +933,441 @@ k_l1_fast(HmPart1Args a)
     HM_STAMP_M(4, 6);
 }
 
+/* ------------------------------------------------------------------------ */
+/* level 1, persistent, with compute and writer waves (round 6): k_l1_ws     */
+/* ------------------------------------------------------------------------ */
+/* k_l1_fast keeps a tile's point loads, its reservation atomics and its key
+ * stores in the same waves.  On gfx9 vmcnt retires in issue order, so a load
+ * of the next tile issued by such a wave is waited for by each later atomic
+ * or store of that wave: a block's points are in flight only while it waits
+ * to project them, and a CU's point stream stops whenever both of its blocks
+ * count, reserve, stage or copy out.
+ *
+ * k_l1_ws: one persistent 1024-thread block per CU walking tiles b, b + G, ...
+ * of HM_TW = 12288 points, with two wave roles:
+ *   compute waves 0-11 (768 threads x 16 points): project tile t, then issue
+ *       the loads of tile t + G at once -- the only VMEM operations these
+ *       waves issue, so nothing they do later waits behind them -- count +
+ *       rank in LDS, take part in the slot scan, stage;
+ *   writer waves 12-15 (256 threads): every global atomic and store: the
+ *       reservations of tile t (issued as soon as its counts are complete,
+ *       waited for a phase later) and the copy-out of tile t, which runs while
+ *       the compute waves project tile t + G.
+ * A round has five block barriers: count | scan (2) | offsets | stage.  The
+ * polynomial and hot-tile tables stay in LDS for the block's life.  The keys,
+ * regions, reservations and deferred points are k_l1_fast's.  LDS: 98.8 KB
+ * stage + 31.8 KB tables + 21 KB slot words (one block per CU). */
+#ifndef HM_L1_WS
+#define HM_L1_WS 0                  /* 1: whole units of tiles through k_l1_ws (measured slower) */
+#endif
+#ifndef HM_WS_PREFETCH_LATE
+#define HM_WS_PREFETCH_LATE 0       /* 1: the next tile's loads after the count (fewer live VGPRs) */
+#endif
+#ifndef HM_WS_PREFETCH_RING
+#define HM_WS_PREFETCH_RING 0       /* 1: each point pair's next-tile load as soon as the pair is projected */
+#endif
+#ifndef HM_WS_C
+#define HM_WS_C 768                 /* compute threads: 12 waves */
+#endif
+#define HM_WS_W (1024 - HM_WS_C)    /* writer threads: the rest of a 1024-thread block */
+#define HM_WS_THREADS (HM_WS_C + HM_WS_W)
+#define HM_TW (HM_WS_C * HM_P1_PPT) /* points per tile: 12288 at 12 compute waves */
+#define HM_WS_NJ ((HM_TW + HM_WS_W - 1) / HM_WS_W)   /* staged entries per writer thread */
+#define HM_WS_DLT 2048              /* delta words (slot index masked to 11 bits) */
+/* tiles per unit: whole units of k_l1_ws tiles end on a k_l1_fast tile boundary */
+#define HM_WS_UNIT (HM_TW % HM_T1 == 0 ? 1 : (2 * HM_TW) % HM_T1 == 0 ? 2 : 4)
+static_assert(HM_P1_PPT == 16 && (HM_WS_UNIT * HM_TW) % HM_T1 == 0, "k_l1_ws: whole units end on a k_l1_fast tile");
+static_assert(HM_WS_C % 64 == 0 && HM_WS_W >= 64, "whole waves of both roles");
+static_assert(HM_L1_SLOTS == HM_WS_THREADS + HM_MAX_HOT && HM_MAX_HOT <= HM_WS_THREADS,
+              "k_l1_ws scan: thread t owns slot t, and slot t + 1024 when t < HM_MAX_HOT");
+static_assert(HM_L1_SLOTS % HM_WS_W == 0, "writer slots per thread");
+static_assert(HM_L1_CW <= HM_WS_DLT, "slot indices fit the delta table");
+
+template <typename OutT, bool KEEP>
+__global__ __launch_bounds__(HM_WS_THREADS) void k_l1_ws(HmPart1Args a, uint32_t ntiles)
+{
+    /* staged (key, slot) + one pad entry per lane */
+    __shared__ __attribute__((aligned(16))) uint2 ent[HM_TW + 64];
+    constexpr int YROWS = HM_YTAB_ROWS + 1;   /* + the NaN poison row (k_l1_fast) */
+    constexpr int YN = YROWS * HM_YTAB_STRIDE;
+    __shared__ __attribute__((aligned(16))) double tab[YN];
+    __shared__ __attribute__((aligned(16))) uint2 hot2[HM_HOT_SLOTS / 2];
+    __shared__ uint32_t cnt[HM_L1_CW];    /* per slot: count + rank atomics (+ 64 dummies) */
+    __shared__ uint32_t off[HM_L1_CW];    /* per slot: stage offset */
+    __shared__ uint32_t dlt[HM_WS_DLT];   /* per slot: destination - stage offset (writer waves) */
+    __shared__ uint32_t scr[HM_WS_THREADS / 64 + 1];
+    __shared__ uint32_t s_over, s_sync;
+    const int tid = threadIdx.x;
+    const uint32_t wave = __builtin_amdgcn_readfirstlane((uint32_t)tid >> 6);
+    const int F = 1 << a.dbits;
+    const uint32_t H = a.hot_z >= 0 ? *a.hot_n : 0u;
+    const uint32_t G = gridDim.x;
+    const int wd = a.dbits >> 1;
+    auto digit_of = [&](uint32_t sl) -> uint32_t {
+        if (sl < HM_MAX_HOT) return HM_MAX_F1 + sl;
+        const uint32_t u = sl - HM_MAX_HOT, m = (1u << wd) - 1u;
+        return HM_SKEW_CUR ? ((u & ~m) | ((u - ((u >> wd) << 3)) & m)) : u;
+    };
+    auto live = [&](uint32_t sl) {
+        return sl < HM_MAX_HOT ? sl < H : (sl - HM_MAX_HOT) < (uint32_t)F;
+    };
+    /* the slot scan, by all 1024 threads (the same three barriers in both
+     * roles): thread t owns slot t and, t < HM_MAX_HOT, slot t + 1024; the
+     * cold slots get the stage's front, the hot ones follow (k_l1_fast) */
+    auto scan_slots = [&](uint32_t& Cc, uint32_t& total) {
+        constexpr int NW = HM_WS_THREADS / 64;
+        /* thread-derived LDS addresses recomputed here: hoisted out of the
+         * tile loop they would hold registers across it */
+        const uint32_t tt = hm_opaque((uint32_t)tid), ln = tt & 63u;
+        const uint32_t s1 = tt + HM_WS_THREADS;
+        const bool two = tt < HM_MAX_HOT;
+        const uint32_t c0 = live(tt) ? cnt[tt] : 0u;
+        const uint32_t c1 = (two && live(s1)) ? cnt[s1] : 0u;
+        const uint32_t v = two ? (c1 | (c0 << 16)) : c0;
+        const uint32_t inc = hm_wave_incl_scan(v);
+        if (ln == 63) scr[wave] = inc;
+        hm_lds_barrier();
+        if (wave == 0) {
+            const uint32_t s = ln < NW ? scr[ln] : 0u;
+            const uint32_t si = hm_wave_incl_scan(s);
+            if (ln < NW) scr[ln] = si - s;
+            if (ln == NW - 1) scr[NW] = si;
+        }
+        hm_lds_barrier();
+        const uint32_t pre = scr[wave] + inc - v, tot = scr[NW];
+        Cc = tot & 0xFFFFu;
+        total = Cc + (tot >> 16);
+        const uint32_t oc = pre & 0xFFFFu;
+        if (two) {
+            off[tt] = Cc + (pre >> 16);
+            off[s1] = oc;
+        } else {
+            off[tt] = oc;
+        }
+        hm_lds_barrier();
+    };
+    if (wave < HM_WS_C / 64) {
+        /* ---------------- compute waves ---------------- */
+        const uint32_t ct = (uint32_t)tid;
+        double2 la[HM_P1_PPT / 2], lo[HM_P1_PPT / 2];
+        uint32_t kp[HM_P1_PPT / 2];
+        /* point pair kk of tile t (lanes interleaved: coalesced 16-B loads) */
+        auto load_pair = [&](uint32_t t, int kk) {
+            const int64_t b = (int64_t)t * HM_TW;
+            const uint32_t o = hm_opaque(ct);
+            if (KEEP) kp[kk] = ((const uint16_t*)(a.keep + b))[kk * HM_WS_C + o];
+            la[kk] = hm_stream_load2((const double2*)(a.lat + b) + kk * HM_WS_C + o);
+            lo[kk] = hm_stream_load2((const double2*)(a.lon + b) + kk * HM_WS_C + o);
+        };
+        auto load_tile = [&](uint32_t t) {
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT / 2; k++) load_pair(t, k);
+        };
+        if (!KEEP) {
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT / 2; k++) kp[k] = 0x0101;
+        }
+        load_tile(blockIdx.x);
+        hm_lds_barrier();   /* the writer waves filled the tables and zeroed the counts */
+        const int hb = a.restbits >> 1;
+        const uint32_t lowm = (1u << hb) - 1u;
+        const uint32_t keym = (uint32_t)((1ull << (2 * hb)) - 1ull);
+        const uint32_t wm = (1u << wd) - 1u;
+        const int hs = a.hot_z >= 0 ? a.Z - a.hot_z : 0;
+#if defined(HM_STAMPS) && HM_STAMPS == 6
+        /* phase cycles per block, summed over its tiles (tools/stamps.py stamps6) */
+        unsigned long long sacc[6] = {0, 0, 0, 0, 0, 0}, sprev = __builtin_amdgcn_s_memtime();
+        auto stamp = [&](int i) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            sacc[i] += now - sprev;
+            sprev = now;
+        };
+#else
+        auto stamp = [&](int) {};
+#endif
+        for (uint32_t t = blockIdx.x; t < ntiles; t += G) {
+            const int64_t base = (int64_t)t * HM_TW;
+            /* the projection's f64 constants, k_l1_fast's values bit for bit,
+             * built per tile from an opaque 52-bit exponent shift in SGPRs:
+             * every one is a power-of-two multiple of a compile-time double
+             * (2^Z scaling is exact), so no 64-bit literal is materialised
+             * and hoisted into registers that live across the tile loop */
+            uint64_t zb = (uint64_t)a.Z << 52;
+            asm volatile("" : "+s"(zb));
+            constexpr double C180 = 180.0 * HM_INV360;   /* 180 kz = RN(180 RN(1/360)) 2^Z */
+            const double nscale = hm_u2d(hm_d2u(-1.0) + zb), hscale = hm_u2d(hm_d2u(0.5) + zb);
+            const double kz = hm_u2d(hm_d2u(HM_INV360) + zb);
+            const double c180 = hm_u2d(hm_d2u(C180) + zb);
+            const double ghalf = 0.5 - hm_u2d(hm_d2u(HM_Y_EPS) + zb);
+            const double ghalf2 = 0.5 - hm_u2d(hm_d2u(0x1p-49) + zb);
+            const uint32_t lane = hm_opaque((uint32_t)tid) & 63u;
+            const uint32_t dummy = HM_L1_SLOTS + lane;
+            uint32_t slot[HM_P1_PPT], key[HM_P1_PPT];
+            uint32_t redo = 0;
+            /* the next tile (the last round reloads its own tile: straight-line
+             * loads, no conditional register set) */
+            const uint32_t tn = t + G < ntiles ? t + G : t;
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT; k++) {
+                /* k_l1_fast's projection, statement for statement */
+                const double pa = (k & 1) ? la[k >> 1].y : la[k >> 1].x;
+                const double po = (k & 1) ? lo[k >> 1].y : lo[k >> 1].x;
+                const double dd = 90.0 - fabs(pa);
+                const uint32_t dh = (uint32_t)(hm_d2u(dd) >> 32);
+                constexpr uint32_t I0 = (1023u + HM_YTAB_E0) << HM_YTAB_K;
+                const uint32_t ii = min((dh >> (20 - HM_YTAB_K)) - I0, (uint32_t)HM_YTAB_ROWS);
+                const double dlo = hm_u2d((uint64_t)(dh & ~((1u << (20 - HM_YTAB_K)) - 1u)) << 32);
+                const double tt = dd - dlo;
+                const double* cf = tab + ii * HM_YTAB_STRIDE;
+                double p = cf[5];
+                p = fma(p, tt, cf[4]);
+                p = fma(p, tt, cf[3]);
+                p = fma(p, tt, cf[2]);
+                p = fma(p, tt, cf[1]);
+                p = fma(p, tt, cf[0]);
+                const double R = fma(copysign(p, pa), nscale, hscale);
+                const double fr = __builtin_amdgcn_fract(R);
+                const double y = fma(po, kz, c180);
+                const double fc = __builtin_amdgcn_fract(y);
+                const bool ok = (int)(dd >= 90.0 - HM_LAT_SQ) & (int)(fabs(fr - 0.5) < ghalf) &
+                                (int)(fabs(po) < 180.0) & (int)(fabs(fc - 0.5) < ghalf2);
+                const uint32_t r = (uint32_t)(int32_t)R;
+                const uint32_t c = (uint32_t)(int32_t)y;
+                const bool kept = ((kp[k >> 1] >> (8 * (k & 1))) & 0xFFu) != 0;
+                redo |= (uint32_t)!ok << k;
+                const uint32_t rd = r >> hb, cd = c >> hb;
+                const uint32_t rdw = (rd << wd) + HM_MAX_HOT;
+                uint32_t sl = HM_SKEW_CUR ? (((cd + (rd << 3)) & wm) | rdw) : (cd | rdw);
+                if (H) sl = min(hm_hot_find(hot2, r >> hs, c >> hs), sl);
+                key[k] = ((r << hb) | (c & lowm)) & keym;
+                slot[k] = (ok & kept) ? sl : dummy;
+                asm volatile("" : "+v"(slot[k]), "+v"(key[k]));
+                /* ring: the pair's registers are free, its next-tile load goes
+                 * out now (the loads stay ~one tile ahead, issued evenly over
+                 * the projection instead of in one burst after it) */
+                if (HM_WS_PREFETCH_RING && !HM_WS_PREFETCH_LATE && (k & 1)) load_pair(tn, k >> 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            stamp(0);   /* wait for the points + projection */
+            /* deferred points (rare; their returning atomic waits for every
+             * load this wave has in flight, so they go before the prefetch) */
+            if (__builtin_amdgcn_ballot_w64(redo != 0)) {
+                /* scalar lane picks and an opaque thread index: nothing of this
+                 * rare block is hoisted into registers that live across the loop */
+                const uint32_t cto = hm_opaque(ct);
+                uint32_t ws = 0;
+#pragma unroll
+                for (int k = 0; k < HM_P1_PPT; k++) {
+                    const bool rd = (redo >> k) & 1u;
+                    const uint64_t m = __builtin_amdgcn_ballot_w64(rd);
+                    if (m) {
+                        const int l = __builtin_ctzll(m);
+                        uint64_t b = 0;
+                        if (hm_lane() == l) b = atomicAdd(a.redo_count, (unsigned long long)__popcll(m));
+                        b = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(b >> 32), l) << 32) |
+                            __builtin_amdgcn_readlane((uint32_t)b, l);
+                        const uint64_t q = b + hm_mbcnt(m);
+                        if (rd && q < a.redo_cap)
+                            a.redo_idx[q] = (uint32_t)(base + 2 * ((int64_t)(k >> 1) * HM_WS_C + cto) + (k & 1));
+                        ws += (uint32_t)__popcll(m);
+                    }
+                }
+                if (hm_lane() == 0) atomicAdd(a.slow_count, (unsigned long long)ws);
+            }
+            if (!HM_WS_PREFETCH_RING && !HM_WS_PREFETCH_LATE) load_tile(tn);
+            /* count + rank (k_l1_fast) */
+            uint32_t rank[HM_P1_PPT];
+            uint32_t merged = 0;
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT; k++) {
+                const uint32_t k0 = __builtin_amdgcn_readfirstlane(slot[k]);
+                const uint64_t m = __builtin_amdgcn_ballot_w64(slot[k] == k0);
+                const uint32_t pm = (uint32_t)__builtin_popcount((uint32_t)m) + (uint32_t)__builtin_popcount((uint32_t)(m >> 32));
+                uint32_t idx = slot[k], inc = 1u;
+                if (pm >= HM_L1_MERGE_MIN) {
+                    merged |= 1u << k;
+                    const bool in = (m >> lane) & 1ull;
+                    idx = (in && lane != 0) ? dummy : idx;
+                    inc = lane == 0 ? pm : inc;
+                }
+                rank[k] = atomicAdd(&cnt[idx], inc);
+            }
+            if (merged) {
+#pragma unroll
+                for (int k = 0; k < HM_P1_PPT; k++)
+                    if ((merged >> k) & 1u) {
+                        const uint32_t k0 = __builtin_amdgcn_readfirstlane(slot[k]);
+                        const uint64_t m = __builtin_amdgcn_ballot_w64(slot[k] == k0);
+                        const uint32_t r0 = __builtin_amdgcn_readfirstlane(rank[k]);
+                        if ((m >> lane) & 1ull) rank[k] = r0 + hm_mbcnt(m);
+                    }
+            }
+            /* slot (11 bits) and rank (< 2^14) share a register from here */
+            uint32_t sr[HM_P1_PPT];
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT; k++) sr[k] = slot[k] | (rank[k] << 11);
+            if (HM_WS_PREFETCH_LATE) load_tile(tn);
+            stamp(1);   /* redo, prefetch issue, count + rank */
+            hm_lds_barrier();   /* counts complete: the writer waves reserve */
+            stamp(2);
+            uint32_t Cc, total;
+            scan_slots(Cc, total);
+            stamp(3);
+            /* staging, branch-free: a point that stages nothing writes its
+             * lane's pad entry; the entry holds the point's slot (the writer
+             * waves look the destination delta up per key) */
+#pragma unroll
+            for (int k = 0; k < HM_P1_PPT; k++) {
+                const uint32_t s = sr[k] & 2047u;
+                const uint32_t o = off[s];
+                const uint32_t pos = s < HM_L1_SLOTS ? o + (sr[k] >> 11) : HM_TW + (uint32_t)lane;
+                ent[pos] = make_uint2(key[k], s);
+            }
+            stamp(4);
+            hm_lds_barrier();   /* staged: the writer waves copy out */
+            stamp(5);
+        }
+        /* the last prefetch is a reload of a tile already counted: drain it */
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if defined(HM_STAMPS) && HM_STAMPS == 6
+        if (tid == 0 && blockIdx.x < HM_STAMP_BLOCKS) {
+            for (int i = 0; i < 6; i++) g_stamps[blockIdx.x * 12 + i] = sacc[i];
+            g_stamps[blockIdx.x * 12 + 11] = (ntiles - blockIdx.x + G - 1) / G;
+        }
+#endif
+    } else {
+        /* ---------------- writer waves ---------------- */
+        const uint32_t wt = (uint32_t)tid - HM_WS_C;
+        /* the tables (while the compute waves' first points are in flight) */
+        for (int i = (int)wt; i < YN; i += HM_WS_W) tab[i] = i >= HM_YTAB_N ? __builtin_nan("") : c_ytab[i];
+        if (H)
+            for (int j = (int)wt; j < HM_HOT_SLOTS / 4; j += HM_WS_W) ((uint4*)hot2)[j] = ((const uint4*)a.hot_hash)[j];
+        for (int i = (int)wt; i < HM_L1_CW; i += HM_WS_W) cnt[i] = 0;
+        if (wt == 0) {
+            s_over = 0;
+            s_sync = 0;
+        }
+        /* reservation slots q * 256 + wt: their region (shard of this block) */
+        constexpr int WQ = HM_L1_SLOTS / HM_WS_W;
+        uint32_t fi[WQ], rc[WQ], rb[WQ];
+#pragma unroll
+        for (int q = 0; q < WQ; q++) {
+            const uint32_t sl = q * HM_WS_W + wt;
+            const uint32_t d = digit_of(sl);
+            const bool lv = live(sl);
+            const uint32_t sh = (lv && a.smask[d] != 0) ? (blockIdx.x & (HM_L1_SHARDS - 1)) : 0u;
+            fi[q] = hm_l1i(d, sh);
+            rc[q] = lv ? a.rcap[fi[q]] : 0u;
+            rb[q] = lv ? a.rbase[fi[q]] : 0u;
+        }
+        hm_lds_barrier();
+        char* const outb = (char*)a.keys_out;
+        char* const houtb = (char*)a.keys_hot;
+        const int hb = a.restbits >> 1;
+        const int hs = a.hot_z >= 0 ? a.Z - a.hot_z : 0;
+        const uint32_t hm = (1u << hs) - 1u;
+        const bool hot32 = a.hot_bytes == 4;
+        auto put_cold = [&](uint2 e) { *(OutT*)(outb + (uint64_t)e.y * sizeof(OutT)) = (OutT)e.x; };
+        /* a hot key: (row offset, col offset) in the hot tile, from the cold
+         * key -- u16 for a last-level bucket tile, u32 for a mid-level one */
+        auto hot_key = [&](uint32_t x) { return (((x >> hb) & hm) << hs) | (x & hm); };
+        uint32_t pc[WQ], gp[WQ];
+#pragma unroll
+        for (int q = 0; q < WQ; q++) pc[q] = gp[q] = 0;
+        uint32_t pC = 0, ptot = 0, nsync = 0;
+#if defined(HM_STAMPS) && HM_STAMPS == 6
+        unsigned long long sacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, sprev = __builtin_amdgcn_s_memtime();
+        auto stamp = [&](int i) {
+            const unsigned long long now = __builtin_amdgcn_s_memtime();
+            sacc[i] += now - sprev;
+            sprev = now;
+        };
+#else
+        auto stamp = [&](int) {};
+#endif
+        /* the previous tile: destination deltas once its reservations are
+         * back, a writer-only rendezvous, then its keys leave lane-parallel */
+        auto copy_out = [&]() {
+            bool over = false;
+#pragma unroll
+            for (int q = 0; q < WQ; q++) {
+                const uint32_t sl = q * HM_WS_W + wt;
+                if (live(sl)) {
+                    const bool fits = (uint64_t)gp[q] + pc[q] <= (uint64_t)rc[q];
+                    over |= pc[q] && !fits;
+                    dlt[sl] = (fits ? rb[q] + gp[q] : 0xFFF00000u) - off[sl];
+                }
+            }
+            if (over) {
+                atomicOr(a.overflow, 1ull);
+                atomicOr(&s_over, 1u);
+            }
+            stamp(0);   /* deltas (the reservations waited for) */
+            nsync += HM_WS_W / 64;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+            if (hm_lane() == 0) atomicAdd(&s_sync, 1u);
+            while (__atomic_load_n(&s_sync, __ATOMIC_RELAXED) < nsync) __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            const bool ov = __atomic_load_n(&s_over, __ATOMIC_RELAXED) != 0;   /* block-uniform */
+            stamp(1);   /* writer rendezvous */
+            /* the cold keys [0, pC) then the hot ones [pC, ptot), each range
+             * lane-consecutive (a wave stores 64 consecutive staged keys), no
+             * per-key kind test; a region that overflowed: destinations
+             * >= 0xFFF00000, dropped (the host re-runs the level) */
+            constexpr int JB = HM_WS_NJ < 16 ? HM_WS_NJ : 16;
+            auto range = [&](uint32_t lo, uint32_t hi, auto put) {
+#pragma unroll 1
+                for (uint32_t b0 = lo; b0 < hi; b0 += JB * HM_WS_W) {   /* block-uniform */
+                    uint2 e[JB];
+#pragma unroll
+                    for (int j = 0; j < JB; j++) {
+                        const uint32_t i = b0 + j * HM_WS_W + wt;
+                        e[j] = ent[min(i, (uint32_t)HM_TW)];
+                        e[j].y = dlt[e[j].y & (HM_WS_DLT - 1)] + i;   /* past hi: unused */
+                    }
+#pragma unroll
+                    for (int j = 0; j < JB; j++) {
+                        const uint32_t i = b0 + j * HM_WS_W + wt;
+                        if (i < hi && (!ov || e[j].y < 0xFFF00000u)) put(e[j]);
+                    }
+                }
+            };
+            range(0, pC, put_cold);
+            if (hot32)
+                range(pC, ptot, [&](uint2 e) { *(uint32_t*)(houtb + (uint64_t)e.y * 4u) = hot_key(e.x); });
+            else
+                range(pC, ptot, [&](uint2 e) { *(uint16_t*)(houtb + (uint64_t)e.y * 2u) = (uint16_t)hot_key(e.x); });
+            stamp(2);   /* copy-out */
+        };
+        bool have = false;
+        for (uint32_t t = blockIdx.x; t < ntiles; t += G) {
+            if (have) copy_out();
+            hm_lds_barrier();   /* this tile's counts are complete */
+            stamp(3);
+            if (wt == 0) s_over = 0;   /* every writer read it in copy_out */
+#pragma unroll
+            for (int q = 0; q < WQ; q++) {
+                const uint32_t sl = q * HM_WS_W + wt;
+                pc[q] = live(sl) ? cnt[sl] : 0u;
+                gp[q] = 0;
+                if (pc[q]) gp[q] = atomicAdd(&a.fill[fi[q]], pc[q]);   /* waited for in the next copy_out */
+            }
+            stamp(4);   /* reservations issued */
+            scan_slots(pC, ptot);
+            stamp(5);
+            for (int i = (int)wt; i < HM_L1_CW; i += HM_WS_W) cnt[i] = 0;   /* the scan has read them */
+            hm_lds_barrier();   /* staged */
+            stamp(6);
+            have = true;
+        }
+        if (have) copy_out();
+#if defined(HM_STAMPS) && HM_STAMPS == 6
+        if (wt == 0 && blockIdx.x < 4096)
+            for (int i = 0; i < 8; i++) g_stamps[(4096 + blockIdx.x) * 12 + i] = sacc[i];
+#endif
+    }
+}
+
 /* Sampled digit histogram of level 1 (every stride-th point, fast projection
  * only): sizes the per-digit key regions k_project_partition fills. */
 #define HM_SAMPLE_HSLOTS 4096   /* per-block hash of sampled hot-zoom tiles */
@@ -3662,6 +4097,19 @@ void hm_launch_project(hipStream_t s, const double* lat, const double* lon, int6
                        err_word, slow);
 }
 
+static uint32_t hm_cu_count()
+{
+    static int cus = 0;   /* every device of a node is the same part */
+    if (cus <= 0) {
+        int dev = 0, c = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&c, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+            c <= 0)
+            c = 256;
+        cus = c;
+    }
+    return (uint32_t)cus;
+}
+
 void hm_launch_part1(hipStream_t s, const HmPart1Args& a0, uint32_t grid, bool out16, int mode)
 {
     if (grid == 0) return;
@@ -3678,17 +4126,38 @@ void hm_launch_part1(hipStream_t s, const HmPart1Args& a0, uint32_t grid, bool o
         else if (mode == 1) HM_P1_CASE(T, 1, FL, G); \
         else HM_P1_CASE(T, 2, FL, G);              \
     } while (0)
-    if (full) {
+    /* whole pairs of 12288-point tiles through the persistent k_l1_ws (one
+     * block per CU); they end on a k_l1_fast tile boundary, t0 */
+    uint32_t t0 = 0;
+    /* (keep-less calls only: with the keep bytes prefetched too the compute
+     * waves pass 128 VGPRs and spill) */
+    if (HM_L1_WS && HM_L1_FAST && mode == 0 && !a0.keep && full && (int64_t)full == a0.n / HM_T1) {
+        const uint32_t m = HM_WS_UNIT * (uint32_t)(a0.n / (HM_WS_UNIT * (int64_t)HM_TW));
+        if (m) {
+            /* a multiple of HM_L1_SHARDS blocks (or one block per tile): the
+             * shard of a tile, block & 7 = tile & 7, is then fixed by the tile,
+             * as a region overflow's exact re-run needs */
+            const uint32_t cus = std::max<uint32_t>(hm_cu_count() & ~(uint32_t)(HM_L1_SHARDS - 1), HM_L1_SHARDS);
+            const dim3 g(m <= cus ? m : cus);
+            const dim3 bw(HM_WS_THREADS);
+            if (out16) hipLaunchKernelGGL((k_l1_ws<uint16_t, false>), g, bw, 0, s, a, m);
+            else hipLaunchKernelGGL((k_l1_ws<uint32_t, false>), g, bw, 0, s, a, m);
+            t0 = (uint32_t)((uint64_t)m * HM_TW / HM_T1);
+        }
+    }
+    if (full > t0) {
+        a.tile0 = t0;
+        const uint32_t nf = full - t0;
         if (mode == 0 && HM_L1_FAST) {
             if (out16) {
-                if (a.keep) hipLaunchKernelGGL((k_l1_fast<uint16_t, true>), dim3(full), b, 0, s, a);
-                else hipLaunchKernelGGL((k_l1_fast<uint16_t, false>), dim3(full), b, 0, s, a);
+                if (a.keep) hipLaunchKernelGGL((k_l1_fast<uint16_t, true>), dim3(nf), b, 0, s, a);
+                else hipLaunchKernelGGL((k_l1_fast<uint16_t, false>), dim3(nf), b, 0, s, a);
             } else {
-                if (a.keep) hipLaunchKernelGGL((k_l1_fast<uint32_t, true>), dim3(full), b, 0, s, a);
-                else hipLaunchKernelGGL((k_l1_fast<uint32_t, false>), dim3(full), b, 0, s, a);
+                if (a.keep) hipLaunchKernelGGL((k_l1_fast<uint32_t, true>), dim3(nf), b, 0, s, a);
+                else hipLaunchKernelGGL((k_l1_fast<uint32_t, false>), dim3(nf), b, 0, s, a);
             }
-        } else if (out16) HM_P1_MODES(uint16_t, true, full);
-        else HM_P1_MODES(uint32_t, true, full);
+        } else if (out16) HM_P1_MODES(uint16_t, true, nf);
+        else HM_P1_MODES(uint32_t, true, nf);
     }
     if (grid > full) {
         a.tile0 = full;
@@ -3726,7 +4195,7 @@ __global__ __launch_bounds__(256) void k_redo(HmRedoArgs a)
 void hm_launch_redo(hipStream_t s, const HmRedoArgs& a, uint64_t n)
 {
     uint64_t blocks = (n + 255) / 256;
-    if (blocks > 4096) blocks = 4096;
+    if (blocks > 1024) blocks = 1024;   /* grid-stride: most calls have a handful of points */
     if (blocks < 1) blocks = 1;
     hipLaunchKernelGGL(k_redo, dim3((unsigned)blocks), dim3(256), 0, s, a);
 }

@@ -130,15 +130,37 @@ class GroupPlan:
 
 
 def _factorize(user_id):
+    """(codes int32[n], uniques): the user ids dictionary-encoded, -1 for None.
+
+    An Arrow column (pyarrow Array / ChunkedArray of strings, or already
+    dictionary-encoded -- io.load_locations reads Parquet's user_id as a
+    dictionary) is encoded by Arrow's C++ kernels without building one Python
+    string per row; a pandas Categorical hands over its codes; anything else
+    goes through pandas.factorize."""
+    try:
+        import pyarrow as pa
+    except ImportError:  # pragma: no cover - pyarrow is part of the image
+        pa = None
+    if pa is not None and isinstance(user_id, (pa.Array, pa.ChunkedArray)):
+        import pyarrow.compute as pc
+
+        arr = user_id.combine_chunks() if isinstance(user_id, pa.ChunkedArray) else user_id
+        if not pa.types.is_dictionary(arr.type):
+            arr = pc.dictionary_encode(arr)
+        idx = arr.indices
+        codes = idx.fill_null(-1).to_numpy(zero_copy_only=False).astype(np.int32, copy=False)
+        return codes, arr.dictionary.to_pylist()
+    if hasattr(user_id, "codes") and hasattr(user_id, "categories"):   # pandas Categorical
+        return np.asarray(user_id.codes, dtype=np.int32), list(user_id.categories)
     try:
         import pandas as pd
 
         codes, uniques = pd.factorize(np.asarray(user_id, dtype=object), use_na_sentinel=True)
-        return codes.astype(np.int64), list(uniques)
+        return codes.astype(np.int32), list(uniques)
     except ImportError:  # pragma: no cover - pandas is part of the image
         uniq, inv = np.unique(np.array([str(u) if u is not None else "\0none" for u in user_id]), return_inverse=True)
         u = [None if x == "\0none" else x for x in uniq.tolist()]
-        codes = inv.astype(np.int64)
+        codes = inv.astype(np.int32)
         if None in u:
             codes[codes == u.index(None)] = -1
         return codes, u
@@ -149,16 +171,20 @@ def group_plan(user_id, keep=None) -> GroupPlan:
     (heatmap.py:64-70).  Background rows are dropped before their user id is
     read (heatmap.py:28-35), so only kept rows raise: a None id as the
     reference's None[:1] would (TypeError), an id containing the key separator
-    as ValueError (heatmap.py:80-84 would mis-split its keys)."""
+    as ValueError (heatmap.py:80-84 would mis-split its keys).  Linear in the
+    rows (a histogram of the codes, not a sort); the per-id work is over the
+    distinct ids only."""
     n = len(user_id)
-    keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool)
+    keep = np.ones(n, dtype=bool) if keep is None else np.asarray(keep).astype(bool, copy=False)
     codes, uniques = _factorize(user_id)
-    kept_codes = np.unique(codes[keep])
-    if kept_codes.size and kept_codes[0] < 0:
+    # which codes occur among the kept rows (slot 0: None)
+    seen = np.bincount(codes[keep] + 1 if not keep.all() else codes + 1, minlength=len(uniques) + 1)
+    if seen[0]:
         raise TypeError("'NoneType' object is not subscriptable")
+    kept_codes = np.flatnonzero(seen[1:])
     labels = ["all"]
     index = {"all": 0}
-    lut = np.full(len(uniques) + 1, -1, dtype=np.int64)      # code -> group id; -1: no group
+    lut = np.full(len(uniques) + 1, -1, dtype=np.int32)      # code + 1 -> group id; -1: no group
     for c in kept_codes.tolist():
         u = uniques[c]
         if not isinstance(u, str):
@@ -172,10 +198,11 @@ def group_plan(user_id, keep=None) -> GroupPlan:
         if label not in index:
             index[label] = len(labels)
             labels.append(label)
-        lut[c] = index[label]
-    g = lut[codes]
+        lut[c + 1] = index[label]
+    g = lut[codes + 1]
     grouped = keep & (g >= 0)
-    return GroupPlan(labels, np.where(grouped, g, 0).astype(np.uint32), grouped)
+    np.maximum(g, 0, out=g)
+    return GroupPlan(labels, g.view(np.uint32), grouped)
 
 
 # --------------------------------------------------------------------------

@@ -31,13 +31,17 @@ COLUMNS = ("latitude", "longitude", "source", "user_id")
 
 
 def _columns(source):
+    """The four columns; from Arrow / Parquet the string columns stay Arrow
+    arrays (Parquet's user_id read as a dictionary: the group coding then
+    needs no Python string per row, heatmap._factorize)."""
     import pyarrow as pa
     import pyarrow.parquet as pq
 
     if isinstance(source, str):
-        source = pq.read_table(source, columns=[c for c in COLUMNS])
+        source = pq.read_table(source, columns=[c for c in COLUMNS], read_dictionary=["user_id"])
     if isinstance(source, pa.Table):
-        return {c: source.column(c).to_numpy(zero_copy_only=False) for c in COLUMNS}
+        return {c: source.column(c) if c in ("source", "user_id") else source.column(c).to_numpy(zero_copy_only=False)
+                for c in COLUMNS}
     if hasattr(source, "to_dict") and hasattr(source, "columns"):  # pandas DataFrame
         return {c: source[c].to_numpy() for c in COLUMNS}
     if isinstance(source, dict):
@@ -47,12 +51,24 @@ def _columns(source):
 
 
 def load_locations(source):
-    """-> (lat f64[n], lon f64[n], keep u8[n], user_ids object[n])."""
+    """-> (lat f64[n], lon f64[n], keep u8[n], user_ids): user_ids an object
+    array, or the Arrow column itself for Arrow / Parquet sources."""
+    import pyarrow as pa
+
     cols = _columns(source)
     lat = np.ascontiguousarray(np.asarray(cols["latitude"], dtype=np.float64))
     lon = np.ascontiguousarray(np.asarray(cols["longitude"], dtype=np.float64))
-    keep = (np.asarray(cols["source"], dtype=object) != "background").astype(np.uint8)
-    users = np.asarray(cols["user_id"], dtype=object)
+    src = cols["source"]
+    if isinstance(src, (pa.Array, pa.ChunkedArray)):
+        import pyarrow.compute as pc
+
+        # heatmap.py:28: row['source'] == 'background' (a null source is kept)
+        keep = pc.fill_null(pc.not_equal(src, "background"), True).to_numpy(zero_copy_only=False).astype(np.uint8)
+    else:
+        keep = (np.asarray(src, dtype=object) != "background").astype(np.uint8)
+    users = cols["user_id"]
+    if not isinstance(users, (pa.Array, pa.ChunkedArray)):
+        users = np.asarray(users, dtype=object)
     if not (lat.size == lon.size == keep.size == len(users)):
         raise ValueError("location columns differ in length")
     return lat, lon, keep, users

@@ -50,7 +50,8 @@ def test_loaders_agree(tmp_path, form):
     assert lat.dtype == np.float64 and np.array_equal(lat, np.array(cols["latitude"]))
     assert np.array_equal(lon, np.array(cols["longitude"]))
     assert keep.tolist() == [int(s != "background") for s in cols["source"]]
-    assert list(users) == cols["user_id"]
+    # Arrow / Parquet sources keep user_id as an Arrow column (dictionary-encoded from Parquet)
+    assert (users.to_pylist() if hasattr(users, "to_pylist") else list(users)) == cols["user_id"]
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -105,8 +106,11 @@ def test_null_user_on_background_row(tmp_path):
     cols = {"latitude": [47.6, 47.61], "longitude": [-122.3, -122.31], "source": ["gps", "background"],
             "user_id": ["u1", None], "timestamp": [0, 1]}
     lat, lon, keep, users = io.load_locations(pa.table(cols))
-    assert keep.tolist() == [1, 0] and users[1] is None
-    heatmap.group_plan(users, keep)
+    assert keep.tolist() == [1, 0] and users.to_pylist()[1] is None
+    p = heatmap.group_plan(users, keep)
+    assert p.labels == ["all", "u1"] and p.grouped.tolist() == [True, False]
+    with pytest.raises(TypeError):   # the same null on a kept row: None[:1]
+        heatmap.group_plan(users, np.ones(2, bool))
 
 
 def test_chain_window_table_matches_reference_chain():

@@ -108,13 +108,17 @@ def bench_table(a):
     user = names[g]
     user[g % 7 == 3] = "x-anon"          # 'x*' ids: counted in 'all' only (heatmap.py:64-70)
     keep = (np.arange(n) % 5 != 2)       # background rows (heatmap.py:28-29)
+    if a.arrow:   # the user_id column as io.load_locations reads it from Parquet (dictionary-encoded)
+        import pyarrow as pa
+
+        user = pa.array(user, type=pa.string()).dictionary_encode()
     hm.heatmap_table(lat[:10000], lon[:10000], user[:10000], keep[:10000], a.zmax - 5, 5)   # warm-up
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     tab = hm.heatmap_table(lat, lon, user, keep, a.zmax - 5, 5)
     ph = dict(hm.LAST_TABLE_PHASES)
     tot = time.perf_counter() - t0
-    print(json.dumps({"part": "heatmap_table", "value": n / tot, "unit": "points/s", "seconds": tot,
+    print(json.dumps({"part": "heatmap_table", "arrow_user_ids": bool(a.arrow), "value": n / tot, "unit": "points/s", "seconds": tot,
                       "points": n, "users": a.users, "rows": tab.num_rows,
                       "detail_zooms": [6, a.zmax], "phases_s": ph}), flush=True)
 
@@ -132,6 +136,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--cap-factor", type=float, default=2.0, help="first record capacity per point")
     ap.add_argument("--no-table", action="store_true")
+    ap.add_argument("--arrow", action="store_true", help="table: user ids as an Arrow dictionary column")
     ap.add_argument("--records", choices=["packed", "int64x5"], default="packed",
                     help="hm_count_grouped_packed (16 B per record) or hm_count_grouped (40 B)")
     a = ap.parse_args()

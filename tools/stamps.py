@@ -30,9 +30,12 @@ NAMES = {
                 "copy+runs"],
     "stamps4": ["start", "issue+lds_setup", "project(loads)", "redo+count_rank", "reserve+scan", "stage", "copy"],
     "stamps5": ["start", "zero+item", "count(stream_runs)", "squeeze", "pyramid+emit"],
+    "stamps6": [],
+    "stamps6w8": [],
+    "stamps6w10": [],
 }[VAR]
 K = len(NAMES)
-n = int(float(os.environ.get("HM_POINTS", "2.5e8")))
+n = int(float(os.environ.get("HM_POINTS", "2.5e8" if not VAR.startswith("stamps6") else "1e9")))
 lat = torch.empty(n, dtype=torch.float64, device="cuda")
 lon = torch.empty(n, dtype=torch.float64, device="cuda")
 device.synth("hotspots", lat, lon)
@@ -44,6 +47,25 @@ L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 st = np.zeros(65536 * 12, np.uint64)
 assert L.hm_debug_stamps(st.ctypes.data, st.nbytes) == 0
 st = st.reshape(-1, 12).astype(np.int64)
+if VAR.startswith("stamps6"):
+    # k_l1_ws: per block, phase cycles summed over its tiles; slot 11 = its tiles;
+    # the writer waves' phases in the rows 4096 + block
+    w = st[4096:4096 + 4096, :8]
+    st = st[:4096]
+    ok = st[:, 11] > 0
+    nt = st[ok, 11:12]
+    per = st[ok, :6] / nt
+    perw = w[ok] / nt
+    names = ["C wait+project", "C redo+prefetch+count", "C BAR1 wait", "C scan(3 bar)", "C stage", "C BAR3 wait"]
+    namesw = ["W deltas (atomics)", "W rendezvous", "W copy-out", "W BAR1 wait", "W reserve issue", "W scan(3 bar)",
+              "W zero+BAR3"]
+    print("stamps6 blocks", int(ok.sum()), "tiles/block", nt.mean())
+    for k, nm in enumerate(names):
+        print("%-24s per tile mean %8.0f  median %8.0f" % (nm, per[:, k].mean(), np.median(per[:, k])))
+    for k, nm in enumerate(namesw):
+        print("%-24s per tile mean %8.0f  median %8.0f" % (nm, perw[:, k].mean(), np.median(perw[:, k])))
+    print("C total per tile %.0f, W total per tile %.0f" % (per.sum(1).mean(), perw[:, :7].sum(1).mean()))
+    sys.exit(0)
 st_all = st.copy()
 extra = st[:, K:K + 3].copy()
 st = st[:, :K]

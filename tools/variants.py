@@ -19,11 +19,20 @@ VDIR = os.path.join(REPO, "heatmap_amd", "_lib", "variants")
 
 VARIANTS = {
     "base": [],
+    "nows": ["HM_L1_WS=0"],                  # level 1 through k_l1_fast only (the shipped default)
+    "wslate": ["HM_WS_PREFETCH_LATE=1"],     # k_l1_ws: next tile's loads after the count
+    "ws": ["HM_L1_WS=1"],                    # k_l1_ws (12 compute + 4 writer waves)
+    "ws8": ["HM_L1_WS=1", "HM_WS_C=512"],                  # k_l1_ws: 8 compute + 8 writer waves, 8192-point tiles
+    "ws10": ["HM_L1_WS=1", "HM_WS_C=640"],                 # k_l1_ws: 10 compute + 6 writer waves, 10240-point tiles
+    "ws12": ["HM_L1_WS=1", "HM_WS_C=768"],                 # k_l1_ws: 12 compute + 4 writer waves, 12288-point tiles
+    "stamps6w8": ["HM_STAMPS=6", "HM_L1_WS=1", "HM_WS_C=512"],
+    "stamps6w10": ["HM_STAMPS=6", "HM_L1_WS=1", "HM_WS_C=640"],
     "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py (k_partition)
     "stamps1": ["HM_STAMPS=2"],              # k_project_partition
     "stamps2": ["HM_STAMPS=3"],              # k_partition_fr
     "stamps4": ["HM_STAMPS=4"],              # k_l1_fast
     "stamps5": ["HM_STAMPS=5"],              # k_aggregate
+    "stamps6": ["HM_STAMPS=6", "HM_L1_WS=1"],              # k_l1_ws: per-block phase cycles summed over its tiles
     "l1old": ["HM_L1_FAST=0"],               # level 1 through k_project_partition (round 3)
     "l1m3": ["HM_L1_MERGE_MIN=3"],
     "l1m12": ["HM_L1_MERGE_MIN=12"],
@@ -98,6 +107,7 @@ VARIANTS = {
 # Timing-only experiments: text patches applied to a copy of the sources (the
 # shipped kernels carry no experiment toggles).  Results are wrong; every
 # access stays in bounds.
+PATCH_DEFINES = {}
 PATCHES = {
     # k_partition / k_aggregate run bodies: no global key loads
     "noload": [("hm_kernels.hip", "                        x[u] = kv[L.bv[r] + (v - L.pre[r])];",
@@ -191,7 +201,6 @@ PATCHES["agplain"] = [("hm_kernels.hip", """            if (HM_AG_FAST)
             else
                 hm_lds_count(grid, dummy, sl(k), v);""", """            atomicAdd(&grid[v ? sl(k) : dummy + (uint32_t)hm_lane()], 1u);""")]
 # compile-time macros added to a patched build
-PATCH_DEFINES = {}
 
 
 def build(names):
