@@ -537,10 +537,12 @@ def _heat_text_gpu(dz, dr, dc, dv, st):
     hm_format_bins, one thread per bin at an exclusive scan of the bins' text
     lengths.  A pyarrow LargeStringArray."""
     import ctypes
+    import time
 
     import pyarrow as pa
     import torch
 
+    _T_JSON[0] = time.perf_counter()
     n = dz.numel()
     head = torch.zeros(n, dtype=torch.uint8, device=dz.device)
     head[st] = 1
@@ -558,8 +560,13 @@ def _heat_text_gpu(dz, dr, dc, dv, st):
     rc = ctx.L.hm_format_bins(ctx.ptr, p(dz), p(dr), p(dc), p(dv), p(head), p(last), p(off), n, p(text))
     if rc != _lib.HM_OK:
         _lib.raise_for(rc)
-    offsets = np.append(off[st].cpu().numpy(), total).astype(np.int64)
-    data = text[:total].cpu().numpy()
+    import time
+
+    t0 = time.perf_counter()
+    torch.cuda.current_stream(dz.device).synchronize()
+    LAST_TABLE_PHASES["JSON: text written (device, of which)"] = time.perf_counter() - _T_JSON[0]
+    offsets = _offsets_to_host(off[st], total)
+    data = _to_host(text[:total])
     return pa.LargeStringArray.from_buffers(int(st.numel()), pa.py_buffer(offsets), pa.py_buffer(data))
 
 
@@ -709,16 +716,64 @@ def build_heatmaps_columnar(lat, lon, user_id, keep=None, max_zoom_level=None, d
 LAST_TABLE_PHASES = {}
 
 
+_POW10 = {}
+
+
 def _digits(x):
-    """decimal digits of non-negative int64 CUDA tensors"""
+    """decimal digits of non-negative int64 CUDA tensors: 1 + the number of
+    powers 10^1 .. 10^18 at or below x, one searchsorted pass (18 compare-adds
+    over the whole array before)"""
     import torch
 
-    d = torch.ones_like(x)
-    p = 10
-    for _ in range(18):
-        d += (x >= p).to(torch.int64)
-        p *= 10
-    return d
+    p = _POW10.get(x.device)
+    if p is None:
+        p = _POW10[x.device] = torch.tensor([10 ** k for k in range(1, 19)], dtype=torch.int64, device=x.device)
+    return torch.searchsorted(p, x, right=True) + 1
+
+
+def _offsets_to_host(off, total: int):
+    """int64 string offsets (a CUDA tensor of the starts, then total) as one
+    host array: appended on the device and copied once (np.append on the
+    host copied the 300 MB of a 1e7-point table's ids twice more)"""
+    import torch
+
+    o = torch.cat([off.to(torch.int64), off.new_full((1,), int(total), dtype=torch.int64)])
+    return _to_host(o.view(torch.uint8)).view(np.int64)
+
+
+_COPY_POOL = None
+_T_JSON = [0.0]
+THREADED_COPY_MIN = 128 << 20   # bytes; smaller texts take one copy
+
+
+def _to_host(t):
+    """A CUDA uint8 tensor (the table's text columns: GBs) as a host numpy
+    array.  A single pageable copy runs at ~8 GB/s and a fresh pinned buffer
+    costs its page locking (~10 GB/s together); 64 MB chunks copied from 8
+    host threads into one pageable array reach ~55 GB/s
+    (tools/copy_probe.py, profiles/r6/copy_probe.json)."""
+    import os
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    global _COPY_POOL
+    n = t.numel()
+    if n < THREADED_COPY_MIN or os.environ.get("HM_TABLE_THREADED_COPY", "1") == "0":
+        return t.cpu().numpy()
+    dst = np.empty(n, np.uint8)
+    step = max(1 << 20, min(64 << 20, THREADED_COPY_MIN // 2))
+    if _COPY_POOL is None:
+        _COPY_POOL = ThreadPoolExecutor(8, thread_name_prefix="hm-d2h")
+    dev = t.device
+    torch.cuda.current_stream(dev).synchronize()   # the text is written
+
+    def part(a):
+        with torch.cuda.device(dev):
+            torch.from_numpy(dst[a:a + step]).copy_(t[a:a + step])
+
+    list(_COPY_POOL.map(part, range(0, n, step)))
+    return dst
 
 
 def _ids_gpu(labels, spans, rl, rs, rz, rr, rc):
@@ -754,8 +809,8 @@ def _ids_gpu(labels, spans, rl, rs, rz, rr, rc):
                                   p(off), n, p(text))
         if rc_ != _lib.HM_OK:
             _lib.raise_for(rc_)
-    offsets = np.append(off.cpu().numpy(), total).astype(np.int64)
-    data = text[:total].cpu().numpy()
+    offsets = _offsets_to_host(off, total)
+    data = _to_host(text[:total])
     return pa.LargeStringArray.from_buffers(int(n), pa.py_buffer(offsets), pa.py_buffer(data))
 
 
@@ -824,8 +879,11 @@ def _device_table(labels, keys, counts, grouped, zmax, d, phases):
     head = torch.ones_like(rk, dtype=torch.bool)
     head[1:] = rk[1:] != rk[:-1]
     st = torch.nonzero(head).flatten()
+    torch.cuda.synchronize()
+    phases["order (device)"] = time.perf_counter() - t0
+    t0 = time.perf_counter()
     heat = _heat_text_gpu(z, r, c, val, st)
-    phases["order + JSON (device)"] = time.perf_counter() - t0
+    phases["JSON (device text + copy to host)"] = time.perf_counter() - t0
     t0 = time.perf_counter()
     rt = rk[st]
     ids = _ids_gpu(labels, ["alltime"], rt >> (6 + 2 * tb), torch.zeros_like(rt), (rt >> (2 * tb)) & 63,

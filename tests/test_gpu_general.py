@@ -276,13 +276,19 @@ def test_cells_to_table_device_matches_host(gpu, override):
     assert dev.column("heatmap").to_pylist() == host.column("heatmap").to_pylist()
 
 
-def test_heatmap_table_device_matches_host(gpu):
+@pytest.mark.parametrize("threaded_copy", [False, True])
+def test_heatmap_table_device_matches_host(gpu, threaded_copy, monkeypatch):
     """heatmap_table end to end on the device (counts resident from hm_count /
     hm_count_grouped through the JSON) == combine_cells + the host
     cells_to_table on the same counts: 200K hotspot points, 300 users with
-    'x*', 'rt-*' and literal 'all' ids, background rows, zooms 6-21."""
+    'x*', 'rt-*' and literal 'all' ids, background rows, zooms 6-21;
+    threaded_copy: the text columns leave in 1 MB chunks from the copy
+    threads (heatmap._to_host) instead of one copy."""
     from heatmap_amd import heatmap as hm
     from heatmap_amd import synth
+
+    if threaded_copy:
+        monkeypatch.setattr(hm, "THREADED_COPY_MIN", 2 << 20)
 
     n = 200_000
     lat, lon = synth.generate("hotspots", n, seed=11)
