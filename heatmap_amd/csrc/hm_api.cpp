@@ -80,7 +80,7 @@ struct hm_ctx {
     int stage_timing = 1;              /* HM_STAGE_TIMING=0: no stage events (hm_last_stats stages read 0) */
     int contig = 1;                    /* HM_CONTIG=0: 3-level plans keep run-streaming at the last level */
     uint32_t ta_min = 16384;           /* HM_TA_MIN: smallest aggregation work item (keys) */
-    uint32_t ta_items = 512;           /* HM_TA_ITEMS: items' worth of points a call must have before ta halves */
+    uint32_t ta_items = 128;           /* HM_TA_ITEMS: items' worth of points a call must have before ta halves */
     /* a stream's tail cells: the count re-keys them under the batch's bucket
      * (read on the device from the stream state) before its last read-back */
     uint64_t* tail_keys = nullptr;

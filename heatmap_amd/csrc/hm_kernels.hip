@@ -3762,10 +3762,12 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
         const bool small = in & (LO == 0 || nkl > LO) & (nkl <= HI);
         const uint32_t rbl = small ? a.B.rbase[bl] : 0u, nrl = small ? a.B.nruns[bl] : 0u;
         const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
-        if (LO == 0 && in && !small) a.spcnt[bl] = 0;
-        if (small) a.totals[bl] = nkl;
-        uint64_t m = __ballot(small);
-        if constexpr (LO == 0) {
+        /* (HM_SP_FUSED: the <= 32-key, <= 4-run buckets are k_small_pairs') */
+        const bool pairb = LO == 0 && HM_SP_FUSED && small && nkl <= 32 && nrl <= HM_SP_PAIR_RUNS;
+        if (LO == 0 && in && (!small || pairb)) a.spcnt[bl] = 0;
+        if (small && !pairb) a.totals[bl] = nkl;
+        uint64_t m = __ballot(small && !pairb);
+        if constexpr (LO == 0 && !HM_SP_FUSED) {
             /* buckets of <= 32 keys in <= 4 runs: two per pass of the wave */
             uint64_t mt = __ballot(small && nkl <= 32 && nrl <= 4);
             m &= ~mt;
@@ -3862,6 +3864,141 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
     }
 }
 
+/* k_small_pairs (HM_SP_FUSED, round 6): the <= 32-key, <= 4-run buckets --
+ * the skew cloud's background, ~24 keys per zoom-11 bucket, 4M of them --
+ * sorted, counted AND emitted in one pass.  A wave sorts every pair of its
+ * batch of 64 buckets (one 32-lane segment each, as k_small_sort) into 4 KB of
+ * LDS, reserves the batch's cells with ONE cursor atomic (~1.5K cells a batch
+ * on the skew cloud: ~65K atomics for 4M buckets, not one per bucket) and
+ * emits them from LDS as k_small_emit does: no sorted codes through HBM, no
+ * per-bucket count array, no scan or reservation launch for these buckets. */
+__global__ __launch_bounds__(HM_SPW_THREADS) void k_small_pairs(HmAggArgs a)
+{
+    constexpr int NWB = HM_SPW_THREADS / 64;
+    __shared__ uint16_t cds[NWB][32][64];   /* a batch's <= 32 pairs of sorted codes */
+    const uint32_t lane = hm_lane();
+    const uint32_t wl = threadIdx.x >> 6;
+    const uint32_t nw = gridDim.x * NWB;
+    const uint32_t zmask = hm_small_zmask(a);
+    const uint32_t wid = blockIdx.x * NWB + wl;
+    const uint32_t step = HmSmallMap<0>::step(nw, a.spbatch);
+    const uint32_t j = lane & 31;
+    const uint64_t segm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+    const uint32_t cm = (1u << a.lg) - 1;
+    for (uint32_t s0 = HmSmallMap<0>::first(wid, a.spbatch); HmSmallMap<0>::bucket(s0, 0, wid, nw) < a.B.count;
+         s0 += step) {
+        const uint64_t bl64 = HmSmallMap<0>::bucket(s0, lane, wid, nw);
+        const bool in = HmSmallMap<0>::lane_in(lane, a.spbatch) & (bl64 < a.B.count);
+        const uint32_t bl = in ? (uint32_t)bl64 : 0u;
+        const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
+        const bool small = in & (nkl <= HM_SPW_SPLIT);
+        const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
+        const bool pair = small && nkl <= 32 && nrl <= HM_SP_PAIR_RUNS;
+        const uint64_t mt = __ballot(pair);
+        if (!mt) continue;   /* wave-uniform */
+        const uint32_t rbl = pair ? a.B.rbase[bl] : 0u;
+        const uint64_t cl = pair ? a.B.coord[bl] : 0ull;
+        if (pair) a.totals[bl] = nkl;
+        /* pass 1: gather, sort and count every pair; lane 2p + g keeps the
+         * cell count of pair p's segment g */
+        uint32_t segcnt = 0;
+        uint32_t np = 0;
+        uint64_t m1 = mt;
+        while (m1) {
+            const int sl = hm_pair_lane(m1);
+            const bool seg = sl >= 0;
+            const int sr = seg ? sl : 0;
+            /* (every shuffle with the whole wave active) */
+            const uint32_t nk0 = __shfl(nkl, sr, 64);
+            const uint32_t nk = seg ? nk0 : 0u;
+            const uint32_t r0 = __shfl(rbl, sr, 64), nr0 = __shfl(nrl, sr, 64);
+            const uint32_t nr = seg ? nr0 : 0u;
+            /* the segment's <= 32 runs, one a lane; lane j's key is in the
+             * first run whose inclusive key count passes j (a segmented scan
+             * and a 5-step search, every lane active) */
+            const uint2 run = j < nr ? a.in.run[r0 + j] : make_uint2(0, 0);
+            uint32_t incl = run.y;
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) {
+                const uint32_t t = __shfl_up(incl, o, 32);
+                incl += j >= (uint32_t)o ? t : 0u;
+            }
+            uint32_t ri = 0;
+#pragma unroll
+            for (int st = 16; st > 0; st >>= 1)
+                if ((uint32_t)__shfl(incl, (int)(ri + st - 1), 32) <= j) ri += st;
+            const uint32_t rx = __shfl(run.x, (int)ri, 32), ry = __shfl(run.y, (int)ri, 32);
+            const uint32_t ric = __shfl(incl, (int)ri, 32);
+            const uint32_t src = rx + (j - (ric - ry));
+            const bool v_ok = seg && j < nk;
+            uint32_t v = 0xFFFFFFFFu;
+            if (v_ok) {
+                const uint32_t key = (uint32_t)a.keys[src];
+                v = hm_spread7(key & cm) | (hm_spread7(key >> a.lg) << 1);
+            }
+            hm_seg32_size<2>(v, lane);
+            cds[wl][np][lane] = (uint16_t)v;
+            const uint32_t nx = __shfl_down(v, 1, 64);
+            const uint32_t hl = (33u - (uint32_t)__clz((int)(v ^ nx))) >> 1;
+            uint32_t total = !v_ok ? 0u
+                                   : (j + 1 == nk) ? (uint32_t)__popc(zmask)
+                                                   : (uint32_t)__popc(zmask & ((1u << hl) - 1u));
+#pragma unroll
+            for (int o = 16; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
+            const uint32_t t0 = __builtin_amdgcn_readlane(total, 0), t1 = __builtin_amdgcn_readlane(total, 32);
+            segcnt = lane == 2 * np ? t0 : lane == 2 * np + 1 ? t1 : segcnt;
+            np++;
+        }
+        /* one reservation for the batch's cells */
+        const uint32_t incl = hm_wave_incl_scan(segcnt);
+        const uint32_t btot = __builtin_amdgcn_readlane(incl, 63);
+        const uint32_t excl = incl - segcnt;
+        unsigned long long b0 = 0;
+        if (lane == 0 && btot) b0 = atomicAdd(a.out.cursor, (unsigned long long)btot);
+        const uint64_t base = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(b0 >> 32), 0) << 32) |
+                              __builtin_amdgcn_readlane((uint32_t)b0, 0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        /* pass 2: the pairs in the same order, their codes from LDS */
+        uint64_t m2 = mt;
+        for (uint32_t p = 0; m2; p++) {
+            const int sl = hm_pair_lane(m2);
+            const bool seg = sl >= 0;
+            const int sr = seg ? sl : 0;
+            const uint32_t nk0 = __shfl(nkl, sr, 64);
+            const uint32_t nk = seg ? nk0 : 0u;
+            const uint64_t coord = __shfl(cl, sr, 64);
+            uint64_t q = base + __shfl(excl, (int)(2 * p + (lane >> 5)), 64);
+            const bool v_ok = seg && j < nk;
+            const uint32_t v = v_ok ? (uint32_t)cds[wl][p][lane] : 0xFFFFFFFFu;
+            const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
+            for (int l = 0; l < a.lg; l++) {
+                if (!((zmask >> l) & 1u)) continue;
+                const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
+                const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
+                /* the segment's last head at or below this lane: the cell's first element */
+                const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
+                const uint32_t hl = hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u;
+                const uint32_t start = (uint32_t)__shfl((int)j, (int)hl, 64);
+                const uint64_t bal = __ballot(end) & segm;
+                if (end) {
+                    const uint32_t code = v >> (2 * l);
+                    const int s = a.lg - l;
+                    const uint32_t idx = (hm_compact7(code >> 1) << s) | hm_compact7(code);
+                    const uint64_t pos = q + hm_mbcnt(bal);
+                    if (pos < a.out.capacity) {
+                        a.out.keys[pos] = hm_cell_key(a.Z - l, coord, s, idx);
+                        a.out.counts[pos] = (uint64_t)(j - start + 1);
+                    }
+                }
+                q += (uint64_t)__popcll(bal);
+            }
+        }
+        __builtin_amdgcn_wave_barrier();   /* cds is free for the next batch */
+    }
+}
+
 /* one reservation for every small bucket's cells */
 __global__ void k_small_reserve(HmAggArgs a)
 {
@@ -3890,7 +4027,11 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
         const uint64_t cl = small ? a.B.coord[bl] : 0ull;
         const uint64_t ol = small ? a.spoff[bl] : 0ull;
         uint64_t m = __ballot(small);
-        if constexpr (LO == 0) {
+        if constexpr (LO == 0 && HM_SP_FUSED) {
+            const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
+            m &= ~__ballot(small && nkl <= 32 && nrl <= HM_SP_PAIR_RUNS);   /* k_small_pairs' */
+        }
+        if constexpr (LO == 0 && !HM_SP_FUSED) {
             /* the <= 32-key buckets in pairs, as k_small_sort took them */
             const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
             uint64_t mt = __ballot(small && nkl <= 32 && nrl <= 4);
@@ -4651,6 +4792,7 @@ void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
     const uint32_t per_block = b.spbatch * (HM_SPW_THREADS / 64);
     const uint32_t wb = (a.B.count + per_block - 1) / per_block;
     const dim3 g(wb < HM_SPW_GRID ? wb : HM_SPW_GRID);
+    if (HM_SP_FUSED) hipLaunchKernelGGL(k_small_pairs, g, dim3(HM_SPW_THREADS), 0, s, b);
     hipLaunchKernelGGL((k_small_sort<0, HM_SPW_SPLIT>), g, dim3(HM_SPW_THREADS), 0, s, b);
     if (HM_SPW_MAX > HM_SPW_SPLIT)
         hipLaunchKernelGGL((k_small_sort<HM_SPW_SPLIT, HM_SPW_MAX>), g, dim3(HM_SPW_THREADS), 0, s, b);

@@ -121,6 +121,14 @@ __host__ __device__ inline uint32_t hm_l1i(uint32_t d, uint32_t sh) { return sh 
 #define HM_SPW_SPLIT 512
 #endif
 static_assert(HM_SPW_MAX >= HM_SP_MAX, "every bucket without a dense work item needs the wavefront path");
+/* HM_SP_FUSED: the <= 32-key, <= 4-run small buckets go through ONE fused
+ * sort + count + emit kernel (k_small_pairs) instead of k_small_sort, a scan
+ * and k_small_emit */
+#ifndef HM_SP_FUSED
+#define HM_SP_FUSED 1
+#endif
+/* runs a fused pair bucket may span (a 32-lane segment gathers them) */
+#define HM_SP_PAIR_RUNS (HM_SP_FUSED ? 32u : 4u)
 #define HM_SPW_THREADS 256
 #define HM_SPW_GRID (256 * 8)
 #define HM_POOL_THREADS 256

@@ -21,6 +21,7 @@ VARIANTS = {
     "base": [],
     "nows": ["HM_L1_WS=0"],                  # level 1 through k_l1_fast only (the shipped default)
     "wslate": ["HM_WS_PREFETCH_LATE=1"],     # k_l1_ws: next tile's loads after the count
+    "spunfused": ["HM_SP_FUSED=0"],          # <= 32-key buckets through k_small_sort / scan / k_small_emit (round 5)
     "ws": ["HM_L1_WS=1"],                    # k_l1_ws (12 compute + 4 writer waves)
     "ws8": ["HM_L1_WS=1", "HM_WS_C=512"],                  # k_l1_ws: 8 compute + 8 writer waves, 8192-point tiles
     "ws10": ["HM_L1_WS=1", "HM_WS_C=640"],                 # k_l1_ws: 10 compute + 6 writer waves, 10240-point tiles
@@ -200,6 +201,10 @@ PATCHES["agplain"] = [("hm_kernels.hip", """            if (HM_AG_FAST)
                 hm_lds_count_fast(grid, dummy + (uint32_t)hm_lane(), sl(k), v);
             else
                 hm_lds_count(grid, dummy, sl(k), v);""", """            atomicAdd(&grid[v ? sl(k) : dummy + (uint32_t)hm_lane()], 1u);""")]
+# k_small_emit's pair path (<= 32-key buckets, the skew cloud's background) without its cell stores (timing only)
+PATCHES["emnostore"] = [("hm_kernels.hip", """                        if (p < a.out.capacity) {
+                            a.out.keys[p] = hm_cell_key(a.Z - l, coord, s, idx);""", """                        if (p == 0x123456789ull) {
+                            a.out.keys[p] = hm_cell_key(a.Z - l, coord, s, idx);""")]
 # compile-time macros added to a patched build
 
 
