@@ -3740,6 +3740,13 @@ struct HmSmallMap {
     static __device__ __forceinline__ bool lane_in(uint32_t lane, uint32_t spb) { return LO ? true : lane < spb; }
 };
 
+/* the small buckets k_small_pairs takes (HM_SP_FUSED): <= 32 keys in <= 32
+ * runs (two a wave pass) or 33-64 keys in <= 64 runs (one) */
+__device__ __forceinline__ bool hm_sp_fused_ok(uint32_t nk, uint32_t nr)
+{
+    return HM_SP_FUSED && nk <= 64 && nr <= (nk <= 32 ? 32u : 64u);
+}
+
 /* Persistent: a bucket is this instantiation's when LO < nkeys <= HI (larger
  * ones are k_aggregate's). The LO == 0 instantiation runs first and zeroes the
  * cell count of every bucket that is not its own. */
@@ -3763,7 +3770,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
         const uint32_t rbl = small ? a.B.rbase[bl] : 0u, nrl = small ? a.B.nruns[bl] : 0u;
         const uint32_t kbl = small ? a.B.keybase[bl] : 0u;
         /* (HM_SP_FUSED: the <= 32-key, <= 4-run buckets are k_small_pairs') */
-        const bool pairb = LO == 0 && HM_SP_FUSED && small && nkl <= 32 && nrl <= HM_SP_PAIR_RUNS;
+        const bool pairb = LO == 0 && small && hm_sp_fused_ok(nkl, nrl);
         if (LO == 0 && in && (!small || pairb)) a.spcnt[bl] = 0;
         if (small && !pairb) a.totals[bl] = nkl;
         uint64_t m = __ballot(small && !pairb);
@@ -3864,27 +3871,104 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
     }
 }
 
-/* k_small_pairs (HM_SP_FUSED, round 6): the <= 32-key, <= 4-run buckets --
+/* k_small_pairs (HM_SP_FUSED, round 6): the small buckets of <= 64 keys --
  * the skew cloud's background, ~24 keys per zoom-11 bucket, 4M of them --
- * sorted, counted AND emitted in one pass.  A wave sorts every pair of its
- * batch of 64 buckets (one 32-lane segment each, as k_small_sort) into 4 KB of
- * LDS, reserves the batch's cells with ONE cursor atomic (~1.5K cells a batch
- * on the skew cloud: ~65K atomics for 4M buckets, not one per bucket) and
- * emits them from LDS as k_small_emit does: no sorted codes through HBM, no
- * per-bucket count array, no scan or reservation launch for these buckets. */
+ * gathered, sorted, counted AND emitted in one pass.  A wave pass ("row")
+ * takes two buckets of <= 32 keys in <= 32 runs (one 32-lane segment each) or
+ * one of 33-64 keys in <= 64 runs; a wave sorts up to 32 rows of its batch of
+ * 64 buckets into 4 KB of LDS, reserves their cells with ONE cursor atomic
+ * (~1.5K cells on the skew cloud: ~65K atomics for 4M buckets, not one per
+ * bucket) and emits them from LDS as k_small_emit does: no sorted codes
+ * through HBM, no per-bucket count array, no scan or reservation launch. */
+
+/* gather + sort + cell count of one row's bucket(s), W = 32 (a pair: lanes
+ * of each half hold their own bucket) or 64 (one bucket); every lane active.
+ * Returns the segment's cell count (the same on every lane of it). */
+template <int W>
+__device__ __forceinline__ uint32_t hm_sp_sort(const HmAggArgs& a, bool seg, uint32_t nk, uint32_t r0, uint32_t nr,
+                                               uint32_t lane, uint32_t zmask, uint32_t& v, bool& v_ok)
+{
+    const uint32_t j = lane & (W - 1);
+    const uint32_t cm = (1u << a.lg) - 1;
+    /* the segment's runs, one a lane; lane j's key is in the first run whose
+     * inclusive key count passes j (segmented scan + binary search) */
+    const uint2 run = (seg && j < nr) ? a.in.run[r0 + j] : make_uint2(0, 0);
+    uint32_t incl = run.y;
+#pragma unroll
+    for (int o = 1; o < W; o <<= 1) {
+        const uint32_t t = __shfl_up(incl, o, W);
+        incl += j >= (uint32_t)o ? t : 0u;
+    }
+    uint32_t ri = 0;
+#pragma unroll
+    for (int st = W / 2; st > 0; st >>= 1)
+        if ((uint32_t)__shfl(incl, (int)(ri + st - 1), W) <= j) ri += st;
+    const uint32_t rx = __shfl(run.x, (int)ri, W), ry = __shfl(run.y, (int)ri, W);
+    const uint32_t ric = __shfl(incl, (int)ri, W);
+    v_ok = seg && j < nk;
+    v = 0xFFFFFFFFu;
+    if (v_ok) {
+        const uint32_t key = (uint32_t)a.keys[rx + (j - (ric - ry))];
+        v = hm_spread7(key & cm) | (hm_spread7(key >> a.lg) << 1);
+    }
+    if constexpr (W == 32) {
+        hm_seg32_size<2>(v, lane);
+    } else {
+        uint32_t vv[1] = {v};
+        hm_wave_bitonic<1>(vv);
+        v = vv[0];
+    }
+    /* cells ended by this element (hm_small_sort), summed over the segment */
+    const uint32_t nx = __shfl_down(v, 1, 64);
+    const uint32_t hl = (33u - (uint32_t)__clz((int)(v ^ nx))) >> 1;
+    uint32_t total = !v_ok ? 0u
+                           : (j + 1 == nk) ? (uint32_t)__popc(zmask) : (uint32_t)__popc(zmask & ((1u << hl) - 1u));
+#pragma unroll
+    for (int o = W / 2; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
+    return total;
+}
+
+/* the cells of one sorted row segment at q: a cell is written by its last
+ * element, its count = that position - the segment's last head at or below */
+template <int W>
+__device__ __forceinline__ void hm_sp_emit(const HmAggArgs& a, uint32_t v, bool v_ok, uint32_t nk, uint64_t coord,
+                                           uint64_t q, uint32_t zmask, uint32_t lane)
+{
+    const uint32_t j = lane & (W - 1);
+    const uint64_t segm = W == 64 ? ~0ull : (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+    const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
+    for (int l = 0; l < a.lg; l++) {
+        if (!((zmask >> l) & 1u)) continue;
+        const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
+        const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
+        const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
+        const uint32_t hl = hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u;
+        const uint32_t start = (uint32_t)__shfl((int)j, (int)hl, 64);
+        const uint64_t bal = __ballot(end) & segm;
+        if (end) {
+            const uint32_t code = v >> (2 * l);
+            const int s = a.lg - l;
+            const uint32_t idx = (hm_compact7(code >> 1) << s) | hm_compact7(code);
+            const uint64_t pos = q + hm_mbcnt(bal);
+            if (pos < a.out.capacity) {
+                a.out.keys[pos] = hm_cell_key(a.Z - l, coord, s, idx);
+                a.out.counts[pos] = (uint64_t)(j - start + 1);
+            }
+        }
+        q += (uint64_t)__popcll(bal);
+    }
+}
+
 __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_pairs(HmAggArgs a)
 {
     constexpr int NWB = HM_SPW_THREADS / 64;
-    __shared__ uint16_t cds[NWB][32][64];   /* a batch's <= 32 pairs of sorted codes */
+    __shared__ uint16_t cds[NWB][32][64];   /* up to 32 rows of sorted codes */
     const uint32_t lane = hm_lane();
     const uint32_t wl = threadIdx.x >> 6;
     const uint32_t nw = gridDim.x * NWB;
     const uint32_t zmask = hm_small_zmask(a);
     const uint32_t wid = blockIdx.x * NWB + wl;
     const uint32_t step = HmSmallMap<0>::step(nw, a.spbatch);
-    const uint32_t j = lane & 31;
-    const uint64_t segm = (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
-    const uint32_t cm = (1u << a.lg) - 1;
     for (uint32_t s0 = HmSmallMap<0>::first(wid, a.spbatch); HmSmallMap<0>::bucket(s0, 0, wid, nw) < a.B.count;
          s0 += step) {
         const uint64_t bl64 = HmSmallMap<0>::bucket(s0, lane, wid, nw);
@@ -3893,109 +3977,77 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_pairs(HmAggArgs a)
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
         const bool small = in & (nkl <= HM_SPW_SPLIT);
         const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
-        const bool pair = small && nkl <= 32 && nrl <= HM_SP_PAIR_RUNS;
-        const uint64_t mt = __ballot(pair);
-        if (!mt) continue;   /* wave-uniform */
-        const uint32_t rbl = pair ? a.B.rbase[bl] : 0u;
-        const uint64_t cl = pair ? a.B.coord[bl] : 0ull;
-        if (pair) a.totals[bl] = nkl;
-        /* pass 1: gather, sort and count every pair; lane 2p + g keeps the
-         * cell count of pair p's segment g */
-        uint32_t segcnt = 0;
-        uint32_t np = 0;
-        uint64_t m1 = mt;
-        while (m1) {
-            const int sl = hm_pair_lane(m1);
-            const bool seg = sl >= 0;
-            const int sr = seg ? sl : 0;
-            /* (every shuffle with the whole wave active) */
-            const uint32_t nk0 = __shfl(nkl, sr, 64);
-            const uint32_t nk = seg ? nk0 : 0u;
-            const uint32_t r0 = __shfl(rbl, sr, 64), nr0 = __shfl(nrl, sr, 64);
-            const uint32_t nr = seg ? nr0 : 0u;
-            /* the segment's <= 32 runs, one a lane; lane j's key is in the
-             * first run whose inclusive key count passes j (a segmented scan
-             * and a 5-step search, every lane active) */
-            const uint2 run = j < nr ? a.in.run[r0 + j] : make_uint2(0, 0);
-            uint32_t incl = run.y;
-#pragma unroll
-            for (int o = 1; o < 32; o <<= 1) {
-                const uint32_t t = __shfl_up(incl, o, 32);
-                incl += j >= (uint32_t)o ? t : 0u;
-            }
-            uint32_t ri = 0;
-#pragma unroll
-            for (int st = 16; st > 0; st >>= 1)
-                if ((uint32_t)__shfl(incl, (int)(ri + st - 1), 32) <= j) ri += st;
-            const uint32_t rx = __shfl(run.x, (int)ri, 32), ry = __shfl(run.y, (int)ri, 32);
-            const uint32_t ric = __shfl(incl, (int)ri, 32);
-            const uint32_t src = rx + (j - (ric - ry));
-            const bool v_ok = seg && j < nk;
-            uint32_t v = 0xFFFFFFFFu;
-            if (v_ok) {
-                const uint32_t key = (uint32_t)a.keys[src];
-                v = hm_spread7(key & cm) | (hm_spread7(key >> a.lg) << 1);
-            }
-            hm_seg32_size<2>(v, lane);
-            cds[wl][np][lane] = (uint16_t)v;
-            const uint32_t nx = __shfl_down(v, 1, 64);
-            const uint32_t hl = (33u - (uint32_t)__clz((int)(v ^ nx))) >> 1;
-            uint32_t total = !v_ok ? 0u
-                                   : (j + 1 == nk) ? (uint32_t)__popc(zmask)
-                                                   : (uint32_t)__popc(zmask & ((1u << hl) - 1u));
-#pragma unroll
-            for (int o = 16; o > 0; o >>= 1) total += __shfl_xor(total, o, 64);
-            const uint32_t t0 = __builtin_amdgcn_readlane(total, 0), t1 = __builtin_amdgcn_readlane(total, 32);
-            segcnt = lane == 2 * np ? t0 : lane == 2 * np + 1 ? t1 : segcnt;
-            np++;
-        }
-        /* one reservation for the batch's cells */
-        const uint32_t incl = hm_wave_incl_scan(segcnt);
-        const uint32_t btot = __builtin_amdgcn_readlane(incl, 63);
-        const uint32_t excl = incl - segcnt;
-        unsigned long long b0 = 0;
-        if (lane == 0 && btot) b0 = atomicAdd(a.out.cursor, (unsigned long long)btot);
-        const uint64_t base = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(b0 >> 32), 0) << 32) |
-                              __builtin_amdgcn_readlane((uint32_t)b0, 0);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        /* pass 2: the pairs in the same order, their codes from LDS */
-        uint64_t m2 = mt;
-        for (uint32_t p = 0; m2; p++) {
-            const int sl = hm_pair_lane(m2);
-            const bool seg = sl >= 0;
-            const int sr = seg ? sl : 0;
-            const uint32_t nk0 = __shfl(nkl, sr, 64);
-            const uint32_t nk = seg ? nk0 : 0u;
-            const uint64_t coord = __shfl(cl, sr, 64);
-            uint64_t q = base + __shfl(excl, (int)(2 * p + (lane >> 5)), 64);
-            const bool v_ok = seg && j < nk;
-            const uint32_t v = v_ok ? (uint32_t)cds[wl][p][lane] : 0xFFFFFFFFu;
-            const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
-            for (int l = 0; l < a.lg; l++) {
-                if (!((zmask >> l) & 1u)) continue;
-                const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
-                const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
-                /* the segment's last head at or below this lane: the cell's first element */
-                const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
-                const uint32_t hl = hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u;
-                const uint32_t start = (uint32_t)__shfl((int)j, (int)hl, 64);
-                const uint64_t bal = __ballot(end) & segm;
-                if (end) {
-                    const uint32_t code = v >> (2 * l);
-                    const int s = a.lg - l;
-                    const uint32_t idx = (hm_compact7(code >> 1) << s) | hm_compact7(code);
-                    const uint64_t pos = q + hm_mbcnt(bal);
-                    if (pos < a.out.capacity) {
-                        a.out.keys[pos] = hm_cell_key(a.Z - l, coord, s, idx);
-                        a.out.counts[pos] = (uint64_t)(j - start + 1);
-                    }
+        const bool mine = small && hm_sp_fused_ok(nkl, nrl);
+        uint64_t mp = __ballot(mine && nkl <= 32), ms = __ballot(mine && nkl > 32);
+        if (!(mp | ms)) continue;   /* wave-uniform */
+        const uint32_t rbl = mine ? a.B.rbase[bl] : 0u;
+        const uint64_t cl = mine ? a.B.coord[bl] : 0ull;
+        if (mine) a.totals[bl] = nkl;
+        while (mp | ms) {
+            /* pass 1: up to 32 rows (pairs first) sorted into LDS; lane 2p + g
+             * keeps row p's segment-g cell count */
+            uint32_t segcnt = 0, np = 0;
+            uint64_t mp1 = mp, ms1 = ms;
+            while (np < 32 && (mp1 | ms1)) {
+                uint32_t v, tot;
+                bool v_ok;
+                const bool paired = mp1 != 0;   /* wave-uniform */
+                if (paired) {
+                    const int sl = hm_pair_lane(mp1);
+                    const bool seg = sl >= 0;
+                    const int sr = seg ? sl : 0;
+                    const uint32_t nk0 = __shfl(nkl, sr, 64), r0 = __shfl(rbl, sr, 64), nr0 = __shfl(nrl, sr, 64);
+                    tot = hm_sp_sort<32>(a, seg, seg ? nk0 : 0u, r0, seg ? nr0 : 0u, lane, zmask, v, v_ok);
+                } else {
+                    const int i = __builtin_ctzll(ms1);
+                    ms1 &= ms1 - 1;
+                    tot = hm_sp_sort<64>(a, true, __shfl(nkl, i, 64), __shfl(rbl, i, 64), __shfl(nrl, i, 64), lane,
+                                         zmask, v, v_ok);
                 }
-                q += (uint64_t)__popcll(bal);
+                cds[wl][np][lane] = (uint16_t)v;
+                /* (a single's segment is the whole wave: lane 32 repeats its total) */
+                const uint32_t t0 = __builtin_amdgcn_readlane(tot, 0);
+                const uint32_t t1 = paired ? __builtin_amdgcn_readlane(tot, 32) : 0u;
+                segcnt = lane == 2 * np ? t0 : lane == 2 * np + 1 ? t1 : segcnt;
+                np++;
             }
+            /* one reservation for the rows' cells */
+            const uint32_t incl = hm_wave_incl_scan(segcnt);
+            const uint32_t btot = __builtin_amdgcn_readlane(incl, 63);
+            const uint32_t excl = incl - segcnt;
+            unsigned long long b0 = 0;
+            if (lane == 0 && btot) b0 = atomicAdd(a.out.cursor, (unsigned long long)btot);
+            const uint64_t base = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(b0 >> 32), 0) << 32) |
+                                  __builtin_amdgcn_readlane((uint32_t)b0, 0);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            /* pass 2: the same rows in the same order, codes from LDS */
+            uint64_t mp2 = mp, ms2 = ms;
+            for (uint32_t p = 0; p < np; p++) {
+                const uint32_t v = cds[wl][p][lane];
+                if (mp2) {
+                    const int sl = hm_pair_lane(mp2);
+                    const bool seg = sl >= 0;
+                    const int sr = seg ? sl : 0;
+                    const uint32_t nk0 = __shfl(nkl, sr, 64);
+                    const uint32_t nk = seg ? nk0 : 0u;
+                    const uint64_t coord = __shfl(cl, sr, 64);
+                    const uint64_t q = base + __shfl(excl, (int)(2 * p + (lane >> 5)), 64);
+                    hm_sp_emit<32>(a, v == 0xFFFFu ? 0xFFFFFFFFu : v, seg && (lane & 31u) < nk, nk, coord, q, zmask, lane);
+                } else {
+                    const int i = __builtin_ctzll(ms2);
+                    ms2 &= ms2 - 1;
+                    const uint32_t nk = __shfl(nkl, i, 64);
+                    const uint64_t coord = __shfl(cl, i, 64);
+                    const uint64_t q = base + __shfl(excl, (int)(2 * p), 64);
+                    hm_sp_emit<64>(a, v == 0xFFFFu ? 0xFFFFFFFFu : v, lane < nk, nk, coord, q, zmask, lane);
+                }
+            }
+            mp = mp1;
+            ms = ms1;
+            __builtin_amdgcn_wave_barrier();   /* cds is free for the next rows */
         }
-        __builtin_amdgcn_wave_barrier();   /* cds is free for the next batch */
     }
 }
 
@@ -4029,7 +4081,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_emit(HmAggArgs a)
         uint64_t m = __ballot(small);
         if constexpr (LO == 0 && HM_SP_FUSED) {
             const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
-            m &= ~__ballot(small && nkl <= 32 && nrl <= HM_SP_PAIR_RUNS);   /* k_small_pairs' */
+            m &= ~__ballot(small && hm_sp_fused_ok(nkl, nrl));   /* k_small_pairs' */
         }
         if constexpr (LO == 0 && !HM_SP_FUSED) {
             /* the <= 32-key buckets in pairs, as k_small_sort took them */

@@ -127,8 +127,6 @@ static_assert(HM_SPW_MAX >= HM_SP_MAX, "every bucket without a dense work item n
 #ifndef HM_SP_FUSED
 #define HM_SP_FUSED 1
 #endif
-/* runs a fused pair bucket may span (a 32-lane segment gathers them) */
-#define HM_SP_PAIR_RUNS (HM_SP_FUSED ? 32u : 4u)
 #define HM_SPW_THREADS 256
 #define HM_SPW_GRID (256 * 8)
 #define HM_POOL_THREADS 256
