@@ -3881,36 +3881,62 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_sort(HmAggArgs a)
  * bucket) and emits them from LDS as k_small_emit does: no sorted codes
  * through HBM, no per-bucket count array, no scan or reservation launch. */
 
-/* gather + sort + cell count of one row's bucket(s), W = 32 (a pair: lanes
- * of each half hold their own bucket) or 64 (one bucket); every lane active.
- * Returns the segment's cell count (the same on every lane of it). */
+/* One row's bucket(s) in three steps, so a wave can keep the next rows'
+ * loads in flight while it sorts: W = 32 (a pair: each 32-lane half holds its
+ * own bucket) or 64 (one bucket); every lane active; the loads are
+ * unconditional (inactive lanes read element 0), so the compiler counts them.
+ *   hm_sp_run:  the segment's runs, one a lane;
+ *   hm_sp_key:  lane j's key: in the first run whose inclusive key count
+ *               passes j (segmented scan + binary search), 0xFFFF if none;
+ *   hm_sp_sort: Morton code, segmented sort, the segment's cell count. */
+__device__ __forceinline__ uint2 hm_sp_run(const HmAggArgs& a, bool seg, uint32_t r0, uint32_t nr, uint32_t j)
+{
+    const bool v = seg && j < nr;
+    const uint2 r = a.in.run[v ? r0 + j : 0u];
+    return v ? r : make_uint2(0, 0);
+}
 template <int W>
-__device__ __forceinline__ uint32_t hm_sp_sort(const HmAggArgs& a, bool seg, uint32_t nk, uint32_t r0, uint32_t nr,
-                                               uint32_t lane, uint32_t zmask, uint32_t& v, bool& v_ok)
+__device__ __forceinline__ uint32_t hm_sp_key(const HmAggArgs& a, uint2 run, bool seg, uint32_t nk, uint32_t lane,
+                                              uint2* sc)
+{
+    const uint32_t j = lane & (W - 1);
+    /* each non-empty run r marks its first key position excl_r in the wave's
+     * 64-slot scratch with x_r - excl_r; lane j's run starts at the last mark
+     * at or below j (a ballot), so its key is at that mark's value + j: a DPP
+     * scan and three LDS round trips instead of a shuffle search */
+    uint32_t incl = run.y;
+    HM_DPP_ADD(incl, 0x111, 0xF);   /* row_shr:1 */
+    HM_DPP_ADD(incl, 0x112, 0xF);   /* row_shr:2 */
+    HM_DPP_ADD(incl, 0x114, 0xF);   /* row_shr:4 */
+    HM_DPP_ADD(incl, 0x118, 0xF);   /* row_shr:8 */
+    HM_DPP_ADD(incl, 0x142, 0xA);   /* row_bcast:15: rows 0 -> 1, 2 -> 3 (each 32-lane half scanned) */
+    if constexpr (W == 64) HM_DPP_ADD(incl, 0x143, 0xC);   /* row_bcast:31: the whole wave */
+    const uint32_t excl = incl - run.y;
+    sc[lane] = make_uint2(0u, 0u);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    if (run.y) sc[(lane & ~(uint32_t)(W - 1)) + excl] = make_uint2(run.x - excl, 1u);   /* (run.y = 0 past nr) */
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint64_t marks = __ballot(sc[lane].y != 0u);
+    const uint64_t below = marks & ((2ull << lane) - 1ull);
+    const uint32_t h = below ? 63u - (uint32_t)__clzll((long long)below) : lane;
+    const uint32_t d = sc[h].x;
+    const bool v_ok = seg && j < nk;
+    const uint32_t k = (uint32_t)a.keys[v_ok ? d + j : 0u];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();   /* sc is free for the next row */
+    return v_ok ? k : 0xFFFFFFFFu;
+}
+template <int W>
+__device__ __forceinline__ uint32_t hm_sp_sort(const HmAggArgs& a, uint32_t key, uint32_t nk, uint32_t lane,
+                                               uint32_t zmask, uint32_t& v)
 {
     const uint32_t j = lane & (W - 1);
     const uint32_t cm = (1u << a.lg) - 1;
-    /* the segment's runs, one a lane; lane j's key is in the first run whose
-     * inclusive key count passes j (segmented scan + binary search) */
-    const uint2 run = (seg && j < nr) ? a.in.run[r0 + j] : make_uint2(0, 0);
-    uint32_t incl = run.y;
-#pragma unroll
-    for (int o = 1; o < W; o <<= 1) {
-        const uint32_t t = __shfl_up(incl, o, W);
-        incl += j >= (uint32_t)o ? t : 0u;
-    }
-    uint32_t ri = 0;
-#pragma unroll
-    for (int st = W / 2; st > 0; st >>= 1)
-        if ((uint32_t)__shfl(incl, (int)(ri + st - 1), W) <= j) ri += st;
-    const uint32_t rx = __shfl(run.x, (int)ri, W), ry = __shfl(run.y, (int)ri, W);
-    const uint32_t ric = __shfl(incl, (int)ri, W);
-    v_ok = seg && j < nk;
-    v = 0xFFFFFFFFu;
-    if (v_ok) {
-        const uint32_t key = (uint32_t)a.keys[rx + (j - (ric - ry))];
-        v = hm_spread7(key & cm) | (hm_spread7(key >> a.lg) << 1);
-    }
+    const bool v_ok = key != 0xFFFFFFFFu;
+    v = v_ok ? hm_spread7(key & cm) | (hm_spread7(key >> a.lg) << 1) : 0xFFFFFFFFu;
     if constexpr (W == 32) {
         hm_seg32_size<2>(v, lane);
     } else {
@@ -3963,6 +3989,7 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_pairs(HmAggArgs a)
 {
     constexpr int NWB = HM_SPW_THREADS / 64;
     __shared__ uint16_t cds[NWB][32][64];   /* up to 32 rows of sorted codes */
+    __shared__ uint2 gsc[NWB][64];          /* hm_sp_key's run marks */
     const uint32_t lane = hm_lane();
     const uint32_t wl = threadIdx.x >> 6;
     const uint32_t nw = gridDim.x * NWB;
@@ -3985,32 +4012,63 @@ __global__ __launch_bounds__(HM_SPW_THREADS) void k_small_pairs(HmAggArgs a)
         if (mine) a.totals[bl] = nkl;
         while (mp | ms) {
             /* pass 1: up to 32 rows (pairs first) sorted into LDS; lane 2p + g
-             * keeps row p's segment-g cell count */
-            uint32_t segcnt = 0, np = 0;
+             * keeps row p's segment-g cell count.  Software-pipelined: while
+             * row p sorts, row p+1's key and row p+2's runs are loading */
+            uint32_t segcnt = 0;
             uint64_t mp1 = mp, ms1 = ms;
-            while (np < 32 && (mp1 | ms1)) {
-                uint32_t v, tot;
-                bool v_ok;
-                const bool paired = mp1 != 0;   /* wave-uniform */
-                if (paired) {
+            const uint32_t nrows = min(32u, (uint32_t)(__popcll(mp) + 1) / 2 + (uint32_t)__popcll(ms));
+            struct Row {
+                bool paired, seg;
+                uint32_t nk, r0, nr;
+            };
+            auto take = [&](bool any) -> Row {
+                Row r;
+                r.paired = !any || mp1 != 0;
+                int src = 0;
+                r.seg = false;
+                if (any && mp1) {
                     const int sl = hm_pair_lane(mp1);
-                    const bool seg = sl >= 0;
-                    const int sr = seg ? sl : 0;
-                    const uint32_t nk0 = __shfl(nkl, sr, 64), r0 = __shfl(rbl, sr, 64), nr0 = __shfl(nrl, sr, 64);
-                    tot = hm_sp_sort<32>(a, seg, seg ? nk0 : 0u, r0, seg ? nr0 : 0u, lane, zmask, v, v_ok);
-                } else {
-                    const int i = __builtin_ctzll(ms1);
+                    r.seg = sl >= 0;
+                    src = r.seg ? sl : 0;
+                } else if (any && ms1) {
+                    src = __builtin_ctzll(ms1);
                     ms1 &= ms1 - 1;
-                    tot = hm_sp_sort<64>(a, true, __shfl(nkl, i, 64), __shfl(rbl, i, 64), __shfl(nrl, i, 64), lane,
-                                         zmask, v, v_ok);
+                    r.seg = true;
                 }
-                cds[wl][np][lane] = (uint16_t)v;
+                const uint32_t nk0 = __shfl(nkl, src, 64), r00 = __shfl(rbl, src, 64), nr0 = __shfl(nrl, src, 64);
+                r.nk = r.seg ? nk0 : 0u;
+                r.r0 = r00;
+                r.nr = r.seg ? nr0 : 0u;
+                return r;
+            };
+            auto key_of = [&](const Row& r, uint2 run) {
+                return r.paired ? hm_sp_key<32>(a, run, r.seg, r.nk, lane, gsc[wl])
+                                : hm_sp_key<64>(a, run, r.seg, r.nk, lane, gsc[wl]);
+            };
+            const uint32_t jl = lane & 31u;
+            Row A = take(true);
+            uint2 runA = hm_sp_run(a, A.seg, A.r0, A.nr, A.paired ? jl : lane);
+            Row B = take(nrows > 1);
+            uint2 runB = hm_sp_run(a, B.seg, B.r0, B.nr, B.paired ? jl : lane);
+            uint32_t keyA = key_of(A, runA);
+            for (uint32_t p = 0; p < nrows; p++) {
+                const Row C = take(p + 2 < nrows);
+                const uint2 runC = hm_sp_run(a, C.seg, C.r0, C.nr, C.paired ? jl : lane);
+                const uint32_t keyB = key_of(B, runB);
+                uint32_t v, tot;
+                if (A.paired) tot = hm_sp_sort<32>(a, keyA, A.nk, lane, zmask, v);
+                else tot = hm_sp_sort<64>(a, keyA, A.nk, lane, zmask, v);
+                cds[wl][p][lane] = (uint16_t)v;
                 /* (a single's segment is the whole wave: lane 32 repeats its total) */
                 const uint32_t t0 = __builtin_amdgcn_readlane(tot, 0);
-                const uint32_t t1 = paired ? __builtin_amdgcn_readlane(tot, 32) : 0u;
-                segcnt = lane == 2 * np ? t0 : lane == 2 * np + 1 ? t1 : segcnt;
-                np++;
+                const uint32_t t1 = A.paired ? __builtin_amdgcn_readlane(tot, 32) : 0u;
+                segcnt = lane == 2 * p ? t0 : lane == 2 * p + 1 ? t1 : segcnt;
+                A = B;
+                keyA = keyB;
+                B = C;
+                runB = runC;
             }
+            const uint32_t np = nrows;
             /* one reservation for the rows' cells */
             const uint32_t incl = hm_wave_incl_scan(segcnt);
             const uint32_t btot = __builtin_amdgcn_readlane(incl, 63);
