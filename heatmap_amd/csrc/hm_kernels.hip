@@ -3963,21 +3963,25 @@ __device__ __forceinline__ void hm_sp_emit(const HmAggArgs& a, uint32_t v, bool 
     const uint32_t j = lane & (W - 1);
     const uint64_t segm = W == 64 ? ~0ull : (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
     const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
+    /* the element's row and column offsets in the bucket, de-interleaved
+     * once: a level-l cell's are these >> l (hm_cell_key's layout) */
+    const uint32_t cr = hm_compact7(v >> 1), cc = hm_compact7(v);
+    const uint32_t crow = (uint32_t)(coord >> 32), ccol = (uint32_t)coord;
     for (int l = 0; l < a.lg; l++) {
         if (!((zmask >> l) & 1u)) continue;
         const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
         const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
+        /* the cell's first element: the last head at or below this lane (the
+         * segment's element 0 is one), as a position in the segment */
         const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
-        const uint32_t hl = hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u;
-        const uint32_t start = (uint32_t)__shfl((int)j, (int)hl, 64);
+        const uint32_t start = (hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u) & (uint32_t)(W - 1);
         const uint64_t bal = __ballot(end) & segm;
         if (end) {
-            const uint32_t code = v >> (2 * l);
             const int s = a.lg - l;
-            const uint32_t idx = (hm_compact7(code >> 1) << s) | hm_compact7(code);
+            const uint32_t row = (crow << s) | (cr >> l), col = (ccol << s) | (cc >> l);
             const uint64_t pos = q + hm_mbcnt(bal);
             if (pos < a.out.capacity) {
-                a.out.keys[pos] = hm_cell_key(a.Z - l, coord, s, idx);
+                a.out.keys[pos] = ((uint64_t)(a.Z - l) << 58) | ((uint64_t)row << 29) | col;
                 a.out.counts[pos] = (uint64_t)(j - start + 1);
             }
         }
