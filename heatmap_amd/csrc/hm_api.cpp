@@ -1428,11 +1428,14 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         const int l = L - 1;
         uint32_t* gslots = nullptr;
         ENSURE(B_GSLOTS, (uint64_t)(nslots ? nslots : 1) * HM_AG_CELLS * 4, gslots);
+        uint64_t* sptot;
+        ENSURE(B_TOTAL, 4 * sizeof(uint64_t), sptot);   /* total, base, k_small_pairs' batch counter */
         {
             HmFill zf;
             zf.k = 0;
             if (nslots) hm_fill_add(zf, gslots, 0, (size_t)nslots * HM_AG_CELLS * 4);
             hm_fill_add(zf, totals[l], 0, ((size_t)lv[l].count + 1) * 8);
+            hm_fill_add(zf, sptot + 2, 0, 8);
             hm_launch_fill(s, zf);
         }
         HmAggArgs a;
@@ -1449,16 +1452,16 @@ static int count_impl(hm_ctx* ctx, const double* lat, const double* lon, const i
         a.items = lv[l].items;
         a.nslots = nslots;
         const uint64_t cnt = (uint64_t)lv[l].count + 1;
-        uint64_t *spcnt, *spoff, *sptot, *partial;
+        uint64_t *spcnt, *spoff, *partial;
         ENSURE(B_VALS, cnt * 8, spcnt);
         ENSURE(B_PREFIX, cnt * 8, spoff);
-        ENSURE(B_TOTAL, 4 * sizeof(uint64_t), sptot);
         ENSURE(B_PARTIAL, 4096 * sizeof(uint64_t), partial);
         ENSURE(B_SPCODES, (level_keys + 8) * 2, a.codes);
         a.spcnt = spcnt;
         a.spoff = spoff;
         a.sptotal = sptot;
         a.spbase = (unsigned long long*)(sptot + 1);
+        a.spq = (uint32_t*)(sptot + 2);
         hm_launch_aggregate(s, a, lv[l].items, nslots);
         hm_launch_small(s, a, partial);
         HIPCHK(hipGetLastError());

@@ -3989,128 +3989,287 @@ __device__ __forceinline__ void hm_sp_emit(const HmAggArgs& a, uint32_t v, bool 
     }
 }
 
-__global__ __launch_bounds__(HM_SPW_THREADS) void k_small_pairs(HmAggArgs a)
+/* HM_SPP_STAGE: the same cells staged in the wave's LDS buffer as one u32
+ * each -- bucket lane (6 bits) | level (3) | row (7) | column (7) | count (7)
+ * -- at q (per lane, relative to the buffer), for hm_sp_flush to write out */
+template <int W>
+__device__ __forceinline__ void hm_sp_stage(const HmAggArgs& a, uint32_t v, bool v_ok, uint32_t nk, uint32_t b,
+                                            uint32_t q, uint32_t zmask, uint32_t lane, uint32_t* sb)
 {
-    constexpr int NWB = HM_SPW_THREADS / 64;
-    __shared__ uint16_t cds[NWB][32][64];   /* up to 32 rows of sorted codes */
+    const uint32_t j = lane & (W - 1);
+    const uint64_t segm = W == 64 ? ~0ull : (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
+    const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
+    const uint32_t cr = hm_compact7(v >> 1), cc = hm_compact7(v);
+    const uint32_t bl = b << 24;
+    for (int l = 0; l < a.lg; l++) {
+        if (!((zmask >> l) & 1u)) continue;
+        const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
+        const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
+        const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
+        const uint32_t start = (hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u) & (uint32_t)(W - 1);
+        const uint64_t bal = __ballot(end) & segm;
+        if (end)
+            sb[q + hm_mbcnt(bal)] = bl | ((uint32_t)l << 21) | ((cr >> l) << 14) | ((cc >> l) << 7) | (j - start + 1);
+        q += (uint32_t)__popcll(bal);
+    }
+}
+
+/* n staged cells to keys / counts [g, g + n): every lane two 8-B stores of
+ * consecutive cells, so each 64-B line is written whole by one instruction
+ * (the per-level stores of hm_sp_emit leave lines written in pieces by
+ * several; this layout measured slower than the same stores spread out) */
+__device__ __forceinline__ void hm_sp_flush(const HmAggArgs& a, const uint32_t* sb, uint32_t n, uint64_t g,
+                                            uint64_t cl, uint32_t lane)
+{
+    const uint32_t clo = (uint32_t)cl, chi = (uint32_t)(cl >> 32);
+    for (uint32_t i0 = 0; i0 < n; i0 += 64) {
+        const uint32_t i = i0 + lane;
+        const uint32_t c = sb[i < n ? i : 0u];
+        const int b = (int)((c >> 24) & 63u), l = (int)((c >> 21) & 7u);
+        const uint32_t crow = (uint32_t)__shfl((int)chi, b, 64), ccol = (uint32_t)__shfl((int)clo, b, 64);
+        const int s = a.lg - l;
+        const uint32_t row = (crow << s) | ((c >> 14) & 127u), col = (ccol << s) | ((c >> 7) & 127u);
+        const uint64_t p = g + i;
+        if (i < n && p < a.out.capacity) {
+            a.out.keys[p] = ((uint64_t)(a.Z - l) << 58) | ((uint64_t)row << 29) | col;
+            a.out.counts[p] = (uint64_t)(c & 127u);
+        }
+    }
+}
+
+/* The waves of a block reserve their cells together: one cursor atomic per
+ * block and round (HM_SPP_WAVES waves' sub-batches of <= 32 rows) instead of
+ * one per wave sub-batch (~65K on the skew cloud; a timing build without
+ * them ran 1.6 ms faster: profiles/r6/small_pairs_atomics_ab.jsonl).  Block
+ * batches (HM_SPP_WAVES x spbatch consecutive buckets) come from a counter,
+ * one atomic per block batch.  Rounds are block-synchronous: pass 1 of every
+ * wave, a barrier, the reservation (wave 0), a barrier, pass 2.  (An extra
+ * wave for the atomics, so that they do not queue behind wave 0's cell
+ * stores, measured slower: 9-wave blocks fit 2 to a CU, not 3.) */
+template <int NWB>
+__global__ __launch_bounds__(64 * NWB) void k_small_pairs(HmAggArgs a)
+{
+    __shared__ uint16_t cds[NWB][HM_SPP_ROWS][64];   /* a round's rows of sorted codes per wave */
     __shared__ uint2 gsc[NWB][64];          /* hm_sp_key's run marks */
+#if HM_SPP_STAGE
+    __shared__ uint32_t sbuf[NWB][HM_SPP_STAGE_CELLS];   /* staged cells (hm_sp_stage) */
+#endif
+    __shared__ uint32_t s_wtot[NWB];        /* the round's cells per wave */
+    __shared__ unsigned long long s_base;   /* the round's reservation */
+    __shared__ uint32_t s_batch;            /* the block's next batch */
+    __shared__ uint32_t s_more[2];          /* a wave has rows for the next round (by round parity) */
     const uint32_t lane = hm_lane();
     const uint32_t wl = threadIdx.x >> 6;
-    const uint32_t nw = gridDim.x * NWB;
+    const bool alloc = wl == 0;   /* the wave of the atomics (wave-uniform) */
+    const uint32_t wc = wl;
     const uint32_t zmask = hm_small_zmask(a);
-    const uint32_t wid = blockIdx.x * NWB + wl;
-    const uint32_t step = HmSmallMap<0>::step(nw, a.spbatch);
-    for (uint32_t s0 = HmSmallMap<0>::first(wid, a.spbatch); HmSmallMap<0>::bucket(s0, 0, wid, nw) < a.B.count;
-         s0 += step) {
-        const uint64_t bl64 = HmSmallMap<0>::bucket(s0, lane, wid, nw);
-        const bool in = HmSmallMap<0>::lane_in(lane, a.spbatch) & (bl64 < a.B.count);
+    const uint32_t per_block = NWB * a.spbatch;
+    /* (block barriers are LDS-only: a __syncthreads would also wait for the
+     * waves' cell stores) */
+    if (alloc && lane == 0) {
+        s_batch = atomicAdd(a.spq, 1u);
+        s_more[0] = s_more[1] = 0u;
+    }
+    hm_lds_barrier();
+    uint32_t rr = 0;   /* round parity */
+#if defined(HM_STAMPS) && HM_STAMPS == 7
+    /* cycles summed per block: worker 0's pass 1, first-barrier wait, second-
+     * barrier wait, pass 2; the atomics (wave 0); rounds; block batches */
+    unsigned long long st7[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    unsigned long long t7 = __builtin_amdgcn_s_memtime();
+#define HM_ST7(k) do { const unsigned long long n7 = __builtin_amdgcn_s_memtime(); st7[k] += n7 - t7; t7 = n7; } while (0)
+#else
+#define HM_ST7(k) do { } while (0)
+#endif
+    for (;;) {
+        const uint32_t kb = s_batch;   /* block-uniform */
+        if ((uint64_t)kb * per_block >= a.B.count) break;
+        uint32_t kn = 0;   /* (thread 0) the block's batch after this one */
+        const uint64_t bl64 = (uint64_t)kb * per_block + wc * a.spbatch + lane;
+        const bool in = lane < a.spbatch && bl64 < a.B.count;
         const uint32_t bl = in ? (uint32_t)bl64 : 0u;
         const uint32_t nkl = in ? a.B.nkeys[bl] : 0u;
         const bool small = in & (nkl <= HM_SPW_SPLIT);
         const uint32_t nrl = small ? a.B.nruns[bl] : 0u;
         const bool mine = small && hm_sp_fused_ok(nkl, nrl);
         uint64_t mp = __ballot(mine && nkl <= 32), ms = __ballot(mine && nkl > 32);
-        if (!(mp | ms)) continue;   /* wave-uniform */
         const uint32_t rbl = mine ? a.B.rbase[bl] : 0u;
         const uint64_t cl = mine ? a.B.coord[bl] : 0ull;
         if (mine) a.totals[bl] = nkl;
-        while (mp | ms) {
+        for (bool first = true;; first = false) {
             /* pass 1: up to 32 rows (pairs first) sorted into LDS; lane 2p + g
              * keeps row p's segment-g cell count.  Software-pipelined: while
              * row p sorts, row p+1's key and row p+2's runs are loading */
             uint32_t segcnt = 0;
             uint64_t mp1 = mp, ms1 = ms;
-            const uint32_t nrows = min(32u, (uint32_t)(__popcll(mp) + 1) / 2 + (uint32_t)__popcll(ms));
-            struct Row {
-                bool paired, seg;
-                uint32_t nk, r0, nr;
-            };
-            auto take = [&](bool any) -> Row {
-                Row r;
-                r.paired = !any || mp1 != 0;
-                int src = 0;
-                r.seg = false;
-                if (any && mp1) {
-                    const int sl = hm_pair_lane(mp1);
-                    r.seg = sl >= 0;
-                    src = r.seg ? sl : 0;
-                } else if (any && ms1) {
-                    src = __builtin_ctzll(ms1);
-                    ms1 &= ms1 - 1;
-                    r.seg = true;
+            const uint32_t nrows = min((uint32_t)HM_SPP_ROWS, (uint32_t)(__popcll(mp) + 1) / 2 + (uint32_t)__popcll(ms));
+            if (mp | ms) {   /* wave-uniform */
+                struct Row {
+                    bool paired, seg;
+                    uint32_t nk, r0, nr;
+                };
+                auto take = [&](bool any) -> Row {
+                    Row r;
+                    r.paired = !any || mp1 != 0;
+                    int src = 0;
+                    r.seg = false;
+                    if (any && mp1) {
+                        const int sl = hm_pair_lane(mp1);
+                        r.seg = sl >= 0;
+                        src = r.seg ? sl : 0;
+                    } else if (any && ms1) {
+                        src = __builtin_ctzll(ms1);
+                        ms1 &= ms1 - 1;
+                        r.seg = true;
+                    }
+                    const uint32_t nk0 = __shfl(nkl, src, 64), r00 = __shfl(rbl, src, 64), nr0 = __shfl(nrl, src, 64);
+                    r.nk = r.seg ? nk0 : 0u;
+                    r.r0 = r00;
+                    r.nr = r.seg ? nr0 : 0u;
+                    return r;
+                };
+                auto key_of = [&](const Row& r, uint2 run) {
+                    return r.paired ? hm_sp_key<32>(a, run, r.seg, r.nk, lane, gsc[wc])
+                                    : hm_sp_key<64>(a, run, r.seg, r.nk, lane, gsc[wc]);
+                };
+                const uint32_t jl = lane & 31u;
+                Row A = take(true);
+                uint2 runA = hm_sp_run(a, A.seg, A.r0, A.nr, A.paired ? jl : lane);
+                Row B = take(nrows > 1);
+                uint2 runB = hm_sp_run(a, B.seg, B.r0, B.nr, B.paired ? jl : lane);
+                uint32_t keyA = key_of(A, runA);
+                for (uint32_t p = 0; p < nrows; p++) {
+                    const Row C = take(p + 2 < nrows);
+                    const uint2 runC = hm_sp_run(a, C.seg, C.r0, C.nr, C.paired ? jl : lane);
+                    const uint32_t keyB = key_of(B, runB);
+                    uint32_t v, tot;
+                    if (A.paired) tot = hm_sp_sort<32>(a, keyA, A.nk, lane, zmask, v);
+                    else tot = hm_sp_sort<64>(a, keyA, A.nk, lane, zmask, v);
+                    cds[wc][p][lane] = (uint16_t)v;
+                    /* (a single's segment is the whole wave: lane 32 repeats its total) */
+                    const uint32_t t0 = __builtin_amdgcn_readlane(tot, 0);
+                    const uint32_t t1 = A.paired ? __builtin_amdgcn_readlane(tot, 32) : 0u;
+                    segcnt = lane == 2 * p ? t0 : lane == 2 * p + 1 ? t1 : segcnt;
+                    A = B;
+                    keyA = keyB;
+                    B = C;
+                    runB = runC;
                 }
-                const uint32_t nk0 = __shfl(nkl, src, 64), r00 = __shfl(rbl, src, 64), nr0 = __shfl(nrl, src, 64);
-                r.nk = r.seg ? nk0 : 0u;
-                r.r0 = r00;
-                r.nr = r.seg ? nr0 : 0u;
-                return r;
-            };
-            auto key_of = [&](const Row& r, uint2 run) {
-                return r.paired ? hm_sp_key<32>(a, run, r.seg, r.nk, lane, gsc[wl])
-                                : hm_sp_key<64>(a, run, r.seg, r.nk, lane, gsc[wl]);
-            };
-            const uint32_t jl = lane & 31u;
-            Row A = take(true);
-            uint2 runA = hm_sp_run(a, A.seg, A.r0, A.nr, A.paired ? jl : lane);
-            Row B = take(nrows > 1);
-            uint2 runB = hm_sp_run(a, B.seg, B.r0, B.nr, B.paired ? jl : lane);
-            uint32_t keyA = key_of(A, runA);
-            for (uint32_t p = 0; p < nrows; p++) {
-                const Row C = take(p + 2 < nrows);
-                const uint2 runC = hm_sp_run(a, C.seg, C.r0, C.nr, C.paired ? jl : lane);
-                const uint32_t keyB = key_of(B, runB);
-                uint32_t v, tot;
-                if (A.paired) tot = hm_sp_sort<32>(a, keyA, A.nk, lane, zmask, v);
-                else tot = hm_sp_sort<64>(a, keyA, A.nk, lane, zmask, v);
-                cds[wl][p][lane] = (uint16_t)v;
-                /* (a single's segment is the whole wave: lane 32 repeats its total) */
-                const uint32_t t0 = __builtin_amdgcn_readlane(tot, 0);
-                const uint32_t t1 = A.paired ? __builtin_amdgcn_readlane(tot, 32) : 0u;
-                segcnt = lane == 2 * p ? t0 : lane == 2 * p + 1 ? t1 : segcnt;
-                A = B;
-                keyA = keyB;
-                B = C;
-                runB = runC;
             }
-            const uint32_t np = nrows;
-            /* one reservation for the rows' cells */
+            HM_ST7(0);
             const uint32_t incl = hm_wave_incl_scan(segcnt);
-            const uint32_t btot = __builtin_amdgcn_readlane(incl, 63);
             const uint32_t excl = incl - segcnt;
-            unsigned long long b0 = 0;
-            if (lane == 0 && btot) b0 = atomicAdd(a.out.cursor, (unsigned long long)btot);
-            const uint64_t base = ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(b0 >> 32), 0) << 32) |
-                                  __builtin_amdgcn_readlane((uint32_t)b0, 0);
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (lane == 0) {
+                s_wtot[wl] = __builtin_amdgcn_readlane(incl, 63);
+                if (mp1 | ms1) s_more[rr] = 1u;
+            }
+            hm_lds_barrier();
+            HM_ST7(1);
+            const bool more = s_more[rr] != 0u;
+            /* one reservation for the block's rows (and, in the first round,
+             * the block's next batch, both atomics in flight together) */
+            uint32_t wpre = 0, btotal = 0;
+#pragma unroll
+            for (int w = 0; w < NWB; w++) {
+                const uint32_t t = s_wtot[w];
+                wpre += (uint32_t)w < wl ? t : 0u;
+                btotal += t;
+            }
+            if (alloc && lane == 0) {
+                s_more[rr ^ 1u] = 0u;   /* (last read before the previous round's second barrier) */
+                if (first) kn = atomicAdd(a.spq, 1u);
+                s_base = btotal ? atomicAdd(a.out.cursor, (unsigned long long)btotal) : 0ull;
+            }
+            HM_ST7(4);
+            hm_lds_barrier();
+            HM_ST7(2);
+            const uint64_t base = s_base + wpre;
             /* pass 2: the same rows in the same order, codes from LDS */
             uint64_t mp2 = mp, ms2 = ms;
-            for (uint32_t p = 0; p < np; p++) {
-                const uint32_t v = cds[wl][p][lane];
+#if HM_SPP_STAGE
+            /* the cells go through the wave's LDS buffer (rows in order: the
+             * wave's cells are written in order), flushed before a row that
+             * does not fit and at the end */
+            uint32_t* sb = sbuf[wc];
+            uint32_t flushed = 0;   /* this round's cells written so far */
+            const auto sync_sb = [&]() {
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            };
+#endif
+            for (uint32_t p = 0; p < ((mp | ms) ? nrows : 0u); p++) {
+                const uint32_t v = cds[wc][p][lane];
+#if HM_SPP_STAGE
+                const uint32_t rlo = __shfl(excl, (int)(2 * p), 64), rhi = __shfl(incl, (int)(2 * p + 1), 64);
+                if (rhi - flushed > HM_SPP_STAGE_CELLS) {
+                    sync_sb();
+                    hm_sp_flush(a, sb, rlo - flushed, base + flushed, cl, lane);
+                    sync_sb();
+                    flushed = rlo;
+                }
+#endif
                 if (mp2) {
                     const int sl = hm_pair_lane(mp2);
                     const bool seg = sl >= 0;
                     const int sr = seg ? sl : 0;
                     const uint32_t nk0 = __shfl(nkl, sr, 64);
                     const uint32_t nk = seg ? nk0 : 0u;
+#if HM_SPP_STAGE
+                    const uint32_t q = __shfl(excl, (int)(2 * p + (lane >> 5)), 64) - flushed;
+                    hm_sp_stage<32>(a, v == 0xFFFFu ? 0xFFFFFFFFu : v, seg && (lane & 31u) < nk, nk, (uint32_t)sr, q, zmask,
+                                    lane, sb);
+#else
                     const uint64_t coord = __shfl(cl, sr, 64);
                     const uint64_t q = base + __shfl(excl, (int)(2 * p + (lane >> 5)), 64);
                     hm_sp_emit<32>(a, v == 0xFFFFu ? 0xFFFFFFFFu : v, seg && (lane & 31u) < nk, nk, coord, q, zmask, lane);
+#endif
                 } else {
                     const int i = __builtin_ctzll(ms2);
                     ms2 &= ms2 - 1;
                     const uint32_t nk = __shfl(nkl, i, 64);
+#if HM_SPP_STAGE
+                    const uint32_t q = __shfl(excl, (int)(2 * p), 64) - flushed;
+                    hm_sp_stage<64>(a, v == 0xFFFFu ? 0xFFFFFFFFu : v, lane < nk, nk, (uint32_t)i, q, zmask, lane, sb);
+#else
                     const uint64_t coord = __shfl(cl, i, 64);
                     const uint64_t q = base + __shfl(excl, (int)(2 * p), 64);
                     hm_sp_emit<64>(a, v == 0xFFFFu ? 0xFFFFFFFFu : v, lane < nk, nk, coord, q, zmask, lane);
+#endif
                 }
             }
+#if HM_SPP_STAGE
+            {
+                const uint32_t wt = __builtin_amdgcn_readlane(incl, 63);
+                sync_sb();
+                hm_sp_flush(a, sb, wt - flushed, base + flushed, cl, lane);
+                sync_sb();
+            }
+#endif
             mp = mp1;
             ms = ms1;
-            __builtin_amdgcn_wave_barrier();   /* cds is free for the next rows */
+            rr ^= 1u;
+            HM_ST7(3);
+#if defined(HM_STAMPS) && HM_STAMPS == 7
+            st7[6]++;
+#endif
+            /* every wave has read s_base and s_wtot before it reaches the next
+             * round's first barrier, and writes them again only after it */
+            __builtin_amdgcn_wave_barrier();   /* cds is free for the next round */
+            if (!more) break;
         }
+        if (alloc && lane == 0) s_batch = kn;   /* (read at this batch's start, before its first round's barriers) */
+        hm_lds_barrier();
+#if defined(HM_STAMPS) && HM_STAMPS == 7
+        st7[7]++;
+#endif
     }
+#if defined(HM_STAMPS) && HM_STAMPS == 7
+    /* wave 0 (which also makes the atomics) in row b, wave 1 in row 4096 + b */
+    if (lane == 0 && wl < 2 && blockIdx.x < 4096)
+        for (int q = 0; q < 8; q++) g_stamps[(blockIdx.x + wl * 4096u) * 12 + q] = st7[q];
+#endif
+#undef HM_ST7
 }
 
 /* one reservation for every small bucket's cells */
@@ -4893,6 +5052,29 @@ void hm_launch_aggregate(hipStream_t s, const HmAggArgs& a, uint32_t items, uint
     if (items) hipLaunchKernelGGL(k_aggregate, hm_grid2(items), dim3(HM_AG_THREADS), 0, s, a);
     if (nslots) hipLaunchKernelGGL(k_aggregate_merged, hm_grid2(nslots), dim3(HM_AG_THREADS), 0, s, a);
 }
+/* HM_SPW_GRID blocks is 8 waves per SIMD, more than is resident of the
+ * kernels holding > 96 SGPRs or > 64 VGPRs (k_small_pairs 7, k_small_sort 5,
+ * k_small_emit 4).  HM_SPW_RESIDENT=1 launches only the blocks that fit at
+ * once; measured slower (profiles/r6/small_grid_ab.jsonl: hotspot aggregation
+ * +50 us, z6-21 +150 us, skew no better): k_small_sort / k_small_emit map
+ * buckets to waves statically, and the blocks of the second round that start
+ * as the first ones drain even out their uneven shares. */
+template <typename K>
+static uint32_t hm_spw_grid(K kernel, int& cache, uint32_t wb)
+{
+    uint32_t g = HM_SPW_GRID;
+    if (HM_SPW_RESIDENT) {
+        if (cache <= 0) {
+            int per = 0;
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kernel, HM_SPW_THREADS, 0) != hipSuccess || per <= 0)
+                per = HM_SPW_GRID / 256;
+            cache = per;
+        }
+        g = (uint32_t)cache * hm_cu_count();
+    }
+    return wb < g ? wb : g;
+}
+
 void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
 {
     if (!a.B.count) return;
@@ -4905,16 +5087,28 @@ void hm_launch_small(hipStream_t s, const HmAggArgs& a, uint64_t* partial)
     while (b.spbatch < 64 && (uint64_t)b.spbatch * waves < a.B.count) b.spbatch <<= 1;
     const uint32_t per_block = b.spbatch * (HM_SPW_THREADS / 64);
     const uint32_t wb = (a.B.count + per_block - 1) / per_block;
-    const dim3 g(wb < HM_SPW_GRID ? wb : HM_SPW_GRID);
-    if (HM_SP_FUSED) hipLaunchKernelGGL(k_small_pairs, g, dim3(HM_SPW_THREADS), 0, s, b);
-    hipLaunchKernelGGL((k_small_sort<0, HM_SPW_SPLIT>), g, dim3(HM_SPW_THREADS), 0, s, b);
+    static int occ[5];
+    const dim3 t(HM_SPW_THREADS);
+    if (HM_SP_FUSED) {
+        /* block batches from a counter: a grid of what fits, plus spare blocks
+         * that find the counter spent */
+        const uint32_t bb = b.spbatch * HM_SPP_WAVES;
+        const uint32_t nbb = (a.B.count + bb - 1) / bb;
+        const uint32_t gp = HM_SPW_GRID * (HM_SPW_THREADS / 64) / HM_SPP_WAVES;
+        hipLaunchKernelGGL(k_small_pairs<HM_SPP_WAVES>, dim3(nbb < gp ? nbb : gp), dim3(64 * HM_SPP_WAVES), 0, s, b);
+    }
+    hipLaunchKernelGGL((k_small_sort<0, HM_SPW_SPLIT>), dim3(hm_spw_grid(k_small_sort<0, HM_SPW_SPLIT>, occ[1], wb)), t,
+                       0, s, b);
     if (HM_SPW_MAX > HM_SPW_SPLIT)
-        hipLaunchKernelGGL((k_small_sort<HM_SPW_SPLIT, HM_SPW_MAX>), g, dim3(HM_SPW_THREADS), 0, s, b);
+        hipLaunchKernelGGL((k_small_sort<HM_SPW_SPLIT, HM_SPW_MAX>),
+                           dim3(hm_spw_grid(k_small_sort<HM_SPW_SPLIT, HM_SPW_MAX>, occ[2], wb)), t, 0, s, b);
     hm_launch_scan(s, b.spcnt, b.B.count, partial, (uint64_t*)b.spoff, b.sptotal);
     hipLaunchKernelGGL(k_small_reserve, dim3(1), dim3(64), 0, s, b);
-    hipLaunchKernelGGL((k_small_emit<0, HM_SPW_SPLIT>), g, dim3(HM_SPW_THREADS), 0, s, b);
+    hipLaunchKernelGGL((k_small_emit<0, HM_SPW_SPLIT>), dim3(hm_spw_grid(k_small_emit<0, HM_SPW_SPLIT>, occ[3], wb)), t,
+                       0, s, b);
     if (HM_SPW_MAX > HM_SPW_SPLIT)
-        hipLaunchKernelGGL((k_small_emit<HM_SPW_SPLIT, HM_SPW_MAX>), g, dim3(HM_SPW_THREADS), 0, s, b);
+        hipLaunchKernelGGL((k_small_emit<HM_SPW_SPLIT, HM_SPW_MAX>),
+                           dim3(hm_spw_grid(k_small_emit<HM_SPW_SPLIT, HM_SPW_MAX>, occ[4], wb)), t, 0, s, b);
 }
 void hm_launch_pool(hipStream_t s, const HmPoolArgs& a, uint32_t nparents)
 {

@@ -129,6 +129,20 @@ static_assert(HM_SPW_MAX >= HM_SP_MAX, "every bucket without a dense work item n
 #endif
 #define HM_SPW_THREADS 256
 #define HM_SPW_GRID (256 * 8)
+#ifndef HM_SPP_WAVES
+#define HM_SPP_WAVES 4      /* k_small_pairs: waves per block (one cursor reservation per block and round) */
+#endif
+#ifndef HM_SPP_STAGE
+#define HM_SPP_STAGE 1      /* k_small_pairs: cells staged in LDS, written a whole line per instruction */
+#endif
+#ifndef HM_SPP_ROWS
+#define HM_SPP_ROWS 32      /* k_small_pairs: rows (wave passes) per wave and round, <= 32 */
+#endif
+static_assert(HM_SPP_ROWS <= 32, "a row's two cell counts sit in lanes 2p, 2p + 1");
+#define HM_SPP_STAGE_CELLS 512   /* >= a row's cells: 2 segments x 32 keys x 7 levels */
+#ifndef HM_SPW_RESIDENT
+#define HM_SPW_RESIDENT 0   /* 1: small-bucket grids of the blocks resident at once (hm_spw_grid; slower) */
+#endif
 #define HM_POOL_THREADS 256
 #define HM_MAX_LEVELS 4
 #define HM_COUNT_MAX_ZOOM 21                /* level-1 keys 2*(Z-5) bits fit u32 */
@@ -397,6 +411,7 @@ struct HmAggArgs {
     uint64_t* sptotal;
     unsigned long long* spbase; /* output position of the small buckets' region */
     uint32_t spbatch;           /* consecutive buckets per wave step (power of 2, <= 64) */
+    uint32_t* spq;              /* k_small_pairs' block-batch counter (zero at launch) */
     unsigned long long* totals;
     uint32_t* gslots;           /* [nslots][HM_AG_CELLS]: a multi-item bucket's summed histogram */
     const uint32_t* slot_bucket;

@@ -33,12 +33,14 @@ NAMES = {
     "stamps6": [],
     "stamps6w8": [],
     "stamps6w10": [],
+    "stamps7": [],
+    "stamps7noatom": [],
 }[VAR]
 K = len(NAMES)
-n = int(float(os.environ.get("HM_POINTS", "2.5e8" if not VAR.startswith("stamps6") else "1e9")))
+n = int(float(os.environ.get("HM_POINTS", "2.5e8" if not VAR.startswith(("stamps6", "stamps7")) else "1e9")))
 lat = torch.empty(n, dtype=torch.float64, device="cuda")
 lon = torch.empty(n, dtype=torch.float64, device="cuda")
-device.synth("hotspots", lat, lon)
+device.synth(os.environ.get("HM_KIND", "skew" if VAR.startswith("stamps7") else "hotspots"), lat, lon)
 bufs = device.CountBuffers(64 << 20)
 device.count_device(lat, lon, None, 0, int(os.environ.get("HM_ZMAX", "18")), 0, buffers=bufs)
 torch.cuda.synchronize()
@@ -47,6 +49,18 @@ L.hm_debug_stamps.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 st = np.zeros(65536 * 12, np.uint64)
 assert L.hm_debug_stamps(st.ctypes.data, st.nbytes) == 0
 st = st.reshape(-1, 12).astype(np.int64)
+if VAR.startswith("stamps7"):
+    # k_small_pairs: per block, wave 0's (it also makes the atomics) and wave 1's phase cycles summed over its rounds
+    w, al = st[:4096, :8], st[4096:8192, :8]
+    ok = w[:, 6] > 0
+    r = w[ok, 6:7].astype(float)
+    print("stamps7 blocks %d rounds/block %.2f batches/block %.2f" % (ok.sum(), r.mean(), w[ok, 7].mean()))
+    for i, nm in enumerate(["W0 pass 1", "W0 barrier A wait", "W0 atomics", "W0 barrier B wait", "W0 pass 2"]):
+        i = [0, 1, 4, 2, 3][i]
+        print("%-24s per round mean %8.0f  median %8.0f" % (nm, (w[ok, i] / r[:, 0]).mean(), np.median(w[ok, i] / r[:, 0])))
+    for i, nm in [(0, "W1 pass 1"), (1, "W1 barrier A wait"), (2, "W1 barrier B wait"), (3, "W1 pass 2")]:
+        print("%-24s per round mean %8.0f  median %8.0f" % (nm, (al[ok, i] / r[:, 0]).mean(), np.median(al[ok, i] / r[:, 0])))
+    sys.exit(0)
 if VAR.startswith("stamps6"):
     # k_l1_ws: per block, phase cycles summed over its tiles; slot 11 = its tiles;
     # the writer waves' phases in the rows 4096 + block

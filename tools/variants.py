@@ -22,12 +22,17 @@ VARIANTS = {
     "nows": ["HM_L1_WS=0"],                  # level 1 through k_l1_fast only (the shipped default)
     "wslate": ["HM_WS_PREFETCH_LATE=1"],     # k_l1_ws: next tile's loads after the count
     "spunfused": ["HM_SP_FUSED=0"],          # <= 32-key buckets through k_small_sort / scan / k_small_emit (round 5)
+    "spres": ["HM_SPW_RESIDENT=1"],          # k_small_sort / k_small_emit on grids of their resident blocks
+    "spp8": ["HM_SPP_WAVES=8"],              # k_small_pairs: 8-wave blocks
+    "sprows16": ["HM_SPP_ROWS=16"],          # k_small_pairs: 16 rows a round (7 blocks per CU with staging)
+    "spnostage": ["HM_SPP_STAGE=0"],         # k_small_pairs: per-level cell stores (no LDS staging)
     "ws": ["HM_L1_WS=1"],                    # k_l1_ws (12 compute + 4 writer waves)
     "ws8": ["HM_L1_WS=1", "HM_WS_C=512"],                  # k_l1_ws: 8 compute + 8 writer waves, 8192-point tiles
     "ws10": ["HM_L1_WS=1", "HM_WS_C=640"],                 # k_l1_ws: 10 compute + 6 writer waves, 10240-point tiles
     "ws12": ["HM_L1_WS=1", "HM_WS_C=768"],                 # k_l1_ws: 12 compute + 4 writer waves, 12288-point tiles
     "stamps6w8": ["HM_STAMPS=6", "HM_L1_WS=1", "HM_WS_C=512"],
     "stamps6w10": ["HM_STAMPS=6", "HM_L1_WS=1", "HM_WS_C=640"],
+    "stamps7": ["HM_STAMPS=7"],              # k_small_pairs: per-round phase cycles (worker 0 and the allocator)
     "stamps": ["HM_STAMPS=1"],               # phase stamps for tools/stamps.py (k_partition)
     "stamps1": ["HM_STAMPS=2"],              # k_project_partition
     "stamps2": ["HM_STAMPS=3"],              # k_partition_fr
@@ -129,6 +134,17 @@ PATCHES["l1nostore"] = [
      "        if (hk == 0xFFFFFFFFu && e.y == 0x1234567u) *(uint16_t*)houtb = (uint16_t)hk;")]
 PATCHES["l1noatom"] = [("hm_kernels.hip", "        if (cnt[q]) gpos[q] = atomicAdd(&a.fill[hm_l1i(d, sh)], cnt[q]);",
                         "        if (cnt[q]) gpos[q] = 0;")]
+# k_small_pairs timing builds: no cursor atomic (a made-up base), no cell
+# stores, no emit pass at all (profiles/r6/small_pairs_atomics_ab.jsonl has
+# the round-6 per-wave-reservation results, incl. sharded and non-returning
+# cursor atomics)
+PATCHES["spnoatom"] = [("hm_kernels.hip", "s_base = btotal ? atomicAdd(a.out.cursor, (unsigned long long)btotal) : 0ull;",
+                        "s_base = (unsigned long long)(kb & 0xFFFFFu) * 96u * HM_SPP_WAVES * 64u;")]
+PATCHES["stamps7noatom"] = PATCHES["spnoatom"]
+PATCH_DEFINES["stamps7noatom"] = ["HM_STAMPS=7"]
+PATCHES["spnostore"] = [("hm_kernels.hip", """            const uint64_t pos = q + hm_mbcnt(bal);
+            if (pos < a.out.capacity) {""", """            const uint64_t pos = q + hm_mbcnt(bal);
+            if (pos == 0x123456789ull) {""")]
 # levels 2.. always on the spread plan (3 zooms per level) when no tile is hot
 PATCHES["spreadall"] = [("hm_api.cpp", "spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, true);",
                          "spread_replan(ctx->host_aux, F, (double)n, zb, zs, &L, ctx->spread_min_keys, false);")]
@@ -216,7 +232,14 @@ def build(names):
 
     for n in names:
         out = os.path.join(VDIR, "lib_%s.so" % n)
-        if n in PATCHES:
+        if n.startswith("git-"):
+            # the sources of a commit ("git-<rev>"): an A/B against a committed state
+            tmp = tempfile.mkdtemp()
+            subprocess.run("git -C %s archive %s heatmap_amd/csrc include | tar -x -C %s" % (REPO, n[4:], tmp),
+                           shell=True, check=True)
+            b.build(force=True, verbose=False, out=out, csrc=os.path.join(tmp, "heatmap_amd", "csrc"))
+            shutil.rmtree(tmp)
+        elif n in PATCHES:
             tmp = tempfile.mkdtemp()
             src = os.path.join(tmp, "pkg", "csrc")       # keeps "../../include/" valid
             shutil.copytree(b.CSRC, src)
@@ -233,7 +256,7 @@ def build(names):
         print("built", out, flush=True)
 
 
-def one(name, points, steps, zmax):
+def one(name, points, steps, zmax, zmin=0):
     if name != "main":     # "main": the in-tree library heatmap_amd/_lib/libheatmap_amd.so
         os.environ["HM_LIB_PATH"] = os.path.join(VDIR, "lib_%s.so" % name)
     import numpy as np
@@ -246,12 +269,12 @@ def one(name, points, steps, zmax):
     device.synth(os.environ.get("HM_KIND", "hotspots"), lat, lon)
     bufs = device.CountBuffers(64 << 20)
     ctx = device.context(0)
-    m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
+    m, bufs = device.count_device(lat, lon, None, zmin, zmax, 0, buffers=bufs)
     torch.cuda.synchronize()
     st = []
     t0 = time.perf_counter()
     for _ in range(steps):
-        m, bufs = device.count_device(lat, lon, None, 0, zmax, 0, buffers=bufs)
+        m, bufs = device.count_device(lat, lon, None, zmin, zmax, 0, buffers=bufs)
         ls = ctx.last_stats()[1]
         st.append(list(ls[:4]) + [ls[6], ls[5]])   # stage times, hot tiles, level-1 re-runs
     torch.cuda.synchronize()
@@ -259,16 +282,16 @@ def one(name, points, steps, zmax):
     tot = int(bufs.counts[:m].sum().item())
     # cell-for-cell parity when the golden digest of this cloud exists
     kind = os.environ.get("HM_KIND", "hotspots")
-    gname = "%s_%de%d_z0-%d" % (kind, int(str("%e" % points)[0]), len(str(points)) - 1, zmax)
+    gname = "%s_%de%d_z%d-%d" % (kind, int(str("%e" % points)[0]), len(str(points)) - 1, zmin, zmax)
     gd = json.load(open(os.path.join(REPO, "tests", "golden", "big_digests.json"))).get(gname)
     digest = None
-    if gd is not None and gd["n"] == points and gd["zmin"] == 0:
+    if gd is not None and gd["n"] == points and gd["zmin"] == zmin:
         sys.path.insert(0, os.path.join(REPO, "tests"))
         from digest import device_digest
 
         digest = device_digest(torch, bufs.keys[:m], bufs.counts[:m]) == gd["digest"]
     print(json.dumps({"variant": name, "ms": dt * 1e3, "gpts": points / dt / 1e9, "cells": m,
-                      "check": tot == points * (zmax + 1), "digest_ok": digest, "kind": kind,
+                      "check": tot == points * (zmax - zmin + 1), "digest_ok": digest, "kind": kind,
                       "stage_us": [round(x, 1) for x in np.mean(np.array(st), axis=0)]}), flush=True)
 
 
@@ -332,7 +355,7 @@ def main():
         merge_one(names[0], int(float(os.environ.get("HM_POINTS", "1.25e9"))), int(os.environ.get("HM_STEPS", "5")))
     elif cmd == "one":
         one(names[0], int(float(os.environ.get("HM_POINTS", "1e9"))), int(os.environ.get("HM_STEPS", "3")),
-            int(os.environ.get("HM_ZMAX", "18")))
+            int(os.environ.get("HM_ZMAX", "18")), int(os.environ.get("HM_ZMIN", "0")))
 
 
 if __name__ == "__main__":
