@@ -3998,18 +3998,24 @@ __device__ __forceinline__ void hm_sp_stage(const HmAggArgs& a, uint32_t v, bool
 {
     const uint32_t j = lane & (W - 1);
     const uint64_t segm = W == 64 ? ~0ull : (lane >> 5) ? 0xFFFFFFFF00000000ull : 0x00000000FFFFFFFFull;
-    const uint32_t nx = __shfl_down(v, 1, 64), pv = __shfl_up(v, 1, 64);
+    const uint32_t nx = __shfl_down(v, 1, 64);
     const uint32_t cr = hm_compact7(v >> 1), cc = hm_compact7(v);
     const uint32_t bl = b << 24;
+    /* the element ends its level-l cell for the levels below half the bit
+     * length of (its code ^ the next one's), every level if it is the last;
+     * a cell starts after the previous end in the segment: one ballot a level */
+    const uint32_t hl = !v_ok ? 0u : (j + 1 == nk) ? 32u : (33u - (uint32_t)__clz((int)(v ^ nx))) >> 1;
+    const uint64_t below = segm & ((1ull << lane) - 1ull);
+    const uint32_t s0 = lane & ~(uint32_t)(W - 1);   /* the segment's first lane */
     for (int l = 0; l < a.lg; l++) {
         if (!((zmask >> l) & 1u)) continue;
-        const bool head = v_ok && ((j == 0) | ((pv >> (2 * l)) != (v >> (2 * l))));
-        const bool end = v_ok && ((j + 1 == nk) | ((nx >> (2 * l)) != (v >> (2 * l))));
-        const uint64_t hm = __ballot(head) & ((2ull << lane) - 1ull);
-        const uint32_t start = (hm ? 63u - (uint32_t)__clzll((long long)hm) : 0u) & (uint32_t)(W - 1);
+        const bool end = (uint32_t)l < hl;
         const uint64_t bal = __ballot(end) & segm;
-        if (end)
-            sb[q + hm_mbcnt(bal)] = bl | ((uint32_t)l << 21) | ((cr >> l) << 14) | ((cc >> l) << 7) | (j - start + 1);
+        if (end) {
+            const uint64_t pe = bal & below;
+            const uint32_t start = pe ? 64u - (uint32_t)__clzll((long long)pe) : s0;
+            sb[q + (uint32_t)__popcll(pe)] = bl | ((uint32_t)l << 21) | ((cr >> l) << 14) | ((cc >> l) << 7) | (lane - start + 1);
+        }
         q += (uint32_t)__popcll(bal);
     }
 }
@@ -4017,7 +4023,8 @@ __device__ __forceinline__ void hm_sp_stage(const HmAggArgs& a, uint32_t v, bool
 /* n staged cells to keys / counts [g, g + n): every lane two 8-B stores of
  * consecutive cells, so each 64-B line is written whole by one instruction
  * (the per-level stores of hm_sp_emit leave lines written in pieces by
- * several; this layout measured slower than the same stores spread out) */
+ * several instructions; skew aggregation 3.88-3.92 -> 3.53-3.77 ms,
+ * profiles/r6/small_pairs_block_res_ab.jsonl) */
 __device__ __forceinline__ void hm_sp_flush(const HmAggArgs& a, const uint32_t* sb, uint32_t n, uint64_t g,
                                             uint64_t cl, uint32_t lane)
 {
@@ -4039,8 +4046,11 @@ __device__ __forceinline__ void hm_sp_flush(const HmAggArgs& a, const uint32_t* 
 
 /* The waves of a block reserve their cells together: one cursor atomic per
  * block and round (HM_SPP_WAVES waves' sub-batches of <= 32 rows) instead of
- * one per wave sub-batch (~65K on the skew cloud; a timing build without
- * them ran 1.6 ms faster: profiles/r6/small_pairs_atomics_ab.jsonl).  Block
+ * one per wave sub-batch (~65K on the skew cloud, on ONE word; skew
+ * aggregation -0.3 ms.  The "no atomic" timing builds of
+ * profiles/r6/small_pairs_atomics_ab.jsonl overstate the atomics' cost: their
+ * made-up positions overlapped, and WRITE_SIZE showed them writing 0.57 of
+ * the 6.1 GB of cells, profiles/r6/small_pairs_pmc_bytes.txt).  Block
  * batches (HM_SPP_WAVES x spbatch consecutive buckets) come from a counter,
  * one atomic per block batch.  Rounds are block-synchronous: pass 1 of every
  * wave, a barrier, the reservation (wave 0), a barrier, pass 2.  (An extra

@@ -9,7 +9,7 @@ mkdir -p "$O"
 cd /tmp
 for v in main spnoatom; do
   for c in FETCH_SIZE WRITE_SIZE; do
-    HM_KIND=skew HM_STEPS=1 timeout -k 10 120 rocprofv3 --pmc $c -d "$O/${v}_$c" -o run -- python3 "$R/tools/variants.py" one $v > "$O/${v}_$c.log" 2>&1 || { tail -20 "$O/${v}_$c.log"; exit 1; }
+    HM_KIND=skew HM_STEPS=1 timeout -k 10 120 rocprofv3 --kernel-trace --pmc $c -f csv -d "$O/${v}_$c" -o run -- python3 "$R/tools/variants.py" one $v > "$O/${v}_$c.log" 2>&1 || { tail -20 "$O/${v}_$c.log"; exit 1; }
   done
 done
 python3 - "$O" <<'PY'

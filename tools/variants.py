@@ -142,6 +142,10 @@ PATCHES["spnoatom"] = [("hm_kernels.hip", "s_base = btotal ? atomicAdd(a.out.cur
                         "s_base = (unsigned long long)(kb & 0xFFFFFu) * 96u * HM_SPP_WAVES * 64u;")]
 PATCHES["stamps7noatom"] = PATCHES["spnoatom"]
 PATCH_DEFINES["stamps7noatom"] = ["HM_STAMPS=7"]
+# k_small_pairs held to 8 waves per SIMD (<= 96 SGPRs), with 16 rows a round (LDS for 8 blocks)
+PATCHES["sp8w16"] = [("hm_kernels.hip", "__global__ __launch_bounds__(64 * NWB) void k_small_pairs(HmAggArgs a)",
+                      "__global__ __launch_bounds__(64 * NWB) __attribute__((amdgpu_waves_per_eu(8, 8))) void k_small_pairs(HmAggArgs a)")]
+PATCH_DEFINES["sp8w16"] = ["HM_SPP_ROWS=16"]
 PATCHES["spnostore"] = [("hm_kernels.hip", """            const uint64_t pos = q + hm_mbcnt(bal);
             if (pos < a.out.capacity) {""", """            const uint64_t pos = q + hm_mbcnt(bal);
             if (pos == 0x123456789ull) {""")]
