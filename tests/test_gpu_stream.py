@@ -320,3 +320,35 @@ def test_stream_forced_plan_on_concurrent_buckets(gpu, knobs):
             for h in range(BASE + 4 * nh, BASE + 5 * nh):
                 _same(s.counts(h), oracle.count(lat, lon, keep & (hour == h).astype(np.uint8), 0, 18))
         s.close()
+
+
+def test_stream_device_views_ragged(gpu):
+    """A ragged batch (n = 4k + 3 points) passed as host arrays and as device
+    views one element in (no array 16-B aligned) gives the oracle's counts,
+    hours and groups.  (A k_stream_buckets with 16-B loads and this fallback
+    measured no faster: profiles/r6/stream_bucket_vec_ab.txt.)"""
+    import torch
+
+    n = 40003
+    lat, lon = synth.generate("skew", n + 1, seed=11)
+    rng = np.random.default_rng(11)
+    keep = (rng.random(n + 1) > 0.1).astype(np.uint8)
+    hour = (BASE + rng.integers(0, 3, n + 1)).astype(np.uint32)
+    gid = rng.integers(0, 5, n + 1).astype(np.uint32)
+    for off in (0, 1):
+        s = StreamingHeatmap(0, 16, base_hour=BASE)
+        sl = slice(off, off + n)
+        if off:
+            dev = lambda x, dt: torch.from_numpy(np.ascontiguousarray(x)).to("cuda")[sl]   # noqa: E731
+            s.add(dev(lat, None), dev(lon, None), dev(keep, None), dev(hour.view(np.int32), None),
+                  group=dev(gid.view(np.int32), None))
+        else:
+            s.add(lat[sl], lon[sl], keep[sl], hour[sl], group=gid[sl])
+        k, h, g = keep[sl], hour[sl], gid[sl]
+        _same(s.counts(), oracle.count(lat[sl], lon[sl], k, 0, 16))
+        for hh, c in s.hourly().items():
+            _same(c, oracle.count(lat[sl], lon[sl], k & (h == hh).astype(np.uint8), 0, 16))
+        gg, _, z, r, c, cnt = s.rollup("alltime", merge_groups=False)
+        m = gg == 3
+        _same(Counts(z[m], r[m], c[m], cnt[m], 0, []), oracle.count(lat[sl], lon[sl], k & (g == 3).astype(np.uint8), 0, 16))
+        s.close()
