@@ -8,7 +8,7 @@ for bench.py.
 
 The SQ_INSTS_* counters count wave instructions: x64 gives lane operations
 (an upper bound where a wave runs with lanes masked off).  One step = one
-mode-0 full-tile k_project_partition launch, as in tools/pmc_traffic.py.
+level-1 whole-tile launch (k_l1_fast), as in tools/pmc_traffic.py.
 """
 import csv
 import glob
@@ -31,8 +31,12 @@ def main():
         k = r["Kernel_Name"].split("(")[0]
         per[k][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[k].add(r.get("Dispatch_Id", r.get("Correlation_Id")))
-    steps = sum(len(v) for k, v in disp.items()
-                if k.startswith("void k_project_partition<") and (k.endswith(", 0>") or k.endswith(", 0, true>")))
+    # one step = one level-1 launch over whole tiles: k_l1_fast (round 4 on),
+    # or the mode-0 k_project_partition of older builds
+    steps = sum(len(v) for k, v in disp.items() if k.startswith("void k_l1_fast<"))
+    if not steps:
+        steps = sum(len(v) for k, v in disp.items()
+                    if k.startswith("void k_project_partition<") and (k.endswith(", 0>") or k.endswith(", 0, true>")))
     steps = max(steps, 1)
     tot = defaultdict(float)
     k1 = defaultdict(float)
@@ -41,7 +45,7 @@ def main():
             continue
         for c in C:
             tot[c] += v.get(c, 0.0)
-            if k.startswith("void k_project_partition<"):
+            if k.startswith(("void k_l1_fast<", "void k_project_partition<", "void k_l1_ws<")):
                 k1[c] += v.get(c, 0.0)
     ops = lambda t: 64.0 * (t["SQ_INSTS_VALU_ADD_F64"] + t["SQ_INSTS_VALU_MUL_F64"] + t["SQ_INSTS_VALU_FMA_F64"] +
                             t["SQ_INSTS_VALU_TRANS_F64"]) / steps / pts   # noqa: E731
