@@ -3143,8 +3143,11 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
  * registers straight off the padded rows (hm_reg_pyramid7), below that from
  * the squeezed histogram; an item of a multi-item bucket adds its squeezed
  * histogram into the bucket's slot and k_aggregate_merged emits it. */
-#define HM_AG_ROW(lg) ((1u << (lg)) + 8u)
-#define HM_AG_PADDED (128u * (128u + 8u))
+#ifndef HM_AG_PADW
+#define HM_AG_PADW 8u   /* pad words per histogram row (a multiple of 4: hm_reg_pyramid7 reads 16-B vectors) */
+#endif
+#define HM_AG_ROW(lg) ((1u << (lg)) + HM_AG_PADW)
+#define HM_AG_PADDED (128u * (128u + HM_AG_PADW))
 static_assert(HM_AG_LG == 7 && HM_AG_CELLS == 128 * 128, "padded histogram");
 
 /* The lg = 7 bucket pyramid from registers (k_aggregate's single-item
@@ -3284,7 +3287,7 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
         uint32_t* grid;
         uint32_t dummy;
         int lg;
-        __device__ __forceinline__ uint32_t sl(uint32_t k) { return k + ((k >> lg) << 3); }   /* padded row */
+        __device__ __forceinline__ uint32_t sl(uint32_t k) { return k + (k >> lg) * HM_AG_PADW; }   /* padded row */
         __device__ __forceinline__ void cnt(uint32_t k, bool v)
         {
             if (HM_AG_FAST)
@@ -3345,7 +3348,7 @@ __global__ __launch_bounds__(HM_AG_THREADS, 8) void k_aggregate(HmAggArgs a)
 #pragma unroll
     for (int k = 0; k < CPT; k++) {
         const uint32_t i = k * HM_AG_THREADS + tid;
-        x[k] = i < ncell ? grid[i + ((i >> a.lg) << 3)] : 0u;
+        x[k] = i < ncell ? grid[i + (i >> a.lg) * HM_AG_PADW] : 0u;
     }
     if (it.nitems > 1) {
         /* added into the bucket's slot (coalesced: consecutive threads,
