@@ -3148,6 +3148,9 @@ __device__ uint64_t hm_bucket_pyramid(uint32_t* v, int lg, int z_top, uint64_t p
 #endif
 #define HM_AG_ROW(lg) ((1u << (lg)) + HM_AG_PADW)
 #define HM_AG_PADDED (128u * (128u + HM_AG_PADW))
+#ifndef HM_AG_STAGE
+#define HM_AG_STAGE 1   /* hm_reg_pyramid7: cells staged in the dead histogram, written a whole line per store */
+#endif
 static_assert(HM_AG_LG == 7 && HM_AG_CELLS == 128 * 128, "padded histogram");
 
 /* The lg = 7 bucket pyramid from registers (k_aggregate's single-item
@@ -3162,7 +3165,7 @@ static_assert(HM_AG_LG == 7 && HM_AG_CELLS == 128 * 128, "padded histogram");
  * bucket total (zoom z_top-7) in wave 0.  Every thread calls; the histogram's
  * rows are ROW words apart; s19 is 1024 words of 16-B-aligned scratch LDS. */
 template <uint32_t ROW>
-__device__ __forceinline__ uint64_t hm_reg_pyramid7(const uint32_t* grid, int z_top, uint64_t prefix, const HmOut& o,
+__device__ __forceinline__ uint64_t hm_reg_pyramid7(uint32_t* grid, int z_top, uint64_t prefix, const HmOut& o,
                                                     uint32_t* s19, uint32_t* scr, unsigned long long* sbase)
 {
     constexpr int NW = HM_AG_THREADS / 64;
@@ -3240,6 +3243,40 @@ __device__ __forceinline__ uint64_t hm_reg_pyramid7(const uint32_t* grid, int z_
     }
     __syncthreads();
     uint64_t base = *sbase + scr[w];
+#if HM_AG_STAGE
+    /* the wave's cells staged in its share of the (now dead) histogram as
+     * (level << 14 | cell, count) pairs and written out a whole line per
+     * store (HM_AG_STAGE; as k_small_pairs' hm_sp_flush) */
+    constexpr uint32_t SC = HM_AG_PADDED / NW / 2 / 64 * 64;   /* cells per wave */
+    uint2* stg = (uint2*)grid + (uint32_t)w * SC;
+    uint32_t fill = 0;
+    const auto flush = [&]() {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        for (uint32_t q0 = 0; q0 < fill; q0 += 64) {
+            const uint32_t q = q0 + (uint32_t)lane;
+            const uint2 x = stg[q < fill ? q : 0u];
+            const int l = (int)(x.x >> 14);
+            const uint64_t pos = base + q;
+            if (q < fill && pos < o.capacity) {
+                o.keys[pos] = hm_cell_key(z_top - l, prefix, 7 - l, x.x & 0x3FFFu);
+                o.counts[pos] = x.y;
+            }
+        }
+        base += fill;
+        fill = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    };
+    auto put = [&](bool nz, int z, int lg, uint32_t i, uint32_t v) {
+        if (fill + 64u > SC) flush();   /* wave-uniform */
+        const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
+        if (nz) stg[fill + hm_mbcnt(m)] = make_uint2(((uint32_t)(z_top - z) << 14) | i, v);
+        fill += (uint32_t)__builtin_popcountll(m);
+    };
+#else
     auto put = [&](bool nz, int z, int lg, uint32_t i, uint32_t v) {
         const uint64_t m = __builtin_amdgcn_ballot_w64(nz);
         const uint64_t pos = base + hm_mbcnt(m);
@@ -3249,6 +3286,8 @@ __device__ __forceinline__ uint64_t hm_reg_pyramid7(const uint32_t* grid, int z_
         }
         base += (uint32_t)__builtin_popcountll(m);
     };
+    const auto flush = [&]() {};
+#endif
     if (i0)
 #pragma unroll
         for (int j = 0; j < 16; j++)
@@ -3257,6 +3296,7 @@ __device__ __forceinline__ uint64_t hm_reg_pyramid7(const uint32_t* grid, int z_
 #pragma unroll
         for (int j = 0; j < 4; j++) put(d[j] != 0, z_top - 1, 6, (2u * br + (j >> 1)) * 64u + 2u * bc + (j & 1), d[j]);
     if (i2) put(e != 0, z_top - 2, 5, br * 32u + bc, e);
+    flush();
     if (w == 0) {
         base = *sbase + scr[NW];
         if (i3)
@@ -3265,6 +3305,7 @@ __device__ __forceinline__ uint64_t hm_reg_pyramid7(const uint32_t* grid, int z_
         if (i4) put(h != 0, z_top - 4, 3, R * 8u + C, h);
         if (i5) put(l5 && h5 != 0, z_top - 5, 2, (R >> 1) * 4u + (C >> 1), h5);
         if (i6) put(l6 && h6 != 0, z_top - 6, 1, (R >> 2) * 2u + (C >> 2), h6);
+        flush();
     }
     return tot;
 }

@@ -24,6 +24,7 @@ VARIANTS = {
     "spunfused": ["HM_SP_FUSED=0"],          # <= 32-key buckets through k_small_sort / scan / k_small_emit (round 5)
     "spres": ["HM_SPW_RESIDENT=1"],          # k_small_sort / k_small_emit on grids of their resident blocks
     "agpad4": ["HM_AG_PADW=4u"],             # k_aggregate histogram rows padded by 4 words (8 shipped)
+    "agnostage": ["HM_AG_STAGE=0"],          # hm_reg_pyramid7: per-level cell stores (no LDS staging)
     "spp8": ["HM_SPP_WAVES=8"],              # k_small_pairs: 8-wave blocks
     "sprows16": ["HM_SPP_ROWS=16"],          # k_small_pairs: 16 rows a round (7 blocks per CU with staging)
     "spnostage": ["HM_SPP_STAGE=0"],         # k_small_pairs: per-level cell stores (no LDS staging)
